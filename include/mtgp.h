@@ -1,0 +1,179 @@
+/*
+ * mtgp.h -- C ABI of the MI355X population-fitness evaluator for MultiTreeGP.
+ *
+ * Drop-in boundary.  The reference has no FFI: its hot path is the
+ * Python call chain
+ *     GeneticProgramming.evaluate_population(populations, data)      gp.py:403-433
+ *       -> jit(shard_map(shard_eval))                                gp.py:259-269
+ *         -> vmap(fitness_function.__call__(coeffs, nodes, data, tree_evaluator))
+ *              dynamic_evaluate.py:37-118 / feedforward_evaluate.py:36-110 /
+ *              SR_evaluator.py:30-94
+ *           -> tree_evaluator = vmap_foriloop / foriloop / body_fun  gp.py:356-401
+ * These entry points are what a ctypes / cffi binding of that chain needs:
+ *     mtgp_flatten   replaces the per-call tree walk of body_fun/foriloop (gp.py:356-388):
+ *                    it turns the [P,T,N,4] population into straight-line programs once
+ *                    per generation;
+ *     mtgp_eval_rk4  replaces shard_eval's vmap over individuals x rollouts of
+ *                    diffeqsolve(ODETerm(_drift)) + fitness post-processing
+ *                    (dyn.py:49-52, gp.py:424) with one HIP kernel launch.
+ * All pointers inside the descriptor structs are DEVICE pointers owned by the caller.
+ * Calls are stream-ordered and asynchronous; nothing allocates or synchronises, so a
+ * caller may capture them into a hipGraph.  Errors are returned as MTGP_ERR_* codes,
+ * never thrown; per-tree flatten failures land in status_out (device).
+ */
+#ifndef MTGP_H
+#define MTGP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MTGP_ABI_VERSION 1
+
+/* ---------------------------------------------------------------- limits */
+#define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
+#define MTGP_MAX_NODES 256   /* max_nodes N per tree (gp.py:69)                */
+#define MTGP_MAX_DATA 64     /* data-vector length D seen by a tree            */
+#define MTGP_STACK_MAX 8     /* operand-stack slots per lane (Sethi-Ullman)    */
+
+/* ---------------------------------------------------------------- errors */
+#define MTGP_OK 0
+#define MTGP_ERR_ARG -1          /* bad size / null pointer / unsupported combination */
+#define MTGP_ERR_LAUNCH -2       /* hipLaunchKernel failed                             */
+#define MTGP_ERR_PROG_TOO_LONG 3 /* status_out: program longer than L                  */
+#define MTGP_ERR_STACK 4         /* status_out: operand stack deeper than MTGP_STACK_MAX */
+
+/* ---------------------------------------------- node library (gp.py:132-199) */
+/* Function code of every opcode of the reference's node library.  Opcode 0 is the
+ * empty node (value 0.0), opcode 1 the coefficient (value column when f == 1.0 exactly,
+ * gp.py:372; otherwise lambda -> 0.0, gp.py:135), operators follow in operator_list
+ * order, variables in first-appearance order (gp.py:143-180). */
+enum {
+  MTGP_FN_ZERO = 0, /* opcode 0 / 1 through the switch: 0.0                       */
+  MTGP_FN_VAR = 1,  /* lambda_leaf(opcode - var_start)             gp.py:30-31    */
+  MTGP_FN_ADD = 2,  /* "+"  (x, y) -> x + y                        gp.py:27-28    */
+  MTGP_FN_SUB = 3,  /* "-"  x - y                                                  */
+  MTGP_FN_MUL = 4,  /* "*"  x * y                                                  */
+  MTGP_FN_DIV = 5,  /* "/"  x / y   (IEEE, unprotected: SymbolicRegression.ipynb)  */
+  MTGP_FN_SIN = 6,  /* "sin" f(x)                                  gp.py:24-25    */
+  MTGP_FN_COS = 7   /* "cos"                                                       */
+};
+
+typedef struct {
+  int32_t n_funcs;   /* 2 + K + V: lax.switch branch count (index is clamped)       */
+  int32_t var_start; /* first variable opcode = 2 + K                               */
+  int8_t fn[MTGP_MAX_FUNCS];
+} MtgpNodeLibrary;
+
+/* One straight-line program to emit per individual: which tree, how long the data
+ * vector is, and which data slots are known to hold +0.0 (e.g. the readout during the
+ * ODE solve sees zeros for y and u, dyn.py:113). */
+typedef struct {
+  int32_t tree;
+  int32_t n_data;
+  uint64_t zero_mask;
+} MtgpProgramSpec;
+
+/* ------------------------------------------------------------ program format */
+/* Accumulator machine, postorder with leaves folded into their parent.
+ * word op: bits 0-7 opcode, bits 8-15 data slot.  imm: f32 constant. */
+enum {
+  MTGP_OP_LDC = 0, MTGP_OP_LDCP, MTGP_OP_LDV, MTGP_OP_LDVP, /* P = push acc first */
+  MTGP_OP_ADDC, MTGP_OP_SUBC, MTGP_OP_RSUBC, MTGP_OP_MULC, MTGP_OP_DIVC, MTGP_OP_RDIVC,
+  MTGP_OP_ADDV, MTGP_OP_SUBV, MTGP_OP_RSUBV, MTGP_OP_MULV, MTGP_OP_DIVV, MTGP_OP_RDIVV,
+  MTGP_OP_ADDS, MTGP_OP_SUBS, MTGP_OP_RSUBS, MTGP_OP_MULS, MTGP_OP_DIVS, MTGP_OP_RDIVS,
+  MTGP_OP_SIN, MTGP_OP_COS,
+  MTGP_OP_COUNT
+};
+typedef struct {
+  uint32_t op;
+  float imm;
+} MtgpInstr;
+
+/* -------------------------------------------------------------- the models */
+enum {
+  MTGP_MODEL_ACROBOT_DYNAMIC = 1, /* dynamic_evaluate.Evaluator + Acrobot  dyn.py:10-118 */
+  MTGP_MODEL_ACROBOT_STATIC = 2,  /* feedforward_evaluate.Evaluator + Acrobot ff.py:10-110 */
+  MTGP_MODEL_SR = 3               /* SR_evaluator.Evaluator             sr.py:9-94       */
+};
+
+typedef struct {
+  int32_t model;
+  int32_t n_var;      /* latent env state (Acrobot 4) / SR state dims            */
+  int32_t state_size; /* dynamic: hidden-state trees (dyn.py:83)                 */
+  int32_t n_obs;      /* Acrobot: 4                                              */
+  int32_t n_control;  /* Acrobot: 1                                              */
+  int32_t n_targets;  /* Acrobot: 0                                              */
+  int32_t n_steps;    /* fixed RK4 steps from ts[0] to ts[-1]                    */
+  int32_t save_every; /* steps between save points; n_save = n_steps/save_every+1 */
+  int32_t n_save;     /* len(ts)                                                 */
+  float h;            /* dt0                                                      */
+  float max_fitness;  /* 1e4 control (dyn.py:27, ff.py:27), 1e5 SR (sr.py:22)    */
+  float parsimony;    /* size_parsinomy (gp.py:424)                               */
+  /* program slots in the flattened table (MtgpProgramSpec order), -1 if unused   */
+  int32_t prog_state;        /* first of state_size (dynamic) / n_var (SR) trees   */
+  int32_t prog_readout;      /* readout / policy during the solve                  */
+  int32_t prog_readout_save; /* readout at the save points (dyn.py:101)            */
+  int32_t readout_save_same; /* 1: equal to prog_readout, 0: differ, -1: compare  */
+} MtgpModel;
+
+typedef struct {
+  const float* x0;      /* [R, n_var]                                       */
+  const float* params;  /* [R, 4] Acrobot (l1, l2, m1, m2) acrobot.py:34-49   */
+  const float* targets; /* [R, n_targets] (may be NULL when n_targets == 0)  */
+  const float* ts;      /* [n_save] save times (fitness mask acrobot.py:82)  */
+  const float* ys_true; /* SR: [n_save, n_var, R] ground truth, time-major   */
+  int32_t R;
+} MtgpRollouts;
+
+/* Outputs.  Trajectories are time-major structure-of-arrays so that every save point
+ * is one coalesced 256-B store per wave: xs[(k*n_var + c)*P*R + p*R + r]. */
+typedef struct {
+  float* fitness;         /* [P] final fitness incl. parsimony (required)     */
+  float* rollout_fitness; /* [P, R] raw per-rollout fitness or NULL           */
+  float* xs;              /* [n_save, n_var, P*R] or NULL                     */
+  float* ys;              /* [n_save, n_obs, P*R] or NULL (control models)    */
+  float* us;              /* [n_save, n_control, P*R] or NULL                 */
+  float* acts;            /* [n_save, state_size, P*R] or NULL (dynamic)      */
+} MtgpOutputs;
+
+/* ------------------------------------------------------------- entry points */
+int mtgp_abi_version(void);
+
+/* Flatten a device population f32 [P, T, N, 4] (gp.py:412 layout) into programs
+ * prog_out[P, n_prog, L], lengths len_out[P, n_prog], node counts nodes_out[P]
+ * (non-empty rows, gp.py:424) and per-program status_out[P, n_prog]. */
+int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N,
+                 const MtgpNodeLibrary* lib, const MtgpProgramSpec* specs, int32_t n_prog,
+                 int32_t L, MtgpInstr* prog_out, int32_t* len_out, int32_t* nodes_out,
+                 int32_t* status_out, void* stream);
+
+/* Same algorithm on the host (one tree), for tests and tooling. Returns program length
+ * or a negative MTGP_ERR_* / -MTGP_ERR_PROG_TOO_LONG / -MTGP_ERR_STACK. */
+int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* lib,
+                           int32_t n_data, uint64_t zero_mask, int32_t L, MtgpInstr* out,
+                           int32_t* stack_need);
+
+/* The tree_evaluator plugin (GeneticProgramming.vmap_foriloop, gp.py:390-401) batched:
+ * every flattened program evaluated on M data vectors data[M, n_data] (shared by all
+ * individuals) -> out[P, n_prog, M]. */
+int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L,
+                       int32_t P, const float* data, int32_t M, int32_t n_data, float* out,
+                       void* stream);
+
+/* Integrate every (individual, rollout) with fixed-step RK4 and reduce fitness. */
+int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,
+                  int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
+                  const MtgpRollouts* rollouts, const MtgpOutputs* out, void* stream);
+
+/* Wall time of the last mtgp_eval_rk4 kernel on `stream`, measured with hipEvents
+ * recorded around the launch (ms); -1 if none.  Synchronises that event. */
+float mtgp_last_kernel_ms(void);
+int mtgp_set_timing(int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MTGP_H */

@@ -1,0 +1,739 @@
+// mtgp_kernels.hip -- MI355X (gfx950) population-fitness evaluator for MultiTreeGP.
+//
+// One wavefront = one individual x up to 64 rollouts (lanes).  Every lane of a wave runs
+// the SAME program, so the opcode stream is wave-uniform: it is fetched with scalar loads
+// and dispatched with scalar branches, while the per-rollout values live in VGPRs.  The
+// data vector a tree reads and the operand stack live in LDS (one 64-lane column per slot,
+// conflict-free).  The interpreter is fused into a fixed-step RK4 integrator: the ODE state
+// stays in registers for the whole rollout, fitness is accumulated online at the save
+// points, and only the [P] fitness (plus optional time-major trajectories) leaves the CU.
+//
+// Reference path replaced: GeneticProgramming.evaluate_population -> shard_eval ->
+// vmap(Evaluator.__call__) -> diffeqsolve(_drift -> vmap_foriloop)  (gp.py:259-269,
+// 403-433; dynamic_evaluate.py:37-118; feedforward_evaluate.py:36-110;
+// SR_evaluator.py:30-94; acrobot.py:29-87).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mtgp.h"
+#include "mtgp_f32math.h"
+#include "mtgp_flatten.h"
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kDMax = 8;  // data slots held in LDS by the small-state kernels
+constexpr int kSMax = MTGP_STACK_MAX;
+constexpr float kInf = __builtin_huge_valf();
+
+__device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// --------------------------------------------------------------------------------------
+// The interpreter.  `dv` = this lane's column of the wave's LDS data vector (stride 64
+// floats per slot), `st` = this lane's column of the operand stack.  `code`/`len` are
+// wave-uniform.
+__device__ __forceinline__ float run_prog(const MtgpInstr* __restrict__ code, int len,
+                                          const float* dv, float* st) {
+  float acc = 0.0f;
+  int sp = 0;
+  for (int i = 0; i < len; ++i) {
+    const uint32_t w = code[i].op;
+    const float imm = code[i].imm;
+    const uint32_t op = w & 0xffu;
+    const uint32_t slot = (w >> 8) & 0xffu;
+    switch (op) {
+      case MTGP_OP_LDC: acc = imm; break;
+      case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; acc = imm; break;
+      case MTGP_OP_LDV: acc = dv[slot * kWave]; break;
+      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = dv[slot * kWave]; break;
+      case MTGP_OP_ADDC: acc = acc + imm; break;
+      case MTGP_OP_SUBC: acc = acc - imm; break;
+      case MTGP_OP_RSUBC: acc = imm - acc; break;
+      case MTGP_OP_MULC: acc = acc * imm; break;
+      case MTGP_OP_DIVC: acc = acc / imm; break;
+      case MTGP_OP_RDIVC: acc = imm / acc; break;
+      case MTGP_OP_ADDV: acc = acc + dv[slot * kWave]; break;
+      case MTGP_OP_SUBV: acc = acc - dv[slot * kWave]; break;
+      case MTGP_OP_RSUBV: acc = dv[slot * kWave] - acc; break;
+      case MTGP_OP_MULV: acc = acc * dv[slot * kWave]; break;
+      case MTGP_OP_DIVV: acc = acc / dv[slot * kWave]; break;
+      case MTGP_OP_RDIVV: acc = dv[slot * kWave] / acc; break;
+      case MTGP_OP_ADDS: --sp; acc = acc + st[sp * kWave]; break;
+      case MTGP_OP_SUBS: --sp; acc = acc - st[sp * kWave]; break;
+      case MTGP_OP_RSUBS: --sp; acc = st[sp * kWave] - acc; break;
+      case MTGP_OP_MULS: --sp; acc = acc * st[sp * kWave]; break;
+      case MTGP_OP_DIVS: --sp; acc = acc / st[sp * kWave]; break;
+      case MTGP_OP_RDIVS: --sp; acc = st[sp * kWave] / acc; break;
+      case MTGP_OP_SIN: acc = mtgp_sinf(acc); break;
+      default: acc = mtgp_cosf(acc); break;  // MTGP_OP_COS
+    }
+  }
+  return acc;
+}
+
+// --------------------------------------------------------------------------------------
+// Acrobot (acrobot.py:7-87).  Per-rollout invariant products are formed once with the same
+// operations/operands as the Python expression, so the per-call result is bit-identical.
+struct AcroConst {
+  float m2, d1a, l1sq_lc2sq, two_l1lc2, lc2sq, l1lc2, m2lc2g, A0, B0, C0, m2l1lc2, den0;
+};
+
+__device__ __forceinline__ AcroConst acro_const(float l1, float l2, float m1, float m2) {
+  AcroConst k;
+  const float lc1 = 0.5f * l1, lc2 = 0.5f * l2, g = 9.81f;
+  k.m2 = m2;
+  k.d1a = m1 * (lc1 * lc1);
+  k.l1sq_lc2sq = (l1 * l1) + (lc2 * lc2);
+  k.two_l1lc2 = (2.0f * l1) * lc2;
+  k.lc2sq = lc2 * lc2;
+  k.l1lc2 = l1 * lc2;
+  k.m2lc2g = (m2 * lc2) * g;
+  k.A0 = ((-m2) * l1) * lc2;
+  k.B0 = ((2.0f * m2) * l1) * lc2;
+  k.C0 = ((m1 * lc1) + (m2 * l1)) * g;
+  k.m2l1lc2 = (m2 * l1) * lc2;
+  k.den0 = (m2 * (lc2 * lc2)) + 1.0f;
+  return k;
+}
+
+__device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4], float u_raw,
+                                           float dx[4]) {
+  const float control = mtgp_clip1(u_raw);
+  const float th1 = x[0], th2 = x[1], thd1 = x[2], thd2 = x[3];
+  const float c2 = mtgp_cosf(th2), s2 = mtgp_sinf(th2), s1 = mtgp_sinf(th1);
+  const float d1 = ((k.d1a + k.m2 * (k.l1sq_lc2sq + k.two_l1lc2 * c2)) + 1.0f) + 1.0f;
+  const float d2 = k.m2 * (k.lc2sq + k.l1lc2 * c2) + 1.0f;
+  const float phi2 = k.m2lc2g * mtgp_cosf((th1 + th2) - MTGP_HALF_PI_F);
+  const float phi1 = (((k.A0 * (thd2 * thd2)) * s2 - ((k.B0 * thd1) * thd2) * s1) +
+                      k.C0 * mtgp_cosf(th1 - MTGP_HALF_PI_F)) + phi2;
+  const float num = ((control + (d2 / d1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
+  const float den = k.den0 - (d2 * d2) / d1;
+  const float a2 = num / den;
+  const float a1 = (-((d2 * a2) + phi1)) / d1;
+  dx[0] = thd1;
+  dx[1] = thd2;
+  dx[2] = a1;
+  dx[3] = a2;
+}
+
+// f_obs with C = I and zero observation noise (cbase.py:43-48): y = C@x + 0, i.e. x_i + 0
+// when every component is finite; C@x propagates NaN from any non-finite x_j (0*inf).
+__device__ __forceinline__ void acro_f_obs(const float x[4], float y[4]) {
+  const bool f0 = mtgp_isfinite(x[0]), f1 = mtgp_isfinite(x[1]), f2 = mtgp_isfinite(x[2]),
+             f3 = mtgp_isfinite(x[3]);
+  const float qn = mtgp_qnan();
+  y[0] = (f1 && f2 && f3) ? x[0] + 0.0f : qn;
+  y[1] = (f0 && f2 && f3) ? x[1] + 0.0f : qn;
+  y[2] = (f0 && f1 && f3) ? x[2] + 0.0f : qn;
+  y[3] = (f0 && f1 && f2) ? x[3] + 0.0f : qn;
+  y[0] = mtgp_wrap_angle(y[0]);
+  y[1] = mtgp_wrap_angle(y[1]);
+}
+
+__device__ __forceinline__ bool acro_bad(const float* s, int n) {
+  bool bad = !(__builtin_fabsf(s[2]) <= MTGP_8PI_F) && !mtgp_isnan(s[2]);
+  bad = bad || (!(__builtin_fabsf(s[3]) <= MTGP_18PI_F) && !mtgp_isnan(s[3]));
+  for (int i = 0; i < n; ++i) bad = bad || !mtgp_isfinite(s[i]);
+  return bad;
+}
+
+struct KArgs {
+  MtgpModel m;
+  const MtgpInstr* prog;
+  const int32_t* plen;
+  int32_t n_prog, L;
+  const int32_t* nodes;
+  int32_t P;
+  MtgpRollouts ro;
+  MtgpOutputs out;
+};
+
+// per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
+struct AcroFit {
+  bool settled;
+  float csum, c0incl, F;
+};
+
+__device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool incl, float u,
+                                                float x0, float x1) {
+  if (f.settled) return;
+  const bool reached = ((-mtgp_cosf(x0)) - mtgp_cosf(x0 + x1)) > 1.5f;
+  const float cost = (u * 0.01f) * u;
+  if (k == 0) {
+    f.c0incl = incl ? cost : 0.0f;
+    f.csum = cost;
+    if (reached) { f.settled = true; f.F = (float)S + f.c0incl; }
+  } else if (reached) {
+    f.settled = true;
+    f.F = (float)k + (f.csum + (incl ? cost : 0.0f));
+  } else {
+    f.csum = f.csum + cost;
+  }
+}
+
+// wave reduction: xor butterfly == pairwise tree in lane order (mirrored by the oracle)
+__device__ __forceinline__ float wave_pairwise_sum(float v) {
+#pragma unroll
+  for (int w = 1; w < kWave; w <<= 1) v = v + __shfl_xor(v, w, kWave);
+  return v;
+}
+
+__device__ __forceinline__ void finish_individual(const KArgs& A, int p, int r, bool active, float F) {
+  const float mx = A.m.max_fitness;
+  if (A.out.rollout_fitness && active) A.out.rollout_fitness[(size_t)p * A.ro.R + r] = F;
+  float fr = active ? (mtgp_isfinite(F) ? F : mx) : 0.0f;
+  const float sum = wave_pairwise_sum(fr);
+  if ((threadIdx.x & 63) == 0) {
+    float mean = sum / (float)A.ro.R;
+    mean = mean < 0.0f ? 0.0f : (mean > mx ? mx : mean);
+    A.out.fitness[p] = mean + A.m.parsimony * (float)A.nodes[p];
+  }
+}
+
+__device__ __forceinline__ bool save_incl(const float* ts, int k) {
+  const float dts = ts[1] - ts[0];
+  return !((ts[k] / dts) > (float)k);
+}
+
+// --------------------------------------------------------------------------------------
+// Common kernel prologue: wave -> individual, lane -> rollout.
+struct Lane {
+  int wave, lane, p, r, rr;
+  bool active;
+};
+
+__device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
+  L.wave = uni(threadIdx.x >> 6);
+  L.lane = threadIdx.x & 63;
+  L.p = uni(blockIdx.x * kWavesPerBlock + L.wave);
+  if (L.p >= A.P) return false;
+  L.r = L.lane;
+  L.active = L.r < A.ro.R;
+  L.rr = L.active ? L.r : 0;
+  return true;
+}
+
+// RK4 stage input: stage 0 -> s, stages 1,2 -> s + h/2 k, stage 3 -> s + h k
+__device__ __forceinline__ float stage_in(int stage, float s, float k, float h, float h2) {
+  return stage == 0 ? s : MTGP_FMAF(stage == 3 ? h : h2, k, s);
+}
+// RK4 accumulator: k1 + 2 k2 + 2 k3 + k4 (fma form shared with the oracle)
+__device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
+  return stage == 0 ? k : (stage == 3 ? acc + k : MTGP_FMAF(2.0f, k, acc));
+}
+
+// --------------------------------------------------------------------------------------
+// Acrobot, dynamic symbolic policy (dynamic_evaluate.py:65-118).  NA = state_size.
+// Data slots: y 0..3 | a 4..4+NA-1 | u 4+NA | targets.  Per stage the programs run in
+// the order of _drift (dyn.py:107-118): readout (y, u folded to 0) -> drift -> f_obs ->
+// state equations; at save points the save-time readout (dyn.py:101) is appended.
+template <int NA, bool TRAJ>
+__global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
+  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  Lane Ln;
+  if (!lane_setup(A, Ln)) return;
+  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  constexpr int uslot = 4 + NA;
+  const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
+                                 A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
+  const size_t PR = (size_t)A.P * R;
+  const size_t unit = (size_t)p * R + r;
+  for (int t = 0; t < A.m.n_targets; ++t) dv[(uslot + 1 + t) * kWave] = A.ro.targets[rr * A.m.n_targets + t];
+
+  // program table of this individual: q = 0 readout, 1..NA state equations, NA+1 save readout
+  const MtgpInstr* base = A.prog + (size_t)p * A.n_prog * A.L;
+  const int32_t* lens = A.plen + (size_t)p * A.n_prog;
+  // readout at save points == readout in the drift when the readout reads no y (u is
+  // zero in both): then the stage-1 u is reused (bit-identical, one tree eval saved)
+  bool same = A.m.readout_save_same > 0;
+  if (A.m.readout_save_same < 0) {
+    const int la = uni(lens[A.m.prog_readout]), lb = uni(lens[A.m.prog_readout_save]);
+    same = la == lb;
+    const MtgpInstr* pa = base + (size_t)A.m.prog_readout * A.L;
+    const MtgpInstr* pb = base + (size_t)A.m.prog_readout_save * A.L;
+    for (int i = 0; same && i < la; ++i)
+      same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
+  }
+
+  float x[4], a[NA], kx[4], ka[NA], ax[4], aa[NA];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = A.ro.x0[rr * 4 + i];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) a[j] = 0.0f;
+
+  AcroFit fit = {!active, 0.0f, 0.0f, 0.0f};
+  bool dead = !active;  // state frozen at +inf once the event state has been saved
+  bool pending = false; // event fired at the end of the previous step
+  bool prev_ok;
+  {
+    float s0[4 + NA];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) s0[i] = x[i];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) s0[4 + j] = a[j];
+    prev_ok = !acro_bad(s0, 4 + NA);
+  }
+
+  for (int step = 0;; ++step) {
+    const bool last = step == n_steps;
+    const bool is_save = (step % save_every) == 0;
+    bool stop = last;
+#pragma unroll 1
+    for (int stage = 0; stage < 4; ++stage) {
+      float xt[4], at[NA], y[4], u = 0.0f, us = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) dv[(4 + j) * kWave] = at[j];
+      const int nq = (stage == 0 && is_save && !same) ? NA + 2 : NA + 1;
+#pragma unroll 1
+      for (int q = 0; q < nq; ++q) {
+        const int slot = uni(q == 0 ? A.m.prog_readout : (q <= NA ? A.m.prog_state + q - 1 : A.m.prog_readout_save));
+        const float v = run_prog(base + (size_t)slot * A.L, uni(lens[slot]), dv, st);
+        if (q == 0) {
+          u = v;
+          acro_drift(K, xt, u, kx);
+          acro_f_obs(xt, y);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) dv[i * kWave] = y[i];
+          dv[uslot * kWave] = u;
+        } else if (q <= NA) {
+#pragma unroll
+          for (int j = 0; j < NA; ++j) ka[j] = (q - 1 == j) ? v : ka[j];
+        } else {
+          us = v;
+        }
+      }
+      if (stage == 0) {
+        if (is_save) {
+          const int k = step / save_every;
+          if (same) us = u;
+          if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), us, x[0], x[1]);
+          if (TRAJ && active) {
+            if (A.out.xs) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) A.out.xs[((size_t)k * 4 + i) * PR + unit] = x[i];
+            }
+            if (A.out.ys) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) A.out.ys[((size_t)k * 4 + i) * PR + unit] = y[i];
+            }
+            if (A.out.us) A.out.us[(size_t)k * PR + unit] = us;
+            if (A.out.acts) {
+#pragma unroll
+              for (int j = 0; j < NA; ++j) A.out.acts[((size_t)k * NA + j) * PR + unit] = a[j];
+            }
+          }
+        }
+        if (pending) {  // the event state has been saved: freeze at +inf (saveat fill)
+          pending = false;
+          dead = true;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = kInf;
+#pragma unroll
+          for (int j = 0; j < NA; ++j) a[j] = kInf;
+        }
+        if (!TRAJ && __all(fit.settled || dead)) stop = true;
+        if (stop) break;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) aa[j] = stage_acc(stage, aa[j], ka[j]);
+    }
+    if (stop) break;
+    if (!dead) {
+      float sn[4 + NA];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { x[i] = MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) { a[j] = MTGP_FMAF(h6, aa[j], a[j]); sn[4 + j] = a[j]; }
+      const bool ok = !acro_bad(sn, 4 + NA);
+      if (prev_ok && !ok) pending = true;
+      prev_ok = ok;
+    }
+  }
+  if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
+  finish_individual(A, p, r, active, fit.F);
+}
+
+// --------------------------------------------------------------------------------------
+// Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
+template <bool TRAJ>
+__global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
+  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  Lane Ln;
+  if (!lane_setup(A, Ln)) return;
+  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
+                                 A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
+  const size_t PR = (size_t)A.P * R;
+  const size_t unit = (size_t)p * R + r;
+  for (int t = 0; t < A.m.n_targets; ++t) dv[(4 + t) * kWave] = A.ro.targets[rr * A.m.n_targets + t];
+  const MtgpInstr* c_pol = A.prog + ((size_t)p * A.n_prog + A.m.prog_readout) * A.L;
+  const int l_pol = uni(A.plen[(size_t)p * A.n_prog + A.m.prog_readout]);
+
+  float x[4], kx[4], ax[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) x[i] = A.ro.x0[rr * 4 + i];
+  AcroFit fit = {!active, 0.0f, 0.0f, 0.0f};
+  bool dead = !active, pending = false;
+  bool prev_ok = !acro_bad(x, 4);
+
+  for (int step = 0;; ++step) {
+    const bool last = step == n_steps;
+    const bool is_save = (step % save_every) == 0;
+    bool stop = last;
+#pragma unroll 1
+    for (int stage = 0; stage < 4; ++stage) {
+      float xt[4], y[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
+      acro_f_obs(xt, y);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dv[i * kWave] = y[i];
+      const float u = run_prog(c_pol, l_pol, dv, st);  // ff.py:106-107 (and :97 at saves)
+      acro_drift(K, xt, u, kx);
+      if (stage == 0) {
+        if (is_save) {
+          const int k = step / save_every;
+          if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), u, x[0], x[1]);
+          if (TRAJ && active) {
+            if (A.out.xs) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) A.out.xs[((size_t)k * 4 + i) * PR + unit] = x[i];
+            }
+            if (A.out.ys) {
+#pragma unroll
+              for (int i = 0; i < 4; ++i) A.out.ys[((size_t)k * 4 + i) * PR + unit] = y[i];
+            }
+            if (A.out.us) A.out.us[(size_t)k * PR + unit] = u;
+          }
+        }
+        if (pending) {
+          pending = false;
+          dead = true;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) x[i] = kInf;
+        }
+        if (!TRAJ && __all(fit.settled || dead)) stop = true;
+        if (stop) break;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+    }
+    if (stop) break;
+    if (!dead) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
+      const bool ok = !acro_bad(x, 4);
+      if (prev_ok && !ok) pending = true;
+      prev_ok = ok;
+    }
+  }
+  if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
+  finish_individual(A, p, r, active, fit.F);
+}
+
+// --------------------------------------------------------------------------------------
+// Symbolic regression of an ODE (SR_evaluator.py:57-94): dx_i = tree_i(x); MSE vs ys_true.
+template <int NV, bool TRAJ>
+__global__ void __launch_bounds__(256) k_sr(KArgs A) {
+  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  Lane Ln;
+  if (!lane_setup(A, Ln)) return;
+  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const size_t PR = (size_t)A.P * R;
+  const size_t unit = (size_t)p * R + r;
+  const MtgpInstr* base = A.prog + (size_t)p * A.n_prog * A.L;
+  const int32_t* lens = A.plen + (size_t)p * A.n_prog;
+  float x[NV], kx[NV], ax[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+  auto bad = [&](const float* s) {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) b = b || !mtgp_isfinite(s[i]);
+    return b;
+  };
+  bool dead = !active, pending = false, prev_ok = !bad(x);
+  float tot = 0.0f;
+  for (int step = 0;; ++step) {
+    if ((step % save_every) == 0) {
+      const int k = step / save_every;
+      float sq = 0.0f;
+#pragma unroll
+      for (int d = 0; d < NV; ++d) {
+        const float e = x[d] - A.ro.ys_true[((size_t)k * NV + d) * R + rr];
+        sq = (d == 0) ? e * e : sq + e * e;
+      }
+      tot = tot + sq;
+      if (TRAJ && active && A.out.xs) {
+#pragma unroll
+        for (int d = 0; d < NV; ++d) A.out.xs[((size_t)k * NV + d) * PR + unit] = x[d];
+      }
+    }
+    if (pending) {
+      pending = false;
+      dead = true;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[i] = kInf;
+    }
+    if (step == n_steps) break;
+    if (!TRAJ && __all(dead)) {  // every remaining save point adds (inf - y)^2
+      if (active && mtgp_isfinite(tot)) tot = kInf;
+      break;
+    }
+#pragma unroll 1
+    for (int stage = 0; stage < 4; ++stage) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) dv[i * kWave] = stage_in(stage, x[i], kx[i], h, h2);
+#pragma unroll 1
+      for (int q = 0; q < NV; ++q) {
+        const int slot = uni(A.m.prog_state + q);
+        const float v = run_prog(base + (size_t)slot * A.L, uni(lens[slot]), dv, st);
+#pragma unroll
+        for (int j = 0; j < NV; ++j) kx[j] = (q == j) ? v : kx[j];
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+    }
+    if (!dead) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
+      const bool ok = !bad(x);
+      if (prev_ok && !ok) pending = true;
+      prev_ok = ok;
+    }
+  }
+  const float F = tot / (float)S;
+  finish_individual(A, p, r, active, F);
+}
+
+// --------------------------------------------------------------------------------------
+// tree_evaluator plugin (gp.py:390-401): every program on M shared data vectors.
+// One wave per (individual, program, chunk of 64 data vectors); data vector in LDS.
+__global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restrict__ prog,
+                                                       const int32_t* __restrict__ plen, int n_prog, int L,
+                                                       int P, const float* __restrict__ data, int M,
+                                                       int n_data, float* __restrict__ out) {
+  extern __shared__ float dyn_lds[];
+  const int wave = uni(threadIdx.x >> 6), lane = threadIdx.x & 63;
+  const int chunks = (M + 63) / 64;
+  const long item = (long)blockIdx.x * kWavesPerBlock + wave;
+  if (item >= (long)P * n_prog * chunks) return;
+  const int ch = uni((int)(item % chunks));
+  const long pj = item / chunks;
+  const int m = ch * 64 + lane;
+  const bool active = m < M;
+  float* dv = dyn_lds + (size_t)wave * (n_data + kSMax) * kWave + lane;
+  float* st = dv + (size_t)n_data * kWave;
+  for (int d = 0; d < n_data; ++d) dv[d * kWave] = active ? data[(size_t)m * n_data + d] : 0.0f;
+  const float v = run_prog(prog + (size_t)pj * L, uni(plen[pj]), dv, st);
+  if (active) out[(size_t)pj * M + m] = v;
+}
+
+// --------------------------------------------------------------------------------------
+// Flatten: one thread per (individual, program spec); per-row scratch in LDS.
+template <int NMAX>
+__global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, int P, int T, int N,
+                                                MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
+                                                int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
+                                                int32_t* nodes_out, int32_t* status_out) {
+  constexpr int TPB = (NMAX <= 64) ? 64 : (NMAX <= 128 ? 32 : 16);
+  __shared__ mtgp::RowInfo info_all[TPB * NMAX];
+  const int t_in = threadIdx.x;
+  if (t_in >= TPB) return;
+  const long gid = (long)blockIdx.x * TPB + t_in;
+  const long total = (long)P * n_prog;
+  if (gid >= total) return;
+  const int p = (int)(gid / n_prog), j = (int)(gid % n_prog);
+  const MtgpProgramSpec sp = specs[j];
+  const float* tree = pop + ((size_t)p * T + sp.tree) * N * 4;
+  mtgp::RowInfo* info = &info_all[t_in * NMAX];
+  MtgpInstr* out = prog_out + ((size_t)p * n_prog + j) * L;
+  int need = 0;
+  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
+  len_out[(size_t)p * n_prog + j] = n > 0 ? n : 0;
+  status_out[(size_t)p * n_prog + j] = n > 0 ? 0 : -n;
+  if (j == 0) {
+    int c = 0;
+    for (int t = 0; t < T; ++t) c += mtgp::count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
+    nodes_out[p] = c;
+  }
+}
+
+hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+bool g_timing = false;
+bool g_have_timing = false;
+
+template <class F>
+int launch_timed(F&& launch, hipStream_t s) {
+  if (g_timing) {
+    if (!g_ev0) { (void)hipEventCreate(&g_ev0); (void)hipEventCreate(&g_ev1); }
+    (void)hipEventRecord(g_ev0, s);
+  }
+  launch();
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  if (g_timing) { (void)hipEventRecord(g_ev1, s); g_have_timing = true; }
+  return MTGP_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mtgp_abi_version(void) { return MTGP_ABI_VERSION; }
+
+int mtgp_set_timing(int enabled) {
+  g_timing = enabled != 0;
+  return MTGP_OK;
+}
+
+float mtgp_last_kernel_ms(void) {
+  if (!g_have_timing) return -1.0f;
+  float ms = -1.0f;
+  (void)hipEventSynchronize(g_ev1);
+  (void)hipEventElapsedTime(&ms, g_ev0, g_ev1);
+  return ms;
+}
+
+int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
+                 const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
+                 int32_t* nodes_out, int32_t* status_out, void* stream) {
+  if (!population || !lib || !specs || !prog_out || !len_out || !nodes_out || !status_out) return MTGP_ERR_ARG;
+  if (P < 0 || T <= 0 || N <= 0 || N > MTGP_MAX_NODES || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+  if (lib->n_funcs <= 0 || lib->n_funcs > MTGP_MAX_FUNCS) return MTGP_ERR_ARG;
+  if (P == 0) return MTGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const long total = (long)P * n_prog;
+  MtgpNodeLibrary libv = *lib;
+  if (N <= 64) {
+    const int tpb = 64;
+    hipLaunchKernelGGL(k_flatten<64>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T, N,
+                       libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+  } else if (N <= 128) {
+    const int tpb = 32;
+    hipLaunchKernelGGL(k_flatten<128>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
+                       N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+  } else {
+    const int tpb = 16;
+    hipLaunchKernelGGL(k_flatten<256>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
+                       N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+  }
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* lib, int32_t n_data,
+                           uint64_t zero_mask, int32_t L, MtgpInstr* out, int32_t* stack_need) {
+  if (!tree || !lib || !out || N <= 0 || N > MTGP_MAX_NODES || L <= 0) return MTGP_ERR_ARG;
+  mtgp::RowInfo info[MTGP_MAX_NODES];
+  int need = 0;
+  const int n = mtgp::flatten_tree(tree, N, lib, n_data, zero_mask, out, L, info, &need);
+  if (stack_need) *stack_need = need;
+  return n;
+}
+
+int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L, int32_t P,
+                       const float* data, int32_t M, int32_t n_data, float* out, void* stream) {
+  if (!prog || !plen || !data || !out || P < 0 || n_prog <= 0 || L <= 0 || M < 0) return MTGP_ERR_ARG;
+  if (n_data <= 0 || n_data > MTGP_MAX_DATA) return MTGP_ERR_ARG;
+  if (P == 0 || M == 0) return MTGP_OK;
+  const long items = (long)P * n_prog * ((M + 63) / 64);
+  const size_t lds = (size_t)kWavesPerBlock * (n_data + kSMax) * kWave * sizeof(float);
+  hipLaunchKernelGGL(k_eval_programs, dim3((unsigned)((items + kWavesPerBlock - 1) / kWavesPerBlock)),
+                     dim3(kWave * kWavesPerBlock), lds, (hipStream_t)stream, prog, plen, n_prog, L, P, data, M,
+                     n_data, out);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L,
+                  const int32_t* nodes, int32_t P, const MtgpRollouts* rollouts, const MtgpOutputs* out,
+                  void* stream) {
+  if (!model || !prog || !plen || !nodes || !rollouts || !out || !out->fitness) return MTGP_ERR_ARG;
+  if (P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+  if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
+  if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
+  if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
+  if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;
+  if (P == 0) return MTGP_OK;
+  KArgs A;
+  A.m = *model;
+  A.prog = prog;
+  A.plen = plen;
+  A.n_prog = n_prog;
+  A.L = L;
+  A.nodes = nodes;
+  A.P = P;
+  A.ro = *rollouts;
+  A.out = *out;
+  hipStream_t s = (hipStream_t)stream;
+  const dim3 grid((unsigned)((P + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
+  const bool traj = out->xs || out->ys || out->us || out->acts;
+  if (model->model == MTGP_MODEL_ACROBOT_DYNAMIC) {
+    if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;
+    if (model->n_targets < 0 || 4 + model->state_size + 1 + model->n_targets > kDMax) return MTGP_ERR_ARG;
+    if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
+#define MTGP_DYN(NA)                                                                                      \
+  case NA:                                                                                                \
+    return launch_timed([&] {                                                                             \
+      if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true>), grid, block, 0, s, A);                     \
+      else hipLaunchKernelGGL((k_acro_dynamic<NA, false>), grid, block, 0, s, A);                         \
+    }, s);
+    switch (model->state_size) {
+      MTGP_DYN(1)
+      MTGP_DYN(2)
+      MTGP_DYN(3)
+      default: return MTGP_ERR_ARG;
+    }
+#undef MTGP_DYN
+  } else if (model->model == MTGP_MODEL_ACROBOT_STATIC) {
+    if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;
+    if (model->n_targets < 0 || 4 + model->n_targets > kDMax) return MTGP_ERR_ARG;
+    if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
+    return launch_timed([&] {
+      if (traj) hipLaunchKernelGGL((k_acro_static<true>), grid, block, 0, s, A);
+      else hipLaunchKernelGGL((k_acro_static<false>), grid, block, 0, s, A);
+    }, s);
+  } else if (model->model == MTGP_MODEL_SR) {
+    if (!rollouts->ys_true) return MTGP_ERR_ARG;
+#define MTGP_SR(NV)                                                                                       \
+  case NV:                                                                                                \
+    return launch_timed([&] {                                                                             \
+      if (traj) hipLaunchKernelGGL((k_sr<NV, true>), grid, block, 0, s, A);                               \
+      else hipLaunchKernelGGL((k_sr<NV, false>), grid, block, 0, s, A);                                   \
+    }, s);
+    switch (model->n_var) {
+      MTGP_SR(1)
+      MTGP_SR(2)
+      MTGP_SR(3)
+      MTGP_SR(4)
+      default: return MTGP_ERR_ARG;
+    }
+#undef MTGP_SR
+  }
+  return MTGP_ERR_ARG;
+}
+
+}  // extern "C"

@@ -1,0 +1,49 @@
+"""Population sharding across GPUs (one process per GPU, torch.distributed over RCCL).
+
+Restates the reference's data parallelism (gp.py:255-262, 412-415): a 1-D mesh over the
+flattened population axis, ``P('i')`` in, ``P('i')`` out, data replicated (``P(None)``).
+Here: rank r evaluates the contiguous block ``[r*P/G, (r+1)*P/G)`` (P padded up to a multiple
+of G), then ONE all-gather of the fp32 fitness shard gives every rank the full ``[P]`` vector
+for the host-side argmin / evolution.  There is no other collective on the data path.
+"""
+from __future__ import annotations
+
+from typing import Callable, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def world() -> Tuple[int, int]:
+    if dist.is_available() and dist.is_initialized():
+        return dist.get_rank(), dist.get_world_size()
+    return 0, 1
+
+
+def shard_bounds(P: int, world_size: int, rank: int) -> Tuple[int, int, int]:
+    """(lo, hi, per_rank) of rank's contiguous block; P is padded to per_rank * world_size."""
+    per = (P + world_size - 1) // world_size
+    lo = min(rank * per, P)
+    hi = min(lo + per, P)
+    return lo, hi, per
+
+
+def gather_fitness(local: torch.Tensor, P: int, per: int, group=None) -> torch.Tensor:
+    """All-gather fixed-size fitness shards (padded to `per`) and trim to [P]."""
+    rank, ws = world()
+    if ws == 1:
+        return local[:P]
+    buf = torch.full((per,), float("inf"), dtype=local.dtype, device=local.device)
+    buf[: local.numel()] = local
+    out = torch.empty((per * ws,), dtype=local.dtype, device=local.device)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    return out[:P]
+
+
+def sharded_fitness(evaluate_shard: Callable[[int, int], torch.Tensor], P: int, group=None) -> torch.Tensor:
+    """evaluate_shard(lo, hi) -> fitness of individuals [lo, hi) on this rank's device;
+    returns the full [P] fitness on every rank."""
+    rank, ws = world()
+    lo, hi, per = shard_bounds(P, ws, rank)
+    local = evaluate_shard(lo, hi)
+    return gather_fitness(local, P, per, group)

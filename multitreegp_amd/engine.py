@@ -1,0 +1,198 @@
+"""Device engine: flatten a population and run the fused RK4 kernel through the C ABI.
+
+PyTorch is used only as device-memory / stream plumbing (caching allocator, current HIP
+stream); all compute is in libmtgp_hip.so.  The engine is the body of
+``GeneticProgramming.evaluate_population`` (gp.py:403-433) and of the per-candidate
+evaluator calls.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import _native as nat
+from .node_library import NodeLibrary
+
+
+def _require_gpu(device) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError("multitreegp_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
+    d = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if d.type != "cuda":
+        raise ValueError(f"device {d} is not a GPU device")
+    return d
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else int(t.data_ptr())
+
+
+@dataclass
+class Flattened:
+    prog: torch.Tensor     # int32 [P, n_prog, L, 2]  (MtgpInstr)
+    plen: torch.Tensor     # int32 [P, n_prog]
+    nodes: torch.Tensor    # int32 [P]
+    status: torch.Tensor   # int32 [P, n_prog]
+    L: int
+    n_prog: int
+
+
+class DeviceEngine:
+    """Binds one fitness-function config + node library to the HIP kernels."""
+
+    def __init__(self, fitness_function, library: NodeLibrary, size_parsinomy: float = 0.0, device=None):
+        self.ff = fitness_function
+        self.lib = library
+        self.parsimony = float(size_parsinomy)
+        self.device = _require_gpu(device)
+        self.native = nat.load()
+        self._node_lib = library.native()
+        self._data_key = None
+        self._data = None
+        self._specs_dev = None
+        self._specs_key = None
+
+    # ------------------------------------------------------------------ data
+    def prepare_data(self, data) -> dict:
+        """Upload the reference data tuple once (cached on the identity of its arrays)."""
+        key = tuple(id(x) for x in data) if isinstance(data, (tuple, list)) else id(data)
+        if self._data is not None and key == self._data_key:
+            return self._data
+        host = self.ff.prepare(data)
+        dev = {}
+        for name in ("x0", "params", "targets", "ts", "ys_true"):
+            a = host.get(name)
+            a = None if a is None else np.asarray(a)
+            dev[name] = None if a is None or a.size == 0 else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
+        host.update({f"{k}_dev": v for k, v in dev.items()})
+        self._data, self._data_key = host, key
+        return host
+
+    def _specs(self):
+        specs, roles = self.ff.program_specs()
+        n_data = self.ff.n_data()
+        if n_data < self.lib.n_variables:
+            # the reference fails too: lambda_leaf(i) indexes past the data vector (gp.py:30-31)
+            raise IndexError(f"data vector has {n_data} entries but the node library defines "
+                             f"{self.lib.n_variables} variables")
+        key = tuple(specs)
+        if key != self._specs_key:
+            arr = (nat.MtgpProgramSpec * len(specs))()
+            for i, (t, d, z) in enumerate(specs):
+                arr[i].tree, arr[i].n_data, arr[i].zero_mask = t, d, z
+            buf = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
+            self._specs_dev, self._specs_key = buf, key
+        return specs, roles
+
+    # -------------------------------------------------------------- flatten
+    def flatten(self, pop: torch.Tensor) -> Flattened:
+        """pop: float32 [P, T, N, 4] on the device."""
+        P, T, N, four = pop.shape
+        if four != 4:
+            raise ValueError("population rows must have 4 columns [f, a, b, value]")
+        if N > nat.MAX_NODES:
+            raise ValueError(f"max_nodes {N} > {nat.MAX_NODES}")
+        specs, _ = self._specs()
+        for (t, _, _) in specs:
+            if t >= T:
+                raise ValueError(f"candidate has {T} trees, the evaluator needs tree {t}")
+        n_prog = len(specs)
+        L = 2 * N + 8
+        dev = self.device
+        prog = torch.empty((P, n_prog, L, 2), dtype=torch.int32, device=dev)
+        plen = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
+        nodes = torch.empty((P,), dtype=torch.int32, device=dev)
+        status = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.native.mtgp_flatten(pop.data_ptr(), P, T, N, ctypes.byref(self._node_lib),
+                                      self._specs_dev.data_ptr(), n_prog, L, prog.data_ptr(),
+                                      plen.data_ptr(), nodes.data_ptr(), status.data_ptr(), stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_flatten failed: {rc}")
+        return Flattened(prog, plen, nodes, status, L, n_prog)
+
+    @staticmethod
+    def check_status(fl: Flattened):
+        worst = int(fl.status.max().item()) if fl.status.numel() else 0
+        if worst == nat.ERR_PROG_TOO_LONG:
+            raise ValueError("a tree flattens to more than 2*max_nodes+8 instructions (shared sub-DAGs?)")
+        if worst == nat.ERR_STACK:
+            raise ValueError(f"a tree needs more than {nat.STACK_MAX} operand-stack slots")
+        if worst != 0:
+            raise RuntimeError(f"flatten status {worst}")
+
+    # ----------------------------------------------------------------- eval
+    def evaluate(self, pop: torch.Tensor, data, trajectories: bool = False, rollout_fitness: bool = False,
+                 flattened: Optional[Flattened] = None, check: bool = True) -> dict:
+        """Run flatten + fused RK4 kernel.  Returns device tensors:
+        fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts time-major [S, c, P*R])."""
+        d = self.prepare_data(data)
+        fl = flattened if flattened is not None else self.flatten(pop)
+        P = pop.shape[0]
+        R, S = d["R"], d["n_save"]
+        _, roles = self._specs()
+        m = nat.MtgpModel()
+        m.model = self.ff.model_id
+        m.n_var = d.get("n_var", 4)
+        m.state_size = getattr(self.ff, "state_size", 0)
+        env = getattr(self.ff, "env", None)
+        m.n_obs = env.n_obs if env is not None else 0
+        m.n_control = env.n_control if env is not None else 0
+        m.n_targets = env.n_targets if env is not None else 0
+        m.n_steps, m.save_every, m.n_save = d["n_steps"], d["save_every"], S
+        m.h = self.ff.dt0
+        m.max_fitness = self.ff.max_fitness
+        m.parsimony = self.parsimony
+        m.prog_state, m.prog_readout = roles["prog_state"], roles["prog_readout"]
+        m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
+        ro = nat.MtgpRollouts()
+        ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
+        ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
+        dev = self.device
+        res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
+        out = nat.MtgpOutputs()
+        out.fitness = res["fitness"].data_ptr()
+        if rollout_fitness:
+            res["rollout_fitness"] = torch.empty((P, R), dtype=torch.float32, device=dev)
+            out.rollout_fitness = res["rollout_fitness"].data_ptr()
+        if trajectories:
+            PR = P * R
+            if self.ff.model_id == nat.MODEL_SR:
+                res["xs"] = torch.empty((S, m.n_var, PR), dtype=torch.float32, device=dev)
+                out.xs = res["xs"].data_ptr()
+            else:
+                for name, c in (("xs", 4), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size)):
+                    if c > 0:
+                        res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
+                        setattr(out, name, res[name].data_ptr())
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        rc = self.native.mtgp_eval_rk4(ctypes.byref(m), fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L,
+                                       fl.nodes.data_ptr(), P, ctypes.byref(ro), ctypes.byref(out), stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_eval_rk4 rejected the configuration (code {rc})")
+        if check:
+            self.check_status(fl)
+        res["_flat"] = fl
+        return res
+
+    def eval_programs(self, fl: Flattened, data_vectors: torch.Tensor) -> torch.Tensor:
+        """Batched tree_evaluator: every program on M data vectors -> [P, n_prog, M]."""
+        P = fl.prog.shape[0]
+        M, D = data_vectors.shape
+        out = torch.empty((P, fl.n_prog, M), dtype=torch.float32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.native.mtgp_eval_programs(fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L, P,
+                                            data_vectors.data_ptr(), M, D, out.data_ptr(), stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_eval_programs failed: {rc}")
+        return out
+
+
+def to_reference_layout(t: torch.Tensor, P: int, R: int) -> np.ndarray:
+    """time-major [S, c, P*R] -> evaluate_candidate layout [P, R, S, c] (host numpy)."""
+    S, c, _ = t.shape
+    return t.reshape(S, c, P, R).permute(2, 3, 0, 1).contiguous().cpu().numpy()

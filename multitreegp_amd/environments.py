@@ -1,0 +1,116 @@
+"""Environments on the hot path (host-side description + synthetic data generators).
+
+Only the pieces the evaluator needs are restated: dimensions, per-rollout parameters and
+initial states.  The dynamics themselves run inside the HIP kernel (Acrobot.drift,
+acrobot.py:51-72) -- the numpy drifts below exist only to generate ground-truth data for
+symbolic regression (SymbolicRegression.ipynb get_data) and are not on the hot path.
+Random draws use numpy PCG64 instead of jax.random (not installable here).
+"""
+from __future__ import annotations
+
+from typing import Tuple
+
+import numpy as np
+
+
+class Acrobot:
+    """acrobot.py:7-87.  n_var 4, n_control 1, n_targets 0, n_obs 4 (default)."""
+
+    def __init__(self, process_noise: float, obs_noise: float, n_obs: int = 4):
+        self.n_var = 4
+        self.n_control = 1
+        self.n_targets = 0
+        self.n_dim = 1
+        self.n_obs = n_obs
+        self.process_noise = process_noise
+        self.obs_noise = obs_noise
+        self.init_bounds = np.array([0.1, 0.1, 0.1, 0.1], dtype=np.float32)
+        self.R = np.array([[0.01]], dtype=np.float32)
+
+    def sample_init_states(self, batch_size: int, rng) -> Tuple[np.ndarray, np.ndarray]:
+        """acrobot.py:18-22: x0 ~ U(-0.1, 0.1)^4, targets [batch, 0]."""
+        rng = np.random.default_rng(rng)
+        x0 = rng.uniform(-self.init_bounds, self.init_bounds, size=(batch_size, self.n_var)).astype(np.float32)
+        targets = np.zeros((batch_size, self.n_targets), dtype=np.float32)
+        return x0, targets
+
+    def sample_params(self, batch_size: int, mode, ts, rng) -> Tuple[np.ndarray, ...]:
+        """acrobot.py:24-27: l1 = l2 = m1 = m2 = 1."""
+        one = np.ones(batch_size, dtype=np.float32)
+        return one, one.copy(), one.copy(), one.copy()
+
+
+class VanDerPolOscillator:
+    """SR_environments/vd_pol_oscillator.py:6-29 (mu = 1)."""
+
+    def __init__(self, process_noise: float = 0.0, obs_noise: float = 0.0, n_obs: int = 2):
+        self.n_var = 2
+        self.n_obs = n_obs
+        self.mu = 1.0
+        self.process_noise = process_noise
+        self.obs_noise = obs_noise
+
+    def sample_init_states(self, batch_size: int, rng) -> np.ndarray:
+        rng = np.random.default_rng(rng)
+        return rng.standard_normal((batch_size, 2)).astype(np.float32)
+
+    def drift(self, t, state):
+        """vd_pol_oscillator.py:22-23 (float64 numpy, ground truth only)."""
+        return np.stack([state[..., 1], self.mu * (1 - state[..., 0] ** 2) * state[..., 1] - state[..., 0]], -1)
+
+
+class LinearSystem:
+    """Stable random linear system dx/dt = A x used as the C5 target (BASELINE C5)."""
+
+    def __init__(self, n_var: int, seed: int = 7):
+        rng = np.random.default_rng(seed)
+        q, _ = np.linalg.qr(rng.standard_normal((n_var, n_var)))
+        eig = -rng.uniform(0.1, 1.0, n_var)
+        self.A = (q * eig) @ q.T
+        self.n_var = n_var
+        self.n_obs = n_var
+
+    def sample_init_states(self, batch_size: int, rng) -> np.ndarray:
+        rng = np.random.default_rng(rng)
+        return rng.standard_normal((batch_size, self.n_var)).astype(np.float32)
+
+    def drift(self, t, state):
+        return state @ self.A.T
+
+
+def ground_truth(env, x0: np.ndarray, ts: np.ndarray, h: float = 1e-3) -> np.ndarray:
+    """Fine float64 RK4 solution of env.drift saved at ts -> [R, S, n_var] float32.
+
+    Replaces the notebook's diffrax Dopri5 (atol = rtol = 1e-7) ground-truth generation
+    (SymbolicRegression.ipynb get_data)."""
+    x = x0.astype(np.float64)
+    ts = np.asarray(ts, dtype=np.float64)
+    out = np.empty((x0.shape[0], len(ts), x0.shape[1]), dtype=np.float64)
+    out[:, 0] = x
+    t = ts[0]
+    for k in range(1, len(ts)):
+        n = max(1, int(round((ts[k] - t) / h)))
+        dt = (ts[k] - t) / n
+        for _ in range(n):
+            k1 = env.drift(t, x)
+            k2 = env.drift(t, x + 0.5 * dt * k1)
+            k3 = env.drift(t, x + 0.5 * dt * k2)
+            k4 = env.drift(t, x + dt * k3)
+            x = x + dt / 6.0 * (k1 + 2 * k2 + 2 * k3 + k4)
+            t = t + dt
+        out[:, k] = x
+    return out.astype(np.float32)
+
+
+def control_data(env, batch_size: int, dt: float, T: float, seed: int = 1, n_steps: int = None):
+    """The notebooks' get_data (DynamicPolicy.ipynb cell 2) with numpy RNG:
+    (x0, ts, targets, process_noise_keys, obs_noise_keys, params)."""
+    rng = np.random.default_rng(seed)
+    x0, targets = env.sample_init_states(batch_size, rng)
+    if n_steps is None:
+        ts = np.arange(0, T, dt, dtype=np.float32)
+    else:
+        ts = (np.arange(n_steps + 1, dtype=np.float32) * np.float32(dt)).astype(np.float32)
+    keys = np.zeros((batch_size, 2), dtype=np.uint32)
+    params = env.sample_params(batch_size, "Constant", ts, rng)
+    return x0, ts, targets, keys, keys.copy(), params

@@ -1,0 +1,257 @@
+"""Fitness-function plugins: MI355X counterparts of MultiTreeGP/evaluators/*.py.
+
+Each class keeps the reference constructor signature and exposes the same two calls --
+``__call__(coefficients, nodes, data, tree_evaluator)`` (one candidate -> fitness) and
+``evaluate_candidate(candidate, data, tree_evaluator)`` (trajectories + per-rollout fitness)
+-- but the work is done by the fused HIP kernel (multitreegp_amd/csrc/mtgp_kernels.hip).
+The population path (``GeneticProgramming.evaluate_population``) batches all candidates into
+one launch; these per-candidate calls exist for API parity and trajectory inspection.
+
+Solver: BASELINE.json prescribes an explicit fixed-step RK4.  ``solver`` must be
+``RK4()`` (or the string "rk4") and ``stepsize_controller`` ``ConstantStepSize()``; adaptive
+Dopri5 + PID (the notebooks' choice) is SURVEY.md §8f row 2 and raises NotImplementedError.
+"""
+from __future__ import annotations
+
+from typing import List, Tuple
+
+import numpy as np
+
+from .. import _native as nat
+
+
+class RK4:
+    """Classical 4-stage Runge-Kutta, fixed step dt0 (diffrax.RK4 + ConstantStepSize)."""
+    name = "RK4"
+
+    def __repr__(self):
+        return "RK4()"
+
+
+class ConstantStepSize:
+    name = "ConstantStepSize"
+
+    def __repr__(self):
+        return "ConstantStepSize()"
+
+
+def _check_solver(solver, controller):
+    sname = solver.lower() if isinstance(solver, str) else getattr(solver, "name", type(solver).__name__)
+    if str(sname).lower() != "rk4":
+        raise NotImplementedError(
+            f"solver {solver!r}: only fixed-step RK4 is implemented on the MI355X path "
+            "(adaptive Dopri5/PID is SURVEY.md §8f row 2)")
+    if controller is not None:
+        cname = getattr(controller, "name", type(controller).__name__)
+        if cname != "ConstantStepSize":
+            raise NotImplementedError(f"stepsize_controller {controller!r}: only ConstantStepSize is implemented")
+
+
+def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
+    """Map (ts, dt0) to (n_steps, save_every, n_save) for save points on step ends.
+
+    Also checks the Acrobot fitness-mask regularity ts[k]/(ts[1]-ts[0]) in (k-1, k+1] that the
+    kernel's one-pass fitness relies on (acrobot.py:82)."""
+    ts = np.asarray(ts, dtype=np.float32)
+    S = int(ts.shape[0])
+    if S < 2:
+        raise ValueError("ts needs at least two save points")
+    dts = float(ts[1]) - float(ts[0])
+    save_every = int(round(dts / float(dt0)))
+    if save_every < 1 or abs(save_every * float(dt0) - dts) > 1e-4 * max(abs(dts), 1e-30):
+        raise ValueError(f"save spacing {dts} is not a multiple of dt0={dt0}")
+    expect = np.float64(ts[0]) + np.arange(S) * dts
+    if np.max(np.abs(ts.astype(np.float64) - expect)) > 1e-4 * max(abs(float(ts[-1])), 1.0):
+        raise ValueError("ts must be uniformly spaced (fixed-step RK4 saves on step ends)")
+    ratio = ts / np.float32(ts[1] - ts[0])
+    k = np.arange(S, dtype=np.float32)
+    if not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
+        raise NotImplementedError("ts with an offset start (ts[0] != 0 style masks) is not supported")
+    n_steps = (S - 1) * save_every
+    if n_steps > max_steps:
+        raise ValueError(f"{n_steps} RK4 steps exceed max_steps={max_steps}")
+    return n_steps, save_every, S
+
+
+def _f32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+class _CandidateAPI:
+    """``__call__`` / ``evaluate_candidate`` of the reference evaluators, run on the GPU."""
+
+    def _single(self, candidate, data, tree_evaluator, traj: bool):
+        import torch
+        if not hasattr(tree_evaluator, "engine"):
+            raise TypeError("tree_evaluator must be GeneticProgramming.vmap_foriloop of multitreegp_amd")
+        eng = tree_evaluator.engine(self)
+        cand = np.asarray(candidate, dtype=np.float32)
+        pop = torch.from_numpy(np.ascontiguousarray(cand[None])).to(eng.device)
+        res = eng.evaluate(pop, data, trajectories=traj, rollout_fitness=True)
+        return res
+
+    def __call__(self, coefficients, nodes, data, tree_evaluator) -> float:
+        """dyn.py:37-52 / ff.py:36-51 / sr.py:30-45: one candidate -> clipped mean fitness."""
+        cand = np.concatenate([np.asarray(nodes, np.float32), np.asarray(coefficients, np.float32)], axis=-1)
+        return float(self._single(cand, data, tree_evaluator, False)["fitness"][0].item())
+
+    def evaluate_candidate(self, candidate, data, tree_evaluator):
+        """dyn.py:54-63 -> (xs, ys, us, activities, fitness); ff.py:53-62 -> (xs, ys, us, fitness);
+        sr.py:47-55 -> (fitness, pred_ys).  Arrays in the reference layout [R, S, c]."""
+        from ..engine import to_reference_layout
+        res = self._single(candidate, data, tree_evaluator, True)
+        R = res["rollout_fitness"].shape[1]
+        fit = res["rollout_fitness"][0].cpu().numpy()
+        get = lambda k: to_reference_layout(res[k], 1, R)[0]
+        if self.model_id == nat.MODEL_SR:
+            return fit, get("xs")
+        if self.model_id == nat.MODEL_ACROBOT_STATIC:
+            return get("xs"), get("ys"), get("us"), fit
+        return get("xs"), get("ys"), get("us"), get("acts"), fit
+
+
+class _TreeOnly:
+    """Pseudo fitness config used by TreeEvaluator: one program per tree, plain data vector."""
+    model_id = 0
+    state_size = 0
+    dt0 = 0.0
+    max_fitness = 0.0
+
+    def __init__(self, n_trees: int, n_data: int):
+        self._t, self._d = n_trees, n_data
+
+    def prepare(self, data):
+        return {}
+
+    def n_data(self):
+        return self._d
+
+    def program_specs(self):
+        return [(t, self._d, 0) for t in range(self._t)], {}
+
+
+class _ControlEvaluator(_CandidateAPI):
+    max_fitness = 1e4
+
+    def __init__(self, env, dt0: float, solver=None, max_steps: int = 16 ** 4, stepsize_controller=None):
+        _check_solver(solver if solver is not None else RK4(), stepsize_controller)
+        if getattr(env, "obs_noise", 0.0) not in (0, 0.0):
+            raise NotImplementedError(
+                "obs_noise > 0 needs the JAX threefry observation-noise stream in-kernel (SURVEY.md §8f row 1)")
+        if type(env).__name__ != "Acrobot":
+            raise NotImplementedError(f"environment {type(env).__name__}: only Acrobot is on the MI355X path")
+        if env.n_obs != 4:
+            raise NotImplementedError("Acrobot with n_obs != 4")
+        self.env = env
+        self.obs_size = env.n_obs
+        self.control_size = env.n_control
+        self.latent_size = env.n_var * env.n_dim
+        self.dt0 = float(dt0)
+        self.solver = solver if solver is not None else RK4()
+        self.max_steps = max_steps
+        self.stepsize_controller = stepsize_controller
+
+    def prepare(self, data) -> dict:
+        """Reference data tuple (x0, ts, targets, process_keys, obs_keys, params) -> arrays."""
+        x0, ts, targets, _pk, _ok, params = data
+        x0 = _f32(x0)
+        R = x0.shape[0]
+        if x0.shape[1] != 4:
+            raise ValueError("Acrobot x0 must be [R, 4]")
+        prm = np.stack([_f32(p).reshape(R) for p in params], axis=1) if params is not None else np.ones((R, 4), np.float32)
+        tg = _f32(targets).reshape(R, -1)
+        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+        return dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R,
+                    n_steps=n_steps, save_every=save_every, n_save=S)
+
+
+class DynamicEvaluator(_ControlEvaluator):
+    """dynamic_evaluate.Evaluator (dynamic_evaluate.py:10-118): state_size hidden-state trees
+    followed by n_control readout trees."""
+    model_id = nat.MODEL_ACROBOT_DYNAMIC
+
+    def __init__(self, env, state_size: int, dt0: float, solver=None, max_steps: int = 16 ** 4,
+                 stepsize_controller=None):
+        super().__init__(env, dt0, solver, max_steps, stepsize_controller)
+        self.state_size = int(state_size)
+
+    def n_trees(self) -> int:
+        return self.state_size + self.control_size
+
+    def n_data(self) -> int:
+        return self.obs_size + self.state_size + self.control_size + self.env.n_targets
+
+    def program_specs(self) -> Tuple[List[Tuple[int, int, int]], dict]:
+        no, ss, nu = self.obs_size, self.state_size, self.control_size
+        D = self.n_data()
+        ymask = (1 << no) - 1
+        umask = ((1 << nu) - 1) << (no + ss)
+        specs = [(t, D, 0) for t in range(ss)]                      # state equation [y, a, u, tg]
+        specs += [(ss + j, D, ymask | umask) for j in range(nu)]    # readout in _drift (dyn.py:113)
+        specs += [(ss + j, D, umask) for j in range(nu)]            # readout at saves (dyn.py:101)
+        roles = dict(prog_state=0, prog_readout=ss, prog_readout_save=ss + nu, readout_save_same=-1)
+        return specs, roles
+
+
+class FeedforwardEvaluator(_ControlEvaluator):
+    """feedforward_evaluate.Evaluator (feedforward_evaluate.py:10-110): u = policy([y, target])."""
+    model_id = nat.MODEL_ACROBOT_STATIC
+    state_size = 0
+
+    def n_trees(self) -> int:
+        return self.control_size
+
+    def n_data(self) -> int:
+        return self.obs_size + self.env.n_targets
+
+    def program_specs(self):
+        specs = [(j, self.n_data(), 0) for j in range(self.control_size)]
+        roles = dict(prog_state=-1, prog_readout=0, prog_readout_save=0, readout_save_same=1)
+        return specs, roles
+
+
+class SREvaluator(_CandidateAPI):
+    """SR_evaluator.Evaluator (SR_evaluator.py:9-94): dx = trees(x), MSE fitness."""
+    model_id = nat.MODEL_SR
+    max_fitness = 1e5
+
+    def __init__(self, solver=None, dt0: float = 0.01, max_steps: int = 16 ** 4, stepsize_controller=None):
+        _check_solver(solver if solver is not None else RK4(), stepsize_controller)
+        self.dt0 = float(dt0)
+        self.solver = solver if solver is not None else RK4()
+        self.max_steps = max_steps
+        self.stepsize_controller = stepsize_controller
+        self.state_size = 0
+        self._n_var = None
+
+    def prepare(self, data) -> dict:
+        """Reference data tuple (x0s, ts, ys, process_noise_keys)."""
+        x0, ts, ys = data[0], data[1], data[2]
+        x0 = _f32(x0)
+        R, nv = x0.shape
+        ys = _f32(ys)
+        if ys.shape[0] != R or ys.shape[2] != nv:
+            raise ValueError("ys must be [R, S, n_var]")
+        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+        if ys.shape[1] != S:
+            raise ValueError("ys must have len(ts) save points")
+        ys_tm = np.ascontiguousarray(np.transpose(ys, (1, 2, 0)))  # [S, n_var, R] time-major
+        self._n_var = nv
+        return dict(x0=x0, params=None, targets=None, ts=_f32(ts), ys_true=ys_tm, R=R,
+                    n_steps=n_steps, save_every=save_every, n_save=S, n_var=nv)
+
+    def n_trees(self) -> int:
+        return self._n_var
+
+    def n_data(self) -> int:
+        return self._n_var
+
+    def program_specs(self):
+        nv = self._n_var
+        specs = [(i, nv, 0) for i in range(nv)]
+        roles = dict(prog_state=0, prog_readout=-1, prog_readout_save=-1, readout_save_same=0)
+        return specs, roles
+
+
+__all__ = ["RK4", "ConstantStepSize", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
+           "rk4_schedule"]

@@ -1,0 +1,170 @@
+"""GeneticProgramming facade: the reference strategy's evaluation half on MI355X.
+
+Keeps the constructor signature, validation and bookkeeping of
+MultiTreeGP/genetic_programming.py:GeneticProgramming (gp.py:61-270, 403-433, 527-537) and
+replaces ``evaluate_population``'s ``jit(shard_map(vmap(fitness_function)))`` with the flatten
++ fused RK4 HIP kernels.  Evolution (``evolve``: genetic_operators/) stays with the reference's
+host code; a maintainer swaps only this method.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import distributed as mdist
+from .engine import DeviceEngine
+from .node_library import NodeLibrary
+from .sampling import sample_population
+
+
+class TreeEvaluator:
+    """Counterpart of ``GeneticProgramming.vmap_foriloop`` (gp.py:390-401).
+
+    Passed to the evaluators as ``tree_evaluator`` like in the reference; it carries the node
+    library, and calling it evaluates every tree of a candidate on one data vector on the GPU."""
+
+    def __init__(self, library: NodeLibrary, max_nodes: int, device=None):
+        self.library = library
+        self.max_nodes = max_nodes
+        self.device = device
+        self._engines = {}
+
+    def engine(self, fitness_function, size_parsinomy: float = 0.0) -> DeviceEngine:
+        key = (id(fitness_function), float(size_parsinomy))
+        if key not in self._engines:
+            self._engines[key] = DeviceEngine(fitness_function, self.library, size_parsinomy, self.device)
+        return self._engines[key]
+
+    def __call__(self, candidate, data) -> np.ndarray:
+        from .evaluators import _TreeOnly
+        cand = np.asarray(candidate, dtype=np.float32)
+        d = np.asarray(data, dtype=np.float32).reshape(1, -1)
+        ff = _TreeOnly(cand.shape[0], d.shape[1])
+        eng = self.engine(ff)
+        pop = torch.from_numpy(cand[None]).to(eng.device)
+        eng.prepare_data(None)
+        fl = eng.flatten(pop)
+        eng.check_status(fl)
+        out = eng.eval_programs(fl, torch.from_numpy(d).to(eng.device))
+        return out[0, :, 0].cpu().numpy()
+
+
+class GeneticProgramming:
+    """Genetic programming strategy (evaluation side).  Parameters as gp.py:61-84."""
+
+    def __init__(self, num_generations: int, population_size: int, fitness_function, operator_list,
+                 variable_list, layer_sizes, num_populations: int = 1, max_init_depth: int = 4,
+                 max_nodes: int = 30, device_type: str = "gpu", tournament_size: int = 7,
+                 size_parsinomy: float = 0.0, coefficient_sd: float = 1.0, migration_period: int = 10,
+                 migration_percentage: float = 0.1, elite_percentage: float = 0.1,
+                 coefficient_optimisation: bool = False, gradient_steps: int = 10, optimiser=None,
+                 selection_pressure_factors=(0.6, 0.9), reproduction_probability_factors=(1.0, 0.5),
+                 crossover_probability_factors=(0.9, 0.4), mutation_probability_factors=(0.1, 0.5),
+                 sample_probability_factors=(0.0, 0.1), device=None, verbose: bool = True):
+        self.layer_sizes = np.asarray(layer_sizes)
+        assert num_populations > 0, "The number of populations should be larger than 0"
+        self.num_populations = num_populations
+        assert population_size > 0 and population_size % 2 == 0, \
+            "The population_size should be larger than 0 and an even number"
+        self.population_size = population_size
+        assert max_init_depth > 0, "The max initial depth should be larger than 0"
+        self.max_init_depth = max_init_depth
+        assert max_nodes > 0, "The max number of nodes should be larger than 0"
+        self.max_nodes = max_nodes
+        self.num_trees = int(np.sum(self.layer_sizes))
+        assert self.num_trees > 0, "The number of trees should be larger than 0"
+        self.current_generation = 0
+        assert num_generations > 0, "The number of generations should be larger than 0"
+        self.num_generations = num_generations
+        self.best_fitnesses = np.zeros(num_generations, dtype=np.float32)
+        self.best_solutions = np.zeros((num_generations, self.num_trees, max_nodes, 4), dtype=np.float32)
+        self.size_parsinomy = size_parsinomy
+        self.coefficient_sd = coefficient_sd
+        assert migration_period > 1, "The migration period should be larger than 1"
+        assert migration_percentage * population_size % 1 == 0, "The migration size should be an integer"
+        assert tournament_size > 1, "The number of gradient steps should be larger than 1"
+        self.elite_size = int(elite_percentage * population_size)
+        assert self.elite_size % 2 == 0, "The elite size should be a multiple of two"
+        if coefficient_optimisation:
+            raise NotImplementedError("coefficient optimisation (gp.py:418-473) is SURVEY.md §8f row 4")
+        self.coefficient_optimisation = False
+        self.fitness_function = fitness_function
+        self.library = NodeLibrary(operator_list, variable_list, self.layer_sizes)
+        self.node_to_string = self.library.node_to_string
+        self.string_to_node = self.library.string_to_node
+        self.slots = self.library.slots
+        self.variable_array = self.library.variable_array
+        if verbose:
+            print(f"Input data should be formatted as: {self.library.input_format}.")
+        self.vmap_foriloop = TreeEvaluator(self.library, max_nodes, device)
+        self.device = device
+
+    # ----------------------------------------------------------------- hot path
+    def _engine(self) -> DeviceEngine:
+        return self.vmap_foriloop.engine(self.fitness_function, self.size_parsinomy)
+
+    def evaluate_population(self, populations, data) -> Tuple[np.ndarray, np.ndarray]:
+        """Fitness of every candidate (gp.py:403-433): flatten, shard over ranks, one fused kernel
+        launch per rank, parsimony in-kernel, all-gather of fitness, best-so-far bookkeeping."""
+        pops = np.asarray(populations, dtype=np.float32)
+        P = self.num_populations * self.population_size
+        flat = pops.reshape(P, *pops.shape[2:])
+        eng = self._engine()
+
+        def shard(lo: int, hi: int) -> torch.Tensor:
+            if hi <= lo:
+                return torch.empty((0,), dtype=torch.float32, device=eng.device)
+            pop_dev = torch.from_numpy(np.ascontiguousarray(flat[lo:hi])).to(eng.device, non_blocking=True)
+            return eng.evaluate(pop_dev, data)["fitness"]
+
+        fitness = mdist.sharded_fitness(shard, P).cpu().numpy()
+        g = self.current_generation
+        best = int(np.argmin(fitness))
+        if g < self.num_generations:
+            self.best_solutions[g] = flat[best]
+            self.best_fitnesses[g] = fitness[best]
+        return fitness.reshape(self.num_populations, self.population_size), \
+            flat.reshape(self.num_populations, self.population_size, *flat.shape[1:])
+
+    # --------------------------------------------------------------- host side
+    def initialize_population(self, key) -> np.ndarray:
+        """gp.py:298-308 with the numpy sampler (multitreegp_amd.sampling)."""
+        seed = int(np.asarray(key).reshape(-1)[-1]) if not isinstance(key, int) else key
+        return sample_population(seed, self.library, self.population_size, self.num_populations,
+                                 self.max_init_depth, self.max_nodes, self.coefficient_sd)
+
+    def evolve(self, populations, fitness, key):
+        raise NotImplementedError(
+            "evolution (genetic_operators/) stays with the reference's host implementation; "
+            "this package replaces evaluate_population only (see INTEGRATION.md)")
+
+    def get_statistics(self, generation: Optional[int] = None):
+        if generation is not None:
+            return self.best_fitnesses[generation], self.best_solutions[generation]
+        return self.best_fitnesses, self.best_solutions
+
+    def tree_to_string(self, tree) -> str:
+        return self.library.tree_to_string(tree)
+
+    def to_string(self, candidate) -> str:
+        """gp.py:330-354 (requires sympy)."""
+        import sympy
+        out = ""
+        tree_index = 0
+        layer_index = 0
+        for tree in candidate:
+            if tree_index == 0:
+                out += "["
+            out += str(sympy.parsing.sympy_parser.parse_expr(self.tree_to_string(tree)))
+            if tree_index < (self.layer_sizes[layer_index] - 1):
+                out += ", "
+                tree_index += 1
+            else:
+                out += "]"
+                if layer_index < (self.layer_sizes.shape[0] - 1):
+                    out += ", "
+                tree_index = 0
+                layer_index += 1
+        return out

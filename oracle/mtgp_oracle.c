@@ -1,0 +1,419 @@
+/*
+ * mtgp_oracle.c -- CPU restatement of the MultiTreeGP population-fitness hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker / CPU baseline.
+ * The product path (multitreegp_amd) never calls it.
+ *
+ * It restates the reference's algorithm literally, independently of the product's
+ * program flattener: trees are interpreted row by row over all N rows exactly like
+ * GeneticProgramming.body_fun/foriloop (gp.py:356-388), the fitness is computed from
+ * the full saved trajectory arrays the way the environments do (acrobot.py:77-84,
+ * SR_evaluator.py:24), not online.  The only shared code is the fp32 arithmetic spec
+ * (include/mtgp_f32math.h: sin/cos/floor-mod), which pins the numerics that the
+ * reference delegates to XLA; fixed-step RK4 replaces diffrax.diffeqsolve as
+ * BASELINE.json prescribes.
+ *
+ * Parity status: the reference (JAX/diffrax) cannot be imported here
+ * (ModuleNotFoundError) and ships no golden vectors -> parity vs the
+ * reference is UNPINNED; this oracle is pinned by analytic known-answer tests, a
+ * float64 numpy restatement and sympy evaluation of the reference's printed
+ * expressions (tests/test_oracle.py).
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include "mtgp_f32math.h"
+
+#define OR_MAX_N 256
+#define OR_MAX_D 64
+#define OR_MAX_S 64 /* state dims */
+
+/* node-function codes (same numbering as include/mtgp.h MTGP_FN_*) */
+enum { FN_ZERO = 0, FN_VAR = 1, FN_ADD = 2, FN_SUB = 3, FN_MUL = 4, FN_DIV = 5, FN_SIN = 6, FN_COS = 7 };
+
+typedef struct {
+  int32_t n_funcs, var_start;
+  const int8_t* fn;
+} OrLib;
+
+/* f32 -> int32: truncation, saturating, NaN -> 0 (astype(int), gp.py:370-372) */
+static int32_t or_f2i(float v) {
+  if (v != v) return 0;
+  if (v >= 2147483648.0f) return 2147483647;
+  if (v <= -2147483648.0f) return -2147483647 - 1;
+  return (int32_t)v;
+}
+/* jnp dynamic index: negative -> + N, then clamp */
+static int or_index(float v, int N) {
+  int64_t j = or_f2i(v);
+  if (j < 0) j += N;
+  if (j < 0) j = 0;
+  if (j > N - 1) j = N - 1;
+  return (int)j;
+}
+
+/* gp.py:356-388: evaluate rows 0..N-1 in order, return the value of row N-1. */
+float oracle_eval_tree(const float* tree, int N, int n_funcs, int var_start, const int8_t* fn,
+                       const float* data, int n_data) {
+  float val[OR_MAX_N];
+  for (int i = 0; i < N; ++i) val[i] = tree[4 * i + 3];
+  for (int i = 0; i < N; ++i) {
+    const float f = tree[4 * i + 0];
+    const float x = val[or_index(tree[4 * i + 1], N)];
+    const float y = val[or_index(tree[4 * i + 2], N)];
+    float v;
+    if (f == 1.0f) {
+      v = tree[4 * i + 3];
+    } else {
+      int32_t k = or_f2i(f);
+      if (k < 0) k = 0;
+      if (k > n_funcs - 1) k = n_funcs - 1;
+      switch (fn[k]) {
+        case FN_VAR: {
+          int d = k - var_start;
+          if (d > n_data - 1) d = n_data - 1;
+          v = data[d];
+          break;
+        }
+        case FN_ADD: v = x + y; break;
+        case FN_SUB: v = x - y; break;
+        case FN_MUL: v = x * y; break;
+        case FN_DIV: v = x / y; break;
+        case FN_SIN: v = mtgp_sinf(x); break;
+        case FN_COS: v = mtgp_cosf(x); break;
+        default: v = 0.0f; break;
+      }
+    }
+    val[i] = v;
+  }
+  return val[N - 1];
+}
+
+/* ------------------------------------------------------------------ models */
+typedef struct {
+  int32_t model; /* 1 dynamic acrobot, 2 static acrobot, 3 SR */
+  int32_t n_var, state_size, n_obs, n_control, n_targets;
+  int32_t n_steps, save_every, n_save;
+  float h, max_fitness, parsimony;
+} OrModel;
+
+typedef struct {
+  const float* x0;      /* [R, n_var] */
+  const float* params;  /* [R, 4] l1 l2 m1 m2 */
+  const float* targets; /* [R, n_targets] */
+  const float* ts;      /* [n_save] */
+  const float* ys_true; /* SR: [R, n_save, n_var] (reference layout) */
+  int32_t R;
+} OrRollouts;
+
+typedef struct {
+  const OrModel* m;
+  const float* cand; /* [T, N, 4] */
+  int N;
+  OrLib lib;
+  const float* target;
+  float l1, l2, m1, m2;
+} OrCtx;
+
+/* EnvironmentBase.f_obs with C = I, W = obs_noise*I, obs_noise = 0 (cbase.py:43-48):
+ * out = C@x + normal@W; the noise term is +0.  Then Acrobot wraps out[0:2]
+ * (acrobot.py:29-32). */
+static void acro_f_obs(const float* x, float* y) {
+  for (int i = 0; i < 4; ++i) {
+    float s = 0.0f;
+    int first = 1;
+    for (int j = 0; j < 4; ++j) {
+      const float term = (i == j ? 1.0f : 0.0f) * x[j];
+      if (first) { s = term; first = 0; } else s = s + term;
+    }
+    y[i] = s + 0.0f;
+  }
+  y[0] = mtgp_wrap_angle(y[0]);
+  y[1] = mtgp_wrap_angle(y[1]);
+}
+
+/* Acrobot.drift (acrobot.py:51-72), evaluation order of the Python source. */
+static void acro_drift(const OrCtx* c, const float* st, float u_raw, float* dx) {
+  const float control = mtgp_clip1(u_raw);
+  const float th1 = st[0], th2 = st[1], thd1 = st[2], thd2 = st[3];
+  const float l1 = c->l1, l2 = c->l2, m1 = c->m1, m2 = c->m2;
+  const float lc1 = 0.5f * l1, lc2 = 0.5f * l2;
+  const float moi1 = 1.0f, moi2 = 1.0f, g = 9.81f;
+  (void)l2;
+  const float d1 = m1 * (lc1 * lc1) + m2 * ((l1 * l1) + (lc2 * lc2) + ((2.0f * l1) * lc2) * mtgp_cosf(th2)) + moi1 + moi2;
+  const float d2 = m2 * ((lc2 * lc2) + (l1 * lc2) * mtgp_cosf(th2)) + moi2;
+  const float phi2 = ((m2 * lc2) * g) * mtgp_cosf((th1 + th2) - MTGP_HALF_PI_F);
+  const float phi1 = ((((-m2) * l1) * lc2) * (thd2 * thd2)) * mtgp_sinf(th2)
+                     - (((((2.0f * m2) * l1) * lc2) * thd1) * thd2) * mtgp_sinf(th1)
+                     + (((m1 * lc1) + (m2 * l1)) * g) * mtgp_cosf(th1 - MTGP_HALF_PI_F) + phi2;
+  const float th2acc = (control + (d2 / d1) * phi1 - (((m2 * l1) * lc2) * (thd1 * thd1)) * mtgp_sinf(th2) - phi2)
+                       / ((m2 * (lc2 * lc2)) + moi2 - (d2 * d2) / d1);
+  const float th1acc = (-((d2 * th2acc) + phi1)) / d1;
+  dx[0] = thd1;
+  dx[1] = thd2;
+  dx[2] = th1acc;
+  dx[3] = th2acc;
+}
+
+static float tree_eval(const OrCtx* c, int t, const float* data, int n_data) {
+  return oracle_eval_tree(c->cand + (size_t)t * c->N * 4, c->N, c->lib.n_funcs, c->lib.var_start, c->lib.fn,
+                          data, n_data);
+}
+
+/* dynamic_evaluate._drift (dyn.py:107-118) */
+static void dyn_rhs(const OrCtx* c, const float* s, float* ds) {
+  const OrModel* m = c->m;
+  const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
+  const int D = no + na + nu + nt;
+  float y[4], data[OR_MAX_D], u[8];
+  acro_f_obs(s, y);
+  /* readout sees [0_obs, a, 0_u, target] */
+  for (int i = 0; i < D; ++i) data[i] = 0.0f;
+  for (int i = 0; i < na; ++i) data[no + i] = s[4 + i];
+  for (int i = 0; i < nt; ++i) data[no + na + nu + i] = c->target[i];
+  for (int j = 0; j < nu; ++j) u[j] = tree_eval(c, na + j, data, D);
+  acro_drift(c, s, u[0], ds);
+  /* state equation sees [y, a, u, target] */
+  for (int i = 0; i < no; ++i) data[i] = y[i];
+  for (int j = 0; j < nu; ++j) data[no + na + j] = u[j];
+  for (int i = 0; i < na; ++i) ds[4 + i] = tree_eval(c, i, data, D);
+}
+
+/* feedforward_evaluate._drift (ff.py:104-110) */
+static void ff_rhs(const OrCtx* c, const float* s, float* ds) {
+  const OrModel* m = c->m;
+  const int no = m->n_obs, nt = m->n_targets;
+  float y[4], data[OR_MAX_D];
+  acro_f_obs(s, y);
+  for (int i = 0; i < no; ++i) data[i] = y[i];
+  for (int i = 0; i < nt; ++i) data[no + i] = c->target[i];
+  const float u = tree_eval(c, 0, data, no + nt);
+  acro_drift(c, s, u, ds);
+}
+
+/* SR_evaluator._drift (sr.py:85-88) */
+static void sr_rhs(const OrCtx* c, const float* s, float* ds) {
+  for (int i = 0; i < c->m->n_var; ++i) ds[i] = tree_eval(c, i, s, c->m->n_var);
+}
+
+static void rhs(const OrCtx* c, const float* s, float* ds) {
+  if (c->m->model == 1) dyn_rhs(c, s, ds);
+  else if (c->m->model == 2) ff_rhs(c, s, ds);
+  else sr_rhs(c, s, ds);
+}
+
+static int state_dim(const OrModel* m) { return m->model == 1 ? 4 + m->state_size : m->n_var; }
+
+/* diffrax.Event(cond_fn) with a float condition: +1 valid, -1 terminate. */
+static float cond_fn(const OrModel* m, const float* s) {
+  const int n = state_dim(m);
+  int bad = 0;
+  for (int i = 0; i < n; ++i) bad |= !mtgp_isfinite(s[i]);
+  if (m->model != 3) { /* acrobot.py:86-87 */
+    bad |= (mtgp_isnan(s[2]) ? 0 : (MTGP_FABSF(s[2]) > MTGP_8PI_F));
+    bad |= (mtgp_isnan(s[3]) ? 0 : (MTGP_FABSF(s[3]) > MTGP_18PI_F));
+  }
+  return bad ? -1.0f : 1.0f;
+}
+
+/* The solver step: classical RK4 (c = 0,1/2,1/2,1; b = 1/6,1/3,1/3,1/6), written with
+ * explicit fma so that the GPU kernel can reproduce it bit-for-bit. */
+static void rk4_step(const OrCtx* c, float* s) {
+  const int n = state_dim(c->m);
+  const float h = c->m->h, h2 = h * 0.5f, h6 = h / 6.0f;
+  float k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
+  rhs(c, s, k);
+  for (int i = 0; i < n; ++i) { acc[i] = k[i]; tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
+  rhs(c, tmp, k);
+  for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
+  rhs(c, tmp, k);
+  for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h, k[i], s[i]); }
+  rhs(c, tmp, k);
+  for (int i = 0; i < n; ++i) { acc[i] = acc[i] + k[i]; s[i] = MTGP_FMAF(h6, acc[i], s[i]); }
+}
+
+/* Solve one rollout: saved[n_save][dim]; unsaved points after termination = +inf. */
+static void solve(const OrCtx* c, const float* s0, float* saved) {
+  const OrModel* m = c->m;
+  const int n = state_dim(m);
+  float s[OR_MAX_S];
+  for (int i = 0; i < n; ++i) s[i] = s0[i];
+  for (int i = 0; i < n; ++i) saved[i] = s[i];
+  float prev = cond_fn(m, s);
+  int k_saved = 0, done = 0;
+  for (int step = 1; step <= m->n_steps && !done; ++step) {
+    rk4_step(c, s);
+    if (step % m->save_every == 0) {
+      ++k_saved;
+      for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];
+    }
+    const float cur = cond_fn(m, s);
+    if (prev > 0.0f && cur < 0.0f) done = 1;
+    prev = cur;
+  }
+  for (int k = k_saved + 1; k < m->n_save; ++k)
+    for (int i = 0; i < n; ++i) saved[(size_t)k * n + i] = mtgp_u2f(0x7f800000u);
+}
+
+/* Acrobot.fitness_function (acrobot.py:77-84) on full arrays. */
+static float acro_fitness(const float* xs, const float* us, const float* ts, int S) {
+  int fs = 0, found = 0;
+  for (int k = 0; k < S && !found; ++k) {
+    const float t1 = xs[4 * k + 0], t2 = xs[4 * k + 1];
+    const int reached = ((-mtgp_cosf(t1)) - mtgp_cosf(t1 + t2)) > 1.5f;
+    if (reached) { fs = k; found = 1; }
+  }
+  const float dts = ts[1] - ts[0];
+  float cs = 0.0f;
+  for (int k = 0; k < S; ++k) {
+    const float cost = (us[k] * 0.01f) * us[k];
+    const float ratio = ts[k] / dts;
+    const float masked = (ratio > (float)fs) ? 0.0f : cost;
+    cs = cs + masked;
+  }
+  return (float)(fs + (fs == 0) * S) + cs;
+}
+
+/* pairwise (xor-butterfly) sum over padded chunks of 64 -- the kernel's reduction order */
+static float pairwise_sum(const float* v, int R) {
+  const int nch = (R + 63) / 64;
+  int np2 = 1;
+  while (np2 < nch) np2 *= 2;
+  float chunk[1024];
+  for (int ch = 0; ch < np2; ++ch) {
+    float lane[64];
+    for (int l = 0; l < 64; ++l) {
+      const int r = ch * 64 + l;
+      lane[l] = (ch < nch && r < R) ? v[r] : 0.0f;
+    }
+    for (int w = 1; w < 64; w *= 2)
+      for (int l = 0; l < 64; l += 2 * w) lane[l] = lane[l] + lane[l + w];
+    chunk[ch] = lane[0];
+  }
+  for (int w = 1; w < np2; w *= 2)
+    for (int ch = 0; ch < np2; ch += 2 * w) chunk[ch] = chunk[ch] + chunk[ch + w];
+  return chunk[0];
+}
+
+/*
+ * Evaluate P candidates (pop [P, T, N, 4]).  Outputs:
+ *   fitness[P]; rollout_fitness[P, R] (raw, before NaN/inf replacement) or NULL;
+ *   trajectories in the reference's evaluate_candidate layout, each nullable:
+ *   xs[P, R, S, n_var], ys[P, R, S, n_obs], us[P, R, S, n_control], acts[P, R, S, state_size].
+ */
+int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
+                const int8_t* fn, const OrRollouts* ro, float* fitness, float* rollout_fitness, float* xs,
+                float* ys, float* us, float* acts) {
+  if (N > OR_MAX_N || state_dim(m) > OR_MAX_S || ro->R > 65536) return -1;
+  const int R = ro->R, S = m->n_save, dim = state_dim(m);
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int p = 0; p < P; ++p) {
+    OrCtx c;
+    c.m = m;
+    c.cand = pop + (size_t)p * T * N * 4;
+    c.N = N;
+    c.lib.n_funcs = n_funcs;
+    c.lib.var_start = var_start;
+    c.lib.fn = fn;
+    float* saved = (float*)malloc(sizeof(float) * (size_t)S * dim);
+    float* uu = (float*)malloc(sizeof(float) * (size_t)S * 8);
+    float* fr = (float*)malloc(sizeof(float) * (size_t)R);
+    for (int r = 0; r < R; ++r) {
+      c.target = ro->targets ? ro->targets + (size_t)r * m->n_targets : NULL;
+      if (ro->params) {
+        c.l1 = ro->params[4 * r + 0]; c.l2 = ro->params[4 * r + 1];
+        c.m1 = ro->params[4 * r + 2]; c.m2 = ro->params[4 * r + 3];
+      } else {
+        c.l1 = c.l2 = c.m1 = c.m2 = 1.0f;
+      }
+      float s0[OR_MAX_S];
+      for (int i = 0; i < dim; ++i) s0[i] = 0.0f;
+      for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
+      solve(&c, s0, saved);
+      float f;
+      const size_t base = ((size_t)p * R + r) * S;
+      if (m->model == 3) {
+        /* MSE: mean over time of sum over dims (sr.py:24) */
+        float tot = 0.0f;
+        for (int k = 0; k < S; ++k) {
+          float sq = 0.0f;
+          for (int d = 0; d < m->n_var; ++d) {
+            const float e = saved[(size_t)k * dim + d] - ro->ys_true[((size_t)r * S + k) * m->n_var + d];
+            sq = (d == 0) ? e * e : sq + e * e;
+          }
+          tot = tot + sq;
+        }
+        f = tot / (float)S;
+        if (xs)
+          for (int k = 0; k < S; ++k)
+            for (int d = 0; d < m->n_var; ++d) xs[(base + k) * m->n_var + d] = saved[(size_t)k * dim + d];
+      } else {
+        /* observations at the saved points (lax.scan f_obs) and the readout/policy */
+        float yk[4], data[OR_MAX_D];
+        float xk[4];
+        for (int k = 0; k < S; ++k) {
+          for (int i = 0; i < 4; ++i) xk[i] = saved[(size_t)k * dim + i];
+          acro_f_obs(xk, yk);
+          if (m->model == 1) { /* dyn.py:101: readout([y, a, 0_u, target]) */
+            const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
+            const int D = no + na + nu + nt;
+            for (int i = 0; i < no; ++i) data[i] = yk[i];
+            for (int i = 0; i < na; ++i) data[no + i] = saved[(size_t)k * dim + 4 + i];
+            for (int i = 0; i < nu; ++i) data[no + na + i] = 0.0f;
+            for (int i = 0; i < nt; ++i) data[no + na + nu + i] = c.target[i];
+            for (int j = 0; j < nu; ++j) uu[(size_t)k * 8 + j] = tree_eval(&c, na + j, data, D);
+          } else { /* ff.py:97: policy([y, target]) */
+            const int no = m->n_obs, nt = m->n_targets;
+            for (int i = 0; i < no; ++i) data[i] = yk[i];
+            for (int i = 0; i < nt; ++i) data[no + i] = c.target[i];
+            uu[(size_t)k * 8] = tree_eval(&c, 0, data, no + nt);
+          }
+          if (xs) for (int i = 0; i < 4; ++i) xs[(base + k) * 4 + i] = xk[i];
+          if (ys) for (int i = 0; i < m->n_obs; ++i) ys[(base + k) * m->n_obs + i] = yk[i];
+          if (us) for (int j = 0; j < m->n_control; ++j) us[(base + k) * m->n_control + j] = uu[(size_t)k * 8 + j];
+          if (acts && m->model == 1)
+            for (int i = 0; i < m->state_size; ++i)
+              acts[(base + k) * m->state_size + i] = saved[(size_t)k * dim + 4 + i];
+        }
+        /* acrobot fitness uses the first control only (R = [[0.01]], n_control = 1) */
+        float ucol[4096];
+        float* up = (S <= 4096) ? ucol : (float*)malloc(sizeof(float) * S);
+        float xcol[4 * 4096];
+        float* xp = (S <= 4096) ? xcol : (float*)malloc(sizeof(float) * 4 * S);
+        for (int k = 0; k < S; ++k) {
+          up[k] = uu[(size_t)k * 8];
+          for (int i = 0; i < 4; ++i) xp[4 * k + i] = saved[(size_t)k * dim + i];
+        }
+        f = acro_fitness(xp, up, ro->ts, S);
+        if (up != ucol) free(up);
+        if (xp != xcol) free(xp);
+      }
+      if (rollout_fitness) rollout_fitness[(size_t)p * R + r] = f;
+      /* dyn.py:49-50 / sr.py:42-43: NaN or inf -> max_fitness */
+      fr[r] = mtgp_isfinite(f) ? f : m->max_fitness;
+    }
+    /* mean over rollouts, clip (dyn.py:51-52) */
+    float mean = pairwise_sum(fr, R) / (float)R;
+    if (mean < 0.0f) mean = 0.0f;
+    if (mean > m->max_fitness) mean = m->max_fitness;
+    /* parsimony on non-empty rows of all trees (gp.py:424) */
+    int cnt = 0;
+    for (int i = 0; i < T * N; ++i) cnt += (c.cand[4 * i] != 0.0f);
+    fitness[p] = mean + m->parsimony * (float)cnt;
+    free(saved);
+    free(uu);
+    free(fr);
+  }
+  return 0;
+}
+
+int oracle_abi_version(void) { return 1; }
+
+/* vectorised helpers for tests */
+void oracle_sincos(const float* x, float* s, float* c, long n) {
+  for (long i = 0; i < n; ++i) { s[i] = mtgp_sinf(x[i]); c[i] = mtgp_cosf(x[i]); }
+}
+void oracle_wrap(const float* x, float* o, long n) {
+  for (long i = 0; i < n; ++i) o[i] = mtgp_wrap_angle(x[i]);
+}

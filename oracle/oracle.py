@@ -1,0 +1,131 @@
+"""ctypes wrapper of oracle/build/libmtgp_oracle.so.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and bench.py's
+cpu_baseline leg, always as the checker / CPU baseline -- never by multitreegp_amd.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "libmtgp_oracle.so")
+
+
+def build(force: bool = False) -> str:
+    src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h")]
+    if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
+        subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
+                       stdout=subprocess.DEVNULL)
+    return LIB
+
+
+class OrModel(ctypes.Structure):
+    _fields_ = [("model", ctypes.c_int32), ("n_var", ctypes.c_int32), ("state_size", ctypes.c_int32),
+                ("n_obs", ctypes.c_int32), ("n_control", ctypes.c_int32), ("n_targets", ctypes.c_int32),
+                ("n_steps", ctypes.c_int32), ("save_every", ctypes.c_int32), ("n_save", ctypes.c_int32),
+                ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float)]
+
+
+class OrRollouts(ctypes.Structure):
+    _fields_ = [("x0", ctypes.c_void_p), ("params", ctypes.c_void_p), ("targets", ctypes.c_void_p),
+                ("ts", ctypes.c_void_p), ("ys_true", ctypes.c_void_p), ("R", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        build()
+        L = ctypes.CDLL(LIB)
+        vp = ctypes.c_void_p
+        L.oracle_eval_tree.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, vp, vp, ctypes.c_int]
+        L.oracle_eval_tree.restype = ctypes.c_float
+        L.oracle_eval.argtypes = [ctypes.POINTER(OrModel), vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(OrRollouts), vp, vp, vp, vp, vp,
+                                  vp]
+        L.oracle_eval.restype = ctypes.c_int
+        L.oracle_sincos.argtypes = [vp, vp, vp, ctypes.c_long]
+        L.oracle_wrap.argtypes = [vp, vp, ctypes.c_long]
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else ctypes.c_void_p(a.ctypes.data)
+
+
+def eval_tree(tree: np.ndarray, fn_codes: np.ndarray, n_funcs: int, var_start: int, data: np.ndarray) -> np.float32:
+    """gp.py:378-388 foriloop on one [N, 4] tree."""
+    t = np.ascontiguousarray(tree, np.float32)
+    fn = np.ascontiguousarray(fn_codes, np.int8)
+    d = np.ascontiguousarray(data, np.float32).reshape(-1)
+    if d.size == 0:
+        d = np.zeros(1, np.float32)
+    return np.float32(lib().oracle_eval_tree(_p(t), t.shape[0], n_funcs, var_start, _p(fn), _p(d),
+                                             max(int(np.asarray(data).size), 1)))
+
+
+def sincos(x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib().oracle_sincos(_p(x), _p(s), _p(c), x.size)
+    return s, c
+
+
+def wrap(x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float32)
+    o = np.empty_like(x)
+    lib().oracle_wrap(_p(x), _p(o), x.size)
+    return o
+
+
+def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories: bool = False):
+    """Evaluate a flat population [P, T, N, 4].
+
+    model: dict(model, n_var, state_size, n_obs, n_control, n_targets, n_steps, save_every, n_save,
+                h, max_fitness, parsimony)
+    rollouts: dict(x0 [R, n_var], params [R, 4] or None, targets [R, nt] or None, ts [S],
+                   ys_true [R, S, n_var] or None)
+    Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c])."""
+    pop = np.ascontiguousarray(pop, np.float32)
+    P, T, N, _ = pop.shape
+    m = OrModel(**{k: model[k] for k, _ in OrModel._fields_})
+    x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
+    R = x0.shape[0]
+    prm = None if rollouts.get("params") is None else np.ascontiguousarray(rollouts["params"], np.float32)
+    tg = rollouts.get("targets")
+    tg = None if tg is None or np.asarray(tg).size == 0 else np.ascontiguousarray(tg, np.float32)
+    ts = np.ascontiguousarray(rollouts["ts"], np.float32)
+    yt = rollouts.get("ys_true")
+    yt = None if yt is None else np.ascontiguousarray(yt, np.float32)
+    ro = OrRollouts(_p(x0).value, None if prm is None else _p(prm).value, None if tg is None else _p(tg).value,
+                    _p(ts).value, None if yt is None else _p(yt).value, R)
+    S = model["n_save"]
+    fit = np.empty(P, np.float32)
+    rf = np.empty((P, R), np.float32)
+    out = {"fitness": fit, "rollout_fitness": rf}
+    bufs = [None, None, None, None]
+    if trajectories:
+        if model["model"] == 3:
+            bufs[0] = np.empty((P, R, S, model["n_var"]), np.float32)
+        else:
+            bufs[0] = np.empty((P, R, S, 4), np.float32)
+            bufs[1] = np.empty((P, R, S, model["n_obs"]), np.float32)
+            bufs[2] = np.empty((P, R, S, model["n_control"]), np.float32)
+            if model["model"] == 1:
+                bufs[3] = np.empty((P, R, S, model["state_size"]), np.float32)
+        for k, b in zip(("xs", "ys", "us", "acts"), bufs):
+            if b is not None:
+                out[k] = b
+    fn = np.ascontiguousarray(library.fn_codes, np.int8)
+    rc = lib().oracle_eval(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
+                           ctypes.byref(ro), _p(fit), _p(rf), *[_p(b) for b in bufs])
+    if rc != 0:
+        raise RuntimeError(f"oracle_eval failed {rc}")
+    return out

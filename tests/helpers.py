@@ -1,0 +1,74 @@
+"""Shared test fixtures: reference-style node libraries, populations and data."""
+import numpy as np
+
+import multitreegp_amd as mt
+from multitreegp_amd.sampling import sample_population
+
+CONTROL_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
+               ("cos", None, 1, 0.1)]  # DynamicPolicy.ipynb
+SR_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("/", None, 2, 0.1)]  # SymbolicRegression.ipynb
+
+
+def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2):
+    env = mt.Acrobot(0.0, 0.0)
+    vl = [["y1", "y2", "y3", "y4"] + [f"a{i + 1}" for i in range(state_size)] + ["u"],
+          [f"a{i + 1}" for i in range(state_size)]]
+    lib = mt.NodeLibrary(CONTROL_OPS, vl, [state_size, 1])
+    ff = mt.DynamicEvaluator(env, state_size, 0.05, solver=mt.RK4())
+    data = mt.control_data(env, R, 0.05, None, seed=seed + 1, n_steps=n_steps)
+    pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
+    return env, lib, ff, data, pop
+
+
+def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0):
+    env = mt.Acrobot(0.0, 0.0)
+    lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1])
+    ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4())
+    data = mt.control_data(env, R, 0.05, None, seed=seed + 1, n_steps=n_steps)
+    pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
+    return env, lib, ff, data, pop
+
+
+def sr_setup(P=24, R=8, n_save=21, save_every=4, h=0.05, depth=5, N=30, seed=0, n_var=2):
+    env = mt.VanDerPolOscillator(0, 0) if n_var == 2 else mt.LinearSystem(n_var)
+    lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(n_var)]], [n_var])
+    ff = mt.SREvaluator(solver=mt.RK4(), dt0=h)
+    rng = np.random.default_rng(seed + 1)
+    x0 = env.sample_init_states(R, rng)
+    ts = (np.arange(n_save, dtype=np.float32) * np.float32(h * save_every)).astype(np.float32)
+    ys = mt.ground_truth(env, x0, ts)
+    data = (x0, ts, ys, np.zeros((R, 2), np.uint32))
+    pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
+    return env, lib, ff, data, pop
+
+
+def oracle_model(ff, d, parsimony=0.0):
+    env = getattr(ff, "env", None)
+    return dict(model=ff.model_id, n_var=d.get("n_var", 4), state_size=getattr(ff, "state_size", 0),
+                n_obs=env.n_obs if env else 0, n_control=env.n_control if env else 0,
+                n_targets=env.n_targets if env else 0, n_steps=d["n_steps"], save_every=d["save_every"],
+                n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony)
+
+
+def oracle_rollouts(d, data=None):
+    ys = None
+    if d.get("ys_true") is not None:
+        ys = np.ascontiguousarray(np.transpose(d["ys_true"], (2, 0, 1)))  # back to [R, S, n_var]
+    return dict(x0=d["x0"], params=d.get("params"), targets=d.get("targets"), ts=d["ts"], ys_true=ys)
+
+
+def bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    if a.shape != b.shape:
+        return False
+    nan = np.isnan(a) & np.isnan(b)
+    return bool(np.all((a.view(np.uint32) == b.view(np.uint32)) | nan))
+
+
+def mismatch_report(a, b, name):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    diff = ~((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b)))
+    idx = np.argwhere(diff)
+    return f"{name}: {diff.sum()} / {diff.size} differ; first {idx[:5].tolist()} gpu={a[tuple(idx[0])] if len(idx) else None} ref={b[tuple(idx[0])] if len(idx) else None}"

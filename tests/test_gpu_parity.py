@@ -1,0 +1,114 @@
+"""GPU parity: the HIP path through the C ABI vs the CPU oracle, bit-for-bit.
+
+Every comparison is exact (uint32 equality, NaN == NaN): kernel and oracle share the fp32
+arithmetic spec (include/mtgp_f32math.h), evaluate identical operations in identical order,
+and the oracle interprets trees row by row like gp.py:356-388 while the kernel runs the
+flattened programs -- so any flattener/interpreter/integrator/fitness bug shows up."""
+import numpy as np
+import pytest
+import torch
+
+import multitreegp_amd as mt
+from multitreegp_amd.engine import DeviceEngine, to_reference_layout
+from oracle import oracle as orc
+from helpers import (bits_equal, dynamic_setup, mismatch_report, oracle_model, oracle_rollouts, sr_setup,
+                     static_setup)
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ff, lib, data, pop, parsimony=0.0, traj=True):
+    eng = DeviceEngine(ff, lib, parsimony, "cuda:0")
+    res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=traj,
+                       rollout_fitness=True)
+    torch.cuda.synchronize()
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d, parsimony), pop, lib, oracle_rollouts(d), trajectories=traj)
+    return res, ref, d
+
+
+def _check(res, ref, P, R, names):
+    assert bits_equal(res["fitness"].cpu().numpy(), ref["fitness"]), \
+        mismatch_report(res["fitness"].cpu().numpy(), ref["fitness"], "fitness")
+    assert bits_equal(res["rollout_fitness"].cpu().numpy(), ref["rollout_fitness"]), \
+        mismatch_report(res["rollout_fitness"].cpu().numpy(), ref["rollout_fitness"], "rollout_fitness")
+    for k in names:
+        got = to_reference_layout(res[k], P, R)
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+
+
+def test_eval_programs_vs_row_order_oracle():
+    env, lib, ff, data, pop = dynamic_setup(P=64)
+    eng = DeviceEngine(mt.evaluators._TreeOnly(3, 7), lib, 0.0, "cuda:0")
+    eng.prepare_data(None)
+    fl = eng.flatten(torch.from_numpy(pop).cuda())
+    eng.check_status(fl)
+    rng = np.random.default_rng(5)
+    dv = rng.standard_normal((100, 7)).astype(np.float32) * 3
+    out = eng.eval_programs(fl, torch.from_numpy(dv).cuda()).cpu().numpy()
+    ref = np.array([[[orc.eval_tree(pop[p, t], lib.fn_codes, lib.n_funcs, lib.var_start, dv[m])
+                      for m in range(dv.shape[0])] for t in range(3)] for p in range(pop.shape[0])], np.float32)
+    assert bits_equal(out, ref), mismatch_report(out, ref, "eval_programs")
+
+
+def test_eval_programs_garbage_arrays():
+    """Arbitrary arrays (bad opcodes, wrapped/clamped indices, forward refs) follow body_fun."""
+    env, lib, ff, data, _ = dynamic_setup(P=4)
+    rng = np.random.default_rng(11)
+    P, N = 200, 20
+    pop = np.empty((P, 3, N, 4), np.float32)
+    pop[..., 0] = rng.integers(-2, lib.n_funcs + 3, (P, 3, N)) + (rng.random((P, 3, N)) < 0.1) * 0.5
+    pop[..., 1] = rng.integers(-N - 3, N + 3, (P, 3, N))
+    pop[..., 2] = rng.integers(-N - 3, N + 3, (P, 3, N))
+    pop[..., 3] = rng.standard_normal((P, 3, N)) * 3
+    eng = DeviceEngine(mt.evaluators._TreeOnly(3, 7), lib, 0.0, "cuda:0")
+    eng.prepare_data(None)
+    fl = eng.flatten(torch.from_numpy(pop).cuda())
+    status = fl.status.cpu().numpy()
+    dv = rng.standard_normal((17, 7)).astype(np.float32)
+    out = eng.eval_programs(fl, torch.from_numpy(dv).cuda()).cpu().numpy()
+    checked = 0
+    for p in range(P):
+        for t in range(3):
+            if status[p, t] != 0:
+                continue
+            ref = np.array([orc.eval_tree(pop[p, t], lib.fn_codes, lib.n_funcs, lib.var_start, dv[m])
+                            for m in range(dv.shape[0])], np.float32)
+            assert bits_equal(out[p, t], ref), mismatch_report(out[p, t], ref, f"tree {p},{t}")
+            checked += 1
+    assert checked > 400
+
+
+@pytest.mark.parametrize("R", [8, 32])
+def test_dynamic_acrobot_bitexact(R):
+    env, lib, ff, data, pop = dynamic_setup(P=40, R=R, n_steps=80)
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], R, ["xs", "ys", "us", "acts"])
+
+
+def test_dynamic_fitness_only_matches_trajectory_mode():
+    env, lib, ff, data, pop = dynamic_setup(P=64, R=16, n_steps=100, seed=3)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    pt = torch.from_numpy(pop).cuda()
+    a = eng.evaluate(pt, data, trajectories=True)["fitness"].cpu().numpy()
+    b = eng.evaluate(pt, data, trajectories=False)["fitness"].cpu().numpy()
+    assert bits_equal(a, b)
+
+
+def test_static_acrobot_bitexact():
+    env, lib, ff, data, pop = static_setup(P=40, R=16, n_steps=80)
+    res, ref, d = _run(ff, lib, data, pop, parsimony=1.0)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us"])
+
+
+def test_sr_vanderpol_bitexact():
+    env, lib, ff, data, pop = sr_setup(P=40, R=16)
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], 16, ["xs"])
+
+
+@pytest.mark.parametrize("R", [1, 33, 64])
+def test_rollout_counts(R):
+    env, lib, ff, data, pop = dynamic_setup(P=9, R=R, n_steps=30, seed=7)
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], R, ["xs", "us"])
