@@ -14,8 +14,9 @@
  *
  *   mtgp_sinf / mtgp_cosf : |error| <= ~2 ulp over the whole float range
  *       |x| < 2^-12        : sin x = x, cos x = 1
- *       |x| < 2^17         : 3-constant Cody-Waite reduction with fma (exact first step)
- *       otherwise (finite) : Payne-Hanek reduction against 128 bits of 2/pi
+ *       |x| < 2^17         : 3-constant float Cody-Waite reduction with fma (exact first step)
+ *       |x| < 2^28         : 3-constant double Cody-Waite reduction
+ *       otherwise (finite) : Payne-Hanek reduction against a 96-bit window of 2/pi
  *   mtgp_floor_mod_2pi    : jnp.remainder(a, float32(2*pi)) semantics, exact fmod core
  *
  * Must be compiled with -ffp-contract=off on both sides (explicit fmaf only).
@@ -31,6 +32,7 @@
 #define MTGP_NOINLINE __attribute__((noinline))
 #define MTGP_FMAF(a, b, c) __builtin_fmaf((a), (b), (c))
 #define MTGP_RINTF(a) __builtin_rintf(a)
+#define MTGP_RINT(a) __builtin_rint(a)
 #define MTGP_TRUNCF(a) __builtin_truncf(a)
 #define MTGP_FABSF(a) __builtin_fabsf(a)
 #else
@@ -39,8 +41,17 @@
 #define MTGP_NOINLINE
 #define MTGP_FMAF(a, b, c) fmaf((a), (b), (c))
 #define MTGP_RINTF(a) rintf(a)
+#define MTGP_RINT(a) rint(a)
 #define MTGP_TRUNCF(a) truncf(a)
 #define MTGP_FABSF(a) fabsf(a)
+#endif
+
+/* wave-uniform "does any lane need the rare path" test: a single scalar branch on the GPU,
+ * the per-element condition on the host (same result per element either way) */
+#if defined(__HIP_DEVICE_COMPILE__)
+#define MTGP_ANY(c) __any(c)
+#else
+#define MTGP_ANY(c) (c)
 #endif
 
 #ifdef __cplusplus
@@ -108,89 +119,104 @@ MTGP_INLINE MTGP_HD uint32_t mtgp_twoopi_word(int k) {
 #endif
 }
 
-/* Payne-Hanek: for finite |x| >= 2^17 returns r in [-pi/4, pi/4] and quadrant q (0..3)
- * with |x| = q*pi/2 + r (mod 2*pi).  Fixed-point product of the 24-bit significand
- * with 128 bits of 2/pi taken at the exponent's window; the fraction is rounded to
- * double then float (all IEEE, so host and device agree). */
-MTGP_NOINLINE MTGP_HD static float mtgp_reduce_large(float ax, int* quadrant) {
+/* Payne-Hanek for finite |x| >= 2^28: |x| = m * 2^e (24-bit m, e >= 5).  The 96-bit window
+ * W of 2/pi bits [b+1, b+96] with b = e - 2 makes m*W*2^-94 = |x|*2/pi mod 4 with the binary
+ * point at a FIXED bit (94) of the product, so no limb is indexed dynamically. */
+MTGP_INLINE MTGP_HD float mtgp_reduce_payne_hanek(float ax, int* quadrant) {
   const uint32_t u = mtgp_f2u(ax);
-  const int bexp = (int)((u >> 23) & 0xffu);
   const uint32_t m = (u & 0x7fffffu) | 0x800000u;
-  const int e = bexp - 127 - 23; /* ax = m * 2^e, e >= -6 here */
-  const int k0 = (e >= 2) ? ((e - 2) >> 5) : 0;
-  uint32_t q[5];
-  uint64_t carry = 0;
-  for (int i = 3; i >= 0; --i) {
-    const uint64_t t = (uint64_t)m * (uint64_t)mtgp_twoopi_word(k0 + i) + carry;
-    q[i + 1] = (uint32_t)t;
-    carry = t >> 32;
-  }
-  q[0] = (uint32_t)carry;
-  /* Q = q[0..4] (160 bits, q[4] least significant); value = Q * 2^-(sh) with: */
-  const int sh = 32 * (k0 + 4) - e; /* number of fractional bits, in [95, 134] */
-  /* bit b of Q (b = 0 is the lsb) lives in q[4 - (b >> 5)] at (b & 31) */
-#define MTGP_QBIT64(b)                                                              \
-  ((((b) >> 5) <= 4) ? (uint64_t)q[4 - ((b) >> 5)] : (uint64_t)0)
-  /* 64 fraction bits: Q bits [sh-64, sh) ; quadrant: Q bits [sh, sh+2) */
-  const int lo = sh - 64;
-  const int wlo = lo >> 5, blo = lo & 31;
-  uint64_t w0 = MTGP_QBIT64(32 * wlo), w1 = MTGP_QBIT64(32 * (wlo + 1)),
-           w2 = MTGP_QBIT64(32 * (wlo + 2));
-  uint64_t frac;
-  if (blo == 0) frac = w0 | (w1 << 32);
-  else frac = (w0 >> blo) | (w1 << (32 - blo)) | (w2 << (64 - blo));
-  const int wq = sh >> 5, bq = sh & 31;
-  uint64_t qa = MTGP_QBIT64(32 * wq), qb = MTGP_QBIT64(32 * (wq + 1));
-  uint32_t quad = (uint32_t)(((qa >> bq) | (qb << (32 - bq))) & 3u);
-  if (bq == 0) quad = (uint32_t)(qa & 3u);
-#undef MTGP_QBIT64
-  /* round the fraction to the nearest quadrant boundary: f in [-1/2, 1/2) */
-  int64_t sf = (int64_t)frac;
-  if (frac & 0x8000000000000000ull) quad = (quad + 1u) & 3u; /* sf already f - 1 */
-  const double fd = (double)sf * 5.42101086242752217e-20; /* 2^-64 */
-  const double rd = fd * 1.57079632679489656e+00;         /* pi/2 (double) */
+  const int e = (int)((u >> 23) & 0xffu) - 150;
+  const int b = e - 2;
+  const int k = b >> 5, s = b & 31;
+  const uint64_t w0 = mtgp_twoopi_word(k), w1 = mtgp_twoopi_word(k + 1), w2 = mtgp_twoopi_word(k + 2),
+                 w3 = mtgp_twoopi_word(k + 3);
+  const uint64_t Whi = (uint32_t)(((w0 << 32) | w1) >> (32 - s));
+  const uint64_t Wmid = (uint32_t)(((w1 << 32) | w2) >> (32 - s));
+  const uint64_t Wlo = (uint32_t)(((w2 << 32) | w3) >> (32 - s));
+  const uint64_t lo = (uint64_t)m * Wlo;
+  const uint64_t mid = (uint64_t)m * Wmid + (lo >> 32);
+  const uint64_t hi = (uint64_t)m * Whi + (mid >> 32);
+  uint32_t quad = (uint32_t)(hi >> 30) & 3u;
+  const uint64_t frac = ((hi & 0x3fffffffull) << 34) | ((mid & 0xffffffffull) << 2) | ((lo & 0xffffffffull) >> 30);
+  /* round to the nearest quadrant: f in [-1/2, 1/2) */
+  if (frac & 0x8000000000000000ull) quad = (quad + 1u) & 3u;
+  const double fd = (double)(int64_t)frac * 5.42101086242752217e-20; /* 2^-64 */
   *quadrant = (int)quad;
-  return (float)rd;
+  return (float)(fd * 1.57079632679489656e+00);
 }
 
-/* shared reduction: returns r, quadrant in *q.  Handles finite x only. */
-MTGP_INLINE MTGP_HD float mtgp_reduce(float x, int* q) {
+/* slow reduction for finite |x| >= 2^17: returns r, quadrant in *q */
+MTGP_INLINE MTGP_HD float mtgp_reduce_slow(float x, int* q) {
   const float ax = MTGP_FABSF(x);
-  if (ax < 131072.0f) { /* 2^17 */
-    const float j = MTGP_RINTF(x * 6.36619747e-01f); /* f32(2/pi) */
-    float r = MTGP_FMAF(j, -1.57079637e+00f, x);     /* exact */
-    r = MTGP_FMAF(j, 4.37113883e-08f, r);
-    r = MTGP_FMAF(j, 1.71512451e-15f, r);
-    *q = ((int)j) & 3;
-    return r;
+  if (ax < 268435456.0f) { /* 2^28: double Cody-Waite, 24+24+53-bit pi/2, first steps exact */
+    const double xd = (double)x;
+    const double j = MTGP_RINT(xd * 6.3661977236758138e-01);
+    double r = xd - j * 1.570796251296997e+00;
+    r = r - j * 7.549789415861596e-08;
+    r = r - j * 5.390302858158119e-15;
+    *q = ((int)(int64_t)j) & 3;
+    return (float)r;
   }
   int qq;
-  float r = mtgp_reduce_large(ax, &qq);
+  float r = mtgp_reduce_payne_hanek(ax, &qq);
   if (x < 0.0f) { r = -r; qq = (4 - qq) & 3; }
   *q = qq;
   return r;
 }
 
-MTGP_INLINE MTGP_HD float mtgp_sinf(float x) {
-  if (MTGP_FABSF(x) < 2.44140625e-04f) return x; /* 2^-12, keeps -0 and denormals */
-  if (!mtgp_isfinite(x)) return mtgp_qnan();
+/* Reduction to r (|r| <~ pi/4) and quadrant.  The float Cody-Waite fast path runs
+ * unconditionally (exact first step for |x| < 2^17; it yields NaN for non-finite x); lanes
+ * with finite |x| >= 2^17 are redone by the slow path behind ONE wave-uniform branch. */
+MTGP_INLINE MTGP_HD float mtgp_reduce(float x, int* q) {
+  const float ax = MTGP_FABSF(x);
+  const float j = MTGP_RINTF(x * 6.36619747e-01f); /* f32(2/pi) */
+  float r = MTGP_FMAF(j, -1.57079637e+00f, x);
+  r = MTGP_FMAF(j, 4.37113883e-08f, r);
+  r = MTGP_FMAF(j, 1.71512451e-15f, r);
+  const int fast = ax < 131072.0f;
+  int qq = fast ? (((int)j) & 3) : 0;
+  const int slow = !fast && mtgp_isfinite(x);
+  if (MTGP_ANY(slow)) {
+    if (slow) r = mtgp_reduce_slow(x, &qq);
+  }
+  *q = qq;
+  return r;
+}
+
+/* sin and cos of x sharing one reduction; |x| < 2^-12 -> (x, 1); non-finite -> NaN */
+MTGP_INLINE MTGP_HD void mtgp_sincosf(float x, float* s, float* c) {
   int q;
   const float r = mtgp_reduce(x, &q);
-  const float s = (q & 1) ? mtgp_cos_poly(r) : mtgp_sin_poly(r);
-  return (q & 2) ? -s : s;
+  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
+  float sv = (q & 1) ? pc : ps;
+  float cv = (q & 1) ? ps : pc;
+  sv = (q & 2) ? -sv : sv;
+  cv = ((q + 1) & 2) ? -cv : cv;
+  const int tiny = MTGP_FABSF(x) < 2.44140625e-04f; /* 2^-12: keeps -0 and denormals */
+  *s = tiny ? x : sv;
+  *c = tiny ? 1.0f : cv;
+}
+
+MTGP_INLINE MTGP_HD float mtgp_sinf(float x) {
+  int q;
+  const float r = mtgp_reduce(x, &q);
+  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
+  float v = (q & 1) ? pc : ps;
+  v = (q & 2) ? -v : v;
+  return (MTGP_FABSF(x) < 2.44140625e-04f) ? x : v;
 }
 
 MTGP_INLINE MTGP_HD float mtgp_cosf(float x) {
-  if (MTGP_FABSF(x) < 2.44140625e-04f) return 1.0f;
-  if (!mtgp_isfinite(x)) return mtgp_qnan();
   int q;
   const float r = mtgp_reduce(x, &q);
-  const float c = (q & 1) ? mtgp_sin_poly(r) : mtgp_cos_poly(r);
-  return ((q + 1) & 2) ? -c : c;
+  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
+  float v = (q & 1) ? ps : pc;
+  v = ((q + 1) & 2) ? -v : v;
+  return (MTGP_FABSF(x) < 2.44140625e-04f) ? 1.0f : v;
 }
 
 /* large |a|: exact binary long division by power-of-two multiples of b (rare path) */
-MTGP_NOINLINE MTGP_HD static float mtgp_fmod_2pi_large(float a) {
+MTGP_INLINE MTGP_HD float mtgp_fmod_2pi_large(float a) {
   const float b = MTGP_TWO_PI_F;
   float r = MTGP_FABSF(a);
   while (r >= b) {
@@ -201,33 +227,28 @@ MTGP_NOINLINE MTGP_HD static float mtgp_fmod_2pi_large(float a) {
   return (a < 0.0f) ? -r : r;
 }
 
-/* Exact C fmod(a, b) for b = f32(2*pi) > 0 (truncated remainder, sign of a). */
+/* Exact C fmod(a, b) for b = f32(2*pi) > 0 (truncated remainder, sign of a).
+ * Fast path (|a| < 2^20): q = trunc(|a| * up(1/b)) is never below the true quotient (the
+ * reciprocal is rounded UP) and at most one above it, so r = fma(-q, b, |a|) lies in (-b, b)
+ * with the lsb of b -> exact; one "+ b" (also exact) fixes the overshoot.  Lanes with
+ * |a| >= 2^20 or non-finite a take the slow path behind one wave-uniform branch. */
 MTGP_INLINE MTGP_HD float mtgp_fmod_2pi(float a) {
   const float b = MTGP_TWO_PI_F;
-  if (!mtgp_isfinite(a)) return mtgp_qnan();
   const float aa = MTGP_FABSF(a);
-  float r;
-  if (aa < b) return a; /* fmod(a, b) = a, keeps the sign of zero */
-  if (aa < 1048576.0f) { /* 2^20: quotient exact, fma remainder exact */
-    const float qt = MTGP_TRUNCF(a / b);
-    r = MTGP_FMAF(-qt, b, a);
-    if (a >= 0.0f) {
-      if (r < 0.0f) r = r + b;       /* quotient rounded up: exact fix */
-      else if (r >= b) r = r - b;
-    } else {
-      if (r > 0.0f) r = r - b;
-      else if (r <= -b) r = r + b;
-    }
-    return r;
+  const float q = MTGP_TRUNCF(aa * 1.59154951572418213e-01f); /* up(1/f32(2pi)) */
+  float r = MTGP_FMAF(-q, b, aa);
+  r = (r < 0.0f) ? r + b : r;
+  const int slow = !(aa < 1048576.0f);
+  if (MTGP_ANY(slow)) {
+    if (slow) r = mtgp_isfinite(a) ? mtgp_fmod_2pi_large(aa) : mtgp_qnan();
   }
-  return mtgp_fmod_2pi_large(a);
+  return mtgp_u2f(mtgp_f2u(r) | (mtgp_f2u(a) & 0x80000000u));
 }
 
 /* jnp.remainder(a, 2pi) (floor-mod): trunc remainder, then + b when signs differ. */
 MTGP_INLINE MTGP_HD float mtgp_floor_mod_2pi(float a) {
-  float r = mtgp_fmod_2pi(a);
-  if (r != 0.0f && r < 0.0f) r = r + MTGP_TWO_PI_F;
-  return r;
+  const float r = mtgp_fmod_2pi(a);
+  return (r < 0.0f) ? r + MTGP_TWO_PI_F : r;
 }
 
 /* Acrobot angle wrap (acrobot.py:31): (v + pi) % (2 pi) - pi, all in f32. */

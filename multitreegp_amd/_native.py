@@ -98,7 +98,7 @@ class NativeLibraryMissing(RuntimeError):
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
     """Load the HIP library (cached).  Raises NativeLibraryMissing if it is not built."""
     global _lib
-    if _lib is not None:
+    if _lib is not None and path == LIB_PATH:
         return _lib
     if not os.path.exists(path):
         raise NativeLibraryMissing(
@@ -123,7 +123,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mtgp_set_timing.restype = ctypes.c_int
     if lib.mtgp_abi_version() != 1:
         raise RuntimeError("libmtgp_hip ABI version mismatch")
-    _lib = lib
+    if path == LIB_PATH:
+        _lib = lib
     return lib
 
 

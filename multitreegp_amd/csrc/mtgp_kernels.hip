@@ -26,48 +26,113 @@ constexpr int kDMax = 8;  // data slots held in LDS by the small-state kernels
 constexpr int kSMax = MTGP_STACK_MAX;
 constexpr float kInf = __builtin_huge_valf();
 
+#ifndef MTGP_V_PREFETCH
+#define MTGP_V_PREFETCH 0
+#endif
+
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // --------------------------------------------------------------------------------------
 // The interpreter.  `dv` = this lane's column of the wave's LDS data vector (stride 64
 // floats per slot), `st` = this lane's column of the operand stack.  `code`/`len` are
 // wave-uniform.
-__device__ __forceinline__ float run_prog(const MtgpInstr* __restrict__ code, int len,
-                                          const float* dv, float* st) {
+// Register data vector (scalar branch tree per variable read): measured 2% slower than the
+// LDS column at C3, off by default.
+#ifndef MTGP_V_REGDATA
+#define MTGP_V_REGDATA 0
+#endif
+
+// The data vector a tree reads.  MTGP_V_REGDATA=1: up to 8 slots in VGPRs, the (wave-uniform)
+// slot picked by a scalar branch tree; 0: one 64-lane LDS column per slot.
+struct DVec {
+  const float* lds;  // this lane's LDS column base (stride kWave per slot)
+  float r[kDMax];
+};
+
+template <bool REG>
+__device__ __forceinline__ float dget(const DVec& d, uint32_t slot) {
+  if (REG) {
+  switch (slot) {
+    case 0: return d.r[0];
+    case 1: return d.r[1];
+    case 2: return d.r[2];
+    case 3: return d.r[3];
+    case 4: return d.r[4];
+    case 5: return d.r[5];
+    case 6: return d.r[6];
+    default: return d.r[7];
+  }
+  }
+  return d.lds[slot * kWave];
+}
+
+__device__ __forceinline__ void dset(DVec& d, float* lds_col, int slot, float v) {
+#if MTGP_V_REGDATA
+  d.r[slot] = v;
+  (void)lds_col;
+#else
+  lds_col[slot * kWave] = v;
+#endif
+}
+
+template <bool REG = (MTGP_V_REGDATA != 0)>
+__device__ __forceinline__ float exec_instr(uint32_t w, float imm, float acc, int& sp, const DVec& dv,
+                                            float* st) {
+  const uint32_t op = w & 0xffu;
+  const uint32_t slot = (w >> 8) & 0xffu;
+  switch (op) {
+    case MTGP_OP_LDC: return imm;
+    case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; return imm;
+    case MTGP_OP_LDV: return dget<REG>(dv, slot);
+    case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; return dget<REG>(dv, slot);
+    case MTGP_OP_ADDC: return acc + imm;
+    case MTGP_OP_SUBC: return acc - imm;
+    case MTGP_OP_RSUBC: return imm - acc;
+    case MTGP_OP_MULC: return acc * imm;
+    case MTGP_OP_DIVC: return acc / imm;
+    case MTGP_OP_RDIVC: return imm / acc;
+    case MTGP_OP_ADDV: return acc + dget<REG>(dv, slot);
+    case MTGP_OP_SUBV: return acc - dget<REG>(dv, slot);
+    case MTGP_OP_RSUBV: return dget<REG>(dv, slot) - acc;
+    case MTGP_OP_MULV: return acc * dget<REG>(dv, slot);
+    case MTGP_OP_DIVV: return acc / dget<REG>(dv, slot);
+    case MTGP_OP_RDIVV: return dget<REG>(dv, slot) / acc;
+    case MTGP_OP_ADDS: --sp; return acc + st[sp * kWave];
+    case MTGP_OP_SUBS: --sp; return acc - st[sp * kWave];
+    case MTGP_OP_RSUBS: --sp; return st[sp * kWave] - acc;
+    case MTGP_OP_MULS: --sp; return acc * st[sp * kWave];
+    case MTGP_OP_DIVS: --sp; return acc / st[sp * kWave];
+    case MTGP_OP_RDIVS: --sp; return st[sp * kWave] / acc;
+    case MTGP_OP_SIN: return mtgp_sinf(acc);
+    default: return mtgp_cosf(acc);  // MTGP_OP_COS
+  }
+}
+
+// Programs are read through the constant address space so the wave-uniform fetch is a
+// scalar s_load (K$) instead of a vector load + readfirstlane.
+typedef const __attribute__((address_space(4))) MtgpInstr* ConstInstrPtr;
+
+template <bool REG = (MTGP_V_REGDATA != 0)>
+__device__ __forceinline__ float run_prog(const MtgpInstr* code_generic, int len,
+                                          const DVec& dv, float* st) {
+  ConstInstrPtr code = (ConstInstrPtr)code_generic;
   float acc = 0.0f;
   int sp = 0;
+#if MTGP_V_PREFETCH
+  // software-pipelined scalar fetch: instruction i+1 is in flight while i executes
+  // (programs are allocated with one spare slot, so code[len] is readable)
+  uint32_t w = code[0].op;
+  float imm = code[0].imm;
   for (int i = 0; i < len; ++i) {
-    const uint32_t w = code[i].op;
-    const float imm = code[i].imm;
-    const uint32_t op = w & 0xffu;
-    const uint32_t slot = (w >> 8) & 0xffu;
-    switch (op) {
-      case MTGP_OP_LDC: acc = imm; break;
-      case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; acc = imm; break;
-      case MTGP_OP_LDV: acc = dv[slot * kWave]; break;
-      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = dv[slot * kWave]; break;
-      case MTGP_OP_ADDC: acc = acc + imm; break;
-      case MTGP_OP_SUBC: acc = acc - imm; break;
-      case MTGP_OP_RSUBC: acc = imm - acc; break;
-      case MTGP_OP_MULC: acc = acc * imm; break;
-      case MTGP_OP_DIVC: acc = acc / imm; break;
-      case MTGP_OP_RDIVC: acc = imm / acc; break;
-      case MTGP_OP_ADDV: acc = acc + dv[slot * kWave]; break;
-      case MTGP_OP_SUBV: acc = acc - dv[slot * kWave]; break;
-      case MTGP_OP_RSUBV: acc = dv[slot * kWave] - acc; break;
-      case MTGP_OP_MULV: acc = acc * dv[slot * kWave]; break;
-      case MTGP_OP_DIVV: acc = acc / dv[slot * kWave]; break;
-      case MTGP_OP_RDIVV: acc = dv[slot * kWave] / acc; break;
-      case MTGP_OP_ADDS: --sp; acc = acc + st[sp * kWave]; break;
-      case MTGP_OP_SUBS: --sp; acc = acc - st[sp * kWave]; break;
-      case MTGP_OP_RSUBS: --sp; acc = st[sp * kWave] - acc; break;
-      case MTGP_OP_MULS: --sp; acc = acc * st[sp * kWave]; break;
-      case MTGP_OP_DIVS: --sp; acc = acc / st[sp * kWave]; break;
-      case MTGP_OP_RDIVS: --sp; acc = st[sp * kWave] / acc; break;
-      case MTGP_OP_SIN: acc = mtgp_sinf(acc); break;
-      default: acc = mtgp_cosf(acc); break;  // MTGP_OP_COS
-    }
+    const uint32_t wn = code[i + 1].op;
+    const float immn = code[i + 1].imm;
+    acc = exec_instr<REG>(w, imm, acc, sp, dv, st);
+    w = wn;
+    imm = immn;
   }
+#else
+  for (int i = 0; i < len; ++i) acc = exec_instr<REG>(code[i].op, code[i].imm, acc, sp, dv, st);
+#endif
   return acc;
 }
 
@@ -100,7 +165,9 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
                                            float dx[4]) {
   const float control = mtgp_clip1(u_raw);
   const float th1 = x[0], th2 = x[1], thd1 = x[2], thd2 = x[3];
-  const float c2 = mtgp_cosf(th2), s2 = mtgp_sinf(th2), s1 = mtgp_sinf(th1);
+  float s2, c2;
+  mtgp_sincosf(th2, &s2, &c2);  // == (mtgp_sinf(th2), mtgp_cosf(th2)) bit-for-bit
+  const float s1 = mtgp_sinf(th1);
   const float d1 = ((k.d1a + k.m2 * (k.l1sq_lc2sq + k.two_l1lc2 * c2)) + 1.0f) + 1.0f;
   const float d2 = k.m2 * (k.lc2sq + k.l1lc2 * c2) + 1.0f;
   const float phi2 = k.m2lc2g * mtgp_cosf((th1 + th2) - MTGP_HALF_PI_F);
@@ -171,23 +238,10 @@ __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool i
   }
 }
 
-// wave reduction: xor butterfly == pairwise tree in lane order (mirrored by the oracle)
-__device__ __forceinline__ float wave_pairwise_sum(float v) {
-#pragma unroll
-  for (int w = 1; w < kWave; w <<= 1) v = v + __shfl_xor(v, w, kWave);
-  return v;
-}
-
-__device__ __forceinline__ void finish_individual(const KArgs& A, int p, int r, bool active, float F) {
-  const float mx = A.m.max_fitness;
-  if (A.out.rollout_fitness && active) A.out.rollout_fitness[(size_t)p * A.ro.R + r] = F;
-  float fr = active ? (mtgp_isfinite(F) ? F : mx) : 0.0f;
-  const float sum = wave_pairwise_sum(fr);
-  if ((threadIdx.x & 63) == 0) {
-    float mean = sum / (float)A.ro.R;
-    mean = mean < 0.0f ? 0.0f : (mean > mx ? mx : mean);
-    A.out.fitness[p] = mean + A.m.parsimony * (float)A.nodes[p];
-  }
+// store v at row `row` (wave-uniform element offset) + lane: keeps addresses in SGPRs
+__device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int lane, float v) {
+  float* p = arr + row;
+  p[lane] = v;
 }
 
 __device__ __forceinline__ bool save_incl(const float* ts, int k) {
@@ -196,21 +250,38 @@ __device__ __forceinline__ bool save_incl(const float* ts, int k) {
 }
 
 // --------------------------------------------------------------------------------------
-// Common kernel prologue: wave -> individual, lane -> rollout.
+// Wave layout.  A wave packs G = 64 / Rp individuals (Rp = R rounded up to a power of two):
+// lane = g * Rp + r -> individual p0 + g, rollout r.  The environment (drift, observation,
+// RK4 update, fitness) is lane-parallel and runs once for all G individuals; only the tree
+// programs differ per individual, so they run once per group under an exec mask, each with a
+// wave-uniform (scalar) instruction stream.  A half-empty wave costs as much as a full one
+// on gfx950 (measured: R=32 and R=64 take the same time), so packing is pure gain.
 struct Lane {
-  int wave, lane, p, r, rr;
+  int wave, lane, Rp, G, p0, g, r, p, rr;
   bool active;
 };
 
 __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.wave = uni(threadIdx.x >> 6);
   L.lane = threadIdx.x & 63;
-  L.p = uni(blockIdx.x * kWavesPerBlock + L.wave);
-  if (L.p >= A.P) return false;
-  L.r = L.lane;
-  L.active = L.r < A.ro.R;
+  int Rp = 1;
+  while (Rp < A.ro.R) Rp <<= 1;
+  L.Rp = uni(Rp);
+  L.G = uni(kWave / Rp);
+  L.p0 = uni((blockIdx.x * kWavesPerBlock + L.wave) * L.G);
+  if (L.p0 >= A.P) return false;
+  L.g = L.lane / L.Rp;
+  L.r = L.lane - L.g * L.Rp;
+  L.p = L.p0 + L.g;
+  L.active = (L.r < A.ro.R) && (L.p < A.P);
   L.rr = L.active ? L.r : 0;
   return true;
+}
+
+// number of groups of this wave that hold a real individual
+__device__ __forceinline__ int groups_live(const KArgs& A, const Lane& L) {
+  const int n = A.P - L.p0;
+  return uni(n < L.G ? n : L.G);
 }
 
 // RK4 stage input: stage 0 -> s, stages 1,2 -> s + h/2 k, stage 3 -> s + h k
@@ -223,6 +294,109 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 }
 
 // --------------------------------------------------------------------------------------
+// Wave-local program cache in VGPR lanes.  Every interpreted instruction would otherwise be
+// a scalar load followed by an s_waitcnt (the wave stalls ~100+ cycles per instruction, and
+// C3 has only 4 waves per SIMD to hide it).  At kernel start the wave copies the programs of
+// its G individuals into two VGPR pairs (lane j holds cache entry j and j + 64: op word and
+// imm bits) and a meta VGPR (lane m = group * n_prog + slot holds start | len << 16 | valid);
+// the interpreter then fetches with v_readlane (SGPR lane index) -- no memory round trip.
+// Programs that do not fit the 128-entry cache fall back to scalar loads.
+struct PCache {
+  uint32_t op0, op1, imm0, imm1, meta;
+};
+
+// VGPR-lane program cache: measured 15% SLOWER than scalar loads at C3 (the fetch latency is
+// hidden; the extra readlane/select work is not), so it is off by default.
+#ifndef MTGP_V_PCACHE
+#define MTGP_V_PCACHE 0
+#endif
+
+__device__ __forceinline__ PCache pcache_build(const KArgs& A, const Lane& L, int ng) {
+  PCache c;
+#if !MTGP_V_PCACHE
+  c.op0 = c.op1 = c.imm0 = c.imm1 = c.meta = 0u;
+  (void)A; (void)L; (void)ng;
+  return c;
+#endif
+  const int nm = uni(ng * A.n_prog);
+  const int lane = L.lane;
+  int len = 0;
+  if (nm <= kWave && lane < nm) len = A.plen[(size_t)L.p0 * A.n_prog + lane];
+  int incl = len;  // inclusive prefix sum over lanes
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int t = __shfl_up(incl, d, kWave);
+    if (lane >= d) incl += t;
+  }
+  const int start = incl - len;
+  const bool cached = (nm <= kWave) && (lane < nm) && (start + len <= 2 * kWave);
+  c.meta = cached ? ((uint32_t)start | ((uint32_t)len << 16) | 0x80000000u) : 0u;
+  c.op0 = c.op1 = c.imm0 = c.imm1 = 0u;
+  if (nm <= kWave) {
+    for (int m = 0; m < nm; ++m) {
+      const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)c.meta, m);
+      if (!(mm >> 31)) continue;
+      const int s0 = (int)(mm & 0xffffu), l = (int)((mm >> 16) & 0x7fffu);
+      const MtgpInstr* src = A.prog + ((size_t)L.p0 * A.n_prog + m) * A.L;
+      const int i0 = lane - s0, i1 = lane + kWave - s0;
+      if (i0 >= 0 && i0 < l) { c.op0 = src[i0].op; c.imm0 = __float_as_uint(src[i0].imm); }
+      if (i1 >= 0 && i1 < l) { c.op1 = src[i1].op; c.imm1 = __float_as_uint(src[i1].imm); }
+    }
+  }
+  return c;
+}
+
+// Program (group gi, slot) through the cache (or the scalar-load fallback).
+__device__ __forceinline__ float run_cached(const KArgs& A, const Lane& L, const PCache& c, int gi, int slot,
+                                            const DVec& dv, float* st) {
+  const int m = gi * A.n_prog + slot;
+  const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)c.meta, m);
+  if (mm >> 31) {
+    const int s0 = (int)(mm & 0xffffu), len = (int)((mm >> 16) & 0x7fffu);
+    float acc = 0.0f;
+    int sp = 0;
+    for (int i = 0; i < len; ++i) {
+      const int idx = s0 + i;
+      const uint32_t w = (uint32_t)(idx < kWave ? __builtin_amdgcn_readlane((int)c.op0, idx)
+                                                : __builtin_amdgcn_readlane((int)c.op1, idx - kWave));
+      const uint32_t ib = (uint32_t)(idx < kWave ? __builtin_amdgcn_readlane((int)c.imm0, idx)
+                                                 : __builtin_amdgcn_readlane((int)c.imm1, idx - kWave));
+      acc = exec_instr(w, __uint_as_float(ib), acc, sp, dv, st);
+    }
+    return acc;
+  }
+  const size_t pj = (size_t)(L.p0 + gi) * A.n_prog + slot;
+  return run_prog(A.prog + pj * A.L, uni(A.plen[pj]), dv, st);
+}
+
+// Run program `slot` of every live group; each lane keeps its own individual's value.
+// The program runs with the FULL exec mask (lanes of other groups compute a discarded value
+// on their own data/stack columns): inside a divergent `if` the CFG structurizer would turn
+// the uniform opcode switch into exec-masked flow blocks (~2x the scalar dispatch cost).
+__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, const PCache& c, int ng, int slot,
+                                            const DVec& dv, float* st, float dflt) {
+  float v = dflt;
+  for (int gi = 0; gi < ng; ++gi) {
+    const float t = run_cached(A, L, c, gi, slot, dv, st);
+    v = (L.g == gi) ? t : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, float F) {
+  const float mx = A.m.max_fitness;
+  if (A.out.rollout_fitness && L.active) A.out.rollout_fitness[(size_t)L.p * A.ro.R + L.r] = F;
+  float v = L.active ? (mtgp_isfinite(F) ? F : mx) : 0.0f;
+  // xor butterfly inside the group == pairwise tree in rollout order (mirrored by the oracle)
+  for (int w = 1; w < L.Rp; w <<= 1) v = v + __shfl_xor(v, w, kWave);
+  if (L.r == 0 && L.p < A.P) {
+    float mean = v / (float)A.ro.R;
+    mean = mean < 0.0f ? 0.0f : (mean > mx ? mx : mean);
+    A.out.fitness[L.p] = mean + A.m.parsimony * (float)A.nodes[L.p];
+  }
+}
+
+// --------------------------------------------------------------------------------------
 // Acrobot, dynamic symbolic policy (dynamic_evaluate.py:65-118).  NA = state_size.
 // Data slots: y 0..3 | a 4..4+NA-1 | u 4+NA | targets.  Per stage the programs run in
 // the order of _drift (dyn.py:107-118): readout (y, u folded to 0) -> drift -> f_obs ->
@@ -232,10 +406,15 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* dcol = &lds[Ln.wave][0][Ln.lane];
+  DVec dv;
+  dv.lds = dcol;
+#pragma unroll
+  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
   float* st = &lds[Ln.wave][kDMax][Ln.lane];
 
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
@@ -244,23 +423,28 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
   const size_t PR = (size_t)A.P * R;
-  const size_t unit = (size_t)p * R + r;
-  for (int t = 0; t < A.m.n_targets; ++t) dv[(uslot + 1 + t) * kWave] = A.ro.targets[rr * A.m.n_targets + t];
+  const size_t pR0 = (size_t)Ln.p0 * R;
+  const int loff = Ln.g * R + r;  // lane offset of this (individual, rollout) in a save row
+#pragma unroll
+  for (int t = 0; t < kDMax - uslot - 1; ++t)  // static slot indices keep dv.r in registers
+    if (t < A.m.n_targets) dset(dv, dcol, uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
-  // program table of this individual: q = 0 readout, 1..NA state equations, NA+1 save readout
-  const MtgpInstr* base = A.prog + (size_t)p * A.n_prog * A.L;
-  const int32_t* lens = A.plen + (size_t)p * A.n_prog;
-  // readout at save points == readout in the drift when the readout reads no y (u is
-  // zero in both): then the stage-1 u is reused (bit-identical, one tree eval saved)
-  bool same = A.m.readout_save_same > 0;
-  if (A.m.readout_save_same < 0) {
-    const int la = uni(lens[A.m.prog_readout]), lb = uni(lens[A.m.prog_readout_save]);
-    same = la == lb;
-    const MtgpInstr* pa = base + (size_t)A.m.prog_readout * A.L;
-    const MtgpInstr* pb = base + (size_t)A.m.prog_readout_save * A.L;
-    for (int i = 0; same && i < la; ++i)
-      same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
+  // groups whose save-time readout differs from the drift readout (it reads y): bit per group
+  uint64_t diff_mask = 0;
+  for (int gi = 0; gi < ng; ++gi) {
+    const size_t pj = (size_t)(Ln.p0 + gi) * A.n_prog;
+    bool same = A.m.readout_save_same > 0;
+    if (A.m.readout_save_same < 0) {
+      const int la = uni(A.plen[pj + A.m.prog_readout]), lb = uni(A.plen[pj + A.m.prog_readout_save]);
+      same = la == lb;
+      const MtgpInstr* pa = A.prog + (pj + A.m.prog_readout) * A.L;
+      const MtgpInstr* pb = A.prog + (pj + A.m.prog_readout_save) * A.L;
+      for (int i = 0; same && i < la; ++i)
+        same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
+    }
+    if (!same) diff_mask |= 1ull << gi;
   }
+  diff_mask = __builtin_amdgcn_readfirstlane(diff_mask);
 
   float x[4], a[NA], kx[4], ka[NA], ax[4], aa[NA];
 #pragma unroll
@@ -287,50 +471,50 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
     bool stop = last;
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
-      float xt[4], at[NA], y[4], u = 0.0f, us = 0.0f;
+      float xt[4], at[NA], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
 #pragma unroll
       for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
 #pragma unroll
-      for (int j = 0; j < NA; ++j) dv[(4 + j) * kWave] = at[j];
-      const int nq = (stage == 0 && is_save && !same) ? NA + 2 : NA + 1;
+      for (int j = 0; j < NA; ++j) dset(dv, dcol, 4 + j, at[j]);
+      const float u = run_groups(A, Ln, pc, ng, A.m.prog_readout, dv, st, 0.0f);
+      acro_drift(K, xt, u, kx);
+      acro_f_obs(xt, y);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) dset(dv, dcol, i, y[i]);
+      dset(dv, dcol, uslot, u);
 #pragma unroll 1
-      for (int q = 0; q < nq; ++q) {
-        const int slot = uni(q == 0 ? A.m.prog_readout : (q <= NA ? A.m.prog_state + q - 1 : A.m.prog_readout_save));
-        const float v = run_prog(base + (size_t)slot * A.L, uni(lens[slot]), dv, st);
-        if (q == 0) {
-          u = v;
-          acro_drift(K, xt, u, kx);
-          acro_f_obs(xt, y);
+      for (int q = 0; q < NA; ++q) {
+        const float v = run_groups(A, Ln, pc, ng, A.m.prog_state + q, dv, st, 0.0f);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) dv[i * kWave] = y[i];
-          dv[uslot * kWave] = u;
-        } else if (q <= NA) {
-#pragma unroll
-          for (int j = 0; j < NA; ++j) ka[j] = (q - 1 == j) ? v : ka[j];
-        } else {
-          us = v;
-        }
+        for (int j = 0; j < NA; ++j) ka[j] = (q == j) ? v : ka[j];
       }
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
-          if (same) us = u;
+          float us = u;
+          if (diff_mask != 0) {
+            for (int gi = 0; gi < ng; ++gi) {
+              if (!((diff_mask >> gi) & 1ull)) continue;
+              const float t = run_cached(A, Ln, pc, gi, A.m.prog_readout_save, dv, st);
+              us = (Ln.g == gi) ? t : us;
+            }
+          }
           if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), us, x[0], x[1]);
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) A.out.xs[((size_t)k * 4 + i) * PR + unit] = x[i];
+              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR + pR0, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) A.out.ys[((size_t)k * 4 + i) * PR + unit] = y[i];
+              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR + pR0, loff, y[i]);
             }
-            if (A.out.us) A.out.us[(size_t)k * PR + unit] = us;
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR + pR0, loff, us);
             if (A.out.acts) {
 #pragma unroll
-              for (int j = 0; j < NA; ++j) A.out.acts[((size_t)k * NA + j) * PR + unit] = a[j];
+              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR + pR0, loff, a[j]);
             }
           }
         }
@@ -363,7 +547,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
     }
   }
   if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
-  finish_individual(A, p, r, active, fit.F);
+  finish_group(A, Ln, fit.F);
 }
 
 // --------------------------------------------------------------------------------------
@@ -373,20 +557,26 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* dcol = &lds[Ln.wave][0][Ln.lane];
+  DVec dv;
+  dv.lds = dcol;
+#pragma unroll
+  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
   float* st = &lds[Ln.wave][kDMax][Ln.lane];
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
   const size_t PR = (size_t)A.P * R;
-  const size_t unit = (size_t)p * R + r;
-  for (int t = 0; t < A.m.n_targets; ++t) dv[(4 + t) * kWave] = A.ro.targets[rr * A.m.n_targets + t];
-  const MtgpInstr* c_pol = A.prog + ((size_t)p * A.n_prog + A.m.prog_readout) * A.L;
-  const int l_pol = uni(A.plen[(size_t)p * A.n_prog + A.m.prog_readout]);
+  const size_t pR0 = (size_t)Ln.p0 * R;
+  const int loff = Ln.g * R + r;
+#pragma unroll
+  for (int t = 0; t < kDMax - 4; ++t)
+    if (t < A.m.n_targets) dset(dv, dcol, 4 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   float x[4], kx[4], ax[4];
 #pragma unroll
@@ -406,8 +596,8 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
       for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
       acro_f_obs(xt, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dv[i * kWave] = y[i];
-      const float u = run_prog(c_pol, l_pol, dv, st);  // ff.py:106-107 (and :97 at saves)
+      for (int i = 0; i < 4; ++i) dset(dv, dcol, i, y[i]);
+      const float u = run_groups(A, Ln, pc, ng, A.m.prog_readout, dv, st, 0.0f);  // ff.py:106-107 (:97 at saves)
       acro_drift(K, xt, u, kx);
       if (stage == 0) {
         if (is_save) {
@@ -416,13 +606,13 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) A.out.xs[((size_t)k * 4 + i) * PR + unit] = x[i];
+              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR + pR0, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) A.out.ys[((size_t)k * 4 + i) * PR + unit] = y[i];
+              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR + pR0, loff, y[i]);
             }
-            if (A.out.us) A.out.us[(size_t)k * PR + unit] = u;
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR + pR0, loff, u);
           }
         }
         if (pending) {
@@ -447,7 +637,7 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
     }
   }
   if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
-  finish_individual(A, p, r, active, fit.F);
+  finish_group(A, Ln, fit.F);
 }
 
 // --------------------------------------------------------------------------------------
@@ -457,17 +647,21 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  const int p = Ln.p, r = Ln.r, rr = Ln.rr;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dv = &lds[Ln.wave][0][Ln.lane];
+  float* dcol = &lds[Ln.wave][0][Ln.lane];
+  DVec dv;
+  dv.lds = dcol;
+#pragma unroll
+  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
   float* st = &lds[Ln.wave][kDMax][Ln.lane];
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const size_t PR = (size_t)A.P * R;
-  const size_t unit = (size_t)p * R + r;
-  const MtgpInstr* base = A.prog + (size_t)p * A.n_prog * A.L;
-  const int32_t* lens = A.plen + (size_t)p * A.n_prog;
+  const size_t pR0 = (size_t)Ln.p0 * R;
+  const int loff = Ln.g * R + r;
   float x[NV], kx[NV], ax[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
@@ -491,7 +685,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       tot = tot + sq;
       if (TRAJ && active && A.out.xs) {
 #pragma unroll
-        for (int d = 0; d < NV; ++d) A.out.xs[((size_t)k * NV + d) * PR + unit] = x[d];
+        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR + pR0, loff, x[d]);
       }
     }
     if (pending) {
@@ -508,11 +702,10 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) dv[i * kWave] = stage_in(stage, x[i], kx[i], h, h2);
+      for (int i = 0; i < NV; ++i) dset(dv, dcol, i, stage_in(stage, x[i], kx[i], h, h2));
 #pragma unroll 1
       for (int q = 0; q < NV; ++q) {
-        const int slot = uni(A.m.prog_state + q);
-        const float v = run_prog(base + (size_t)slot * A.L, uni(lens[slot]), dv, st);
+        const float v = run_groups(A, Ln, pc, ng, A.m.prog_state + q, dv, st, 0.0f);
 #pragma unroll
         for (int j = 0; j < NV; ++j) kx[j] = (q == j) ? v : kx[j];
       }
@@ -528,7 +721,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
     }
   }
   const float F = tot / (float)S;
-  finish_individual(A, p, r, active, F);
+  finish_group(A, Ln, F);
 }
 
 // --------------------------------------------------------------------------------------
@@ -547,10 +740,12 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
   const long pj = item / chunks;
   const int m = ch * 64 + lane;
   const bool active = m < M;
-  float* dv = dyn_lds + (size_t)wave * (n_data + kSMax) * kWave + lane;
-  float* st = dv + (size_t)n_data * kWave;
-  for (int d = 0; d < n_data; ++d) dv[d * kWave] = active ? data[(size_t)m * n_data + d] : 0.0f;
-  const float v = run_prog(prog + (size_t)pj * L, uni(plen[pj]), dv, st);
+  float* dcol = dyn_lds + (size_t)wave * (n_data + kSMax) * kWave + lane;
+  float* st = dcol + (size_t)n_data * kWave;
+  for (int d = 0; d < n_data; ++d) dcol[d * kWave] = active ? data[(size_t)m * n_data + d] : 0.0f;
+  DVec dv;
+  dv.lds = dcol;
+  const float v = run_prog<false>(prog + (size_t)pj * L, uni(plen[pj]), dv, st);
   if (active) out[(size_t)pj * M + m] = v;
 }
 
@@ -574,7 +769,7 @@ __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, i
   mtgp::RowInfo* info = &info_all[t_in * NMAX];
   MtgpInstr* out = prog_out + ((size_t)p * n_prog + j) * L;
   int need = 0;
-  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
+  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L - 1, info, &need);
   len_out[(size_t)p * n_prog + j] = n > 0 ? n : 0;
   status_out[(size_t)p * n_prog + j] = n > 0 ? 0 : -n;
   if (j == 0) {
@@ -689,7 +884,11 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
   A.ro = *rollouts;
   A.out = *out;
   hipStream_t s = (hipStream_t)stream;
-  const dim3 grid((unsigned)((P + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
+  int Rp = 1;
+  while (Rp < rollouts->R) Rp <<= 1;
+  const int G = kWave / Rp;  // individuals packed per wave
+  const long waves = ((long)P + G - 1) / G;
+  const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
   if (model->model == MTGP_MODEL_ACROBOT_DYNAMIC) {
     if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;

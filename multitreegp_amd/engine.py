@@ -44,12 +44,13 @@ class Flattened:
 class DeviceEngine:
     """Binds one fitness-function config + node library to the HIP kernels."""
 
-    def __init__(self, fitness_function, library: NodeLibrary, size_parsinomy: float = 0.0, device=None):
+    def __init__(self, fitness_function, library: NodeLibrary, size_parsinomy: float = 0.0, device=None,
+                 native=None):
         self.ff = fitness_function
         self.lib = library
         self.parsimony = float(size_parsinomy)
         self.device = _require_gpu(device)
-        self.native = nat.load()
+        self.native = native if native is not None else nat.load()
         self._node_lib = library.native()
         self._data_key = None
         self._data = None
@@ -119,7 +120,7 @@ class DeviceEngine:
     def check_status(fl: Flattened):
         worst = int(fl.status.max().item()) if fl.status.numel() else 0
         if worst == nat.ERR_PROG_TOO_LONG:
-            raise ValueError("a tree flattens to more than 2*max_nodes+8 instructions (shared sub-DAGs?)")
+            raise ValueError("a tree flattens to more than 2*max_nodes+7 instructions (shared sub-DAGs?)")
         if worst == nat.ERR_STACK:
             raise ValueError(f"a tree needs more than {nat.STACK_MAX} operand-stack slots")
         if worst != 0:

@@ -1,0 +1,28 @@
+#!/usr/bin/env python3
+"""Kernel-only driver for rocprofv3 PMC passes: C3 workload, N evaluations."""
+import argparse
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from multitreegp_amd import _native as nat  # noqa: E402
+from multitreegp_amd.engine import DeviceEngine  # noqa: E402
+import bench  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--iters", type=int, default=2)
+ap.add_argument("--pop", type=int, default=8192)
+ap.add_argument("--rollouts", type=int, default=32)
+ap.add_argument("--no-traj", action="store_true")
+ap.add_argument("--lib", default=nat.LIB_PATH)
+a = ap.parse_args()
+env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=200), 0)
+eng = DeviceEngine(ff, lib, 0.0, "cuda:0", native=nat.load(a.lib))
+pd = torch.from_numpy(pop).cuda()
+for _ in range(a.iters):
+    eng.evaluate(pd, data, trajectories=not a.no_traj)
+torch.cuda.synchronize()
+print("done")

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B timing of kernel variants (multitreegp_amd/lib/variants/*.so) on one workload,
+interleaved rounds in ONE process (cdna_hip_programming.md §5.4 rule 24)."""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+from multitreegp_amd import _native as nat  # noqa: E402
+from multitreegp_amd.engine import DeviceEngine  # noqa: E402
+import bench  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="base")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--pop", type=int, default=8192)
+    ap.add_argument("--rollouts", type=int, default=32)
+    ap.add_argument("--ode-steps", type=int, default=200)
+    ap.add_argument("--no-traj", action="store_true")
+    ap.add_argument("--tag", default="")
+    a = ap.parse_args()
+    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps)
+    env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
+    dev = torch.device("cuda", 0)
+    engines = {}
+    for v in a.variants.split(","):
+        path = nat.LIB_PATH if v == "prod" else os.path.join(ROOT, "multitreegp_amd", "lib", "variants",
+                                                             f"libmtgp_hip_{v}.so")
+        engines[v] = DeviceEngine(ff, lib, 0.0, dev, native=nat.load(path))
+    pop_dev = torch.from_numpy(pop).to(dev)
+    first = next(iter(engines.values()))
+    fl = first.flatten(pop_dev)
+    first.check_status(fl)
+    ref = None
+    times = {v: [] for v in engines}
+    for r in range(a.rounds + 1):
+        for v, eng in engines.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=fl, check=False)
+            e1.record()
+            torch.cuda.synchronize()
+            f = res["fitness"].cpu().numpy()
+            if ref is None:
+                ref = f
+            same = bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32)))
+            if r > 0:
+                times[v].append(e0.elapsed_time(e1))
+            if not same:
+                print(f"WARNING variant {v} fitness differs from first variant", flush=True)
+    units = a.pop * a.rollouts * a.ode_steps
+    for v, t in times.items():
+        print(json.dumps({"tag": a.tag, "variant": v, "pop": a.pop, "R": a.rollouts, "traj": not a.no_traj,
+                          "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                          "Gsteps_per_s": units / (np.median(t) / 1e3) / 1e9}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
