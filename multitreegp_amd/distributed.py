@@ -36,7 +36,12 @@ def gather_fitness(local: torch.Tensor, P: int, per: int, group=None) -> torch.T
     buf = torch.full((per,), float("inf"), dtype=local.dtype, device=local.device)
     buf[: local.numel()] = local
     out = torch.empty((per * ws,), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, buf, group=group)
+    if dist.get_backend(group) == "gloo":  # CPU test path: gloo has no all_gather_into_tensor
+        parts = list(out.chunk(ws))
+        dist.all_gather(parts, buf, group=group)
+        out = torch.cat(parts)
+    else:
+        dist.all_gather_into_tensor(out, buf, group=group)
     return out[:P]
 
 

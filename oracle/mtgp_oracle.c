@@ -417,3 +417,16 @@ void oracle_sincos(const float* x, float* s, float* c, long n) {
 void oracle_wrap(const float* x, float* o, long n) {
   for (long i = 0; i < n; ++i) o[i] = mtgp_wrap_angle(x[i]);
 }
+
+/* unit-test hooks: Acrobot pieces in isolation */
+void oracle_acro_drift(const float* params4, const float* state4, float u, float* out4) {
+  OrCtx c;
+  memset(&c, 0, sizeof(c));
+  c.l1 = params4[0]; c.l2 = params4[1]; c.m1 = params4[2]; c.m2 = params4[3];
+  acro_drift(&c, state4, u, out4);
+}
+void oracle_acro_f_obs(const float* x4, float* y4) { acro_f_obs(x4, y4); }
+float oracle_acro_fitness(const float* xs, const float* us, const float* ts, int S) {
+  return acro_fitness(xs, us, ts, S);
+}
+float oracle_pairwise_sum(const float* v, int R) { return pairwise_sum(v, R); }

@@ -52,6 +52,12 @@ def lib():
         L.oracle_eval.restype = ctypes.c_int
         L.oracle_sincos.argtypes = [vp, vp, vp, ctypes.c_long]
         L.oracle_wrap.argtypes = [vp, vp, ctypes.c_long]
+        L.oracle_acro_drift.argtypes = [vp, vp, ctypes.c_float, vp]
+        L.oracle_acro_f_obs.argtypes = [vp, vp]
+        L.oracle_acro_fitness.argtypes = [vp, vp, vp, ctypes.c_int]
+        L.oracle_acro_fitness.restype = ctypes.c_float
+        L.oracle_pairwise_sum.argtypes = [vp, ctypes.c_int]
+        L.oracle_pairwise_sum.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -129,3 +135,30 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
     if rc != 0:
         raise RuntimeError(f"oracle_eval failed {rc}")
     return out
+
+
+def acro_drift(params4, state4, u):
+    p = np.ascontiguousarray(params4, np.float32)
+    x = np.ascontiguousarray(state4, np.float32)
+    o = np.empty(4, np.float32)
+    lib().oracle_acro_drift(_p(p), _p(x), ctypes.c_float(u), _p(o))
+    return o
+
+
+def acro_f_obs(x4):
+    x = np.ascontiguousarray(x4, np.float32)
+    o = np.empty(4, np.float32)
+    lib().oracle_acro_f_obs(_p(x), _p(o))
+    return o
+
+
+def acro_fitness(xs, us, ts):
+    xs = np.ascontiguousarray(xs, np.float32)
+    us = np.ascontiguousarray(us, np.float32).reshape(-1)
+    ts = np.ascontiguousarray(ts, np.float32)
+    return np.float32(lib().oracle_acro_fitness(_p(xs), _p(us), _p(ts), ts.shape[0]))
+
+
+def pairwise_sum(v):
+    v = np.ascontiguousarray(v, np.float32)
+    return np.float32(lib().oracle_pairwise_sum(_p(v), v.shape[0]))

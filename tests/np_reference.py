@@ -1,0 +1,93 @@
+"""Independent float64 numpy restatement of the reference hot path (test helper).
+
+Written directly from the reference source text, sharing no code with oracle/mtgp_oracle.c or
+the product: row-order tree interpretation (gp.py:356-388), Acrobot observation/drift
+(control_environment_base.py:43-48, acrobot.py:29-72), the dynamic / feedforward / SR drifts
+(dynamic_evaluate.py:107-118, feedforward_evaluate.py:104-110, SR_evaluator.py:85-88) and a
+textbook RK4.  float64 + numpy's libm sin/cos, so agreement with the fp32 oracle is to a
+tolerance, which pins the oracle's SEMANTICS (layouts, operand order, zero slots, wraps)."""
+import numpy as np
+
+
+def eval_tree(tree, lib, data):
+    tree = np.asarray(tree, np.float64)
+    N = tree.shape[0]
+    val = tree[:, 3].copy()
+
+    def idx(v):
+        j = int(v) if np.isfinite(v) else 0
+        if j < 0:
+            j += N
+        return min(max(j, 0), N - 1)
+
+    with np.errstate(all="ignore"):
+        for i in range(N):
+            f, a, b, c = tree[i]
+            x, y = val[idx(a)], val[idx(b)]
+            if f == 1:
+                v = c
+            else:
+                k = min(max(int(f), 0), lib.n_funcs - 1)
+                name = lib.node_to_string.get(k)
+                if k < 2:
+                    v = 0.0
+                elif k >= lib.var_start:
+                    v = data[min(k - lib.var_start, len(data) - 1)]
+                else:
+                    v = {"+": lambda: x + y, "-": lambda: x - y, "*": lambda: x * y, "/": lambda: x / y,
+                         "sin": lambda: np.sin(x), "cos": lambda: np.cos(x)}[name]()
+            val[i] = v
+    return val[N - 1]
+
+
+def acro_f_obs(x):
+    y = np.array(x, np.float64)  # C = I, no noise
+    y[0] = np.remainder(y[0] + np.pi, 2 * np.pi) - np.pi
+    y[1] = np.remainder(y[1] + np.pi, 2 * np.pi) - np.pi
+    return y
+
+
+def acro_drift(x, u, l1=1.0, l2=1.0, m1=1.0, m2=1.0):
+    control = np.clip(u, -1, 1)
+    t1, t2, td1, td2 = x
+    lc1, lc2, moi1, moi2, g = 0.5 * l1, 0.5 * l2, 1.0, 1.0, 9.81
+    d1 = m1 * lc1 ** 2 + m2 * (l1 ** 2 + lc2 ** 2 + 2 * l1 * lc2 * np.cos(t2)) + moi1 + moi2
+    d2 = m2 * (lc2 ** 2 + l1 * lc2 * np.cos(t2)) + moi2
+    phi2 = m2 * lc2 * g * np.cos(t1 + t2 - np.pi / 2)
+    phi1 = -m2 * l1 * lc2 * td2 ** 2 * np.sin(t2) - 2 * m2 * l1 * lc2 * td1 * td2 * np.sin(t1) \
+        + (m1 * lc1 + m2 * l1) * g * np.cos(t1 - np.pi / 2) + phi2
+    a2 = (control + d2 / d1 * phi1 - m2 * l1 * lc2 * td1 ** 2 * np.sin(t2) - phi2) / (m2 * lc2 ** 2 + moi2 - d2 ** 2 / d1)
+    a1 = -(d2 * a2 + phi1) / d1
+    return np.array([td1, td2, a1, a2])
+
+
+def dyn_rhs(cand, lib, s, state_size, params=(1, 1, 1, 1)):
+    x, a = s[:4], s[4:]
+    y = acro_f_obs(x)
+    u = eval_tree(cand[state_size], lib, np.concatenate([np.zeros(4), a, np.zeros(1)]))
+    dx = acro_drift(x, u, *params)
+    d = np.concatenate([y, a, [u]])
+    da = [eval_tree(cand[i], lib, d) for i in range(state_size)]
+    return np.concatenate([dx, da])
+
+
+def ff_rhs(cand, lib, s, params=(1, 1, 1, 1)):
+    return acro_drift(s, eval_tree(cand[0], lib, acro_f_obs(s)), *params)
+
+
+def sr_rhs(cand, lib, s):
+    return np.array([eval_tree(cand[i], lib, s) for i in range(len(s))])
+
+
+def rk4(rhs, s0, h, n):
+    s = np.array(s0, np.float64)
+    out = [s.copy()]
+    with np.errstate(all="ignore"):
+        for _ in range(n):
+            k1 = rhs(s)
+            k2 = rhs(s + 0.5 * h * k1)
+            k3 = rhs(s + 0.5 * h * k2)
+            k4 = rhs(s + h * k3)
+            s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+            out.append(s.copy())
+    return np.array(out)

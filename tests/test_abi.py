@@ -1,0 +1,58 @@
+"""The C ABI library: loads without a GPU, exports every declared symbol, struct layouts match."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+
+from multitreegp_amd import _native as nat
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HDR = os.path.join(ROOT, "include", "mtgp.h")
+
+
+def test_declared_symbols_exported():
+    text = open(HDR).read()
+    declared = set(re.findall(r"^\s*(?:int|float)\s+(mtgp_\w+)\s*\(", text, re.M))
+    assert declared == set(nat.EXPORTED_SYMBOLS)
+    lib = nat.load()
+    for sym in declared:
+        assert hasattr(lib, sym)
+    assert lib.mtgp_abi_version() == 1
+
+
+def test_struct_layouts_match_header(tmp_path):
+    src = tmp_path / "sz.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mtgp.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
+                   'sizeof(MtgpNodeLibrary), sizeof(MtgpProgramSpec), sizeof(MtgpInstr), sizeof(MtgpModel),'
+                   'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
+    want = [ctypes.sizeof(t) for t in (nat.MtgpNodeLibrary, nat.MtgpProgramSpec, nat.MtgpInstr, nat.MtgpModel,
+                                       nat.MtgpRollouts, nat.MtgpOutputs)] + [nat.MtgpModel.readout_save_same.offset]
+    assert got == want
+
+
+def test_argument_validation_without_gpu():
+    """Bad arguments are rejected before any device call (no GPU needed)."""
+    lib = nat.load()
+    nl = nat.MtgpNodeLibrary()
+    assert lib.mtgp_flatten(None, 1, 1, 1, ctypes.byref(nl), None, 1, 8, None, None, None, None, None) == nat.ERR_ARG
+    m = nat.MtgpModel()
+    ro = nat.MtgpRollouts()
+    out = nat.MtgpOutputs()
+    assert lib.mtgp_eval_rk4(ctypes.byref(m), None, None, 1, 1, None, 1, ctypes.byref(ro), ctypes.byref(out),
+                             None) == nat.ERR_ARG
+    one = np.zeros(4, np.int32)
+    m.n_steps, m.save_every, m.n_save = 10, 3, 4  # n_steps not a multiple of save_every
+    ro.R = 4
+    out.fitness = one.ctypes.data
+    assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 1, one.ctypes.data, 1,
+                             ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
+    ro.R = 65  # more than one wave of rollouts per individual
+    m.save_every = 2
+    m.n_save = 6
+    assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 1, one.ctypes.data, 1,
+                             ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG

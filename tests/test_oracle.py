@@ -1,0 +1,243 @@
+"""Pinning the CPU oracle (the reference itself cannot run here: JAX/diffrax are absent).
+
+* an independent float64 numpy restatement (tests/np_reference.py) -> semantics;
+* sympy evaluation of the reference's own printer output (gp.py:310-328) -> tree semantics;
+* analytic known answers: RK4 on a linear system is an exact matrix polynomial;
+* hand-built fitness cases for acrobot.py:77-84 (first success, float mask, penalty);
+* event termination -> +inf fill, NaN observations (diffrax SaveAt semantics)."""
+import numpy as np
+import pytest
+import sympy
+
+import multitreegp_amd as mt
+import np_reference as npr
+from oracle import oracle as orc
+from helpers import CONTROL_OPS, SR_OPS, dynamic_setup, oracle_model, oracle_rollouts, sr_setup, static_setup
+from multitreegp_amd.sampling import sample_population
+
+
+def _expr(tree, lib):
+    """tree_to_string (gp.py:310-328) with full-precision coefficients."""
+    if tree[-1, 0] == 1:
+        return repr(float(tree[-1, 3]))
+    if tree[-1, 1] < 0:
+        return lib.node_to_string[int(tree[-1, 0])]
+    if tree[-1, 2] < 0:
+        return f"{lib.node_to_string[int(tree[-1, 0])]}({_expr(tree[: int(tree[-1, 1]) + 1], lib)})"
+    a = _expr(tree[: int(tree[-1, 1]) + 1], lib)
+    b = _expr(tree[: int(tree[-1, 2]) + 1], lib)
+    return f"({a}){lib.node_to_string[int(tree[-1, 0])]}({b})"
+
+
+def test_interpreter_vs_sympy_of_reference_printer():
+    lib = mt.NodeLibrary(SR_OPS + [("sin", None, 1), ("cos", None, 1)], [["x0", "x1", "x2"]], [3])
+    pop = sample_population(5, lib, 80, 1, max_init_depth=5, max_nodes=30)[0]
+    syms = sympy.symbols("x0 x1 x2")
+    rng = np.random.default_rng(0)
+    checked = 0
+    for cand in pop:
+        for tree in cand:
+            f = sympy.lambdify(syms, sympy.sympify(_expr(tree, lib), evaluate=False), "numpy")
+            for _ in range(3):
+                d = rng.uniform(-2, 2, 3).astype(np.float32)
+                with np.errstate(all="ignore"):
+                    want = float(f(*d.astype(np.float64)))
+                got = float(orc.eval_tree(tree, lib.fn_codes, lib.n_funcs, lib.var_start, d))
+                if not np.isfinite(want) or abs(want) > 1e4:
+                    continue
+                assert abs(got - want) <= 1e-3 * max(1.0, abs(want)), (_expr(tree, lib), d, got, want)
+                checked += 1
+    assert checked > 300
+
+
+def test_interpreter_vs_float64_restatement_on_garbage_arrays():
+    lib = mt.NodeLibrary(SR_OPS + [("sin", None, 1), ("cos", None, 1)], [["x0", "x1", "x2"]], [3])
+    rng = np.random.default_rng(1)
+    for _ in range(400):
+        N = int(rng.integers(1, 16))
+        t = np.empty((N, 4), np.float32)
+        t[:, 0] = rng.integers(-1, lib.n_funcs + 2, N)
+        t[:, 1] = rng.integers(-N - 2, N + 2, N)
+        t[:, 2] = rng.integers(-N - 2, N + 2, N)
+        t[:, 3] = rng.uniform(-2, 2, N)
+        d = rng.uniform(-2, 2, 3).astype(np.float32)
+        want = npr.eval_tree(t, lib, d.astype(np.float64))
+        got = float(orc.eval_tree(t, lib.fn_codes, lib.n_funcs, lib.var_start, d))
+        if not np.isfinite(want) or abs(want) > 1e5:
+            continue
+        assert abs(got - want) <= 2e-3 * max(1.0, abs(want))
+
+
+def test_acrobot_drift_and_obs_vs_float64():
+    rng = np.random.default_rng(2)
+    for _ in range(500):
+        x = rng.uniform(-4, 4, 4).astype(np.float32)
+        u = np.float32(rng.uniform(-2, 2))
+        prm = rng.uniform(0.5, 1.5, 4).astype(np.float32)
+        got = orc.acro_drift(prm, x, u)
+        want = npr.acro_drift(x.astype(np.float64), float(u), *prm.astype(np.float64))
+        np.testing.assert_allclose(got, want, rtol=2e-4, atol=2e-4)
+        np.testing.assert_allclose(orc.acro_f_obs(x), npr.acro_f_obs(x), rtol=1e-6, atol=2e-6)
+    # C @ x propagates NaN from a non-finite component into every other observation
+    y = orc.acro_f_obs(np.array([np.inf, 0.5, 0.1, 0.2], np.float32))
+    assert np.isnan(y).all()
+    y = orc.acro_f_obs(np.array([0.5, 0.5, np.inf, 0.2], np.float32))
+    assert np.isnan(y[[0, 1, 3]]).all() and np.isinf(y[2])
+
+
+def test_rk4_linear_system_known_answer():
+    """dx0 = x1, dx1 = -x0 (trees [x1, -x0]): one RK4 step is exactly the matrix polynomial
+    I + hA + (hA)^2/2 + (hA)^3/6 + (hA)^4/24; the trajectory is its powers applied to x0."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    N = 4
+    cand = np.zeros((1, 2, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 1] = [lib.string_to_node["x1"], -1, -1, 0]
+    cand[0, 1, N - 3] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 1, N - 2] = [1, -1, -1, 0.0]                              # coefficient 0
+    cand[0, 1, N - 1] = [lib.string_to_node["-"], N - 2, N - 3, 0]   # 0 - x0
+    h, n, R = 0.05, 400, 3
+    x0 = np.array([[1.0, 0.0], [0.3, -0.7], [-2.0, 1.5]], np.float32)
+    ts = (np.arange(n + 1) * np.float32(h)).astype(np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=n, save_every=1,
+                 n_save=n + 1, h=h, max_fitness=1e5, parsimony=0.0)
+    ys = np.zeros((R, n + 1, 2), np.float32)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=ys), trajectories=True)
+    A = np.array([[0.0, 1.0], [-1.0, 0.0]])
+    hA = h * A
+    M = np.eye(2) + hA + hA @ hA / 2 + hA @ hA @ hA / 6 + hA @ hA @ hA @ hA / 24
+    want = np.zeros((R, n + 1, 2))
+    for r in range(R):
+        s = x0[r].astype(np.float64)
+        for k in range(n + 1):
+            want[r, k] = s
+            s = M @ s
+    np.testing.assert_allclose(out["xs"][0], want, rtol=0, atol=5e-5)
+    # and the analytic solution within RK4's global error O(h^4)
+    t = ts.astype(np.float64)
+    exact = np.stack([x0[:, :1] * np.cos(t) + x0[:, 1:] * np.sin(t), -x0[:, :1] * np.sin(t) + x0[:, 1:] * np.cos(t)], -1)
+    np.testing.assert_allclose(out["xs"][0], exact, atol=2e-4)
+    # MSE fitness against zeros = mean_t sum_d x^2 (energy is ~conserved)
+    e = (x0.astype(np.float64) ** 2).sum(1)
+    np.testing.assert_allclose(out["rollout_fitness"][0], e, rtol=1e-3)
+
+
+def _acro_fitness_np(xs, us, ts):
+    """acrobot.py:77-84 literally, in float32 numpy."""
+    xs, us, ts = np.float32(xs), np.float32(us).reshape(-1, 1), np.float32(ts)
+    with np.errstate(all="ignore"):
+        reached = (-np.cos(xs[:, 0]) - np.cos(xs[:, 0] + xs[:, 1])) > 1.5
+    fs = int(np.argmax(reached))
+    cost = (us[:, 0] * np.float32(0.01)) * us[:, 0]
+    ratio = ts / (ts[1] - ts[0])
+    costs = np.where(ratio > np.float32(fs), np.float32(0), cost)
+    return np.float32(fs + (fs == 0) * ts.shape[0]) + np.float32(np.sum(costs, dtype=np.float32))
+
+
+@pytest.mark.parametrize("case", ["success7", "never", "at0", "nan_before", "nan_after", "inf_tail"])
+def test_acrobot_fitness_cases(case):
+    S = 40
+    ts = (np.arange(S, dtype=np.float32) * np.float32(0.2)).astype(np.float32)
+    rng = np.random.default_rng(4)
+    xs = rng.uniform(-0.3, 0.3, (S, 4)).astype(np.float32)
+    us = rng.uniform(-2, 2, S).astype(np.float32)
+    up = np.array([np.pi, 0, 0, 0], np.float32)  # -cos(pi) - cos(pi) = 2 > 1.5
+    if case == "success7":
+        xs[7] = up
+        xs[20] = up
+    elif case == "at0":
+        xs[0] = up
+        xs[9] = up
+    elif case == "nan_before":
+        xs[12] = up
+        us[3] = np.nan
+    elif case == "nan_after":
+        xs[12] = up
+        us[30] = np.nan
+    elif case == "inf_tail":
+        xs[25:] = np.inf
+        us[25:] = np.nan
+    got = orc.acro_fitness(xs, us, ts)
+    want = _acro_fitness_np(xs, us, ts)
+    if np.isnan(want):
+        assert np.isnan(got)
+    else:
+        assert abs(float(got) - float(want)) <= 1e-5 * abs(float(want)), (got, want)
+    if case == "success7":
+        assert 7 < got < 8 + 0.5
+    if case in ("never", "at0", "inf_tail"):
+        assert got >= S
+
+
+@pytest.mark.parametrize("setup", ["dynamic", "static", "sr"])
+def test_oracle_vs_float64_short_horizon(setup):
+    """Full evaluator semantics (data layout, zero slots, readout/state order, RK4, saving)."""
+    if setup == "dynamic":
+        env, lib, ff, data, pop = dynamic_setup(P=12, R=3, n_steps=20)
+    elif setup == "static":
+        env, lib, ff, data, pop = static_setup(P=12, R=3, n_steps=20)
+    else:
+        env, lib, ff, data, pop = sr_setup(P=12, R=3, n_save=6, save_every=4)
+    d = ff.prepare(data)
+    out = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    compared = tight = 0
+    for p in range(pop.shape[0]):
+        for r in range(d["R"]):
+            x0 = d["x0"][r].astype(np.float64)
+            if setup == "dynamic":
+                traj = npr.rk4(lambda s: npr.dyn_rhs(pop[p], lib, s, 2), np.concatenate([x0, [0, 0]]), 0.05, 20)
+                got = np.concatenate([out["xs"][p, r], out["acts"][p, r]], -1)
+            elif setup == "static":
+                traj = npr.rk4(lambda s: npr.ff_rhs(pop[p], lib, s), x0, 0.05, 20)
+                got = out["xs"][p, r]
+            else:
+                traj = npr.rk4(lambda s: npr.sr_rhs(pop[p], lib, s), x0, 0.05, 20)[::4]
+                got = out["xs"][p, r]
+            ok = np.all(np.isfinite(traj)) and np.all(np.abs(traj) < 1e3) and np.all(np.isfinite(got))
+            if not ok:
+                continue
+            # fp32 vs fp64: trees with poles (x / (x0 + c)) amplify rounding near the pole,
+            # so require agreement for the large majority rather than for every rollout
+            tight += bool(np.allclose(got, traj, rtol=2e-3, atol=2e-3))
+            compared += 1
+    assert compared >= 10 and tight >= 0.9 * compared
+
+
+def test_event_termination_fills_inf():
+    """da = 1 + a*a blows up like tan(t): the event fires, later saves are +inf, observations NaN."""
+    env, lib, ff, data, _ = dynamic_setup(P=1, R=2, n_steps=60)
+    N = 8
+    cand = np.zeros((1, 3, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    a1 = lib.string_to_node["a1"]
+    # tree 0: 1 + a1*a1 ; rows: a1, a1, *, coef, +
+    cand[0, 0, 3] = [a1, -1, -1, 0]
+    cand[0, 0, 4] = [a1, -1, -1, 0]
+    cand[0, 0, 5] = [lib.string_to_node["*"], 4, 3, 0]
+    cand[0, 0, 6] = [1, -1, -1, 1.0]
+    cand[0, 0, 7] = [lib.string_to_node["+"], 6, 5, 0]
+    cand[0, 1, 7] = [1, -1, -1, 0.0]
+    cand[0, 2, 7] = [1, -1, -1, 0.3]
+    d = ff.prepare(data)
+    out = orc.evaluate(oracle_model(ff, d), cand, lib, oracle_rollouts(d), trajectories=True)
+    acts = out["acts"][0, 0, :, 0]
+    xs = out["xs"][0, 0]
+    k_fill = int(np.argmax(np.all(np.isinf(xs) & (xs > 0), axis=1)))  # first +inf save point
+    assert 25 < k_fill < 45
+    assert not np.isfinite(acts[k_fill - 1]) and np.all(np.isfinite(xs[:k_fill]))  # event state saved
+    assert np.all(np.isinf(xs[k_fill:])) and np.all(np.isinf(acts[k_fill:]))
+    assert np.all(np.isnan(out["ys"][0, 0, k_fill:]))
+
+
+def test_pairwise_sum_and_postprocessing():
+    v = np.arange(1, 33, dtype=np.float32)
+    assert orc.pairwise_sum(v) == v.sum()
+    env, lib, ff, data, pop = static_setup(P=6, R=5, n_steps=10)
+    d = ff.prepare(data)
+    out = orc.evaluate(oracle_model(ff, d, parsimony=0.5), pop, lib, oracle_rollouts(d))
+    for p in range(6):
+        fr = out["rollout_fitness"][p]
+        fr = np.where(np.isfinite(fr), fr, np.float32(1e4))
+        mean = np.clip(orc.pairwise_sum(fr) / np.float32(5), 0, 1e4)
+        cnt = int((pop[p, :, :, 0] != 0).sum())
+        assert out["fitness"][p] == np.float32(mean + np.float32(0.5) * np.float32(cnt))
