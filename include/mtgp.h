@@ -30,12 +30,13 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 1
+#define MTGP_ABI_VERSION 2
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
 #define MTGP_MAX_NODES 256   /* max_nodes N per tree (gp.py:69)                */
 #define MTGP_MAX_DATA 64     /* data-vector length D seen by a tree            */
+#define MTGP_MAX_PROGRAMS 64 /* programs per individual (mtgp_schedule weights) */
 #define MTGP_STACK_MAX 8     /* operand-stack slots per lane (Sethi-Ullman)    */
 
 /* ---------------------------------------------------------------- errors */
@@ -78,7 +79,25 @@ typedef struct {
 
 /* ------------------------------------------------------------ program format */
 /* Accumulator machine, postorder with leaves folded into their parent.
- * word op: bits 0-7 opcode, bits 8-15 data slot.  imm: f32 constant. */
+ * word op: bits 0-7 opcode, bits 8-15 data slot, and the opcode pre-decoded for the
+ * branch-free (SIMT) interpreter: bit 16 push acc first, bits 17-18 operand source
+ * (MTGP_SRC_*), bits 19-21 ALU operation (MTGP_ALU_*), bit 22 cos (for MTGP_ALU_UNARY),
+ * bit 23 pop (== source MTGP_SRC_STACK).
+ * imm: f32 constant.
+ * Program stride L (instructions per program slot) must be a multiple of 4 for the
+ * evaluators: they fetch instructions in blocks of four (one 32-byte scalar load). */
+enum { MTGP_SRC_IMM = 0, MTGP_SRC_VAR = 1, MTGP_SRC_STACK = 2, MTGP_SRC_ACC = 3 };
+enum {
+  MTGP_ALU_LOAD = 0, MTGP_ALU_ADD = 1, MTGP_ALU_SUB = 2, MTGP_ALU_RSUB = 3, MTGP_ALU_MUL = 4,
+  MTGP_ALU_DIV = 5, MTGP_ALU_RDIV = 6, MTGP_ALU_UNARY = 7
+};
+#define MTGP_W_PUSH (1u << 16)
+#define MTGP_W_SRC_SHIFT 17
+#define MTGP_W_ALU_SHIFT 19
+#define MTGP_W_COS (1u << 22)
+#define MTGP_W_POP (1u << 23)
+/* no-op padding word: acc = acc (src ACC, ALU LOAD) */
+#define MTGP_W_NOP ((uint32_t)MTGP_SRC_ACC << MTGP_W_SRC_SHIFT)
 enum {
   MTGP_OP_LDC = 0, MTGP_OP_LDCP, MTGP_OP_LDV, MTGP_OP_LDVP, /* P = push acc first */
   MTGP_OP_ADDC, MTGP_OP_SUBC, MTGP_OP_RSUBC, MTGP_OP_MULC, MTGP_OP_DIVC, MTGP_OP_RDIVC,
@@ -126,6 +145,10 @@ typedef struct {
   const float* ts;      /* [n_save] save times (fitness mask acrobot.py:82)  */
   const float* ys_true; /* SR: [n_save, n_var, R] ground truth, time-major   */
   int32_t R;
+  const int32_t* order; /* optional [P] evaluation schedule: a permutation of  */
+                        /* [0, P) from mtgp_schedule (NULL = identity).  Only   */
+                        /* which individuals share a wave changes; results are  */
+                        /* bit-identical and stay indexed by individual.        */
 } MtgpRollouts;
 
 /* Outputs.  Trajectories are time-major structure-of-arrays so that every save point
@@ -162,6 +185,20 @@ int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* 
 int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L,
                        int32_t P, const float* data, int32_t M, int32_t n_data, float* out,
                        void* stream);
+
+/* Evaluation schedule (load balance).  A wave packs G = 64 / pow2ceil(R) individuals and
+ * interprets their programs one after another, so its cost follows the sum of their program
+ * lengths; all waves are resident at once, so the kernel takes as long as its slowest SIMD.
+ * mtgp_schedule sorts individuals by cost = sum_j weights[j] * plen[p, j] (counting sort,
+ * costs clamped to MTGP_SCHED_BINS - 1) and writes order_out[P] pairing the most expensive
+ * with the cheapest (G >= 2), or most expensive first (G == 1).  weights: host array
+ * [n_prog] (e.g. how often each program runs per step).  scratch: device int32
+ * [MTGP_SCHED_SCRATCH].  Ties are ordered arbitrarily; results do not depend on the order.
+ * (No reference counterpart: this is GPU scheduling.) */
+#define MTGP_SCHED_BINS 4096
+#define MTGP_SCHED_SCRATCH (2 * MTGP_SCHED_BINS)
+int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t* weights, int32_t R,
+                  int32_t* order_out, int32_t* scratch, void* stream);
 
 /* Integrate every (individual, rollout) with fixed-step RK4 and reduce fitness. */
 int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,

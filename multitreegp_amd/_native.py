@@ -19,6 +19,10 @@ MAX_FUNCS = 128
 MAX_NODES = 256
 MAX_DATA = 64
 STACK_MAX = 8
+MAX_PROGRAMS = 64
+SCHED_BINS = 4096
+SCHED_SCRATCH = 2 * SCHED_BINS
+ABI_VERSION = 2
 
 OK = 0
 ERR_ARG = -1
@@ -68,7 +72,8 @@ class MtgpModel(ctypes.Structure):
 
 class MtgpRollouts(ctypes.Structure):
     _fields_ = [("x0", ctypes.c_void_p), ("params", ctypes.c_void_p), ("targets", ctypes.c_void_p),
-                ("ts", ctypes.c_void_p), ("ys_true", ctypes.c_void_p), ("R", ctypes.c_int32)]
+                ("ts", ctypes.c_void_p), ("ys_true", ctypes.c_void_p), ("R", ctypes.c_int32),
+                ("order", ctypes.c_void_p)]
 
 
 class MtgpOutputs(ctypes.Structure):
@@ -84,6 +89,7 @@ EXPORTED_SYMBOLS = (
     "mtgp_flatten_tree_host",
     "mtgp_eval_programs",
     "mtgp_eval_rk4",
+    "mtgp_schedule",
     "mtgp_last_kernel_ms",
     "mtgp_set_timing",
 )
@@ -118,10 +124,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     lib.mtgp_eval_rk4.argtypes = [ctypes.POINTER(MtgpModel), vp, vp, i32, i32, vp, i32,
                                   ctypes.POINTER(MtgpRollouts), ctypes.POINTER(MtgpOutputs), vp]
     lib.mtgp_eval_rk4.restype = ctypes.c_int
+    lib.mtgp_schedule.argtypes = [vp, i32, i32, ctypes.POINTER(i32), i32, vp, vp, vp]
+    lib.mtgp_schedule.restype = ctypes.c_int
     lib.mtgp_last_kernel_ms.restype = ctypes.c_float
     lib.mtgp_set_timing.argtypes = [ctypes.c_int]
     lib.mtgp_set_timing.restype = ctypes.c_int
-    if lib.mtgp_abi_version() != 1:
+    if lib.mtgp_abi_version() != ABI_VERSION:
         raise RuntimeError("libmtgp_hip ABI version mismatch")
     if path == LIB_PATH:
         _lib = lib

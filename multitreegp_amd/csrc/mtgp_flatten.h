@@ -156,13 +156,35 @@ MTGP_INLINE MTGP_HD void size_row(int i, RowInfo* info) {
   else { r.afirst = 0; r.need = (uint8_t)((q > p + 1) ? q : p + 1); }
 }
 
+// opcode -> pre-decoded fields (push | src | alu | cos) for the SIMT interpreter
+MTGP_INLINE MTGP_HD uint32_t decode_bits(uint32_t op) {
+  uint32_t push = 0, src, alu, cs = 0;
+  if (op <= MTGP_OP_LDVP) {
+    push = (op == MTGP_OP_LDCP || op == MTGP_OP_LDVP) ? 1u : 0u;
+    src = (op == MTGP_OP_LDC || op == MTGP_OP_LDCP) ? MTGP_SRC_IMM : MTGP_SRC_VAR;
+    alu = MTGP_ALU_LOAD;
+  } else if (op <= MTGP_OP_RDIVS) {
+    const uint32_t fam = (op - MTGP_OP_ADDC) % 6;  // ADD SUB RSUB MUL DIV RDIV
+    const uint32_t kind = (op - MTGP_OP_ADDC) / 6;  // C V S
+    src = kind == 0 ? MTGP_SRC_IMM : (kind == 1 ? MTGP_SRC_VAR : MTGP_SRC_STACK);
+    const uint32_t map[6] = {MTGP_ALU_ADD, MTGP_ALU_SUB, MTGP_ALU_RSUB, MTGP_ALU_MUL, MTGP_ALU_DIV, MTGP_ALU_RDIV};
+    alu = map[fam];
+  } else {
+    src = MTGP_SRC_ACC;
+    alu = MTGP_ALU_UNARY;
+    cs = (op == MTGP_OP_COS) ? 1u : 0u;
+  }
+  const uint32_t pop = (src == MTGP_SRC_STACK) ? 1u : 0u;
+  return (push << 16) | (src << MTGP_W_SRC_SHIFT) | (alu << MTGP_W_ALU_SHIFT) | (cs << 22) | (pop << 23);
+}
+
 struct Emitter {
   MtgpInstr* out;
   int cap;
   int n;
   int pending_push;
   MTGP_HD void put(uint32_t op, uint32_t slot, float imm) {
-    if (n < cap) { out[n].op = op | (slot << 8); out[n].imm = imm; }
+    if (n < cap) { out[n].op = op | (slot << 8) | decode_bits(op); out[n].imm = imm; }
     ++n;
   }
   // load a leaf operand into acc (pushing the previous acc when a push is pending)

@@ -1,12 +1,16 @@
 // mtgp_kernels.hip -- MI355X (gfx950) population-fitness evaluator for MultiTreeGP.
 //
-// One wavefront = one individual x up to 64 rollouts (lanes).  Every lane of a wave runs
-// the SAME program, so the opcode stream is wave-uniform: it is fetched with scalar loads
-// and dispatched with scalar branches, while the per-rollout values live in VGPRs.  The
-// data vector a tree reads and the operand stack live in LDS (one 64-lane column per slot,
-// conflict-free).  The interpreter is fused into a fixed-step RK4 integrator: the ODE state
-// stays in registers for the whole rollout, fitness is accumulated online at the save
-// points, and only the [P] fitness (plus optional time-major trajectories) leaves the CU.
+// One wavefront = G = 64 / Rp individuals x Rp (R rounded up to a power of two) rollouts.
+// The environment (drift, observation, RK4 update, fitness) is lane-parallel; each
+// individual's tree programs are wave-uniform instruction streams, fetched with scalar loads
+// (four instructions per s_load_dwordx8) and dispatched with scalar branches, while the
+// per-rollout values live in VGPRs.  The data vector a tree reads and its operand stack live
+// in LDS (one 64-lane column per slot, conflict-free).  The interpreter is fused into a
+// fixed-step RK4 integrator: the ODE state stays in registers for the whole rollout, fitness
+// is accumulated online at the save points, and only the [P] fitness (plus optional
+// time-major trajectories) leaves the CU.  Individuals are mapped to waves through an
+// optional schedule (MtgpRollouts.order, built by mtgp_schedule) that balances per-wave
+// interpreter work.
 //
 // Reference path replaced: GeneticProgramming.evaluate_population -> shard_eval ->
 // vmap(Evaluator.__call__) -> diffeqsolve(_drift -> vmap_foriloop)  (gp.py:259-269,
@@ -24,79 +28,47 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kDMax = 8;  // data slots held in LDS by the small-state kernels
 constexpr int kSMax = MTGP_STACK_MAX;
+constexpr int kLdsWaveWords = (kDMax + kSMax) * kWave;  // per wave: data columns | stack columns
 constexpr float kInf = __builtin_huge_valf();
-
-#ifndef MTGP_V_PREFETCH
-#define MTGP_V_PREFETCH 0
-#endif
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 // --------------------------------------------------------------------------------------
-// The interpreter.  `dv` = this lane's column of the wave's LDS data vector (stride 64
+// The interpreter.  `dcol` = this lane's column of the wave's LDS data vector (stride 64
 // floats per slot), `st` = this lane's column of the operand stack.  `code`/`len` are
-// wave-uniform.
-// Register data vector (scalar branch tree per variable read): measured 2% slower than the
-// LDS column at C3, off by default.
-#ifndef MTGP_V_REGDATA
-#define MTGP_V_REGDATA 0
-#endif
-
-// The data vector a tree reads.  MTGP_V_REGDATA=1: up to 8 slots in VGPRs, the (wave-uniform)
-// slot picked by a scalar branch tree; 0: one 64-lane LDS column per slot.
-struct DVec {
-  const float* lds;  // this lane's LDS column base (stride kWave per slot)
-  float r[kDMax];
-};
-
-template <bool REG>
-__device__ __forceinline__ float dget(const DVec& d, uint32_t slot) {
-  if (REG) {
-  switch (slot) {
-    case 0: return d.r[0];
-    case 1: return d.r[1];
-    case 2: return d.r[2];
-    case 3: return d.r[3];
-    case 4: return d.r[4];
-    case 5: return d.r[5];
-    case 6: return d.r[6];
-    default: return d.r[7];
-  }
-  }
-  return d.lds[slot * kWave];
-}
-
-__device__ __forceinline__ void dset(DVec& d, float* lds_col, int slot, float v) {
-#if MTGP_V_REGDATA
-  d.r[slot] = v;
-  (void)lds_col;
-#else
-  lds_col[slot * kWave] = v;
-#endif
-}
-
-template <bool REG = (MTGP_V_REGDATA != 0)>
-__device__ __forceinline__ float exec_instr(uint32_t w, float imm, float acc, int& sp, const DVec& dv,
+// wave-uniform, so the opcode switch compiles to a scalar branch tree and each handler is
+// 1-3 vector instructions.
+//
+// Measured alternatives (C3, see DESIGN.md "Interpreter design record"):
+//  * SIMT interpreter (every lane runs its own individual's program, branch-free select/fma
+//    ALU): 1.5x slower at G = 2 -- ~35 VALU per step vs the scalar dispatch's ~4.
+//  * branch-free uniform decode with SGPR select masks, data/stack in VGPRs via
+//    s_set_gpr_idx: 1.9x slower (an indexed VGPR access costs ~70 cycles on gfx950,
+//    scripts/micro/gpridx_cost.hip); the same with LDS data: 1.45x slower (2x the per-wave
+//    instruction stream; issue, not branch latency, bounds this loop).
+//  * per-instruction scalar loads (no blocks): 6-10% slower; a VGPR-lane program cache: 15%
+//    slower; data vector in VGPRs behind a scalar branch tree: 2% slower.
+__device__ __forceinline__ float exec_instr(uint32_t w, float imm, float acc, int& sp, const float* dcol,
                                             float* st) {
   const uint32_t op = w & 0xffu;
-  const uint32_t slot = (w >> 8) & 0xffu;
+  const float* dv = dcol + ((w >> 8) & 0xffu) * kWave;
   switch (op) {
     case MTGP_OP_LDC: return imm;
     case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; return imm;
-    case MTGP_OP_LDV: return dget<REG>(dv, slot);
-    case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; return dget<REG>(dv, slot);
+    case MTGP_OP_LDV: return *dv;
+    case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; return *dv;
     case MTGP_OP_ADDC: return acc + imm;
     case MTGP_OP_SUBC: return acc - imm;
     case MTGP_OP_RSUBC: return imm - acc;
     case MTGP_OP_MULC: return acc * imm;
     case MTGP_OP_DIVC: return acc / imm;
     case MTGP_OP_RDIVC: return imm / acc;
-    case MTGP_OP_ADDV: return acc + dget<REG>(dv, slot);
-    case MTGP_OP_SUBV: return acc - dget<REG>(dv, slot);
-    case MTGP_OP_RSUBV: return dget<REG>(dv, slot) - acc;
-    case MTGP_OP_MULV: return acc * dget<REG>(dv, slot);
-    case MTGP_OP_DIVV: return acc / dget<REG>(dv, slot);
-    case MTGP_OP_RDIVV: return dget<REG>(dv, slot) / acc;
+    case MTGP_OP_ADDV: return acc + *dv;
+    case MTGP_OP_SUBV: return acc - *dv;
+    case MTGP_OP_RSUBV: return *dv - acc;
+    case MTGP_OP_MULV: return acc * *dv;
+    case MTGP_OP_DIVV: return acc / *dv;
+    case MTGP_OP_RDIVV: return *dv / acc;
     case MTGP_OP_ADDS: --sp; return acc + st[sp * kWave];
     case MTGP_OP_SUBS: --sp; return acc - st[sp * kWave];
     case MTGP_OP_RSUBS: --sp; return st[sp * kWave] - acc;
@@ -109,32 +81,28 @@ __device__ __forceinline__ float exec_instr(uint32_t w, float imm, float acc, in
 }
 
 // Programs are read through the constant address space so the wave-uniform fetch is a
-// scalar s_load (K$) instead of a vector load + readfirstlane.
-typedef const __attribute__((address_space(4))) MtgpInstr* ConstInstrPtr;
+// scalar load (K$), four instructions (32 B) per s_load_dwordx8.  The program stride L is a
+// multiple of 4 (checked by the entry points), so a block never crosses a program slot.
+typedef uint32_t u8v __attribute__((ext_vector_type(8)));
+typedef const __attribute__((address_space(4))) u8v* ConstBlockPtr;
 
-template <bool REG = (MTGP_V_REGDATA != 0)>
-__device__ __forceinline__ float run_prog(const MtgpInstr* code_generic, int len,
-                                          const DVec& dv, float* st) {
-  ConstInstrPtr code = (ConstInstrPtr)code_generic;
+__device__ __forceinline__ float run_prog(const MtgpInstr* code, int len, const float* dcol, float* st) {
+  ConstBlockPtr blk = (ConstBlockPtr)code;
   float acc = 0.0f;
   int sp = 0;
-#if MTGP_V_PREFETCH
-  // software-pipelined scalar fetch: instruction i+1 is in flight while i executes
-  // (programs are allocated with one spare slot, so code[len] is readable)
-  uint32_t w = code[0].op;
-  float imm = code[0].imm;
-  for (int i = 0; i < len; ++i) {
-    const uint32_t wn = code[i + 1].op;
-    const float immn = code[i + 1].imm;
-    acc = exec_instr<REG>(w, imm, acc, sp, dv, st);
-    w = wn;
-    imm = immn;
+  const int nblk = (len + 3) >> 2;
+  for (int b = 0; b < nblk; ++b) {
+    const u8v c = blk[b];
+    const int rem = len - 4 * b;
+    acc = exec_instr(c[0], __uint_as_float(c[1]), acc, sp, dcol, st);
+    if (rem > 1) acc = exec_instr(c[2], __uint_as_float(c[3]), acc, sp, dcol, st);
+    if (rem > 2) acc = exec_instr(c[4], __uint_as_float(c[5]), acc, sp, dcol, st);
+    if (rem > 3) acc = exec_instr(c[6], __uint_as_float(c[7]), acc, sp, dcol, st);
   }
-#else
-  for (int i = 0; i < len; ++i) acc = exec_instr<REG>(code[i].op, code[i].imm, acc, sp, dv, st);
-#endif
   return acc;
 }
+
+__device__ __forceinline__ void dset(float* dcol, int slot, float v) { dcol[slot * kWave] = v; }
 
 // --------------------------------------------------------------------------------------
 // Acrobot (acrobot.py:7-87).  Per-rollout invariant products are formed once with the same
@@ -238,10 +206,11 @@ __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool i
   }
 }
 
-// store v at row `row` (wave-uniform element offset) + lane: keeps addresses in SGPRs
-__device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int lane, float v) {
+// store v at row `row` (wave-uniform element offset) + off (per lane): the 64-bit row base
+// stays in SGPRs, only the 32-bit lane offset is a VGPR
+__device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
   float* p = arr + row;
-  p[lane] = v;
+  p[off] = v;
 }
 
 __device__ __forceinline__ bool save_incl(const float* ts, int k) {
@@ -251,15 +220,18 @@ __device__ __forceinline__ bool save_incl(const float* ts, int k) {
 
 // --------------------------------------------------------------------------------------
 // Wave layout.  A wave packs G = 64 / Rp individuals (Rp = R rounded up to a power of two):
-// lane = g * Rp + r -> individual p0 + g, rollout r.  The environment (drift, observation,
-// RK4 update, fitness) is lane-parallel and runs once for all G individuals; only the tree
-// programs differ per individual, so they run once per group under an exec mask, each with a
-// wave-uniform (scalar) instruction stream.  A half-empty wave costs as much as a full one
-// on gfx950 (measured: R=32 and R=64 take the same time), so packing is pure gain.
+// lane = g * Rp + r -> schedule slot q0 + g, rollout r; the individual at slot q is
+// order[q] (identity without a schedule).  The environment (drift, observation, RK4 update,
+// fitness) is lane-parallel and runs once for all G individuals; only the tree programs
+// differ per individual, so they run once per group, each with a wave-uniform (scalar)
+// instruction stream.  A half-empty wave costs as much as a full one on gfx950 (measured: R=32
+// and R=64 take the same time), so packing is pure gain.
 struct Lane {
-  int wave, lane, Rp, G, p0, g, r, p, rr;
+  int wave, lane, Rp, G, q0, g, r, p, rr;
   bool active;
 };
+
+__device__ __forceinline__ int sched_ind(const KArgs& A, int q) { return A.ro.order ? A.ro.order[q] : q; }
 
 __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.wave = uni(threadIdx.x >> 6);
@@ -268,20 +240,26 @@ __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   while (Rp < A.ro.R) Rp <<= 1;
   L.Rp = uni(Rp);
   L.G = uni(kWave / Rp);
-  L.p0 = uni((blockIdx.x * kWavesPerBlock + L.wave) * L.G);
-  if (L.p0 >= A.P) return false;
+  L.q0 = uni((blockIdx.x * kWavesPerBlock + L.wave) * L.G);
+  if (L.q0 >= A.P) return false;
   L.g = L.lane / L.Rp;
   L.r = L.lane - L.g * L.Rp;
-  L.p = L.p0 + L.g;
-  L.active = (L.r < A.ro.R) && (L.p < A.P);
+  const int q = L.q0 + L.g;
+  L.p = q < A.P ? sched_ind(A, q) : A.P;  // A.P marks a padding group
+  L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
   return true;
 }
 
 // number of groups of this wave that hold a real individual
 __device__ __forceinline__ int groups_live(const KArgs& A, const Lane& L) {
-  const int n = A.P - L.p0;
+  const int n = A.P - L.q0;
   return uni(n < L.G ? n : L.G);
+}
+
+// individual of group gi (wave-uniform)
+__device__ __forceinline__ int group_ind(const KArgs& A, const Lane& L, int gi) {
+  return uni(sched_ind(A, L.q0 + gi));
 }
 
 // RK4 stage input: stage 0 -> s, stages 1,2 -> s + h/2 k, stage 3 -> s + h k
@@ -294,90 +272,29 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 }
 
 // --------------------------------------------------------------------------------------
-// Wave-local program cache in VGPR lanes.  Every interpreted instruction would otherwise be
-// a scalar load followed by an s_waitcnt (the wave stalls ~100+ cycles per instruction, and
-// C3 has only 4 waves per SIMD to hide it).  At kernel start the wave copies the programs of
-// its G individuals into two VGPR pairs (lane j holds cache entry j and j + 64: op word and
-// imm bits) and a meta VGPR (lane m = group * n_prog + slot holds start | len << 16 | valid);
-// the interpreter then fetches with v_readlane (SGPR lane index) -- no memory round trip.
-// Programs that do not fit the 128-entry cache fall back to scalar loads.
-struct PCache {
-  uint32_t op0, op1, imm0, imm1, meta;
-};
-
-// VGPR-lane program cache: measured 15% SLOWER than scalar loads at C3 (the fetch latency is
-// hidden; the extra readlane/select work is not), so it is off by default.
-#ifndef MTGP_V_PCACHE
-#define MTGP_V_PCACHE 0
-#endif
-
-__device__ __forceinline__ PCache pcache_build(const KArgs& A, const Lane& L, int ng) {
-  PCache c;
-#if !MTGP_V_PCACHE
-  c.op0 = c.op1 = c.imm0 = c.imm1 = c.meta = 0u;
-  (void)A; (void)L; (void)ng;
-  return c;
-#endif
-  const int nm = uni(ng * A.n_prog);
-  const int lane = L.lane;
-  int len = 0;
-  if (nm <= kWave && lane < nm) len = A.plen[(size_t)L.p0 * A.n_prog + lane];
-  int incl = len;  // inclusive prefix sum over lanes
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    const int t = __shfl_up(incl, d, kWave);
-    if (lane >= d) incl += t;
-  }
-  const int start = incl - len;
-  const bool cached = (nm <= kWave) && (lane < nm) && (start + len <= 2 * kWave);
-  c.meta = cached ? ((uint32_t)start | ((uint32_t)len << 16) | 0x80000000u) : 0u;
-  c.op0 = c.op1 = c.imm0 = c.imm1 = 0u;
-  if (nm <= kWave) {
-    for (int m = 0; m < nm; ++m) {
-      const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)c.meta, m);
-      if (!(mm >> 31)) continue;
-      const int s0 = (int)(mm & 0xffffu), l = (int)((mm >> 16) & 0x7fffu);
-      const MtgpInstr* src = A.prog + ((size_t)L.p0 * A.n_prog + m) * A.L;
-      const int i0 = lane - s0, i1 = lane + kWave - s0;
-      if (i0 >= 0 && i0 < l) { c.op0 = src[i0].op; c.imm0 = __float_as_uint(src[i0].imm); }
-      if (i1 >= 0 && i1 < l) { c.op1 = src[i1].op; c.imm1 = __float_as_uint(src[i1].imm); }
-    }
-  }
-  return c;
+// Run program `slot` of group gi (its individual's program, wave-uniform).
+__device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
+                                         float* st) {
+  const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
+  return run_prog(A.prog + pj * A.L, uni(A.plen[pj]), dcol, st);
 }
 
-// Program (group gi, slot) through the cache (or the scalar-load fallback).
-__device__ __forceinline__ float run_cached(const KArgs& A, const Lane& L, const PCache& c, int gi, int slot,
-                                            const DVec& dv, float* st) {
-  const int m = gi * A.n_prog + slot;
-  const uint32_t mm = (uint32_t)__builtin_amdgcn_readlane((int)c.meta, m);
-  if (mm >> 31) {
-    const int s0 = (int)(mm & 0xffffu), len = (int)((mm >> 16) & 0x7fffu);
-    float acc = 0.0f;
-    int sp = 0;
-    for (int i = 0; i < len; ++i) {
-      const int idx = s0 + i;
-      const uint32_t w = (uint32_t)(idx < kWave ? __builtin_amdgcn_readlane((int)c.op0, idx)
-                                                : __builtin_amdgcn_readlane((int)c.op1, idx - kWave));
-      const uint32_t ib = (uint32_t)(idx < kWave ? __builtin_amdgcn_readlane((int)c.imm0, idx)
-                                                 : __builtin_amdgcn_readlane((int)c.imm1, idx - kWave));
-      acc = exec_instr(w, __uint_as_float(ib), acc, sp, dv, st);
-    }
-    return acc;
-  }
-  const size_t pj = (size_t)(L.p0 + gi) * A.n_prog + slot;
-  return run_prog(A.prog + pj * A.L, uni(A.plen[pj]), dv, st);
-}
+#ifndef MTGP_V_NOINTERP
+#define MTGP_V_NOINTERP 0  // diagnostic only: skip interpretation (cost attribution), never shipped
+#endif
 
 // Run program `slot` of every live group; each lane keeps its own individual's value.
 // The program runs with the FULL exec mask (lanes of other groups compute a discarded value
 // on their own data/stack columns): inside a divergent `if` the CFG structurizer would turn
 // the uniform opcode switch into exec-masked flow blocks (~2x the scalar dispatch cost).
-__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, const PCache& c, int ng, int slot,
-                                            const DVec& dv, float* st, float dflt) {
+__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, int ng, int slot, const float* dcol,
+                                            float* st, float dflt) {
+#if MTGP_V_NOINTERP
+  return 0.01f * (float)(slot + 1) + 0.001f * dcol[4 * kWave];
+#endif
   float v = dflt;
   for (int gi = 0; gi < ng; ++gi) {
-    const float t = run_cached(A, L, c, gi, slot, dv, st);
+    const float t = run_one(A, L, gi, slot, dcol, st);
     v = (L.g == gi) ? t : v;
   }
   return v;
@@ -403,19 +320,14 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
 // state equations; at save points the save-time readout (dyn.py:101) is appended.
 template <int NA, bool TRAJ>
 __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
-  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
-  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dcol = &lds[Ln.wave][0][Ln.lane];
-  DVec dv;
-  dv.lds = dcol;
-#pragma unroll
-  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
-  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+  float* dcol = &lds[Ln.wave][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
 
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
@@ -423,16 +335,15 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
   const size_t PR = (size_t)A.P * R;
-  const size_t pR0 = (size_t)Ln.p0 * R;
-  const int loff = Ln.g * R + r;  // lane offset of this (individual, rollout) in a save row
+  const int loff = Ln.p * R + r;  // element offset of this (individual, rollout) in a save row
 #pragma unroll
-  for (int t = 0; t < kDMax - uslot - 1; ++t)  // static slot indices keep dv.r in registers
-    if (t < A.m.n_targets) dset(dv, dcol, uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
+  for (int t = 0; t < kDMax - uslot - 1; ++t)
+    if (t < A.m.n_targets) dset(dcol, uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   // groups whose save-time readout differs from the drift readout (it reads y): bit per group
   uint64_t diff_mask = 0;
   for (int gi = 0; gi < ng; ++gi) {
-    const size_t pj = (size_t)(Ln.p0 + gi) * A.n_prog;
+    const size_t pj = (size_t)group_ind(A, Ln, gi) * A.n_prog;
     bool same = A.m.readout_save_same > 0;
     if (A.m.readout_save_same < 0) {
       const int la = uni(A.plen[pj + A.m.prog_readout]), lb = uni(A.plen[pj + A.m.prog_readout_save]);
@@ -477,16 +388,16 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 #pragma unroll
       for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
 #pragma unroll
-      for (int j = 0; j < NA; ++j) dset(dv, dcol, 4 + j, at[j]);
-      const float u = run_groups(A, Ln, pc, ng, A.m.prog_readout, dv, st, 0.0f);
+      for (int j = 0; j < NA; ++j) dset(dcol, 4 + j, at[j]);
+      const float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);
       acro_drift(K, xt, u, kx);
       acro_f_obs(xt, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dset(dv, dcol, i, y[i]);
-      dset(dv, dcol, uslot, u);
+      for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
+      dset(dcol, uslot, u);
 #pragma unroll 1
       for (int q = 0; q < NA; ++q) {
-        const float v = run_groups(A, Ln, pc, ng, A.m.prog_state + q, dv, st, 0.0f);
+        const float v = run_groups(A, Ln, ng, A.m.prog_state + q, dcol, st, 0.0f);
 #pragma unroll
         for (int j = 0; j < NA; ++j) ka[j] = (q == j) ? v : ka[j];
       }
@@ -497,7 +408,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
           if (diff_mask != 0) {
             for (int gi = 0; gi < ng; ++gi) {
               if (!((diff_mask >> gi) & 1ull)) continue;
-              const float t = run_cached(A, Ln, pc, gi, A.m.prog_readout_save, dv, st);
+              const float t = run_one(A, Ln, gi, A.m.prog_readout_save, dcol, st);
               us = (Ln.g == gi) ? t : us;
             }
           }
@@ -505,16 +416,16 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR + pR0, loff, x[i]);
+              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR + pR0, loff, y[i]);
+              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR, loff, y[i]);
             }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR + pR0, loff, us);
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us);
             if (A.out.acts) {
 #pragma unroll
-              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR + pR0, loff, a[j]);
+              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR, loff, a[j]);
             }
           }
         }
@@ -554,29 +465,23 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 // Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
 template <bool TRAJ>
 __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
-  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
-  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dcol = &lds[Ln.wave][0][Ln.lane];
-  DVec dv;
-  dv.lds = dcol;
-#pragma unroll
-  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
-  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+  float* dcol = &lds[Ln.wave][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
   const size_t PR = (size_t)A.P * R;
-  const size_t pR0 = (size_t)Ln.p0 * R;
-  const int loff = Ln.g * R + r;
+  const int loff = Ln.p * R + r;
 #pragma unroll
   for (int t = 0; t < kDMax - 4; ++t)
-    if (t < A.m.n_targets) dset(dv, dcol, 4 + t, A.ro.targets[rr * A.m.n_targets + t]);
+    if (t < A.m.n_targets) dset(dcol, 4 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   float x[4], kx[4], ax[4];
 #pragma unroll
@@ -596,8 +501,8 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
       for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
       acro_f_obs(xt, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dset(dv, dcol, i, y[i]);
-      const float u = run_groups(A, Ln, pc, ng, A.m.prog_readout, dv, st, 0.0f);  // ff.py:106-107 (:97 at saves)
+      for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
+      const float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);  // ff.py:106-107 (:97 at saves)
       acro_drift(K, xt, u, kx);
       if (stage == 0) {
         if (is_save) {
@@ -606,13 +511,13 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR + pR0, loff, x[i]);
+              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR + pR0, loff, y[i]);
+              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR, loff, y[i]);
             }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR + pR0, loff, u);
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u);
           }
         }
         if (pending) {
@@ -644,24 +549,18 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
 // Symbolic regression of an ODE (SR_evaluator.py:57-94): dx_i = tree_i(x); MSE vs ys_true.
 template <int NV, bool TRAJ>
 __global__ void __launch_bounds__(256) k_sr(KArgs A) {
-  __shared__ float lds[kWavesPerBlock][kDMax + kSMax][kWave];
+  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
-  const PCache pc = pcache_build(A, Ln, ng);
   const bool active = Ln.active;
   const int R = A.ro.R;
-  float* dcol = &lds[Ln.wave][0][Ln.lane];
-  DVec dv;
-  dv.lds = dcol;
-#pragma unroll
-  for (int i = 0; i < kDMax; ++i) dv.r[i] = 0.0f;
-  float* st = &lds[Ln.wave][kDMax][Ln.lane];
+  float* dcol = &lds[Ln.wave][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const size_t PR = (size_t)A.P * R;
-  const size_t pR0 = (size_t)Ln.p0 * R;
-  const int loff = Ln.g * R + r;
+  const int loff = Ln.p * R + r;
   float x[NV], kx[NV], ax[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
@@ -685,7 +584,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       tot = tot + sq;
       if (TRAJ && active && A.out.xs) {
 #pragma unroll
-        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR + pR0, loff, x[d]);
+        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, x[d]);
       }
     }
     if (pending) {
@@ -702,10 +601,10 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) dset(dv, dcol, i, stage_in(stage, x[i], kx[i], h, h2));
+      for (int i = 0; i < NV; ++i) dset(dcol, i, stage_in(stage, x[i], kx[i], h, h2));
 #pragma unroll 1
       for (int q = 0; q < NV; ++q) {
-        const float v = run_groups(A, Ln, pc, ng, A.m.prog_state + q, dv, st, 0.0f);
+        const float v = run_groups(A, Ln, ng, A.m.prog_state + q, dcol, st, 0.0f);
 #pragma unroll
         for (int j = 0; j < NV; ++j) kx[j] = (q == j) ? v : kx[j];
       }
@@ -743,9 +642,7 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
   float* dcol = dyn_lds + (size_t)wave * (n_data + kSMax) * kWave + lane;
   float* st = dcol + (size_t)n_data * kWave;
   for (int d = 0; d < n_data; ++d) dcol[d * kWave] = active ? data[(size_t)m * n_data + d] : 0.0f;
-  DVec dv;
-  dv.lds = dcol;
-  const float v = run_prog<false>(prog + (size_t)pj * L, uni(plen[pj]), dv, st);
+  const float v = run_prog(prog + (size_t)pj * L, uni(plen[pj]), dcol, st);
   if (active) out[(size_t)pj * M + m] = v;
 }
 
@@ -777,6 +674,62 @@ __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, i
     for (int t = 0; t < T; ++t) c += mtgp::count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
     nodes_out[p] = c;
   }
+}
+
+// --------------------------------------------------------------------------------------
+// Schedule: counting sort of per-individual interpreter cost, then a slot permutation.
+struct SchedW {
+  int32_t w[MTGP_MAX_PROGRAMS];
+};
+
+__device__ __forceinline__ int sched_cost(const int32_t* plen, int p, int n_prog, const SchedW& W) {
+  int c = 0;
+  for (int j = 0; j < n_prog; ++j) c += W.w[j] * plen[(size_t)p * n_prog + j];
+  return c < 0 ? 0 : (c >= MTGP_SCHED_BINS ? MTGP_SCHED_BINS - 1 : c);
+}
+
+__global__ void __launch_bounds__(256) k_sched_hist(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
+                                                    int32_t* __restrict__ hist) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < P) atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
+}
+
+// exclusive scan of the histogram (one block, MTGP_SCHED_BINS / 1024 bins per thread)
+__global__ void __launch_bounds__(1024) k_sched_scan(const int32_t* __restrict__ hist, int32_t* __restrict__ offs) {
+  constexpr int kPer = MTGP_SCHED_BINS / 1024;
+  __shared__ int32_t part[1024];
+  const int t = threadIdx.x;
+  int loc[kPer], sum = 0;
+  for (int i = 0; i < kPer; ++i) { loc[i] = sum; sum += hist[t * kPer + i]; }
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int base = part[t] - sum;
+  for (int i = 0; i < kPer; ++i) offs[t * kPer + i] = base + loc[i];
+}
+
+// ascending rank s -> slot: G >= 2 interleaves (most expensive, cheapest, 2nd, 2nd cheapest, ...)
+// so every wave holds a balanced mix; G == 1 runs the most expensive first.
+__global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
+                                                       int G, int32_t* __restrict__ offs, int32_t* __restrict__ order) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const int s = atomicAdd(&offs[sched_cost(plen, p, n_prog, W)], 1);
+  int q;
+  if (G == 1) {
+    q = P - 1 - s;
+  } else {
+    const int h = P / 2;
+    if (s < h) q = 2 * s + 1;
+    else if (s >= P - h) q = 2 * (P - 1 - s);
+    else q = P - 1;  // middle element of an odd P
+  }
+  order[q] = p;
 }
 
 hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
@@ -850,10 +803,31 @@ int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* 
   return n;
 }
 
+int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t* weights, int32_t R,
+                  int32_t* order_out, int32_t* scratch, void* stream) {
+  if (!plen || !order_out || !scratch || P < 0 || n_prog <= 0 || n_prog > MTGP_MAX_PROGRAMS) return MTGP_ERR_ARG;
+  if (R <= 0 || R > kWave) return MTGP_ERR_ARG;
+  if (P == 0) return MTGP_OK;
+  SchedW W;
+  for (int j = 0; j < MTGP_MAX_PROGRAMS; ++j) W.w[j] = (j < n_prog) ? (weights ? weights[j] : 1) : 0;
+  int Rp = 1;
+  while (Rp < R) Rp <<= 1;
+  const int G = kWave / Rp;
+  hipStream_t s = (hipStream_t)stream;
+  int32_t* hist = scratch;
+  int32_t* offs = scratch + MTGP_SCHED_BINS;
+  if (hipMemsetAsync(hist, 0, MTGP_SCHED_BINS * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+  const unsigned nb = (unsigned)((P + 255) / 256);
+  hipLaunchKernelGGL(k_sched_hist, dim3(nb), dim3(256), 0, s, plen, P, n_prog, W, hist);
+  hipLaunchKernelGGL(k_sched_scan, dim3(1), dim3(1024), 0, s, hist, offs);
+  hipLaunchKernelGGL(k_sched_scatter, dim3(nb), dim3(256), 0, s, plen, P, n_prog, W, G, offs, order_out);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
 int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L, int32_t P,
                        const float* data, int32_t M, int32_t n_data, float* out, void* stream) {
   if (!prog || !plen || !data || !out || P < 0 || n_prog <= 0 || L <= 0 || M < 0) return MTGP_ERR_ARG;
-  if (n_data <= 0 || n_data > MTGP_MAX_DATA) return MTGP_ERR_ARG;
+  if (n_data <= 0 || n_data > MTGP_MAX_DATA || (L & 3) != 0) return MTGP_ERR_ARG;
   if (P == 0 || M == 0) return MTGP_OK;
   const long items = (long)P * n_prog * ((M + 63) / 64);
   const size_t lds = (size_t)kWavesPerBlock * (n_data + kSMax) * kWave * sizeof(float);
@@ -867,8 +841,9 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
                   const int32_t* nodes, int32_t P, const MtgpRollouts* rollouts, const MtgpOutputs* out,
                   void* stream) {
   if (!model || !prog || !plen || !nodes || !rollouts || !out || !out->fitness) return MTGP_ERR_ARG;
-  if (P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+  if (P < 0 || n_prog <= 0 || L <= 0 || (L & 3) != 0) return MTGP_ERR_ARG;
   if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
+  if ((int64_t)P * rollouts->R > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
   if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
   if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
   if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;

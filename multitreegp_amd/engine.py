@@ -39,6 +39,7 @@ class Flattened:
     status: torch.Tensor   # int32 [P, n_prog]
     L: int
     n_prog: int
+    order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
 
 
 class DeviceEngine:
@@ -102,7 +103,7 @@ class DeviceEngine:
             if t >= T:
                 raise ValueError(f"candidate has {T} trees, the evaluator needs tree {t}")
         n_prog = len(specs)
-        L = 2 * N + 8
+        L = (2 * N + 8 + 3) // 4 * 4  # multiple of 4: block-fetch fast path (mtgp.h)
         dev = self.device
         prog = torch.empty((P, n_prog, L, 2), dtype=torch.int32, device=dev)
         plen = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
@@ -126,11 +127,37 @@ class DeviceEngine:
         if worst != 0:
             raise RuntimeError(f"flatten status {worst}")
 
+    # ------------------------------------------------------------- schedule
+    def schedule_weights(self) -> list:
+        """Relative run count of each program per RK4 step (cost model of mtgp_schedule)."""
+        specs, roles = self._specs()
+        w = [4] * len(specs)  # state equations and the drift readout run in all 4 stages
+        if roles["prog_readout_save"] != roles["prog_readout"]:
+            w[roles["prog_readout_save"]] = 1  # once per save point
+        return w
+
+    def schedule(self, fl: Flattened, R: int) -> torch.Tensor:
+        """Build (once per flattened population) the wave schedule that balances interpreter work."""
+        if fl.order is None:
+            P = fl.plen.shape[0]
+            order = torch.empty((P,), dtype=torch.int32, device=self.device)
+            scratch = torch.empty((nat.SCHED_SCRATCH,), dtype=torch.int32, device=self.device)
+            w = self.schedule_weights()
+            wts = (ctypes.c_int32 * len(w))(*w)
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+            rc = self.native.mtgp_schedule(fl.plen.data_ptr(), P, fl.n_prog, wts, R, order.data_ptr(),
+                                           scratch.data_ptr(), stream)
+            if rc != nat.OK:
+                raise RuntimeError(f"mtgp_schedule failed: {rc}")
+            fl.order = order
+        return fl.order
+
     # ----------------------------------------------------------------- eval
     def evaluate(self, pop: torch.Tensor, data, trajectories: bool = False, rollout_fitness: bool = False,
-                 flattened: Optional[Flattened] = None, check: bool = True) -> dict:
+                 flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True) -> dict:
         """Run flatten + fused RK4 kernel.  Returns device tensors:
-        fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts time-major [S, c, P*R])."""
+        fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts time-major [S, c, P*R]).
+        schedule: pair expensive with cheap individuals in each wave (results are identical)."""
         d = self.prepare_data(data)
         fl = flattened if flattened is not None else self.flatten(pop)
         P = pop.shape[0]
@@ -153,6 +180,7 @@ class DeviceEngine:
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
+        ro.order = _ptr(self.schedule(fl, R)) if schedule and P > 1 else None
         dev = self.device
         res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
         out = nat.MtgpOutputs()

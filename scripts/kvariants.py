@@ -26,6 +26,8 @@ def main():
     ap.add_argument("--ode-steps", type=int, default=200)
     ap.add_argument("--no-traj", action="store_true")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--order", default="orig", help="orig | pair (long with short) | sorted (host reorder)")
+    ap.add_argument("--no-schedule", action="store_true", help="disable the device schedule (mtgp_schedule)")
     a = ap.parse_args()
     bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps)
     env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
@@ -38,6 +40,14 @@ def main():
     pop_dev = torch.from_numpy(pop).to(dev)
     first = next(iter(engines.values()))
     fl = first.flatten(pop_dev)
+    if a.order != "orig":
+        cost = fl.plen.sum(dim=1).cpu().numpy()
+        o = np.argsort(cost, kind="stable")
+        if a.order == "pair":
+            h = len(o) // 2
+            o = np.stack([o[::-1][:h], o[:h]], axis=1).reshape(-1)
+        pop_dev = torch.from_numpy(pop[o]).to(dev)
+        fl = first.flatten(pop_dev)
     first.check_status(fl)
     ref = None
     times = {v: [] for v in engines}
@@ -45,7 +55,8 @@ def main():
         for v, eng in engines.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=fl, check=False)
+            res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=fl, check=False,
+                               schedule=not a.no_schedule)
             e1.record()
             torch.cuda.synchronize()
             f = res["fitness"].cpu().numpy()

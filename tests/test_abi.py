@@ -19,7 +19,7 @@ def test_declared_symbols_exported():
     lib = nat.load()
     for sym in declared:
         assert hasattr(lib, sym)
-    assert lib.mtgp_abi_version() == 1
+    assert lib.mtgp_abi_version() == nat.ABI_VERSION
 
 
 def test_struct_layouts_match_header(tmp_path):
