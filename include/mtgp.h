@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 2
+#define MTGP_ABI_VERSION 3
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -79,31 +79,21 @@ typedef struct {
 
 /* ------------------------------------------------------------ program format */
 /* Accumulator machine, postorder with leaves folded into their parent.
- * word op: bits 0-7 opcode, bits 8-15 data slot, and the opcode pre-decoded for the
- * branch-free (SIMT) interpreter: bit 16 push acc first, bits 17-18 operand source
- * (MTGP_SRC_*), bits 19-21 ALU operation (MTGP_ALU_*), bit 22 cos (for MTGP_ALU_UNARY),
- * bit 23 pop (== source MTGP_SRC_STACK).
- * imm: f32 constant.
- * Program stride L (instructions per program slot) must be a multiple of 4 for the
- * evaluators: they fetch instructions in blocks of four (one 32-byte scalar load). */
-enum { MTGP_SRC_IMM = 0, MTGP_SRC_VAR = 1, MTGP_SRC_STACK = 2, MTGP_SRC_ACC = 3 };
-enum {
-  MTGP_ALU_LOAD = 0, MTGP_ALU_ADD = 1, MTGP_ALU_SUB = 2, MTGP_ALU_RSUB = 3, MTGP_ALU_MUL = 4,
-  MTGP_ALU_DIV = 5, MTGP_ALU_RDIV = 6, MTGP_ALU_UNARY = 7
-};
-#define MTGP_W_PUSH (1u << 16)
-#define MTGP_W_SRC_SHIFT 17
-#define MTGP_W_ALU_SHIFT 19
-#define MTGP_W_COS (1u << 22)
-#define MTGP_W_POP (1u << 23)
-/* no-op padding word: acc = acc (src ACC, ALU LOAD) */
-#define MTGP_W_NOP ((uint32_t)MTGP_SRC_ACC << MTGP_W_SRC_SHIFT)
+ *   op : the opcode (MTGP_OP_*), nothing else -- the evaluator switches on the raw word.
+ *   imm: *C opcodes: the f32 constant; *V opcodes: the data slot as a u32 byte offset
+ *        slot * MTGP_SLOT_BYTES (the evaluator's LDS column stride), so no decode is needed;
+ *        other opcodes: 0.
+ * Every program ends with MTGP_OP_END (not counted in its length), so a program slot holds
+ * at most L - 1 instructions.  The program stride L must be a multiple of 4: the evaluators
+ * fetch instructions in blocks of four (one 32-byte scalar load). */
+#define MTGP_SLOT_BYTES 256u
 enum {
   MTGP_OP_LDC = 0, MTGP_OP_LDCP, MTGP_OP_LDV, MTGP_OP_LDVP, /* P = push acc first */
   MTGP_OP_ADDC, MTGP_OP_SUBC, MTGP_OP_RSUBC, MTGP_OP_MULC, MTGP_OP_DIVC, MTGP_OP_RDIVC,
   MTGP_OP_ADDV, MTGP_OP_SUBV, MTGP_OP_RSUBV, MTGP_OP_MULV, MTGP_OP_DIVV, MTGP_OP_RDIVV,
   MTGP_OP_ADDS, MTGP_OP_SUBS, MTGP_OP_RSUBS, MTGP_OP_MULS, MTGP_OP_DIVS, MTGP_OP_RDIVS,
   MTGP_OP_SIN, MTGP_OP_COS,
+  MTGP_OP_END,
   MTGP_OP_COUNT
 };
 typedef struct {

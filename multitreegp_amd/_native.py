@@ -22,7 +22,7 @@ STACK_MAX = 8
 MAX_PROGRAMS = 64
 SCHED_BINS = 4096
 SCHED_SCRATCH = 2 * SCHED_BINS
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 OK = 0
 ERR_ARG = -1
@@ -41,8 +41,17 @@ OP_NAMES = [
     "ADDC", "SUBC", "RSUBC", "MULC", "DIVC", "RDIVC",
     "ADDV", "SUBV", "RSUBV", "MULV", "DIVV", "RDIVV",
     "ADDS", "SUBS", "RSUBS", "MULS", "DIVS", "RDIVS",
-    "SIN", "COS",
+    "SIN", "COS", "END",
 ]
+SLOT_BYTES = 256  # V opcodes carry slot * SLOT_BYTES in the imm bits (mtgp.h program format)
+
+
+def decode_instr(op: int, imm_bits: int):
+    """(name, slot, imm) of one MtgpInstr; slot is 0 except for V opcodes."""
+    name = OP_NAMES[op]
+    if name[-1] == "V" or name in ("LDV", "LDVP"):
+        return name, imm_bits // SLOT_BYTES, 0.0
+    return name, 0, float(np.array(imm_bits, dtype=np.uint32).view(np.float32))
 
 
 class MtgpNodeLibrary(ctypes.Structure):
@@ -161,5 +170,7 @@ def flatten_tree_host(tree: np.ndarray, node_lib: MtgpNodeLibrary, n_data: int, 
                                    ctypes.addressof(out), ctypes.byref(need))
     if n <= 0:
         raise ValueError(f"flatten failed with code {n}")
-    prog = [(OP_NAMES[out[i].op & 0xFF], (out[i].op >> 8) & 0xFF, float(out[i].imm)) for i in range(n)]
+    raw = np.frombuffer(bytes(out), dtype=np.uint32).reshape(-1, 2)
+    assert raw[n, 0] == OP_NAMES.index("END")
+    prog = [decode_instr(int(raw[i, 0]), int(raw[i, 1])) for i in range(n)]
     return prog, int(need.value)

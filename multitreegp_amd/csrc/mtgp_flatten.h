@@ -156,26 +156,14 @@ MTGP_INLINE MTGP_HD void size_row(int i, RowInfo* info) {
   else { r.afirst = 0; r.need = (uint8_t)((q > p + 1) ? q : p + 1); }
 }
 
-// opcode -> pre-decoded fields (push | src | alu | cos) for the SIMT interpreter
-MTGP_INLINE MTGP_HD uint32_t decode_bits(uint32_t op) {
-  uint32_t push = 0, src, alu, cs = 0;
-  if (op <= MTGP_OP_LDVP) {
-    push = (op == MTGP_OP_LDCP || op == MTGP_OP_LDVP) ? 1u : 0u;
-    src = (op == MTGP_OP_LDC || op == MTGP_OP_LDCP) ? MTGP_SRC_IMM : MTGP_SRC_VAR;
-    alu = MTGP_ALU_LOAD;
-  } else if (op <= MTGP_OP_RDIVS) {
-    const uint32_t fam = (op - MTGP_OP_ADDC) % 6;  // ADD SUB RSUB MUL DIV RDIV
-    const uint32_t kind = (op - MTGP_OP_ADDC) / 6;  // C V S
-    src = kind == 0 ? MTGP_SRC_IMM : (kind == 1 ? MTGP_SRC_VAR : MTGP_SRC_STACK);
-    const uint32_t map[6] = {MTGP_ALU_ADD, MTGP_ALU_SUB, MTGP_ALU_RSUB, MTGP_ALU_MUL, MTGP_ALU_DIV, MTGP_ALU_RDIV};
-    alu = map[fam];
-  } else {
-    src = MTGP_SRC_ACC;
-    alu = MTGP_ALU_UNARY;
-    cs = (op == MTGP_OP_COS) ? 1u : 0u;
-  }
-  const uint32_t pop = (src == MTGP_SRC_STACK) ? 1u : 0u;
-  return (push << 16) | (src << MTGP_W_SRC_SHIFT) | (alu << MTGP_W_ALU_SHIFT) | (cs << 22) | (pop << 23);
+MTGP_INLINE MTGP_HD bool is_var_op(uint32_t op) {
+  return op == MTGP_OP_LDV || op == MTGP_OP_LDVP || (op >= MTGP_OP_ADDV && op <= MTGP_OP_RDIVV);
+}
+
+MTGP_INLINE MTGP_HD float bits_to_f32(uint32_t u) {
+  float f;
+  __builtin_memcpy(&f, &u, sizeof f);
+  return f;
 }
 
 struct Emitter {
@@ -184,7 +172,8 @@ struct Emitter {
   int n;
   int pending_push;
   MTGP_HD void put(uint32_t op, uint32_t slot, float imm) {
-    if (n < cap) { out[n].op = op | (slot << 8) | decode_bits(op); out[n].imm = imm; }
+    // V opcodes carry the slot as an LDS byte offset (mtgp.h program format)
+    if (n < cap) { out[n].op = op; out[n].imm = is_var_op(op) ? bits_to_f32(slot * MTGP_SLOT_BYTES) : imm; }
     ++n;
   }
   // load a leaf operand into acc (pushing the previous acc when a push is pending)
@@ -300,10 +289,12 @@ MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* o
   return em.n;
 }
 
-// Full flatten of one tree. Returns length (>0) or -MTGP_ERR_*.
-MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLibrary* lib,
-                                     int n_data, uint64_t zero_mask, MtgpInstr* out, int cap,
-                                     RowInfo* info, int* stack_need) {
+// Full flatten of one tree into `slots` instructions: the program (at most slots - 1) and
+// its MTGP_OP_END.  Returns the program length (>0, END excluded) or -MTGP_ERR_*; on error
+// the slot holds a bare END (an empty program), so an evaluator never runs stale words.
+MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNodeLibrary* lib,
+                                          int n_data, uint64_t zero_mask, MtgpInstr* out, int cap,
+                                          RowInfo* info, int* stack_need) {
   for (int i = 0; i < N; ++i) {
     resolve_row(tree, N, i, lib, n_data, zero_mask, info);
     size_row(i, info);
@@ -314,6 +305,17 @@ MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLib
   if (info[N - 1].len > cap) return -MTGP_ERR_PROG_TOO_LONG;
   const int n = emit_program(N - 1, info, out, cap);
   if (n > cap) return -MTGP_ERR_PROG_TOO_LONG;
+  return n;
+}
+
+MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLibrary* lib,
+                                     int n_data, uint64_t zero_mask, MtgpInstr* out, int slots,
+                                     RowInfo* info, int* stack_need) {
+  if (slots < 1) return -MTGP_ERR_PROG_TOO_LONG;
+  const int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
+  const int at = n > 0 ? n : 0;
+  out[at].op = MTGP_OP_END;
+  out[at].imm = 0.0f;
   return n;
 }
 

@@ -48,57 +48,61 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 //    instruction stream; issue, not branch latency, bounds this loop).
 //  * per-instruction scalar loads (no blocks): 6-10% slower; a VGPR-lane program cache: 15%
 //    slower; data vector in VGPRs behind a scalar branch tree: 2% slower.
-__device__ __forceinline__ float exec_instr(uint32_t w, float imm, float acc, int& sp, const float* dcol,
-                                            float* st) {
-  const uint32_t op = w & 0xffu;
-  const float* dv = dcol + ((w >> 8) & 0xffu) * kWave;
-  switch (op) {
-    case MTGP_OP_LDC: return imm;
-    case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; return imm;
-    case MTGP_OP_LDV: return *dv;
-    case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; return *dv;
-    case MTGP_OP_ADDC: return acc + imm;
-    case MTGP_OP_SUBC: return acc - imm;
-    case MTGP_OP_RSUBC: return imm - acc;
-    case MTGP_OP_MULC: return acc * imm;
-    case MTGP_OP_DIVC: return acc / imm;
-    case MTGP_OP_RDIVC: return imm / acc;
-    case MTGP_OP_ADDV: return acc + *dv;
-    case MTGP_OP_SUBV: return acc - *dv;
-    case MTGP_OP_RSUBV: return *dv - acc;
-    case MTGP_OP_MULV: return acc * *dv;
-    case MTGP_OP_DIVV: return acc / *dv;
-    case MTGP_OP_RDIVV: return *dv / acc;
-    case MTGP_OP_ADDS: --sp; return acc + st[sp * kWave];
-    case MTGP_OP_SUBS: --sp; return acc - st[sp * kWave];
-    case MTGP_OP_RSUBS: --sp; return st[sp * kWave] - acc;
-    case MTGP_OP_MULS: --sp; return acc * st[sp * kWave];
-    case MTGP_OP_DIVS: --sp; return acc / st[sp * kWave];
-    case MTGP_OP_RDIVS: --sp; return st[sp * kWave] / acc;
-    case MTGP_OP_SIN: return mtgp_sinf(acc);
-    default: return mtgp_cosf(acc);  // MTGP_OP_COS
+// One instruction: `w` = opcode, `ib` = imm bits (f32 constant, or the data slot's LDS byte
+// offset for V opcodes).  Expanded inline at each of the four block positions; END leaves the
+// program (so there is no per-instruction length test).
+#define MTGP_EXEC(w, ib)                                                                          \
+  {                                                                                               \
+    const float imm_ = __uint_as_float(ib);                                                       \
+    const float* dv_ = (const float*)((const char*)dcol + (ib));                                  \
+    switch (w) {                                                                                  \
+      case MTGP_OP_LDC: acc = imm_; break;                                                        \
+      case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; acc = imm_; break;                           \
+      case MTGP_OP_LDV: acc = *dv_; break;                                                        \
+      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = *dv_; break;                           \
+      case MTGP_OP_ADDC: acc = acc + imm_; break;                                                 \
+      case MTGP_OP_SUBC: acc = acc - imm_; break;                                                 \
+      case MTGP_OP_RSUBC: acc = imm_ - acc; break;                                                \
+      case MTGP_OP_MULC: acc = acc * imm_; break;                                                 \
+      case MTGP_OP_DIVC: acc = acc / imm_; break;                                                 \
+      case MTGP_OP_RDIVC: acc = imm_ / acc; break;                                                \
+      case MTGP_OP_ADDV: acc = acc + *dv_; break;                                                 \
+      case MTGP_OP_SUBV: acc = acc - *dv_; break;                                                 \
+      case MTGP_OP_RSUBV: acc = *dv_ - acc; break;                                                \
+      case MTGP_OP_MULV: acc = acc * *dv_; break;                                                 \
+      case MTGP_OP_DIVV: acc = acc / *dv_; break;                                                 \
+      case MTGP_OP_RDIVV: acc = *dv_ / acc; break;                                                \
+      case MTGP_OP_ADDS: --sp; acc = acc + st[sp * kWave]; break;                                 \
+      case MTGP_OP_SUBS: --sp; acc = acc - st[sp * kWave]; break;                                 \
+      case MTGP_OP_RSUBS: --sp; acc = st[sp * kWave] - acc; break;                                \
+      case MTGP_OP_MULS: --sp; acc = acc * st[sp * kWave]; break;                                 \
+      case MTGP_OP_DIVS: --sp; acc = acc / st[sp * kWave]; break;                                 \
+      case MTGP_OP_RDIVS: --sp; acc = st[sp * kWave] / acc; break;                                \
+      case MTGP_OP_SIN: acc = mtgp_sinf(acc); break;                                              \
+      case MTGP_OP_COS: acc = mtgp_cosf(acc); break;                                              \
+      default: goto done; /* MTGP_OP_END */                                                       \
+    }                                                                                             \
   }
-}
 
 // Programs are read through the constant address space so the wave-uniform fetch is a
 // scalar load (K$), four instructions (32 B) per s_load_dwordx8.  The program stride L is a
-// multiple of 4 (checked by the entry points), so a block never crosses a program slot.
+// multiple of 4 (checked by the entry points), so a block never crosses a program slot, and
+// a program's END lies inside its slot.
 typedef uint32_t u8v __attribute__((ext_vector_type(8)));
 typedef const __attribute__((address_space(4))) u8v* ConstBlockPtr;
 
-__device__ __forceinline__ float run_prog(const MtgpInstr* code, int len, const float* dcol, float* st) {
+__device__ __forceinline__ float run_prog(const MtgpInstr* code, const float* dcol, float* st) {
   ConstBlockPtr blk = (ConstBlockPtr)code;
   float acc = 0.0f;
   int sp = 0;
-  const int nblk = (len + 3) >> 2;
-  for (int b = 0; b < nblk; ++b) {
-    const u8v c = blk[b];
-    const int rem = len - 4 * b;
-    acc = exec_instr(c[0], __uint_as_float(c[1]), acc, sp, dcol, st);
-    if (rem > 1) acc = exec_instr(c[2], __uint_as_float(c[3]), acc, sp, dcol, st);
-    if (rem > 2) acc = exec_instr(c[4], __uint_as_float(c[5]), acc, sp, dcol, st);
-    if (rem > 3) acc = exec_instr(c[6], __uint_as_float(c[7]), acc, sp, dcol, st);
+  for (;; ++blk) {
+    const u8v c = *blk;
+    MTGP_EXEC(c[0], c[1])
+    MTGP_EXEC(c[2], c[3])
+    MTGP_EXEC(c[4], c[5])
+    MTGP_EXEC(c[6], c[7])
   }
+done:
   return acc;
 }
 
@@ -276,7 +280,7 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 __device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
                                          float* st) {
   const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
-  return run_prog(A.prog + pj * A.L, uni(A.plen[pj]), dcol, st);
+  return run_prog(A.prog + pj * A.L, dcol, st);
 }
 
 #ifndef MTGP_V_NOINTERP
@@ -642,7 +646,7 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
   float* dcol = dyn_lds + (size_t)wave * (n_data + kSMax) * kWave + lane;
   float* st = dcol + (size_t)n_data * kWave;
   for (int d = 0; d < n_data; ++d) dcol[d * kWave] = active ? data[(size_t)m * n_data + d] : 0.0f;
-  const float v = run_prog(prog + (size_t)pj * L, uni(plen[pj]), dcol, st);
+  const float v = run_prog(prog + (size_t)pj * L, dcol, st);
   if (active) out[(size_t)pj * M + m] = v;
 }
 
@@ -666,7 +670,7 @@ __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, i
   mtgp::RowInfo* info = &info_all[t_in * NMAX];
   MtgpInstr* out = prog_out + ((size_t)p * n_prog + j) * L;
   int need = 0;
-  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L - 1, info, &need);
+  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
   len_out[(size_t)p * n_prog + j] = n > 0 ? n : 0;
   status_out[(size_t)p * n_prog + j] = n > 0 ? 0 : -n;
   if (j == 0) {

@@ -56,3 +56,39 @@ def test_argument_validation_without_gpu():
     m.n_save = 6
     assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 1, one.ctypes.data, 1,
                              ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
+
+
+def _define(text, name):
+    m = re.search(rf"#define\s+{name}\s+\(?([0-9]+)u?\s*(?:\*\s*(\w+))?\)?", text)
+    assert m, name
+    v = int(m.group(1))
+    return v * _define(text, m.group(2)) if m.group(2) else v
+
+
+def test_constants_match_header():
+    text = open(HDR).read()
+    assert _define(text, "MTGP_ABI_VERSION") == nat.ABI_VERSION
+    assert _define(text, "MTGP_SLOT_BYTES") == nat.SLOT_BYTES
+    assert _define(text, "MTGP_SCHED_BINS") == nat.SCHED_BINS
+    assert _define(text, "MTGP_SCHED_SCRATCH") == nat.SCHED_SCRATCH
+    assert _define(text, "MTGP_MAX_PROGRAMS") == nat.MAX_PROGRAMS
+    assert _define(text, "MTGP_STACK_MAX") == nat.STACK_MAX
+    enum = re.search(r"MTGP_OP_LDC = 0,(.*?)MTGP_OP_COUNT", text, re.S).group(1)
+    names = ["LDC"] + re.findall(r"MTGP_OP_(\w+)", enum)
+    assert names == nat.OP_NAMES
+
+
+def test_unaligned_program_stride_rejected():
+    """The evaluators fetch four instructions per scalar load: L % 4 != 0 is an argument error."""
+    lib = nat.load()
+    one = np.zeros(8, np.int32)
+    m = nat.MtgpModel()
+    m.n_steps, m.save_every, m.n_save = 4, 1, 5
+    ro = nat.MtgpRollouts()
+    ro.R, ro.x0, ro.ts = 4, one.ctypes.data, one.ctypes.data
+    out = nat.MtgpOutputs()
+    out.fitness = one.ctypes.data
+    assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 6, one.ctypes.data, 1,
+                             ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
+    assert lib.mtgp_eval_programs(one.ctypes.data, one.ctypes.data, 1, 6, 1, one.ctypes.data, 1, 1,
+                                  one.ctypes.data, None) == nat.ERR_ARG
