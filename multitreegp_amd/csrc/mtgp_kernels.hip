@@ -628,6 +628,152 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 }
 
 // --------------------------------------------------------------------------------------
+// Symbolic regression with a wide state (5 <= n_var <= MTGP_MAX_DATA, BASELINE C5: the 64-dim
+// "neural-ODE" SR).  One workgroup = NW = ceil(n_var / 8) waves over the same lanes (G
+// individuals x Rp rollouts, like every kernel here); wave w owns components [8w, 8w + 8): it
+// runs their trees, keeps x and the RK4 accumulator of those components in VGPRs, and
+// publishes stage outputs through a shared, ping-ponged LDS stage vector (the data vector
+// every tree reads).  The MSE (summed over components in index order, as the oracle and
+// sr.py:24 do) and the termination event (any non-finite component) are reduced across the
+// waves through LDS.  Per workgroup LDS: 2 x n_var columns + NW stacks + NW flag columns.
+constexpr int kWideComp = 8;  // components (trees) per wave
+
+__device__ __forceinline__ bool lane_setup_wide(const KArgs& A, Lane& L) {
+  L.wave = uni(threadIdx.x >> 6);
+  L.lane = threadIdx.x & 63;
+  int Rp = 1;
+  while (Rp < A.ro.R) Rp <<= 1;
+  L.Rp = uni(Rp);
+  L.G = uni(kWave / Rp);
+  L.q0 = uni(blockIdx.x * L.G);
+  if (L.q0 >= A.P) return false;
+  L.g = L.lane / L.Rp;
+  L.r = L.lane - L.g * L.Rp;
+  const int q = L.q0 + L.g;
+  L.p = q < A.P ? sched_ind(A, q) : A.P;
+  L.active = (L.r < A.ro.R) && (q < A.P);
+  L.rr = L.active ? L.r : 0;
+  return true;
+}
+
+template <bool TRAJ>
+__global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
+  extern __shared__ float wl[];
+  Lane Ln;
+  if (!lane_setup_wide(A, Ln)) return;  // uniform over the workgroup
+  const int NV = A.m.n_var;
+  const int NW = (NV + kWideComp - 1) / kWideComp;
+  const int w = Ln.wave, lane = Ln.lane, r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* bufA = wl + lane;
+  float* bufB = wl + (size_t)NV * kWave + lane;
+  float* st = wl + (size_t)(2 * NV + w * kSMax) * kWave + lane;
+  float* flags = wl + (size_t)(2 * NV + NW * kSMax) * kWave + lane;  // [NW] columns
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  const int c0 = w * kWideComp;
+
+  float x[kWideComp], ax[kWideComp];
+#pragma unroll
+  for (int t = 0; t < kWideComp; ++t) {
+    x[t] = (c0 + t < NV) ? A.ro.x0[rr * NV + c0 + t] : 0.0f;
+    ax[t] = 0.0f;
+  }
+  // workgroup-wide "any component non-finite" of this lane's state
+  auto any_bad = [&]() {
+    bool b = false;
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) b = b || ((c0 + t < NV) && !mtgp_isfinite(x[t]));
+    flags[w * kWave] = b ? 1.0f : 0.0f;
+    __syncthreads();
+    bool all = false;
+    for (int v = 0; v < NW; ++v) all = all || (flags[v * kWave] != 0.0f);
+    __syncthreads();
+    return all;
+  };
+  float* cur = bufA;
+  float* nxt = bufB;
+#pragma unroll
+  for (int t = 0; t < kWideComp; ++t)
+    if (c0 + t < NV) cur[(c0 + t) * kWave] = x[t];
+  bool dead = !active, pending = false;
+  bool prev_ok = !any_bad();  // (its barrier also publishes cur)
+  float tot = 0.0f;
+  for (int step = 0;; ++step) {
+    if ((step % save_every) == 0) {
+      const int k = step / save_every;
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) {
+        const int c = c0 + t;
+        if (c < NV) {
+          const float e = x[t] - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
+          nxt[c * kWave] = e * e;
+          if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, x[t]);
+        }
+      }
+      __syncthreads();
+      float sq = nxt[0];
+      for (int d = 1; d < NV; ++d) sq = sq + nxt[d * kWave];
+      tot = tot + sq;
+      __syncthreads();
+    }
+    if (pending) {
+      pending = false;
+      dead = true;
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) {
+        x[t] = kInf;
+        if (c0 + t < NV) cur[(c0 + t) * kWave] = kInf;
+      }
+      __syncthreads();
+    }
+    if (step == n_steps) break;
+    if (!TRAJ && __all(dead)) {  // dead is identical in every wave: a uniform exit
+      if (active && mtgp_isfinite(tot)) tot = kInf;
+      break;
+    }
+#pragma unroll 1
+    for (int stage = 0; stage < 4; ++stage) {
+      // trees of this wave's components on the shared stage vector; k parks in nxt
+      for (int t = 0; t < kWideComp; ++t) {
+        const int c = c0 + t;
+        if (c >= NV) break;
+        nxt[c * kWave] = run_groups(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+      }
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) {
+        const int c = c0 + t;
+        if (c < NV) {
+          const float kv = nxt[c * kWave];
+          ax[t] = stage_acc(stage, ax[t], kv);
+          if (stage < 3) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, h, h2);
+        }
+      }
+      __syncthreads();
+      float* tmp = cur;
+      cur = nxt;
+      nxt = tmp;
+    }
+    if (!dead) {
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) x[t] = MTGP_FMAF(h6, ax[t], x[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t)
+      if (c0 + t < NV) cur[(c0 + t) * kWave] = x[t];
+    const bool bad = any_bad();  // (its barrier also publishes cur)
+    if (!dead) {
+      if (prev_ok && bad) pending = true;
+      prev_ok = !bad;
+    }
+  }
+  if (w == 0) finish_group(A, Ln, tot / (float)S);
+}
+
+// --------------------------------------------------------------------------------------
 // tree_evaluator plugin (gp.py:390-401): every program on M shared data vectors.
 // One wave per (individual, program, chunk of 64 data vectors); data vector in LDS.
 __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restrict__ prog,
@@ -896,6 +1042,16 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
     }, s);
   } else if (model->model == MTGP_MODEL_SR) {
     if (!rollouts->ys_true) return MTGP_ERR_ARG;
+    if (model->n_var > 4) {
+      if (model->n_var > MTGP_MAX_DATA || n_prog < model->prog_state + model->n_var) return MTGP_ERR_ARG;
+      const int nw = (model->n_var + kWideComp - 1) / kWideComp;
+      const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+      const dim3 wgrid((unsigned)(((long)P + G - 1) / G)), wblock(kWave * nw);
+      return launch_timed([&] {
+        if (traj) hipLaunchKernelGGL((k_sr_wide<true>), wgrid, wblock, lds, s, A);
+        else hipLaunchKernelGGL((k_sr_wide<false>), wgrid, wblock, lds, s, A);
+      }, s);
+    }
 #define MTGP_SR(NV)                                                                                       \
   case NV:                                                                                                \
     return launch_timed([&] {                                                                             \

@@ -112,3 +112,24 @@ def test_rollout_counts(R):
     env, lib, ff, data, pop = dynamic_setup(P=9, R=R, n_steps=30, seed=7)
     res, ref, d = _run(ff, lib, data, pop)
     _check(res, ref, pop.shape[0], R, ["xs", "us"])
+
+
+@pytest.mark.parametrize("n_var,R,N,depth", [(5, 8, 30, 5), (12, 3, 64, 8), (64, 8, 128, 16)])
+def test_sr_wide_state_bitexact(n_var, R, N, depth):
+    """n_var > 4: the workgroup-per-lane-set SR kernel (BASELINE C5 shape at n_var = 64,
+    max_nodes 128, depth <= 16), trajectories and fitness bit-exact vs the oracle."""
+    env, lib, ff, data, pop = sr_setup(P=19, R=R, n_save=9, save_every=3, h=0.01, depth=depth, N=N,
+                                       n_var=n_var, seed=2)
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], R, ["xs"])
+
+
+def test_sr_wide_fitness_only_matches_trajectory_mode():
+    env, lib, ff, data, pop = sr_setup(P=21, R=8, n_save=9, save_every=3, h=0.05, depth=8, N=64, n_var=16,
+                                       seed=4)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    pd = torch.from_numpy(pop).cuda()
+    a = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True)
+    b = eng.evaluate(pd, data, trajectories=False, rollout_fitness=True)
+    assert bits_equal(a["fitness"].cpu().numpy(), b["fitness"].cpu().numpy())
+    assert bits_equal(a["rollout_fitness"].cpu().numpy(), b["rollout_fitness"].cpu().numpy())
