@@ -5,9 +5,14 @@ Workload (N=1 line): BASELINE config C3 -- DynamicPolicy Acrobot, pop 8192 per G
 per individual (2 hidden-state + 1 readout), max_nodes 64 / max_init_depth 10 (reference
 sampler distribution), 32 rollouts, fixed-step RK4 h=0.05 x 200 steps, 201 save points,
 trajectories written (xs, us, activities -> 28 B per unit-step, BASELINE.md byte accounting).
-A "step" = one evaluate_population pass: device flatten + fused RK4 kernel + all-gather of
-fitness.  Multi-GPU: one process per GPU (torchrun), weak scaling (8192 individuals per rank),
-the only collective is the fitness all-gather (RCCL).
+A "step" = one evaluate_population pass: device flatten + schedule + fused RK4 kernel +
+all-gather of fitness.  Multi-GPU: one process per GPU (torchrun), weak scaling (8192
+individuals per rank), the only collective is the fitness all-gather (RCCL).
+
+Other BASELINE configs (not the driver's line; for DESIGN.md): --config c2 (Acrobot static
+policy, pop 1024, 1 tree, depth <= 4, 16 rollouts) and --config c5 (64-dim SR "neural ODE":
+64 trees, max_nodes 128, depth <= 16, 8 rollouts, RK4 h = 0.01 x 200, pop 4096 per GPU =
+32768 over 8 GPUs).
 """
 from __future__ import annotations
 
@@ -28,34 +33,82 @@ PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--pop", type=int, default=8192, help="individuals per GPU")
-    ap.add_argument("--rollouts", type=int, default=32)
+    ap.add_argument("--pop", type=int, default=None, help="individuals per GPU (default: the config's)")
+    ap.add_argument("--rollouts", type=int, default=None)
     ap.add_argument("--ode-steps", type=int, default=200)
     ap.add_argument("--no-traj", action="store_true", help="fitness-only mode (early exit allowed)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    return ap.parse_args()
+    a = ap.parse_args()
+    defaults = {"c2": (1024, 16), "c3": (8192, 32), "c5": (4096, 8)}[a.config]
+    a.pop = a.pop or defaults[0]
+    a.rollouts = a.rollouts or defaults[1]
+    return a
+
+
+def _cached_population(name, make):
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mtgp_pop_{name}.npy")
+    if os.path.exists(cache):
+        return np.load(cache)
+    pop = make()
+    os.makedirs(os.path.dirname(cache), exist_ok=True)
+    np.save(cache, pop)
+    return pop
+
+
+def _sample_block(job):
+    from multitreegp_amd.sampling import sample_population
+    seed, lib, n, depth, nodes = job
+    return sample_population(seed, lib, n, 1, max_init_depth=depth, max_nodes=nodes)[0]
+
+
+def _parallel_population(seed, lib, P, depth, nodes, block=256):
+    """Reference-distribution trees, sampled in blocks of `block` individuals (seed + block id)."""
+    import multiprocessing as mp
+    jobs = [(seed * 100003 + b, lib, min(block, P - b * block), depth, nodes) for b in range((P + block - 1) // block)]
+    workers = min(16, len(jobs), os.cpu_count() or 1)
+    if workers <= 1:
+        return np.concatenate([_sample_block(j) for j in jobs])
+    with mp.get_context("fork").Pool(workers) as pool:
+        return np.concatenate(pool.map(_sample_block, jobs))
 
 
 def setup_workload(args, rank):
     import multitreegp_amd as mt
     from multitreegp_amd.sampling import sample_population
+    if args.config == "c5":
+        nv = 64
+        env = mt.LinearSystem(nv)
+        lib = mt.NodeLibrary([("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("/", None, 2, 0.1)],
+                             [[f"x{i}" for i in range(nv)]], [nv])
+        ff = mt.SREvaluator(solver=mt.RK4(), dt0=0.01)
+        x0 = env.sample_init_states(args.rollouts, np.random.default_rng(1))
+        ts = (np.arange(args.ode_steps + 1, dtype=np.float32) * np.float32(0.01)).astype(np.float32)
+        data = (x0, ts, mt.ground_truth(env, x0, ts), np.zeros((args.rollouts, 2), np.uint32))
+        pop = _cached_population(f"c5_{args.pop}_r{rank}",
+                                 lambda: _parallel_population(2000 + rank, lib, args.pop, 16, 128))
+        return env, lib, ff, data, pop
     env = mt.Acrobot(0.0, 0.0)
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
            ("cos", None, 1, 0.1)]
+    if args.config == "c2":
+        lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4"]], [1])
+        ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4(), max_steps=1000)
+        data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
+        pop = _cached_population(f"c2_{args.pop}_r{rank}",
+                                 lambda: sample_population(3000 + rank, lib, args.pop, 1, max_init_depth=4,
+                                                           max_nodes=30)[0])
+        return env, lib, ff, data, pop
     lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
     ff = mt.DynamicEvaluator(env, 2, 0.05, solver=mt.RK4(), max_steps=1000)
     data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mtgp_pop_c3_{args.pop}_r{rank}.npy")
-    if os.path.exists(cache):
-        pop = np.load(cache)
-    else:
-        pop = sample_population(1000 + rank, lib, args.pop, 1, max_init_depth=10, max_nodes=64)[0]
-        os.makedirs(os.path.dirname(cache), exist_ok=True)
-        np.save(cache, pop)
+    pop = _cached_population(f"c3_{args.pop}_r{rank}",
+                             lambda: sample_population(1000 + rank, lib, args.pop, 1, max_init_depth=10,
+                                                       max_nodes=64)[0])
     return env, lib, ff, data, pop
 
 
@@ -78,7 +131,8 @@ def cpu_baseline(args, lib, ff, data, pop):
         n = min(pop.shape[0], int(n * max(2.0, args.cpu_seconds / 4 / max(dt, 1e-3))))
     units = n * d["R"] * d["n_steps"]
     return {"value": units / dt, "unit": "ODE-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} individuals x {d['R']} rollouts x {d['n_steps']} RK4 steps of the C3 workload, "
+            "sample": f"{n} individuals x {d['R']} rollouts x {d['n_steps']} RK4 steps of the "
+                      f"{args.config.upper()} workload, "
                       f"trajectories on, oracle/mtgp_oracle.c row-order interpreter, {threads} OpenMP threads, "
                       f"{dt:.2f} s"}
 
@@ -142,20 +196,38 @@ def main():
     # roofline of the dominant kernel (the fused RK4 evaluator): algorithmic bytes per launch
     plen = res["_flat"].plen
     prog_bytes = int(plen.sum().item()) * 8 + plen.numel() * 4
-    traj_bytes = (S * P * R * (4 + 1 + 2) * 4) if traj else 0
-    io_bytes = R * (4 + 4) * 4 + S * 4 + P * 4 + P * 4
+    traj_bytes = sum(res[k].numel() * 4 for k in ("xs", "ys", "us", "acts") if k in res)  # S*P*R*(4+4+1+2)*4
+    io_bytes = sum(int(np.asarray(d[k]).nbytes) for k in ("x0", "params", "targets", "ts", "ys_true")
+                   if d.get(k) is not None) + P * 4 * 2  # rollout data + nodes in + fitness out
     alg_bytes = traj_bytes + prog_bytes + io_bytes
     kmean = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kmean / 1e3) / 1e9
     traffic = None
-    if os.path.exists(args.traffic_json):
+    tj = args.traffic_json if args.config == "c3" else args.traffic_json.replace(".json", f"_{args.config}.json")
+    if os.path.exists(tj):
         try:
-            traffic = json.load(open(args.traffic_json)).get("hbm_bytes_per_launch")
+            t = json.load(open(tj))
+            if t.get("trajectories", True) == traj:
+                traffic = t.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    workloads = {
+        "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, 3 trees, max_nodes 64, depth<=10, "
+              "RK4 h=0.05 x %d, S=%d" % (P, R, n_steps, S),
+        "c2": "C2 StaticPolicy Acrobot: pop %d/GPU x %d rollouts, 1 tree, max_nodes 30, depth<=4, "
+              "RK4 h=0.05 x %d, S=%d" % (P, R, n_steps, S),
+        "c5": "C5 64-dim SR (neural-ODE style): pop %d/GPU x %d rollouts, 64 trees, max_nodes 128, depth<=16, "
+              "RK4 h=0.01 x %d, S=%d, MSE vs a stable linear system" % (P, R, n_steps, S),
+    }
+    data_desc = {
+        "c3": "synthetic: reference-distribution random trees (numpy PCG64), x0 ~ U(-0.1,0.1)^4",
+        "c2": "synthetic: reference-distribution random trees (numpy PCG64), x0 ~ U(-0.1,0.1)^4",
+        "c5": "synthetic: reference-distribution random trees (numpy PCG64), x0 ~ N(0,1)^64, "
+              "target = fine RK4 of a random stable 64x64 linear system",
+    }
 
     out = {
-        "metric": "population x rollout ODE-steps/sec (C3 DynamicPolicy Acrobot, fixed-step RK4)",
+        "metric": "population x rollout ODE-steps/sec (fixed-step RK4)",
         "value": value,
         "unit": "ODE-steps/s",
         "n_gpus": ws,
@@ -166,11 +238,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic: reference-distribution random trees (numpy PCG64), x0 ~ U(-0.1,0.1)^4",
-        "config": {"workload": "C3 DynamicPolicy Acrobot: pop 8192/GPU x 32 rollouts, 3 trees, max_nodes 64, "
-                               "depth<=10, RK4 h=0.05 x 200, S=201, trajectories on" if traj else
-                               "C3 fitness-only", "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps,
-                   "trajectories": traj, "parallelism": f"population-sharded dp{ws}"},
+        "data": data_desc[args.config],
+        "config": {"workload": workloads[args.config] + (", trajectories on" if traj else ", fitness only"),
+                   "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps, "trajectories": traj,
+                   "parallelism": f"population-sharded dp{ws}"},
         "kernel_ms": kmean,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,

@@ -35,69 +35,82 @@ def create_map_b_to_d(depth: int) -> np.ndarray:
 
 def _prune(tree: np.ndarray, max_nodes: int) -> np.ndarray:
     """prune_tree (initialization.py:56-98): keep non-empty rows, highest first, at the end."""
-    keep = [j for j in range(tree.shape[0] - 1, -1, -1) if tree[j, 0] != 0]
-    n = len(keep)
-    out = np.tile(np.array([0.0, -1.0, -1.0, 0.0], dtype=np.float32), (max_nodes, 1))
-    new_pos = {}
-    for rank, j in enumerate(keep):
-        new_pos[j] = max_nodes - 1 - rank
-    for j in keep:
-        row = tree[j].copy()
-        for c in (1, 2):
-            if row[c] > -1:
-                row[c] = new_pos[int(row[c])]
-        out[new_pos[j]] = row
+    keep = np.nonzero(tree[:, 0] != 0)[0][::-1]  # rows in descending order
+    n = keep.size
     assert n <= max_nodes
+    out = np.tile(np.array([0.0, -1.0, -1.0, 0.0], dtype=np.float32), (max_nodes, 1))
+    new_pos = np.full(tree.shape[0], -1, dtype=np.int64)
+    new_pos[keep] = max_nodes - 1 - np.arange(n)
+    rows = tree[keep].copy()
+    for c in (1, 2):
+        m = rows[:, c] > -1
+        rows[m, c] = new_pos[rows[m, c].astype(np.int64)]
+    out[new_pos[keep]] = rows
     return out
 
 
 def sample_tree(rng: np.random.Generator, lib: NodeLibrary, var_mask: np.ndarray, max_init_depth: int,
                 max_nodes: int, coefficient_sd: float = 1.0, map_b_to_d: np.ndarray = None) -> np.ndarray:
-    """sample_tree (initialization.py:100-124) for one tree with allowed-variable mask."""
+    """sample_tree (initialization.py:100-124) for one tree with allowed-variable mask.
+
+    The breadth-first sampling visits only the rows it fills, so they are kept sparsely
+    (row -> [f, a, b, value]) and pruned directly (prune_tree, initialization.py:56-98):
+    non-empty rows, highest first, packed at the end of max_nodes rows."""
     if map_b_to_d is None:
         map_b_to_d = create_map_b_to_d(max_init_depth)
     tree_size = 2 ** max_init_depth - 1
-    tree = np.zeros((tree_size, 4), dtype=np.float32)
     slots = lib.slots
     op_p = lib.operator_probabilities.astype(np.float64)
     op_p = op_p / op_p.sum()
     var_p = var_mask.astype(np.float64)
     var_p = var_p / var_p.sum()
-    # bulk draws (the reference splits a key per node; only the distribution matters here)
-    coef = (rng.standard_normal(tree_size) * coefficient_sd).astype(np.float32)
-    u_leaf = rng.random(tree_size)
-    u_var = rng.random(tree_size)
-    u_node = rng.random(tree_size)
-    u_op = rng.random(tree_size)
+    # bulk draws (the reference splits a key per node; only the distribution matters here):
+    # one chunk for trees of depth <= 10, chunks of 64 nodes for deeper ones (most deep trees
+    # stop after a few dozen nodes, and the chunked stream keeps sampling O(tree) not O(2^depth))
+    chunk = tree_size if tree_size <= 1023 else 64
+
+    def draws():
+        return ((rng.standard_normal(chunk) * coefficient_sd).astype(np.float32), rng.random(chunk),
+                rng.random(chunk), rng.random(chunk), rng.random(chunk))
+
     var_cdf = np.cumsum(var_p)
     op_cdf = np.cumsum(op_p)
     nv, no = len(var_cdf), len(op_cdf)
+    rows = {}
     open_slots = 1
     for i in range(tree_size):
         if open_slots == 0:
             break  # every remaining node is empty and pruned away
-        _i = int(map_b_to_d[i])
+        if i % chunk == 0:
+            coef, u_leaf, u_var, u_node, u_op = draws()
+        j = i % chunk
         depth = (i + 1).bit_length() - 1
-        if u_leaf[i] < 0.5:
+        if u_leaf[j] < 0.5:
             leaf = 1
         else:
-            leaf = int(lib.variable_indices[min(int(np.searchsorted(var_cdf, u_var[i], side="right")), nv - 1)])
-        if (open_slots < max_nodes - i - 1) and (depth + 1 < max_init_depth) and u_node[i] < 0.7 ** depth:
-            index = int(lib.operator_indices[min(int(np.searchsorted(op_cdf, u_op[i], side="right")), no - 1)])
+            leaf = int(lib.variable_indices[min(int(np.searchsorted(var_cdf, u_var[j], side="right")), nv - 1)])
+        if (open_slots < max_nodes - i - 1) and (depth + 1 < max_init_depth) and u_node[j] < 0.7 ** depth:
+            index = int(lib.operator_indices[min(int(np.searchsorted(op_cdf, u_op[j], side="right")), no - 1)])
         else:
             index = leaf
         if i > 0:
-            parent_row = int(map_b_to_d[(i + (i % 2) - 2) // 2])
-            if not (slots[max(int(tree[parent_row, 0]), 0)] + i % 2) > 1:
+            parent = rows.get(int(map_b_to_d[(i + (i % 2) - 2) // 2]))
+            if not (slots[max(int(parent[0]) if parent else 0, 0)] + i % 2) > 1:
                 index = 0
-        tree[_i, 1] = map_b_to_d[2 * i + 1] if slots[index] > 0 else -1
-        tree[_i, 2] = map_b_to_d[2 * i + 2] if slots[index] > 1 else -1
-        if index == 1:
-            tree[_i, 3] = coef[i]
-        tree[_i, 0] = index
         if index != 0:
+            rows[int(map_b_to_d[i])] = (index,
+                                        int(map_b_to_d[2 * i + 1]) if slots[index] > 0 else -1,
+                                        int(map_b_to_d[2 * i + 2]) if slots[index] > 1 else -1,
+                                        coef[j] if index == 1 else 0.0)
             open_slots = max(0, open_slots + int(slots[index]) - 1)
-    return _prune(tree, max_nodes)
+    keep = sorted(rows, reverse=True)
+    assert len(keep) <= max_nodes
+    new_pos = {r: max_nodes - 1 - k for k, r in enumerate(keep)}
+    out = np.tile(np.array([0.0, -1.0, -1.0, 0.0], dtype=np.float32), (max_nodes, 1))
+    for r in keep:
+        f, a, b, v = rows[r]
+        out[new_pos[r]] = (f, new_pos[a] if a > -1 else -1, new_pos[b] if b > -1 else -1, v)
+    return out
 
 
 def sample_population(seed: int, lib: NodeLibrary, population_size: int, num_populations: int = 1,
