@@ -51,27 +51,27 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 // One instruction: `w` = opcode, `ib` = imm bits (f32 constant, or the data slot's LDS byte
 // offset for V opcodes).  Expanded inline at each of the four block positions; END leaves the
 // program (so there is no per-instruction length test).
-#define MTGP_EXEC(w, ib)                                                                          \
+#define MTGP_VOPND(k, ib) (*(const float*)((const char*)dcol + (ib)))
+#define MTGP_EXEC(k, w, ib)                                                                       \
   {                                                                                               \
     const float imm_ = __uint_as_float(ib);                                                       \
-    const float* dv_ = (const float*)((const char*)dcol + (ib));                                  \
     switch (w) {                                                                                  \
       case MTGP_OP_LDC: acc = imm_; break;                                                        \
       case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; acc = imm_; break;                           \
-      case MTGP_OP_LDV: acc = *dv_; break;                                                        \
-      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = *dv_; break;                           \
+      case MTGP_OP_LDV: acc = MTGP_VOPND(k, ib); break;                                           \
+      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = MTGP_VOPND(k, ib); break;              \
       case MTGP_OP_ADDC: acc = acc + imm_; break;                                                 \
       case MTGP_OP_SUBC: acc = acc - imm_; break;                                                 \
       case MTGP_OP_RSUBC: acc = imm_ - acc; break;                                                \
       case MTGP_OP_MULC: acc = acc * imm_; break;                                                 \
       case MTGP_OP_DIVC: acc = acc / imm_; break;                                                 \
       case MTGP_OP_RDIVC: acc = imm_ / acc; break;                                                \
-      case MTGP_OP_ADDV: acc = acc + *dv_; break;                                                 \
-      case MTGP_OP_SUBV: acc = acc - *dv_; break;                                                 \
-      case MTGP_OP_RSUBV: acc = *dv_ - acc; break;                                                \
-      case MTGP_OP_MULV: acc = acc * *dv_; break;                                                 \
-      case MTGP_OP_DIVV: acc = acc / *dv_; break;                                                 \
-      case MTGP_OP_RDIVV: acc = *dv_ / acc; break;                                                \
+      case MTGP_OP_ADDV: acc = acc + MTGP_VOPND(k, ib); break;                                                 \
+      case MTGP_OP_SUBV: acc = acc - MTGP_VOPND(k, ib); break;                                                 \
+      case MTGP_OP_RSUBV: acc = MTGP_VOPND(k, ib) - acc; break;                                                \
+      case MTGP_OP_MULV: acc = acc * MTGP_VOPND(k, ib); break;                                                 \
+      case MTGP_OP_DIVV: acc = acc / MTGP_VOPND(k, ib); break;                                                 \
+      case MTGP_OP_RDIVV: acc = MTGP_VOPND(k, ib) / acc; break;                                                \
       case MTGP_OP_ADDS: --sp; acc = acc + st[sp * kWave]; break;                                 \
       case MTGP_OP_SUBS: --sp; acc = acc - st[sp * kWave]; break;                                 \
       case MTGP_OP_RSUBS: --sp; acc = st[sp * kWave] - acc; break;                                \
@@ -97,10 +97,10 @@ __device__ __forceinline__ float run_prog(const MtgpInstr* code, const float* dc
   int sp = 0;
   for (;; ++blk) {
     const u8v c = *blk;
-    MTGP_EXEC(c[0], c[1])
-    MTGP_EXEC(c[2], c[3])
-    MTGP_EXEC(c[4], c[5])
-    MTGP_EXEC(c[6], c[7])
+    MTGP_EXEC(0, c[0], c[1])
+    MTGP_EXEC(1, c[2], c[3])
+    MTGP_EXEC(2, c[4], c[5])
+    MTGP_EXEC(3, c[6], c[7])
   }
 done:
   return acc;
@@ -233,7 +233,19 @@ __device__ __forceinline__ bool save_incl(const float* ts, int k) {
 struct Lane {
   int wave, lane, Rp, G, q0, g, r, p, rr;
   bool active;
+  uint32_t ptab;  // lane gi (< G): byte offset of group gi's program block in A.prog
 };
+
+#ifndef MTGP_V_PTAB
+#define MTGP_V_PTAB 1
+#endif
+
+// program-block offsets of the wave's groups, one per lane (read back with v_readlane)
+__device__ __forceinline__ uint32_t prog_table(const KArgs& A, const Lane& L) {
+  const int q = L.q0 + L.lane;
+  const int ind = (L.lane < L.G && q < A.P) ? (A.ro.order ? A.ro.order[q] : q) : 0;
+  return (uint32_t)ind * (uint32_t)A.n_prog * (uint32_t)A.L * (uint32_t)sizeof(MtgpInstr);
+}
 
 __device__ __forceinline__ int sched_ind(const KArgs& A, int q) { return A.ro.order ? A.ro.order[q] : q; }
 
@@ -252,6 +264,7 @@ __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.p = q < A.P ? sched_ind(A, q) : A.P;  // A.P marks a padding group
   L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
+  L.ptab = prog_table(A, L);
   return true;
 }
 
@@ -279,8 +292,14 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 // Run program `slot` of group gi (its individual's program, wave-uniform).
 __device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
                                          float* st) {
+#if MTGP_V_PTAB
+  const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.ptab, gi) +
+                       (uint32_t)slot * (uint32_t)A.L * (uint32_t)sizeof(MtgpInstr);
+  return run_prog((const MtgpInstr*)((const char*)A.prog + off), dcol, st);
+#else
   const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
   return run_prog(A.prog + pj * A.L, dcol, st);
+#endif
 }
 
 #ifndef MTGP_V_NOINTERP
@@ -653,6 +672,7 @@ __device__ __forceinline__ bool lane_setup_wide(const KArgs& A, Lane& L) {
   L.p = q < A.P ? sched_ind(A, q) : A.P;
   L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
+  L.ptab = prog_table(A, L);
   return true;
 }
 
@@ -994,6 +1014,7 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
   if (P < 0 || n_prog <= 0 || L <= 0 || (L & 3) != 0) return MTGP_ERR_ARG;
   if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
   if ((int64_t)P * rollouts->R > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
+  if ((int64_t)P * n_prog * L * (int64_t)sizeof(MtgpInstr) > UINT32_MAX) return MTGP_ERR_ARG;  // 32-bit program offsets
   if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
   if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
   if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;
