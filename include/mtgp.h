@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 3
+#define MTGP_ABI_VERSION 4
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -78,24 +78,19 @@ typedef struct {
 } MtgpProgramSpec;
 
 /* ------------------------------------------------------------ program format */
-/* Accumulator machine, postorder with leaves folded into their parent.
- *   op : the opcode (MTGP_OP_*), nothing else -- the evaluator switches on the raw word.
- *   imm: *C opcodes: the f32 constant; *V opcodes: the data slot as a u32 byte offset
- *        slot * MTGP_SLOT_BYTES (the evaluator's LDS column stride), so no decode is needed;
- *        other opcodes: 0.
- * Every program ends with MTGP_OP_END (not counted in its length), so a program slot holds
- * at most L - 1 instructions.  The program stride L must be a multiple of 4: the evaluators
- * fetch instructions in blocks of four (one 32-byte scalar load). */
+/* Accumulator machine, postorder with leaves folded into their parent, adjacent leaf
+ * load + leaf operation fused into one superinstruction.
+ *   op : opcode << MTGP_OP_SHIFT | aux.  aux (24 bits) = the second operand of the fused
+ *        forms: VC*_f / SINV / COSV: aux = slot of V;  VV*_f: aux = slot of the right operand.
+ *   imm: C forms and VC*: the f32 constant; V forms, VV* (left operand), SINV/COSV: the data
+ *        slot as a u32.
+ * Slots are stored as byte offsets slot * MTGP_SLOT_BYTES (the evaluator's LDS column stride),
+ * so a handler addresses its operand without decoding.  Every program ends with MTGP_OP_END
+ * (not counted in its length), so a program slot holds at most L - 1 instructions.  The program
+ * stride L must be a multiple of 4: the evaluators fetch four instructions per scalar load.
+ * Opcode values come from scripts/gen_opcodes.py (a frequency-shaped dispatch tree). */
 #define MTGP_SLOT_BYTES 256u
-enum {
-  MTGP_OP_LDC = 0, MTGP_OP_LDCP, MTGP_OP_LDV, MTGP_OP_LDVP, /* P = push acc first */
-  MTGP_OP_ADDC, MTGP_OP_SUBC, MTGP_OP_RSUBC, MTGP_OP_MULC, MTGP_OP_DIVC, MTGP_OP_RDIVC,
-  MTGP_OP_ADDV, MTGP_OP_SUBV, MTGP_OP_RSUBV, MTGP_OP_MULV, MTGP_OP_DIVV, MTGP_OP_RDIVV,
-  MTGP_OP_ADDS, MTGP_OP_SUBS, MTGP_OP_RSUBS, MTGP_OP_MULS, MTGP_OP_DIVS, MTGP_OP_RDIVS,
-  MTGP_OP_SIN, MTGP_OP_COS,
-  MTGP_OP_END,
-  MTGP_OP_COUNT
-};
+#include "mtgp_opcodes.h"
 typedef struct {
   uint32_t op;
   float imm;

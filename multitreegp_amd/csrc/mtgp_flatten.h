@@ -156,8 +156,28 @@ MTGP_INLINE MTGP_HD void size_row(int i, RowInfo* info) {
   else { r.afirst = 0; r.need = (uint8_t)((q > p + 1) ? q : p + 1); }
 }
 
+// Opcode of family member idx (ADD, SUB, RSUB, MUL, DIV, RDIV) for operand kind C / V / S and
+// of the fused forms (opcode values are generated, not contiguous).
+enum { FK_C = 0, FK_V = 1, FK_S = 2, FK_VC = 3, FK_VCP = 4 };
+MTGP_INLINE MTGP_HD uint32_t fam_op(int kind, int idx) {
+  switch (kind) {
+    case FK_C: { const uint32_t t[6] = {MTGP_OP_ADDC, MTGP_OP_SUBC, MTGP_OP_RSUBC, MTGP_OP_MULC, MTGP_OP_DIVC, MTGP_OP_RDIVC}; return t[idx]; }
+    case FK_V: { const uint32_t t[6] = {MTGP_OP_ADDV, MTGP_OP_SUBV, MTGP_OP_RSUBV, MTGP_OP_MULV, MTGP_OP_DIVV, MTGP_OP_RDIVV}; return t[idx]; }
+    case FK_S: { const uint32_t t[6] = {MTGP_OP_ADDS, MTGP_OP_SUBS, MTGP_OP_RSUBS, MTGP_OP_MULS, MTGP_OP_DIVS, MTGP_OP_RDIVS}; return t[idx]; }
+    case FK_VC: { const uint32_t t[6] = {MTGP_OP_VC_ADD, MTGP_OP_VC_SUB, MTGP_OP_VC_RSUB, MTGP_OP_VC_MUL, MTGP_OP_VC_DIV, MTGP_OP_VC_RDIV}; return t[idx]; }
+    default: { const uint32_t t[6] = {MTGP_OP_VCP_ADD, MTGP_OP_VCP_SUB, MTGP_OP_VCP_RSUB, MTGP_OP_VCP_MUL, MTGP_OP_VCP_DIV, MTGP_OP_VCP_RDIV}; return t[idx]; }
+  }
+}
+
+// family index of a C / V opcode (-1 if op is not one)
+MTGP_INLINE MTGP_HD int fam_idx(uint32_t op, int kind) {
+  for (int i = 0; i < 6; ++i)
+    if (fam_op(kind, i) == op) return i;
+  return -1;
+}
+
 MTGP_INLINE MTGP_HD bool is_var_op(uint32_t op) {
-  return op == MTGP_OP_LDV || op == MTGP_OP_LDVP || (op >= MTGP_OP_ADDV && op <= MTGP_OP_RDIVV);
+  return op == MTGP_OP_LDV || op == MTGP_OP_LDVP || fam_idx(op, FK_V) >= 0;
 }
 
 MTGP_INLINE MTGP_HD float bits_to_f32(uint32_t u) {
@@ -173,7 +193,10 @@ struct Emitter {
   int pending_push;
   MTGP_HD void put(uint32_t op, uint32_t slot, float imm) {
     // V opcodes carry the slot as an LDS byte offset (mtgp.h program format)
-    if (n < cap) { out[n].op = op; out[n].imm = is_var_op(op) ? bits_to_f32(slot * MTGP_SLOT_BYTES) : imm; }
+    if (n < cap) {
+      out[n].op = op << MTGP_OP_SHIFT;
+      out[n].imm = is_var_op(op) ? bits_to_f32(slot * MTGP_SLOT_BYTES) : imm;
+    }
     ++n;
   }
   // load a leaf operand into acc (pushing the previous acc when a push is pending)
@@ -195,10 +218,10 @@ struct Emitter {
       case MTGP_FN_MUL: base = 3; rev = 0; break;
       default: base = 4; break;  // DIV
     }
-    // layout within a family: ADD, SUB, RSUB, MUL, DIV, RDIV
+    // family members: ADD, SUB, RSUB, MUL, DIV, RDIV
     int idx = base + ((base == 1 || base == 4) ? rev : 0);
-    if (isc) put(MTGP_OP_ADDC + idx, 0, v);
-    else put(MTGP_OP_ADDV + idx, info[x.row].slot, 0.0f);
+    if (isc) put(fam_op(FK_C, idx), 0, v);
+    else put(fam_op(FK_V, idx), info[x.row].slot, 0.0f);
   }
   MTGP_HD void op_stack(int fn, int rev) {
     int idx;
@@ -208,7 +231,7 @@ struct Emitter {
       case MTGP_FN_MUL: idx = 3; break;
       default: idx = rev ? 5 : 4; break;
     }
-    put(MTGP_OP_ADDS + idx, 0, 0.0f);
+    put(fam_op(FK_S, idx), 0, 0.0f);
   }
 };
 
@@ -308,13 +331,80 @@ MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNo
   return n;
 }
 
+// Superinstructions (peephole over an emitted program): a leaf load followed by the leaf
+// operation or unary that consumes it becomes one instruction.  Exact: the fused handler
+// performs the same single fp32 operation on the same operands; the only rewrites swap the
+// operands of + and * (commutative in IEEE arithmetic, signed zeros included) or turn
+// "c - v" / "c / v" into the reversed VC forms.
+MTGP_INLINE MTGP_HD bool fuse_pair(const MtgpInstr& a, const MtgpInstr& b, MtgpInstr* f) {
+  const uint32_t oa = a.op >> MTGP_OP_SHIFT, ob = b.op >> MTGP_OP_SHIFT;
+  uint32_t ia, ib;
+  __builtin_memcpy(&ia, &a.imm, 4);
+  __builtin_memcpy(&ib, &b.imm, 4);
+  const bool push = (oa == MTGP_OP_LDVP || oa == MTGP_OP_LDCP);
+  if (oa == MTGP_OP_LDV || oa == MTGP_OP_LDVP) {  // acc = v_a ...
+    const int kc = fam_idx(ob, FK_C);
+    if (kc >= 0) {  // ... op c
+      f->op = (fam_op(push ? FK_VCP : FK_VC, kc) << MTGP_OP_SHIFT) | ia;
+      f->imm = b.imm;
+      return true;
+    }
+    const int kv = fam_idx(ob, FK_V);
+    if (kv >= 0) {  // ... op v_b  ->  VV(left, right)
+      uint32_t l = ia, r = ib, op;
+      switch (kv) {
+        case 0: op = push ? MTGP_OP_VVP_ADD : MTGP_OP_VV_ADD; break;
+        case 1: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; break;
+        case 2: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; l = ib; r = ia; break;  // v_b - v_a
+        case 3: op = push ? MTGP_OP_VVP_MUL : MTGP_OP_VV_MUL; break;
+        case 4: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; break;
+        default: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; l = ib; r = ia; break;  // v_b / v_a
+      }
+      f->op = (op << MTGP_OP_SHIFT) | r;
+      f->imm = bits_to_f32(l);
+      return true;
+    }
+    if (ob == MTGP_OP_SIN || ob == MTGP_OP_COS) {
+      const uint32_t op = ob == MTGP_OP_SIN ? (push ? MTGP_OP_SINVP : MTGP_OP_SINV) : (push ? MTGP_OP_COSVP : MTGP_OP_COSV);
+      f->op = op << MTGP_OP_SHIFT;
+      f->imm = a.imm;
+      return true;
+    }
+    return false;
+  }
+  if (oa == MTGP_OP_LDC || oa == MTGP_OP_LDCP) {  // acc = c op v_b
+    const int kv = fam_idx(ob, FK_V);
+    if (kv < 0) return false;
+    const int map[6] = {0, 2, 1, 3, 5, 4};  // c+v = v+c, c-v = RSUB, v-c = SUB, c*v, c/v = RDIV, v/c = DIV
+    f->op = (fam_op(push ? FK_VCP : FK_VC, map[kv]) << MTGP_OP_SHIFT) | ib;
+    f->imm = a.imm;
+    return true;
+  }
+  return false;
+}
+
+MTGP_INLINE MTGP_HD int fuse_program(MtgpInstr* out, int n) {
+  int j = 0;
+  for (int i = 0; i < n;) {
+    MtgpInstr f;
+    if (i + 1 < n && fuse_pair(out[i], out[i + 1], &f)) {
+      out[j++] = f;
+      i += 2;
+    } else {
+      out[j++] = out[i++];
+    }
+  }
+  return j;
+}
+
 MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLibrary* lib,
                                      int n_data, uint64_t zero_mask, MtgpInstr* out, int slots,
                                      RowInfo* info, int* stack_need) {
   if (slots < 1) return -MTGP_ERR_PROG_TOO_LONG;
-  const int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
+  int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
+  if (n > 0) n = fuse_program(out, n);
   const int at = n > 0 ? n : 0;
-  out[at].op = MTGP_OP_END;
+  out[at].op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
   out[at].imm = 0.0f;
   return n;
 }

@@ -48,41 +48,11 @@ __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlan
 //    instruction stream; issue, not branch latency, bounds this loop).
 //  * per-instruction scalar loads (no blocks): 6-10% slower; a VGPR-lane program cache: 15%
 //    slower; data vector in VGPRs behind a scalar branch tree: 2% slower.
-// One instruction: `w` = opcode, `ib` = imm bits (f32 constant, or the data slot's LDS byte
-// offset for V opcodes).  Expanded inline at each of the four block positions; END leaves the
-// program (so there is no per-instruction length test).
-#define MTGP_VOPND(k, ib) (*(const float*)((const char*)dcol + (ib)))
-#define MTGP_EXEC(k, w, ib)                                                                       \
-  {                                                                                               \
-    const float imm_ = __uint_as_float(ib);                                                       \
-    switch (w) {                                                                                  \
-      case MTGP_OP_LDC: acc = imm_; break;                                                        \
-      case MTGP_OP_LDCP: st[sp * kWave] = acc; ++sp; acc = imm_; break;                           \
-      case MTGP_OP_LDV: acc = MTGP_VOPND(k, ib); break;                                           \
-      case MTGP_OP_LDVP: st[sp * kWave] = acc; ++sp; acc = MTGP_VOPND(k, ib); break;              \
-      case MTGP_OP_ADDC: acc = acc + imm_; break;                                                 \
-      case MTGP_OP_SUBC: acc = acc - imm_; break;                                                 \
-      case MTGP_OP_RSUBC: acc = imm_ - acc; break;                                                \
-      case MTGP_OP_MULC: acc = acc * imm_; break;                                                 \
-      case MTGP_OP_DIVC: acc = acc / imm_; break;                                                 \
-      case MTGP_OP_RDIVC: acc = imm_ / acc; break;                                                \
-      case MTGP_OP_ADDV: acc = acc + MTGP_VOPND(k, ib); break;                                                 \
-      case MTGP_OP_SUBV: acc = acc - MTGP_VOPND(k, ib); break;                                                 \
-      case MTGP_OP_RSUBV: acc = MTGP_VOPND(k, ib) - acc; break;                                                \
-      case MTGP_OP_MULV: acc = acc * MTGP_VOPND(k, ib); break;                                                 \
-      case MTGP_OP_DIVV: acc = acc / MTGP_VOPND(k, ib); break;                                                 \
-      case MTGP_OP_RDIVV: acc = MTGP_VOPND(k, ib) / acc; break;                                                \
-      case MTGP_OP_ADDS: --sp; acc = acc + st[sp * kWave]; break;                                 \
-      case MTGP_OP_SUBS: --sp; acc = acc - st[sp * kWave]; break;                                 \
-      case MTGP_OP_RSUBS: --sp; acc = st[sp * kWave] - acc; break;                                \
-      case MTGP_OP_MULS: --sp; acc = acc * st[sp * kWave]; break;                                 \
-      case MTGP_OP_DIVS: --sp; acc = acc / st[sp * kWave]; break;                                 \
-      case MTGP_OP_RDIVS: --sp; acc = st[sp * kWave] / acc; break;                                \
-      case MTGP_OP_SIN: acc = mtgp_sinf(acc); break;                                              \
-      case MTGP_OP_COS: acc = mtgp_cosf(acc); break;                                              \
-      default: goto done; /* MTGP_OP_END */                                                       \
-    }                                                                                             \
-  }
+// One instruction: the generated dispatch tree (scripts/gen_opcodes.py -> mtgp_dispatch.inc):
+// range compares on the raw word w = opcode << 24 | aux, shaped by measured opcode
+// frequencies; each leaf is the opcode's 1-3 instruction handler.  Expanded inline at each of
+// the four block positions; END leaves the program (no per-instruction length test).
+#include "mtgp_dispatch.inc"
 
 // Programs are read through the constant address space so the wave-uniform fetch is a
 // scalar load (K$), four instructions (32 B) per s_load_dwordx8.  The program stride L is a
@@ -97,10 +67,10 @@ __device__ __forceinline__ float run_prog(const MtgpInstr* code, const float* dc
   int sp = 0;
   for (;; ++blk) {
     const u8v c = *blk;
-    MTGP_EXEC(0, c[0], c[1])
-    MTGP_EXEC(1, c[2], c[3])
-    MTGP_EXEC(2, c[4], c[5])
-    MTGP_EXEC(3, c[6], c[7])
+    MTGP_DISPATCH(c[0], c[1])
+    MTGP_DISPATCH(c[2], c[3])
+    MTGP_DISPATCH(c[4], c[5])
+    MTGP_DISPATCH(c[6], c[7])
   }
 done:
   return acc;

@@ -17,44 +17,38 @@ def _cos(x):
     return orc.sincos(np.array([x], np.float32))[1][0]
 
 
+_FAM = {"ADD": lambda x, y: x + y, "SUB": lambda x, y: x - y, "RSUB": lambda x, y: y - x,
+        "MUL": lambda x, y: x * y, "DIV": lambda x, y: x / y, "RDIV": lambda x, y: y / x}
+
+
 def run(prog, data):
+    """prog: decoded instructions (name, a, b) from _native.decode_instr."""
     acc = f32(0)
     st = []
     d = [f32(v) for v in np.asarray(data, np.float32).reshape(-1)]
     with np.errstate(all="ignore"):
-        for name, slot, imm in prog:
-            imm = f32(imm)
-            fam = name[:-1] if name[-1] in "CVS" and name not in ("LDC", "LDV") else name
-            if name in ("LDCP", "LDVP"):
+        for name, a, b in prog:
+            if name in ("LDCP", "LDVP", "SINVP", "COSVP") or name.startswith(("VCP_", "VVP_")):
                 st.append(acc)
             if name in ("LDC", "LDCP"):
-                acc = imm
-                continue
-            if name in ("LDV", "LDVP"):
-                acc = d[slot]
-                continue
-            if name == "SIN":
+                acc = f32(b)
+            elif name in ("LDV", "LDVP"):
+                acc = d[a]
+            elif name == "SIN":
                 acc = _sin(acc)
-                continue
-            if name == "COS":
+            elif name == "COS":
                 acc = _cos(acc)
-                continue
-            kind = name[-1]
-            opnd = imm if kind == "C" else (d[slot] if kind == "V" else st.pop())
-            fam = name[:-1]
-            if fam == "ADD":
-                acc = f32(acc + opnd)
-            elif fam == "SUB":
-                acc = f32(acc - opnd)
-            elif fam == "RSUB":
-                acc = f32(opnd - acc)
-            elif fam == "MUL":
-                acc = f32(acc * opnd)
-            elif fam == "DIV":
-                acc = f32(acc / opnd)
-            elif fam == "RDIV":
-                acc = f32(opnd / acc)
+            elif name in ("SINV", "SINVP"):
+                acc = _sin(d[a])
+            elif name in ("COSV", "COSVP"):
+                acc = _cos(d[a])
+            elif name.startswith(("VC_", "VCP_")):
+                acc = f32(_FAM[name.split("_")[1]](d[a], f32(b)))
+            elif name.startswith(("VV_", "VVP_")):
+                acc = f32(_FAM[name.split("_")[1]](d[a], d[b]))
             else:
-                raise ValueError(name)
+                fam, kind = name[:-1], name[-1]
+                opnd = f32(b) if kind == "C" else (d[a] if kind == "V" else st.pop())
+                acc = f32(_FAM[fam](acc, opnd))
     assert not st, "stack not empty at program end"
     return f32(acc)

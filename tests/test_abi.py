@@ -73,9 +73,20 @@ def test_constants_match_header():
     assert _define(text, "MTGP_SCHED_SCRATCH") == nat.SCHED_SCRATCH
     assert _define(text, "MTGP_MAX_PROGRAMS") == nat.MAX_PROGRAMS
     assert _define(text, "MTGP_STACK_MAX") == nat.STACK_MAX
-    enum = re.search(r"MTGP_OP_LDC = 0,(.*?)MTGP_OP_COUNT", text, re.S).group(1)
-    names = ["LDC"] + re.findall(r"MTGP_OP_(\w+)", enum)
-    assert names == nat.OP_NAMES
+    ops = open(os.path.join(ROOT, "include", "mtgp_opcodes.h")).read()
+    pairs = re.findall(r"MTGP_OP_(\w+) = (\d+),", ops)
+    assert [n for n, _ in pairs] == nat.OP_NAMES and [int(v) for _, v in pairs] == list(range(len(pairs)))
+
+
+def test_generated_opcode_files_up_to_date():
+    """include/mtgp_opcodes.h, csrc/mtgp_dispatch.inc and _opcodes.py match scripts/gen_opcodes.py."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_opcodes", os.path.join(ROOT, "scripts", "gen_opcodes.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    out = gen.generate()
+    for path, i in gen.targets().items():
+        assert open(path).read() == out[i], f"{path} is stale: run scripts/gen_opcodes.py"
 
 
 def test_unaligned_program_stride_rejected():

@@ -90,6 +90,8 @@ def test_stack_limit_and_length_errors():
     with pytest.raises(ValueError, match=str(-nat.ERR_STACK)):
         nat.flatten_tree_host(t, nl, 4, L=1 << 14)
     prog, need = nat.flatten_tree_host(t[:8], nl, 4, L=1 << 14)  # need 6: fine, but 191 instructions
-    assert need == 6 and len(prog) == 191  # len(k) = 2 len(k-1) + 1, len(1) = 2
+    # emitted: len(k) = 2 len(k-1) + 1, len(1) = 2 -> 191; the 64 leaf pairs fuse -> 127
+    assert need == 6 and len(prog) == 127 and sum(n == "VV_ADD" or n == "VVP_ADD" for n, _, _ in prog) == 64
+    # the length cap applies to the program as emitted (before fusion)
     with pytest.raises(ValueError, match=str(-nat.ERR_PROG_TOO_LONG)):
         nat.flatten_tree_host(t[:8], nl, 4, L=64)
