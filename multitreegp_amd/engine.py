@@ -105,7 +105,9 @@ class DeviceEngine:
         n_prog = len(specs)
         L = (2 * N + 8 + 3) // 4 * 4  # multiple of 4: block-fetch fast path (mtgp.h)
         dev = self.device
-        prog = torch.empty((P, n_prog, L, 2), dtype=torch.int32, device=dev)
+        # one spare 32-byte block after the last program: a block prefetch never leaves the buffer
+        prog_buf = torch.empty((P * n_prog * L * 2 + 8,), dtype=torch.int32, device=dev)
+        prog = prog_buf[: P * n_prog * L * 2].view(P, n_prog, L, 2)
         plen = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
         nodes = torch.empty((P,), dtype=torch.int32, device=dev)
         status = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
