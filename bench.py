@@ -40,6 +40,8 @@ def parse():
     ap.add_argument("--rollouts", type=int, default=None)
     ap.add_argument("--ode-steps", type=int, default=200)
     ap.add_argument("--no-traj", action="store_true", help="fitness-only mode (early exit allowed)")
+    ap.add_argument("--obs-noise", type=float, default=0.0,
+                    help="Acrobot observation noise (the notebooks use 0.1): in-kernel threefry normals per stage")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
@@ -92,7 +94,7 @@ def setup_workload(args, rank):
         pop = _cached_population(f"c5_{args.pop}_r{rank}",
                                  lambda: _parallel_population(2000 + rank, lib, args.pop, 16, 128))
         return env, lib, ff, data, pop
-    env = mt.Acrobot(0.0, 0.0)
+    env = mt.Acrobot(0.0, args.obs_noise)
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
            ("cos", None, 1, 0.1)]
     if args.config == "c2":
@@ -197,14 +199,15 @@ def main():
     plen = res["_flat"].plen
     prog_bytes = int(plen.sum().item()) * 8 + plen.numel() * 4
     traj_bytes = sum(res[k].numel() * 4 for k in ("xs", "ys", "us", "acts") if k in res)  # S*P*R*(4+4+1+2)*4
-    io_bytes = sum(int(np.asarray(d[k]).nbytes) for k in ("x0", "params", "targets", "ts", "ys_true")
+    io_bytes = sum(int(np.asarray(d[k]).nbytes) for k in ("x0", "params", "targets", "ts", "ys_true", "obs_keys",
+                                                           "obs_w")
                    if d.get(k) is not None) + P * 4 * 2  # rollout data + nodes in + fitness out
     alg_bytes = traj_bytes + prog_bytes + io_bytes
     kmean = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kmean / 1e3) / 1e9
     traffic = None
     tj = args.traffic_json if args.config == "c3" else args.traffic_json.replace(".json", f"_{args.config}.json")
-    if os.path.exists(tj):
+    if os.path.exists(tj) and not args.obs_noise:
         try:
             t = json.load(open(tj))
             if t.get("trajectories", True) == traj:
@@ -239,7 +242,8 @@ def main():
         "vs_baseline": None,
         "dtype": "f32",
         "data": data_desc[args.config],
-        "config": {"workload": workloads[args.config] + (", trajectories on" if traj else ", fitness only"),
+        "config": {"workload": workloads[args.config] + (", trajectories on" if traj else ", fitness only")
+                   + (f", obs_noise {args.obs_noise} (threefry in-kernel)" if args.obs_noise else ""),
                    "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps, "trajectories": traj,
                    "parallelism": f"population-sharded dp{ws}"},
         "kernel_ms": kmean,

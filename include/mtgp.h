@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 4
+#define MTGP_ABI_VERSION 5
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -121,6 +121,9 @@ typedef struct {
   int32_t prog_readout;      /* readout / policy during the solve                  */
   int32_t prog_readout_save; /* readout at the save points (dyn.py:101)            */
   int32_t readout_save_same; /* 1: equal to prog_readout, 0: differ, -1: compare  */
+  int32_t prng_impl;         /* observation-noise random-bits layout (mtgp_prng.h): */
+                             /* 0 threefry original (JAX <= 0.4.x default),        */
+                             /* 1 threefry partitionable (JAX >= 0.5 default)      */
 } MtgpModel;
 
 typedef struct {
@@ -134,6 +137,11 @@ typedef struct {
                         /* [0, P) from mtgp_schedule (NULL = identity).  Only   */
                         /* which individuals share a wave changes; results are  */
                         /* bit-identical and stay indexed by individual.        */
+  /* Observation noise (control models, control_environment_base.py:43-48):      */
+  /*   y = C@x + normal(fold_in(obs_keys[r], bitcast(t)), (n_obs,)) @ obs_w       */
+  /* at every RK4 stage time t = ts[0] + n*h + c_i*h and at every save time ts[k]. */
+  const uint32_t* obs_keys; /* [R, 2] obs_noise_keys (dyn.py:65) or NULL = noise-free */
+  const float* obs_w;       /* [n_obs, n_obs] W = obs_noise * I (acrobot.py:49)        */
 } MtgpRollouts;
 
 /* Outputs.  Trajectories are time-major structure-of-arrays so that every save point

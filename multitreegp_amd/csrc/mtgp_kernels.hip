@@ -20,6 +20,7 @@
 #include <stdint.h>
 #include "mtgp.h"
 #include "mtgp_f32math.h"
+#include "mtgp_prng.h"
 #include "mtgp_flatten.h"
 
 namespace {
@@ -135,6 +136,51 @@ __device__ __forceinline__ void acro_f_obs(const float x[4], float y[4]) {
   y[1] = (f0 && f2 && f3) ? x[1] + 0.0f : qn;
   y[2] = (f0 && f1 && f3) ? x[2] + 0.0f : qn;
   y[3] = (f0 && f1 && f2) ? x[3] + 0.0f : qn;
+  y[0] = mtgp_wrap_angle(y[0]);
+  y[1] = mtgp_wrap_angle(y[1]);
+}
+
+// Observation noise (cbase.py:43-48): out = C@x + normal(fold_in(key, bitcast(t)), (4,)) @ W.
+// The key is per rollout (obs_noise_keys, dyn.py:65), W (= obs_noise * I, acrobot.py:49) is
+// shared.  C@x and the noise product are summed in index order exactly like the oracle.
+struct ObsNoise {
+  uint32_t k0, k1;  // this lane's rollout key
+  float W[16];      // [n_obs, n_obs] row-major, wave-uniform
+  int impl;         // MTGP_PRNG_* random-bits layout
+};
+
+__device__ __forceinline__ ObsNoise obs_noise_setup(const MtgpModel& m, const MtgpRollouts& ro, int rr) {
+  ObsNoise z;
+  z.k0 = ro.obs_keys[2 * rr + 0];
+  z.k1 = ro.obs_keys[2 * rr + 1];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) z.W[i] = ro.obs_w[i];
+  z.impl = m.prng_impl;
+  return z;
+}
+
+template <bool NOISE>
+__device__ __forceinline__ void acro_obs(const ObsNoise& z, float t, const float x[4], float y[4]) {
+  if (!NOISE) {
+    acro_f_obs(x, y);
+    return;
+  }
+  float n[4], nz[4];
+  mtgp_obs_normals(z.k0, z.k1, t, 4, z.impl, n);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float acc = n[0] * z.W[j];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) acc = acc + n[i] * z.W[i * 4 + j];
+    nz[j] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    float cx = (i == 0) ? x[0] : 0.0f * x[0];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) cx = cx + ((i == j) ? x[j] : 0.0f * x[j]);
+    y[i] = cx + nz[i];
+  }
   y[0] = mtgp_wrap_angle(y[0]);
   y[1] = mtgp_wrap_angle(y[1]);
 }
@@ -311,7 +357,9 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
 // Data slots: y 0..3 | a 4..4+NA-1 | u 4+NA | targets.  Per stage the programs run in
 // the order of _drift (dyn.py:107-118): readout (y, u folded to 0) -> drift -> f_obs ->
 // state equations; at save points the save-time readout (dyn.py:101) is appended.
-template <int NA, bool TRAJ>
+// NOISE: observation noise on; the save-point observation uses ts[k] (dyn.py:99), which is
+// recomputed when it differs from the stage-0 time of that step.
+template <int NA, bool TRAJ, bool NOISE>
 __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
@@ -324,6 +372,9 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const float t0 = A.ro.ts[0];
+  ObsNoise nzc;
+  if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
   constexpr int uslot = 4 + NA;
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
@@ -384,7 +435,8 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
       for (int j = 0; j < NA; ++j) dset(dcol, 4 + j, at[j]);
       const float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);
       acro_drift(K, xt, u, kx);
-      acro_f_obs(xt, y);
+      const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
+      acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
       dset(dcol, uslot, u);
@@ -398,6 +450,14 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
         if (is_save) {
           const int k = step / save_every;
           float us = u;
+          if (NOISE) {
+            const float tsk = A.ro.ts[k];
+            if (__float_as_uint(tsk) != __float_as_uint(t0 + (float)step * h)) {
+              acro_obs<true>(nzc, tsk, x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
+#pragma unroll
+              for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
+            }
+          }
           if (diff_mask != 0) {
             for (int gi = 0; gi < ng; ++gi) {
               if (!((diff_mask >> gi) & 1ull)) continue;
@@ -456,7 +516,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 
 // --------------------------------------------------------------------------------------
 // Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
-template <bool TRAJ>
+template <bool TRAJ, bool NOISE>
 __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
@@ -468,6 +528,9 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const float t0 = A.ro.ts[0];
+  ObsNoise nzc;
+  if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
   const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
                                  A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
   const size_t PR = (size_t)A.P * R;
@@ -492,14 +555,24 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
       float xt[4], y[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
-      acro_f_obs(xt, y);
+      const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
+      acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
       for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
-      const float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);  // ff.py:106-107 (:97 at saves)
+      float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);  // ff.py:106-107 (:97 at saves)
       acro_drift(K, xt, u, kx);
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
+          if (NOISE) {
+            const float tsk = A.ro.ts[k];
+            if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
+              acro_obs<true>(nzc, tsk, x, y);
+#pragma unroll
+              for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
+              u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);
+            }
+          }
           if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), u, x[0], x[1]);
           if (TRAJ && active) {
             if (A.out.xs) {
@@ -1006,6 +1079,10 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
   const long waves = ((long)P + G - 1) / G;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
+  const bool noise = rollouts->obs_keys != nullptr;
+  if (noise && (!rollouts->obs_w || model->model == MTGP_MODEL_SR || model->n_obs != 4)) return MTGP_ERR_ARG;
+  if (model->prng_impl != MTGP_PRNG_THREEFRY_ORIGINAL && model->prng_impl != MTGP_PRNG_THREEFRY_PARTITIONABLE)
+    return MTGP_ERR_ARG;
   if (model->model == MTGP_MODEL_ACROBOT_DYNAMIC) {
     if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;
     if (model->n_targets < 0 || 4 + model->state_size + 1 + model->n_targets > kDMax) return MTGP_ERR_ARG;
@@ -1013,8 +1090,13 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
 #define MTGP_DYN(NA)                                                                                      \
   case NA:                                                                                                \
     return launch_timed([&] {                                                                             \
-      if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true>), grid, block, 0, s, A);                     \
-      else hipLaunchKernelGGL((k_acro_dynamic<NA, false>), grid, block, 0, s, A);                         \
+      if (noise) {                                                                                        \
+        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true>), grid, block, 0, s, A);             \
+        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true>), grid, block, 0, s, A);                 \
+      } else {                                                                                            \
+        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false>), grid, block, 0, s, A);            \
+        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false>), grid, block, 0, s, A);                \
+      }                                                                                                   \
     }, s);
     switch (model->state_size) {
       MTGP_DYN(1)
@@ -1028,8 +1110,13 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
     if (model->n_targets < 0 || 4 + model->n_targets > kDMax) return MTGP_ERR_ARG;
     if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
     return launch_timed([&] {
-      if (traj) hipLaunchKernelGGL((k_acro_static<true>), grid, block, 0, s, A);
-      else hipLaunchKernelGGL((k_acro_static<false>), grid, block, 0, s, A);
+      if (noise) {
+        if (traj) hipLaunchKernelGGL((k_acro_static<true, true>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_acro_static<false, true>), grid, block, 0, s, A);
+      } else {
+        if (traj) hipLaunchKernelGGL((k_acro_static<true, false>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_acro_static<false, false>), grid, block, 0, s, A);
+      }
     }, s);
   } else if (model->model == MTGP_MODEL_SR) {
     if (!rollouts->ys_true) return MTGP_ERR_ARG;

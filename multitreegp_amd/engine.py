@@ -61,12 +61,13 @@ class DeviceEngine:
     # ------------------------------------------------------------------ data
     def prepare_data(self, data) -> dict:
         """Upload the reference data tuple once (cached on the identity of its arrays)."""
-        key = tuple(id(x) for x in data) if isinstance(data, (tuple, list)) else id(data)
+        from . import prng
+        key = (tuple(id(x) for x in data) if isinstance(data, (tuple, list)) else id(data), prng.prng_impl_code())
         if self._data is not None and key == self._data_key:
             return self._data
         host = self.ff.prepare(data)
         dev = {}
-        for name in ("x0", "params", "targets", "ts", "ys_true"):
+        for name in ("x0", "params", "targets", "ts", "ys_true", "obs_keys", "obs_w"):
             a = host.get(name)
             a = None if a is None else np.asarray(a)
             dev[name] = None if a is None or a.size == 0 else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
@@ -179,10 +180,12 @@ class DeviceEngine:
         m.parsimony = self.parsimony
         m.prog_state, m.prog_readout = roles["prog_state"], roles["prog_readout"]
         m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
+        m.prng_impl = d.get("prng_impl", 0)
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
         ro.order = _ptr(self.schedule(fl, R)) if schedule and P > 1 else None
+        ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
         dev = self.device
         res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
         out = nat.MtgpOutputs()

@@ -12,6 +12,8 @@ from typing import Tuple
 
 import numpy as np
 
+from . import prng
+
 
 class Acrobot:
     """acrobot.py:7-87.  n_var 4, n_control 1, n_targets 0, n_obs 4 (default)."""
@@ -104,13 +106,36 @@ def ground_truth(env, x0: np.ndarray, ts: np.ndarray, h: float = 1e-3) -> np.nda
 
 def control_data(env, batch_size: int, dt: float, T: float, seed: int = 1, n_steps: int = None):
     """The notebooks' get_data (DynamicPolicy.ipynb cell 2) with numpy RNG:
-    (x0, ts, targets, process_noise_keys, obs_noise_keys, params)."""
+    (x0, ts, targets, process_noise_keys, obs_noise_keys, params).  The noise keys are
+    distinct JAX-format keys (split of PRNGKey(seed)); see jax_control_data for the
+    notebook's exact key derivation."""
     rng = np.random.default_rng(seed)
     x0, targets = env.sample_init_states(batch_size, rng)
     if n_steps is None:
         ts = np.arange(0, T, dt, dtype=np.float32)
     else:
         ts = (np.arange(n_steps + 1, dtype=np.float32) * np.float32(dt)).astype(np.float32)
-    keys = np.zeros((batch_size, 2), dtype=np.uint32)
+    _, k1, k2 = prng.split(prng.PRNGKey(seed), 3)
     params = env.sample_params(batch_size, "Constant", ts, rng)
-    return x0, ts, targets, keys, keys.copy(), params
+    return x0, ts, targets, prng.split(k1, batch_size), prng.split(k2, batch_size), params
+
+
+def jax_control_data(key, env, batch_size: int, dt: float, T: float = None, n_steps: int = None):
+    """DynamicPolicy.ipynb get_data restated with the JAX-compatible host PRNG:
+        init_key, noise_key1, noise_key2, param_key = jr.split(key, 4)
+        x0 ~ uniform(split(init_key)[0], (batch, 4), -init_bounds, init_bounds)  (acrobot.py:18-22)
+        process/obs noise keys = jr.split(noise_key1/2, batch_size)
+        ts = jnp.arange(0, T, dt)
+    For Acrobot this reproduces the notebook's arrays bit for bit (threefry restated in prng.py)."""
+    key = np.asarray(key, np.uint32)
+    init_key, nk1, nk2, _param_key = prng.split(key, 4)
+    ik, _tk = prng.split(init_key)
+    b = np.asarray(env.init_bounds, np.float32)
+    x0 = prng.uniform(ik, (batch_size, env.n_var), -b, b)
+    targets = np.zeros((batch_size, env.n_targets), np.float32)
+    if n_steps is None:
+        ts = np.arange(0, T, dt, dtype=np.float32)
+    else:
+        ts = (np.arange(n_steps + 1, dtype=np.float32) * np.float32(dt)).astype(np.float32)
+    params = env.sample_params(batch_size, "Constant", ts, None)
+    return x0, ts, targets, prng.split(nk1, batch_size), prng.split(nk2, batch_size), params

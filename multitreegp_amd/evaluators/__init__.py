@@ -18,6 +18,7 @@ from typing import List, Tuple
 import numpy as np
 
 from .. import _native as nat
+from .. import prng
 
 
 class RK4:
@@ -135,9 +136,6 @@ class _ControlEvaluator(_CandidateAPI):
 
     def __init__(self, env, dt0: float, solver=None, max_steps: int = 16 ** 4, stepsize_controller=None):
         _check_solver(solver if solver is not None else RK4(), stepsize_controller)
-        if getattr(env, "obs_noise", 0.0) not in (0, 0.0):
-            raise NotImplementedError(
-                "obs_noise > 0 needs the JAX threefry observation-noise stream in-kernel (SURVEY.md §8f row 1)")
         if type(env).__name__ != "Acrobot":
             raise NotImplementedError(f"environment {type(env).__name__}: only Acrobot is on the MI355X path")
         if env.n_obs != 4:
@@ -152,8 +150,12 @@ class _ControlEvaluator(_CandidateAPI):
         self.stepsize_controller = stepsize_controller
 
     def prepare(self, data) -> dict:
-        """Reference data tuple (x0, ts, targets, process_keys, obs_keys, params) -> arrays."""
-        x0, ts, targets, _pk, _ok, params = data
+        """Reference data tuple (x0, ts, targets, process_keys, obs_keys, params) -> arrays.
+
+        With env.obs_noise != 0 the per-rollout obs_noise_keys (uint32 [R, 2], jax.random key
+        data) drive the in-kernel observation noise (control_environment_base.py:43-48); the
+        random-bits layout follows ``prng.set_threefry_partitionable`` (JAX's config flag)."""
+        x0, ts, targets, _pk, obs_keys, params = data
         x0 = _f32(x0)
         R = x0.shape[0]
         if x0.shape[1] != 4:
@@ -161,8 +163,17 @@ class _ControlEvaluator(_CandidateAPI):
         prm = np.stack([_f32(p).reshape(R) for p in params], axis=1) if params is not None else np.ones((R, 4), np.float32)
         tg = _f32(targets).reshape(R, -1)
         n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
-        return dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R,
-                    n_steps=n_steps, save_every=save_every, n_save=S)
+        out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R,
+                   n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code())
+        obs_noise = float(getattr(self.env, "obs_noise", 0.0))
+        if obs_noise != 0.0:
+            keys = np.ascontiguousarray(np.asarray(obs_keys), dtype=np.uint32)
+            if keys.shape != (R, 2):
+                raise ValueError(f"obs_noise_keys must be uint32 [R, 2] key data, got {keys.shape}")
+            out["obs_keys"] = keys
+            # W = obs_noise * eye(n_obs) (acrobot.py:49), formed in float32 like the reference
+            out["obs_w"] = (np.float32(obs_noise) * np.eye(self.obs_size, dtype=np.float32)).astype(np.float32)
+        return out
 
 
 class DynamicEvaluator(_ControlEvaluator):

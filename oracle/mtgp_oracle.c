@@ -18,12 +18,15 @@
  * (ModuleNotFoundError) and ships no golden vectors -> parity vs the
  * reference is UNPINNED; this oracle is pinned by analytic known-answer tests, a
  * float64 numpy restatement and sympy evaluation of the reference's printed
- * expressions (tests/test_oracle.py).
+ * expressions (tests/test_oracle.py).  The observation noise uses the PRNG spec
+ * include/mtgp_prng.h, pinned by the Random123 threefry KATs and JAX's published
+ * split/normal outputs for PRNGKey(0) (tests/test_prng.py).
  */
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 #include "mtgp_f32math.h"
+#include "mtgp_prng.h"
 
 #define OR_MAX_N 256
 #define OR_MAX_D 64
@@ -96,6 +99,7 @@ typedef struct {
   int32_t n_var, state_size, n_obs, n_control, n_targets;
   int32_t n_steps, save_every, n_save;
   float h, max_fitness, parsimony;
+  int32_t prng_impl; /* mtgp_prng.h: 0 threefry original layout, 1 partitionable */
 } OrModel;
 
 typedef struct {
@@ -105,6 +109,8 @@ typedef struct {
   const float* ts;      /* [n_save] */
   const float* ys_true; /* SR: [R, n_save, n_var] (reference layout) */
   int32_t R;
+  const uint32_t* obs_keys; /* [R, 2] obs_noise_keys (dyn.py:65) or NULL: noise-free */
+  const float* obs_w;       /* [n_obs, n_obs] W = obs_noise * I (acrobot.py:49) */
 } OrRollouts;
 
 typedef struct {
@@ -114,12 +120,27 @@ typedef struct {
   OrLib lib;
   const float* target;
   float l1, l2, m1, m2;
+  const uint32_t* key; /* this rollout's obs_noise_key or NULL */
+  const float* W;
 } OrCtx;
 
-/* EnvironmentBase.f_obs with C = I, W = obs_noise*I, obs_noise = 0 (cbase.py:43-48):
- * out = C@x + normal@W; the noise term is +0.  Then Acrobot wraps out[0:2]
- * (acrobot.py:29-32). */
-static void acro_f_obs(const float* x, float* y) {
+/* EnvironmentBase.f_obs (cbase.py:43-48) with C = I (acrobot.py:48):
+ *   out = C@x + normal(fold_in(key, bitcast_i32(t)), (n_obs,)) @ W
+ * matrix products summed in index order; without a key (obs_noise = 0) the noise term is
+ * +0.  Then Acrobot wraps out[0:2] (acrobot.py:29-32). */
+static void acro_f_obs(const OrCtx* c, float t, const float* x, float* y) {
+  float nz[4];
+  if (c->key) {
+    float n[4];
+    mtgp_obs_normals(c->key[0], c->key[1], t, 4, c->m->prng_impl, n);
+    for (int j = 0; j < 4; ++j) {
+      float s = n[0] * c->W[0 * 4 + j];
+      for (int i = 1; i < 4; ++i) s = s + n[i] * c->W[i * 4 + j];
+      nz[j] = s;
+    }
+  } else {
+    for (int j = 0; j < 4; ++j) nz[j] = 0.0f;
+  }
   for (int i = 0; i < 4; ++i) {
     float s = 0.0f;
     int first = 1;
@@ -127,7 +148,7 @@ static void acro_f_obs(const float* x, float* y) {
       const float term = (i == j ? 1.0f : 0.0f) * x[j];
       if (first) { s = term; first = 0; } else s = s + term;
     }
-    y[i] = s + 0.0f;
+    y[i] = s + nz[i];
   }
   y[0] = mtgp_wrap_angle(y[0]);
   y[1] = mtgp_wrap_angle(y[1]);
@@ -162,12 +183,12 @@ static float tree_eval(const OrCtx* c, int t, const float* data, int n_data) {
 }
 
 /* dynamic_evaluate._drift (dyn.py:107-118) */
-static void dyn_rhs(const OrCtx* c, const float* s, float* ds) {
+static void dyn_rhs(const OrCtx* c, float t, const float* s, float* ds) {
   const OrModel* m = c->m;
   const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
   const int D = no + na + nu + nt;
   float y[4], data[OR_MAX_D], u[8];
-  acro_f_obs(s, y);
+  acro_f_obs(c, t, s, y);
   /* readout sees [0_obs, a, 0_u, target] */
   for (int i = 0; i < D; ++i) data[i] = 0.0f;
   for (int i = 0; i < na; ++i) data[no + i] = s[4 + i];
@@ -181,11 +202,11 @@ static void dyn_rhs(const OrCtx* c, const float* s, float* ds) {
 }
 
 /* feedforward_evaluate._drift (ff.py:104-110) */
-static void ff_rhs(const OrCtx* c, const float* s, float* ds) {
+static void ff_rhs(const OrCtx* c, float t, const float* s, float* ds) {
   const OrModel* m = c->m;
   const int no = m->n_obs, nt = m->n_targets;
   float y[4], data[OR_MAX_D];
-  acro_f_obs(s, y);
+  acro_f_obs(c, t, s, y);
   for (int i = 0; i < no; ++i) data[i] = y[i];
   for (int i = 0; i < nt; ++i) data[no + i] = c->target[i];
   const float u = tree_eval(c, 0, data, no + nt);
@@ -193,14 +214,15 @@ static void ff_rhs(const OrCtx* c, const float* s, float* ds) {
 }
 
 /* SR_evaluator._drift (sr.py:85-88) */
-static void sr_rhs(const OrCtx* c, const float* s, float* ds) {
+static void sr_rhs(const OrCtx* c, float t, const float* s, float* ds) {
+  (void)t;
   for (int i = 0; i < c->m->n_var; ++i) ds[i] = tree_eval(c, i, s, c->m->n_var);
 }
 
-static void rhs(const OrCtx* c, const float* s, float* ds) {
-  if (c->m->model == 1) dyn_rhs(c, s, ds);
-  else if (c->m->model == 2) ff_rhs(c, s, ds);
-  else sr_rhs(c, s, ds);
+static void rhs(const OrCtx* c, float t, const float* s, float* ds) {
+  if (c->m->model == 1) dyn_rhs(c, t, s, ds);
+  else if (c->m->model == 2) ff_rhs(c, t, s, ds);
+  else sr_rhs(c, t, s, ds);
 }
 
 static int state_dim(const OrModel* m) { return m->model == 1 ? 4 + m->state_size : m->n_var; }
@@ -218,23 +240,25 @@ static float cond_fn(const OrModel* m, const float* s) {
 }
 
 /* The solver step: classical RK4 (c = 0,1/2,1/2,1; b = 1/6,1/3,1/3,1/6), written with
- * explicit fma so that the GPU kernel can reproduce it bit-for-bit. */
-static void rk4_step(const OrCtx* c, float* s) {
+ * explicit fma so that the GPU kernel can reproduce it bit-for-bit.  Step n starts at
+ * t = ts[0] + f32(n) * h; stage i is evaluated at t + c_i * h (t, t + h/2, t + h/2, t + h),
+ * which matters only for the time-dependent observation noise (cbase.py:45). */
+static void rk4_step(const OrCtx* c, float t, float* s) {
   const int n = state_dim(c->m);
   const float h = c->m->h, h2 = h * 0.5f, h6 = h / 6.0f;
   float k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
-  rhs(c, s, k);
+  rhs(c, t, s, k);
   for (int i = 0; i < n; ++i) { acc[i] = k[i]; tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
-  rhs(c, tmp, k);
+  rhs(c, t + h2, tmp, k);
   for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
-  rhs(c, tmp, k);
+  rhs(c, t + h2, tmp, k);
   for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h, k[i], s[i]); }
-  rhs(c, tmp, k);
+  rhs(c, t + h, tmp, k);
   for (int i = 0; i < n; ++i) { acc[i] = acc[i] + k[i]; s[i] = MTGP_FMAF(h6, acc[i], s[i]); }
 }
 
 /* Solve one rollout: saved[n_save][dim]; unsaved points after termination = +inf. */
-static void solve(const OrCtx* c, const float* s0, float* saved) {
+static void solve(const OrCtx* c, float t0, const float* s0, float* saved) {
   const OrModel* m = c->m;
   const int n = state_dim(m);
   float s[OR_MAX_S];
@@ -243,7 +267,7 @@ static void solve(const OrCtx* c, const float* s0, float* saved) {
   float prev = cond_fn(m, s);
   int k_saved = 0, done = 0;
   for (int step = 1; step <= m->n_steps && !done; ++step) {
-    rk4_step(c, s);
+    rk4_step(c, t0 + (float)(step - 1) * m->h, s);
     if (step % m->save_every == 0) {
       ++k_saved;
       for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];
@@ -330,7 +354,9 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
       float s0[OR_MAX_S];
       for (int i = 0; i < dim; ++i) s0[i] = 0.0f;
       for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
-      solve(&c, s0, saved);
+      c.key = ro->obs_keys ? ro->obs_keys + 2 * (size_t)r : NULL;
+      c.W = ro->obs_w;
+      solve(&c, ro->ts[0], s0, saved);
       float f;
       const size_t base = ((size_t)p * R + r) * S;
       if (m->model == 3) {
@@ -354,7 +380,7 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
         float xk[4];
         for (int k = 0; k < S; ++k) {
           for (int i = 0; i < 4; ++i) xk[i] = saved[(size_t)k * dim + i];
-          acro_f_obs(xk, yk);
+          acro_f_obs(&c, ro->ts[k], xk, yk); /* lax.scan(f_obs, key, (ts, xs)), dyn.py:99 */
           if (m->model == 1) { /* dyn.py:101: readout([y, a, 0_u, target]) */
             const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
             const int D = no + na + nu + nt;
@@ -425,7 +451,31 @@ void oracle_acro_drift(const float* params4, const float* state4, float u, float
   c.l1 = params4[0]; c.l2 = params4[1]; c.m1 = params4[2]; c.m2 = params4[3];
   acro_drift(&c, state4, u, out4);
 }
-void oracle_acro_f_obs(const float* x4, float* y4) { acro_f_obs(x4, y4); }
+void oracle_acro_f_obs(const float* x4, float* y4) {
+  OrCtx c;
+  memset(&c, 0, sizeof(c));
+  acro_f_obs(&c, 0.0f, x4, y4);
+}
+/* PRNG spec hooks: normals of fold_in(key, bitcast(t)), normals of a key, threefry, erfinv, log1p */
+void oracle_obs_normals(const uint32_t* key, float t, int n, int impl, float* out) {
+  mtgp_obs_normals(key[0], key[1], t, n, impl, out);
+}
+void oracle_random_normals(const uint32_t* key, int n, int impl, float* out) {
+  uint32_t bits[64];
+  if (n > 64) n = 64;
+  mtgp_random_bits(key[0], key[1], n, impl, bits);
+  for (int i = 0; i < n; ++i) out[i] = mtgp_normal_from_bits(bits[i]);
+}
+void oracle_threefry(const uint32_t* key, const uint32_t* x0, const uint32_t* x1, uint32_t* y0, uint32_t* y1,
+                     long n) {
+  for (long i = 0; i < n; ++i) mtgp_threefry2x32(key[0], key[1], x0[i], x1[i], &y0[i], &y1[i]);
+}
+void oracle_erfinv(const float* x, float* o, long n) {
+  for (long i = 0; i < n; ++i) o[i] = mtgp_erfinvf(x[i]);
+}
+void oracle_log1p(const float* x, float* o, long n) {
+  for (long i = 0; i < n; ++i) o[i] = mtgp_log1pf(x[i]);
+}
 float oracle_acro_fitness(const float* xs, const float* us, const float* ts, int S) {
   return acro_fitness(xs, us, ts, S);
 }

@@ -16,7 +16,8 @@ LIB = os.path.join(HERE, "build", "libmtgp_oracle.so")
 
 
 def build(force: bool = False) -> str:
-    src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h")]
+    src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h"),
+           os.path.join(HERE, "..", "include", "mtgp_prng.h")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
         subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
                        stdout=subprocess.DEVNULL)
@@ -27,12 +28,14 @@ class OrModel(ctypes.Structure):
     _fields_ = [("model", ctypes.c_int32), ("n_var", ctypes.c_int32), ("state_size", ctypes.c_int32),
                 ("n_obs", ctypes.c_int32), ("n_control", ctypes.c_int32), ("n_targets", ctypes.c_int32),
                 ("n_steps", ctypes.c_int32), ("save_every", ctypes.c_int32), ("n_save", ctypes.c_int32),
-                ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float)]
+                ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float),
+                ("prng_impl", ctypes.c_int32)]
 
 
 class OrRollouts(ctypes.Structure):
     _fields_ = [("x0", ctypes.c_void_p), ("params", ctypes.c_void_p), ("targets", ctypes.c_void_p),
-                ("ts", ctypes.c_void_p), ("ys_true", ctypes.c_void_p), ("R", ctypes.c_int32)]
+                ("ts", ctypes.c_void_p), ("ys_true", ctypes.c_void_p), ("R", ctypes.c_int32),
+                ("obs_keys", ctypes.c_void_p), ("obs_w", ctypes.c_void_p)]
 
 
 _lib = None
@@ -58,6 +61,11 @@ def lib():
         L.oracle_acro_fitness.restype = ctypes.c_float
         L.oracle_pairwise_sum.argtypes = [vp, ctypes.c_int]
         L.oracle_pairwise_sum.restype = ctypes.c_float
+        L.oracle_obs_normals.argtypes = [vp, ctypes.c_float, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_random_normals.argtypes = [vp, ctypes.c_int, ctypes.c_int, vp]
+        L.oracle_threefry.argtypes = [vp, vp, vp, vp, vp, ctypes.c_long]
+        L.oracle_erfinv.argtypes = [vp, vp, ctypes.c_long]
+        L.oracle_log1p.argtypes = [vp, vp, ctypes.c_long]
         _lib = L
     return _lib
 
@@ -95,13 +103,13 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
     """Evaluate a flat population [P, T, N, 4].
 
     model: dict(model, n_var, state_size, n_obs, n_control, n_targets, n_steps, save_every, n_save,
-                h, max_fitness, parsimony)
+                h, max_fitness, parsimony[, prng_impl])
     rollouts: dict(x0 [R, n_var], params [R, 4] or None, targets [R, nt] or None, ts [S],
-                   ys_true [R, S, n_var] or None)
+                   ys_true [R, S, n_var] or None[, obs_keys uint32 [R, 2], obs_w [n_obs, n_obs]])
     Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c])."""
     pop = np.ascontiguousarray(pop, np.float32)
     P, T, N, _ = pop.shape
-    m = OrModel(**{k: model[k] for k, _ in OrModel._fields_})
+    m = OrModel(**{k: model.get(k, 0) if k == "prng_impl" else model[k] for k, _ in OrModel._fields_})
     x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
     R = x0.shape[0]
     prm = None if rollouts.get("params") is None else np.ascontiguousarray(rollouts["params"], np.float32)
@@ -110,8 +118,12 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
     ts = np.ascontiguousarray(rollouts["ts"], np.float32)
     yt = rollouts.get("ys_true")
     yt = None if yt is None else np.ascontiguousarray(yt, np.float32)
+    keys = rollouts.get("obs_keys")
+    keys = None if keys is None else np.ascontiguousarray(keys, np.uint32)
+    W = None if keys is None else np.ascontiguousarray(rollouts["obs_w"], np.float32)
     ro = OrRollouts(_p(x0).value, None if prm is None else _p(prm).value, None if tg is None else _p(tg).value,
-                    _p(ts).value, None if yt is None else _p(yt).value, R)
+                    _p(ts).value, None if yt is None else _p(yt).value, R,
+                    None if keys is None else _p(keys).value, None if W is None else _p(W).value)
     S = model["n_save"]
     fit = np.empty(P, np.float32)
     rf = np.empty((P, R), np.float32)
@@ -157,6 +169,45 @@ def acro_fitness(xs, us, ts):
     us = np.ascontiguousarray(us, np.float32).reshape(-1)
     ts = np.ascontiguousarray(ts, np.float32)
     return np.float32(lib().oracle_acro_fitness(_p(xs), _p(us), _p(ts), ts.shape[0]))
+
+
+def obs_normals(key, t, n=4, impl=0):
+    """normal(fold_in(key, bitcast(t)), (n,)) of the PRNG spec (include/mtgp_prng.h)."""
+    k = np.ascontiguousarray(key, np.uint32)
+    o = np.empty(n, np.float32)
+    lib().oracle_obs_normals(_p(k), ctypes.c_float(t), n, impl, _p(o))
+    return o
+
+
+def random_normals(key, n, impl=0):
+    """jax.random.normal(key, (n,)) of the PRNG spec."""
+    k = np.ascontiguousarray(key, np.uint32)
+    o = np.empty(n, np.float32)
+    lib().oracle_random_normals(_p(k), n, impl, _p(o))
+    return o
+
+
+def threefry(key, x0, x1):
+    k = np.ascontiguousarray(key, np.uint32)
+    x0 = np.ascontiguousarray(x0, np.uint32)
+    x1 = np.ascontiguousarray(x1, np.uint32)
+    y0, y1 = np.empty_like(x0), np.empty_like(x1)
+    lib().oracle_threefry(_p(k), _p(x0), _p(x1), _p(y0), _p(y1), x0.size)
+    return y0, y1
+
+
+def erfinv(x):
+    x = np.ascontiguousarray(x, np.float32)
+    o = np.empty_like(x)
+    lib().oracle_erfinv(_p(x), _p(o), x.size)
+    return o
+
+
+def log1p(x):
+    x = np.ascontiguousarray(x, np.float32)
+    o = np.empty_like(x)
+    lib().oracle_log1p(_p(x), _p(o), x.size)
+    return o
 
 
 def pairwise_sum(v):

@@ -9,8 +9,8 @@ CONTROL_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("
 SR_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("/", None, 2, 0.1)]  # SymbolicRegression.ipynb
 
 
-def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2):
-    env = mt.Acrobot(0.0, 0.0)
+def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2, obs_noise=0.0):
+    env = mt.Acrobot(0.0, obs_noise)
     vl = [["y1", "y2", "y3", "y4"] + [f"a{i + 1}" for i in range(state_size)] + ["u"],
           [f"a{i + 1}" for i in range(state_size)]]
     lib = mt.NodeLibrary(CONTROL_OPS, vl, [state_size, 1])
@@ -20,8 +20,8 @@ def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2):
     return env, lib, ff, data, pop
 
 
-def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0):
-    env = mt.Acrobot(0.0, 0.0)
+def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0):
+    env = mt.Acrobot(0.0, obs_noise)
     lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1])
     ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4())
     data = mt.control_data(env, R, 0.05, None, seed=seed + 1, n_steps=n_steps)
@@ -47,14 +47,16 @@ def oracle_model(ff, d, parsimony=0.0):
     return dict(model=ff.model_id, n_var=d.get("n_var", 4), state_size=getattr(ff, "state_size", 0),
                 n_obs=env.n_obs if env else 0, n_control=env.n_control if env else 0,
                 n_targets=env.n_targets if env else 0, n_steps=d["n_steps"], save_every=d["save_every"],
-                n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony)
+                n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony,
+                prng_impl=d.get("prng_impl", 0))
 
 
 def oracle_rollouts(d, data=None):
     ys = None
     if d.get("ys_true") is not None:
         ys = np.ascontiguousarray(np.transpose(d["ys_true"], (2, 0, 1)))  # back to [R, S, n_var]
-    return dict(x0=d["x0"], params=d.get("params"), targets=d.get("targets"), ts=d["ts"], ys_true=ys)
+    return dict(x0=d["x0"], params=d.get("params"), targets=d.get("targets"), ts=d["ts"], ys_true=ys,
+                obs_keys=d.get("obs_keys"), obs_w=d.get("obs_w"))
 
 
 def bits_equal(a, b):

@@ -40,8 +40,29 @@ def eval_tree(tree, lib, data):
     return val[N - 1]
 
 
-def acro_f_obs(x):
-    y = np.array(x, np.float64)  # C = I, no noise
+def obs_noise(key, t, W, partitionable=False):
+    """normal(fold_in(key, bitcast_i32(t)), (n,)) @ W (control_environment_base.py:43-48):
+    threefry words from the host restatement, the normal map in float64 with scipy's erfinv
+    (independent of the fp32 spec's Giles polynomial)."""
+    from scipy.special import erfinv
+    from multitreegp_amd import prng
+    old = prng.threefry_partitionable()
+    prng.set_threefry_partitionable(partitionable)
+    try:
+        k = prng.fold_in(key, int(np.array(t, np.float32).view(np.uint32)))
+        bits = prng.random_bits(k, (W.shape[0],))
+    finally:
+        prng.set_threefry_partitionable(old)
+    f = ((bits >> np.uint32(9)) | np.uint32(0x3F800000)).view(np.float32).astype(np.float64) - 1.0
+    lo = float(np.nextafter(np.float32(-1), np.float32(0)))
+    u = np.maximum(lo, f * 2.0 + lo)
+    return (np.sqrt(2.0) * erfinv(u)) @ np.asarray(W, np.float64)
+
+
+def acro_f_obs(x, noise=None):
+    y = np.array(x, np.float64)  # C = I
+    if noise is not None:
+        y = y + noise
     y[0] = np.remainder(y[0] + np.pi, 2 * np.pi) - np.pi
     y[1] = np.remainder(y[1] + np.pi, 2 * np.pi) - np.pi
     return y
@@ -61,9 +82,9 @@ def acro_drift(x, u, l1=1.0, l2=1.0, m1=1.0, m2=1.0):
     return np.array([td1, td2, a1, a2])
 
 
-def dyn_rhs(cand, lib, s, state_size, params=(1, 1, 1, 1)):
+def dyn_rhs(cand, lib, s, state_size, params=(1, 1, 1, 1), noise=None):
     x, a = s[:4], s[4:]
-    y = acro_f_obs(x)
+    y = acro_f_obs(x, noise)
     u = eval_tree(cand[state_size], lib, np.concatenate([np.zeros(4), a, np.zeros(1)]))
     dx = acro_drift(x, u, *params)
     d = np.concatenate([y, a, [u]])
@@ -71,12 +92,33 @@ def dyn_rhs(cand, lib, s, state_size, params=(1, 1, 1, 1)):
     return np.concatenate([dx, da])
 
 
-def ff_rhs(cand, lib, s, params=(1, 1, 1, 1)):
-    return acro_drift(s, eval_tree(cand[0], lib, acro_f_obs(s)), *params)
+def ff_rhs(cand, lib, s, params=(1, 1, 1, 1), noise=None):
+    return acro_drift(s, eval_tree(cand[0], lib, acro_f_obs(s, noise)), *params)
 
 
 def sr_rhs(cand, lib, s):
     return np.array([eval_tree(cand[i], lib, s) for i in range(len(s))])
+
+
+def rk4_t(rhs, s0, t0, h, n):
+    """Textbook RK4 of a time-dependent rhs(t, s).  The stage TIMES are float32 like the
+    kernel's (t = t0 + f32(i) * h; t + h/2, t + h/2, t + h): the observation noise is keyed on
+    their bit patterns (cbase.py:45)."""
+    s = np.array(s0, np.float64)
+    out = [s.copy()]
+    f = np.float32
+    hf = f(h)
+    with np.errstate(all="ignore"):
+        for i in range(n):
+            t = f(f(t0) + f(i) * hf)
+            th, t1 = f(t + f(hf * f(0.5))), f(t + hf)
+            k1 = rhs(t, s)
+            k2 = rhs(th, s + 0.5 * h * k1)
+            k3 = rhs(th, s + 0.5 * h * k2)
+            k4 = rhs(t1, s + h * k3)
+            s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+            out.append(s.copy())
+    return np.array(out)
 
 
 def rk4(rhs, s0, h, n):

@@ -15,14 +15,32 @@ def test_notebook_schedule():
     assert rk4_schedule(ts, 0.05, 1000) == (996, 4, 250)
 
 
-def test_rejects_adaptive_solver_and_noise():
+def test_rejects_adaptive_solver():
     env = mt.Acrobot(0.05, 0.0)
     with pytest.raises(NotImplementedError):
         mt.DynamicEvaluator(env, 2, 0.05, solver=Dopri5())
-    with pytest.raises(NotImplementedError):
-        mt.DynamicEvaluator(mt.Acrobot(0.05, 0.1), 2, 0.05)  # obs_noise > 0
     ev = mt.DynamicEvaluator(env, 2, 0.05, solver="rk4")
     assert ev.max_fitness == 1e4 and ev.latent_size == 4 and ev.obs_size == 4
+
+
+def test_obs_noise_data_preparation():
+    """obs_noise > 0: the per-rollout keys and W = obs_noise * I go to the kernel (cbase.py:43-48)."""
+    from multitreegp_amd import prng
+    env = mt.Acrobot(0.05, 0.1)
+    ev = mt.DynamicEvaluator(env, 2, 0.05)
+    data = mt.control_data(env, 8, 0.05, None, seed=3, n_steps=10)
+    d = ev.prepare(data)
+    assert d["obs_keys"].dtype == np.uint32 and d["obs_keys"].shape == (8, 2)
+    assert np.array_equal(d["obs_w"], np.float32(0.1) * np.eye(4, dtype=np.float32)) and d["prng_impl"] == 0
+    prng.set_threefry_partitionable(True)
+    try:
+        assert ev.prepare(data)["prng_impl"] == 1
+    finally:
+        prng.set_threefry_partitionable(False)
+    bad = data[:4] + (np.zeros((7, 2), np.uint32),) + data[5:]
+    with pytest.raises(ValueError):
+        ev.prepare(bad)
+    assert "obs_keys" not in mt.DynamicEvaluator(mt.Acrobot(0.05, 0.0), 2, 0.05).prepare(data)
 
 
 def test_schedule_errors():

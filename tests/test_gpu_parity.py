@@ -133,3 +133,52 @@ def test_sr_wide_fitness_only_matches_trajectory_mode():
     b = eng.evaluate(pd, data, trajectories=False, rollout_fitness=True)
     assert bits_equal(a["fitness"].cpu().numpy(), b["fitness"].cpu().numpy())
     assert bits_equal(a["rollout_fitness"].cpu().numpy(), b["rollout_fitness"].cpu().numpy())
+
+
+@pytest.mark.parametrize("impl", [0, 1])
+def test_dynamic_obs_noise_bitexact(impl):
+    """Observation noise (threefry fold_in + normal, control_environment_base.py:43-48) drawn
+    in-kernel at every stage time and save time, bit-exact vs the oracle."""
+    from multitreegp_amd import prng
+    prng.set_threefry_partitionable(bool(impl))
+    try:
+        env, lib, ff, data, pop = dynamic_setup(P=40, R=32, n_steps=60, obs_noise=0.1, seed=2)
+        res, ref, d = _run(ff, lib, data, pop)
+        assert d["prng_impl"] == impl
+        _check(res, ref, pop.shape[0], 32, ["xs", "ys", "us", "acts"])
+    finally:
+        prng.set_threefry_partitionable(False)
+
+
+def test_static_obs_noise_bitexact():
+    env, lib, ff, data, pop = static_setup(P=40, R=16, n_steps=60, obs_noise=0.1, seed=4)
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us"])
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "static"])
+def test_obs_noise_save_time_differs_from_step_time(kind):
+    """dt0 = 0.1, save spacing f32(0.3): several ts[k] differ in their bits from the step start
+    t0 + f32(3k) * h, so the save observation is redrawn at ts[k] (dyn.py:99 / ff.py:96)."""
+    if kind == "dynamic":
+        env = mt.Acrobot(0.0, 0.1)
+        from helpers import CONTROL_OPS
+        vl = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
+        lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
+        ff = mt.DynamicEvaluator(env, 2, 0.1, solver=mt.RK4())
+        names = ["xs", "ys", "us", "acts"]
+    else:
+        env = mt.Acrobot(0.0, 0.1)
+        from helpers import CONTROL_OPS
+        lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1])
+        ff = mt.FeedforwardEvaluator(env, 0.1, solver=mt.RK4())
+        names = ["xs", "ys", "us"]
+    from multitreegp_amd.sampling import sample_population
+    data = mt.control_data(env, 16, 0.3, None, seed=5, n_steps=40)
+    ts = data[1]
+    tk = np.array([np.float32(ts[0]) + np.float32(3 * k) * np.float32(0.1) for k in range(len(ts))], np.float32)
+    assert (ts.view(np.uint32) != tk.view(np.uint32)).sum() > 5
+    pop = sample_population(3, lib, 30, 1, max_init_depth=5, max_nodes=30)[0]
+    res, ref, d = _run(ff, lib, data, pop)
+    assert d["save_every"] == 3
+    _check(res, ref, pop.shape[0], 16, names)

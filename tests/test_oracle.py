@@ -241,3 +241,47 @@ def test_pairwise_sum_and_postprocessing():
         mean = np.clip(orc.pairwise_sum(fr) / np.float32(5), 0, 1e4)
         cnt = int((pop[p, :, :, 0] != 0).sum())
         assert out["fitness"][p] == np.float32(mean + np.float32(0.5) * np.float32(cnt))
+
+
+@pytest.mark.parametrize("setup,impl", [("dynamic", 0), ("static", 0), ("dynamic", 1)])
+def test_oracle_obs_noise_vs_float64_short_horizon(setup, impl):
+    """Observation noise (cbase.py:43-48) inside every RHS stage and at the save points:
+    the oracle vs the float64 restatement driven by the host threefry + scipy erfinv."""
+    from multitreegp_amd import prng
+    prng.set_threefry_partitionable(bool(impl))
+    try:
+        if setup == "dynamic":
+            env, lib, ff, data, pop = dynamic_setup(P=10, R=3, n_steps=20, obs_noise=0.1)
+        else:
+            env, lib, ff, data, pop = static_setup(P=10, R=3, n_steps=20, obs_noise=0.1)
+        d = ff.prepare(data)
+        assert d["prng_impl"] == impl and d["obs_keys"].shape == (3, 2)
+        out = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+        W = d["obs_w"].astype(np.float64)
+        compared = tight = 0
+        for p in range(pop.shape[0]):
+            for r in range(d["R"]):
+                key = d["obs_keys"][r]
+                nz = lambda t: npr.obs_noise(key, t, W, bool(impl))  # noqa: E731
+                x0 = d["x0"][r].astype(np.float64)
+                if setup == "dynamic":
+                    traj = npr.rk4_t(lambda t, s: npr.dyn_rhs(pop[p], lib, s, 2, noise=nz(t)),
+                                     np.concatenate([x0, [0, 0]]), 0.0, 0.05, 20)
+                    got = np.concatenate([out["xs"][p, r], out["acts"][p, r]], -1)
+                else:
+                    traj = npr.rk4_t(lambda t, s: npr.ff_rhs(pop[p], lib, s, noise=nz(t)), x0, 0.0, 0.05, 20)
+                    got = out["xs"][p, r]
+                ys_want = np.array([npr.acro_f_obs(traj[k, :4], nz(d["ts"][k])) for k in range(traj.shape[0])])
+                ok = np.all(np.isfinite(traj)) and np.all(np.abs(traj) < 1e3) and np.all(np.isfinite(got))
+                if not ok:
+                    continue
+                tight += bool(np.allclose(got, traj, rtol=2e-3, atol=2e-3)
+                              and np.allclose(out["ys"][p, r], ys_want, rtol=2e-3, atol=2e-3))
+                compared += 1
+        assert compared >= 10 and tight >= 0.9 * compared
+        # the noise is really there: ys - C x is not zero and has the obs_noise scale
+        res = out["ys"][..., 2:] - out["xs"][..., 2:]
+        res = res[np.isfinite(res)]
+        assert 0.05 < np.std(res) < 0.2
+    finally:
+        prng.set_threefry_partitionable(False)
