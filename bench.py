@@ -94,7 +94,7 @@ def setup_workload(args, rank):
         pop = _cached_population(f"c5_{args.pop}_r{rank}",
                                  lambda: _parallel_population(2000 + rank, lib, args.pop, 16, 128))
         return env, lib, ff, data, pop
-    env = mt.Acrobot(0.0, args.obs_noise)
+    env = mt.Acrobot(0.0, getattr(args, "obs_noise", 0.0))
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
            ("cos", None, 1, 0.1)]
     if args.config == "c2":

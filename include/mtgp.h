@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 5
+#define MTGP_ABI_VERSION 6
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -197,6 +197,37 @@ int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t*
 int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,
                   int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
                   const MtgpRollouts* rollouts, const MtgpOutputs* out, void* stream);
+
+/* ------------------------------------------------------------- program JIT */
+/* The programs of a flattened population are fixed for a whole evaluation (every RK4 stage
+ * of every rollout runs them), so they can be translated once into gfx950 machine code that
+ * the evaluator calls directly instead of interpreting (multitreegp_amd/csrc/mtgp_jit.h; no
+ * reference counterpart -- this replaces XLA's compile of the vmapped tree evaluator).
+ * Results are bit-identical to the interpreter.  Usage per flattened population:
+ *   mtgp_jit_plan   -> offsets[P*n_prog + 1] (byte offset of each program's code, last =
+ *                      total) and info[2] = {0 or a negative code if some program cannot be
+ *                      translated (data slot >= 8), total bytes}   (device, stream-ordered)
+ *   (host reads info, sizes an executable buffer from mtgp_jit_alloc)
+ *   mtgp_jit_emit   -> writes the code
+ *   mtgp_eval_rk4_jit with MtgpJitCode{code, offsets}.
+ * The acrobot evaluators and SR with n_var <= 4 use the code; other models ignore it. */
+typedef struct {
+  const void* code;         /* executable device memory from mtgp_jit_alloc */
+  const uint32_t* offsets;  /* [P*n_prog + 1] from mtgp_jit_plan            */
+} MtgpJitCode;
+
+int mtgp_jit_alloc(int32_t device, size_t bytes, void** code);
+int mtgp_jit_free(void* code);
+int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, uint32_t* offsets_out,
+                  int32_t* info_out, void* stream);
+int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, const uint32_t* offsets,
+                  void* code, size_t code_bytes, void* stream);
+/* host translation of one program (tests/tooling): number of code words, or < 0 */
+int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
+int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,
+                      int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
+                      const MtgpRollouts* rollouts, const MtgpOutputs* out, const MtgpJitCode* jit,
+                      void* stream);
 
 /* Wall time of the last mtgp_eval_rk4 kernel on `stream`, measured with hipEvents
  * recorded around the launch (ms); -1 if none.  Synchronises that event. */

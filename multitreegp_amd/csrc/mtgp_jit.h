@@ -1,0 +1,214 @@
+// mtgp_jit.h -- program JIT: flattened MtgpInstr programs -> straight-line gfx950 machine code.
+//
+// The interpreter (mtgp_kernels.hip run_prog) pays a scalar fetch + dispatch-tree walk per
+// program instruction (~50 SIMD cycles); the programs are fixed for a whole
+// population evaluation (800 RK4 stages at C3), so they are translated once per flattened
+// population into machine code the evaluator calls with s_swappc_b64.  Each program
+// instruction becomes 1-3 VOP1/VOP2 words (operands straight from registers: the data
+// vector and the operand stack live in VGPRs, the stack depth is resolved at translation
+// time), sin/cos/division copy the templates of mtgp_jit_blobs.h.  Results are
+// bit-identical to the interpreter: every IEEE operation has the same operands in the same
+// order; the templates follow include/mtgp_f32math.h op for op; lanes that would need the
+// spec's slow sin/cos reduction (finite |x| >= 2^17) are reported in s[32:33] and the
+// evaluator re-runs that program with the interpreter.
+//
+// Register ABI of a generated program (the evaluator's call site pins these):
+//   v0-v7    data slots 0-7 (read only)          v8      accumulator = result
+//   v9-v16   operand stack (depth <= 8)          v17-v24 template temporaries
+//   s[30:31] return address (s_swappc_b64)       s[32:33] fallback lanes (OR-accumulated)
+//   s[34:39] template temporaries, vcc           exec    never written
+// The host ABI (mtgp.h mtgp_jit_*) places the code in executable device memory.
+#ifndef MTGP_JIT_H
+#define MTGP_JIT_H
+
+#include <stdint.h>
+#include "mtgp.h"
+#include "mtgp_jit_blobs.h"
+
+#if defined(__HIPCC__)
+#define MTGP_JIT_HD __host__ __device__
+#else
+#define MTGP_JIT_HD
+#endif
+
+namespace mtgp {
+
+constexpr int kJitData = 0, kJitAcc = 8, kJitStack = 9, kJitT0 = 17, kJitT1 = 18;
+constexpr int kJitMaxData = 8;
+constexpr uint32_t kJitSrcLiteral = 255u;
+// VOP2 opcodes (gfx9 encoding)
+constexpr uint32_t kVop2Add = 1u, kVop2Sub = 2u, kVop2Subrev = 3u, kVop2Mul = 5u;
+constexpr uint32_t kSetpcS30 = 0xbe801d1eu;  // s_setpc_b64 s[30:31]
+// largest translation of one program instruction (push + two moves + the sin template)
+constexpr int kJitMaxWordsPerInstr = 1 + 4 + MTGP_JIT_SIN_WORDS;
+
+struct JitOut {
+  uint32_t* out;  // nullptr: count only
+  int n;
+  MTGP_JIT_HD void w(uint32_t v) {
+    if (out) out[n] = v;
+    ++n;
+  }
+  MTGP_JIT_HD void blob(const uint32_t* b, int len) {
+    for (int i = 0; i < len; ++i) w(b[i]);
+  }
+  // v_mov_b32 vdst, src (src: 256 + vgpr or literal)
+  MTGP_JIT_HD void mov(int vdst, uint32_t src, uint32_t lit = 0) {
+    w(0x7e000000u | (uint32_t)vdst << 17 | 1u << 9 | src);
+    if (src == kJitSrcLiteral) w(lit);
+  }
+  MTGP_JIT_HD void movv(int vdst, int vsrc) { mov(vdst, 256u + (uint32_t)vsrc); }
+  MTGP_JIT_HD void movc(int vdst, uint32_t bits) { mov(vdst, kJitSrcLiteral, bits); }
+  // VOP2: vdst = src0 OP vsrc1 (src0: 256 + vgpr or literal)
+  MTGP_JIT_HD void vop2(uint32_t op, int vdst, uint32_t src0, int vsrc1, uint32_t lit = 0) {
+    w(op << 25 | (uint32_t)vdst << 17 | (uint32_t)vsrc1 << 9 | src0);
+    if (src0 == kJitSrcLiteral) w(lit);
+  }
+};
+
+// Source descriptor of an operand: a VGPR or a literal constant.
+struct JitSrc {
+  bool lit;
+  int reg;
+  uint32_t bits;
+};
+
+MTGP_JIT_HD inline JitSrc jit_reg(int r) { return JitSrc{false, r, 0u}; }
+MTGP_JIT_HD inline JitSrc jit_lit(uint32_t b) { return JitSrc{true, 0, b}; }
+
+// acc = x OP y for the four IEEE operations, operand order preserved.
+MTGP_JIT_HD inline void jit_binop(JitOut& o, int fn, JitSrc x, JitSrc y) {
+  if (fn == MTGP_FN_DIV) {  // the template divides v17 by v18
+    if (x.lit) o.movc(kJitT0, x.bits); else o.movv(kJitT0, x.reg);
+    if (y.lit) o.movc(kJitT1, y.bits); else o.movv(kJitT1, y.reg);
+    o.blob(mtgp_jit_div_blob, MTGP_JIT_DIV_WORDS);
+    return;
+  }
+  // VOP2 takes a literal only as src0 and needs src1 in a VGPR
+  if (y.lit && x.lit) {
+    o.movc(kJitT0, y.bits);
+    y = jit_reg(kJitT0);
+  }
+  const bool comm = fn == MTGP_FN_ADD || fn == MTGP_FN_MUL;
+  const uint32_t opc = fn == MTGP_FN_ADD ? kVop2Add : fn == MTGP_FN_MUL ? kVop2Mul : kVop2Sub;
+  if (y.lit) {  // x is a register: put the literal in src0
+    if (comm) o.vop2(opc, kJitAcc, kJitSrcLiteral, x.reg, y.bits);  // c OP x == x OP c (commutative)
+    else o.vop2(kVop2Subrev, kJitAcc, kJitSrcLiteral, x.reg, y.bits);  // x - c = subrev(c, x)
+    return;
+  }
+  if (x.lit) o.vop2(opc, kJitAcc, kJitSrcLiteral, y.reg, x.bits);
+  else o.vop2(opc, kJitAcc, 256u + (uint32_t)x.reg, y.reg);
+}
+
+MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
+  if (x.lit) o.movc(kJitT0, x.bits); else o.movv(kJitT0, x.reg);
+  if (is_sin) o.blob(mtgp_jit_sin_blob, MTGP_JIT_SIN_WORDS);
+  else o.blob(mtgp_jit_cos_blob, MTGP_JIT_COS_WORDS);
+}
+
+enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJitErrNoEnd = -4 };
+
+// Translate one END-terminated program (at most L instructions).  Returns the number of
+// 32-bit code words (out == nullptr: count only) or a negative kJitErr* code.
+MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out) {
+  JitOut o{out, 0};
+  int sp = 0;
+  for (int i = 0; i < L; ++i) {
+    const uint32_t w = prog[i].op;
+    const uint32_t code = w >> MTGP_OP_SHIFT, ax = w & 0xffffffu;
+    union { float f; uint32_t u; } cv;
+    cv.f = prog[i].imm;
+    const uint32_t ib = cv.u;
+    const int sib = (int)(ib / MTGP_SLOT_BYTES), sax = (int)(ax / MTGP_SLOT_BYTES);
+    auto push = [&]() -> bool {
+      if (sp >= MTGP_STACK_MAX) return false;
+      o.movv(kJitStack + sp, kJitAcc);
+      ++sp;
+      return true;
+    };
+    const JitSrc acc = jit_reg(kJitAcc), c = jit_lit(ib);
+    const JitSrc vib = jit_reg(kJitData + sib), vax = jit_reg(kJitData + sax);
+    // which operand kinds this opcode reads (checked below)
+    bool uses_ib_slot = false, uses_ax_slot = false, ok = true;
+    int fam = -1, kind = -1;  // family ADD SUB RSUB MUL DIV RDIV; kind 0 C, 1 V, 2 S
+    switch (code) {
+      case MTGP_OP_END:
+        o.w(kSetpcS30);
+        return o.n;
+      case MTGP_OP_LDC: o.movc(kJitAcc, ib); continue;
+      case MTGP_OP_LDCP: ok = push(); o.movc(kJitAcc, ib); break;
+      case MTGP_OP_LDV: uses_ib_slot = true; if (sib >= kJitMaxData) return kJitErrSlot; o.movv(kJitAcc, kJitData + sib); continue;
+      case MTGP_OP_LDVP: if (sib >= kJitMaxData) return kJitErrSlot; ok = push(); o.movv(kJitAcc, kJitData + sib); break;
+      case MTGP_OP_SIN: jit_trig(o, true, acc); continue;
+      case MTGP_OP_COS: jit_trig(o, false, acc); continue;
+      case MTGP_OP_SINV: case MTGP_OP_COSV: case MTGP_OP_SINVP: case MTGP_OP_COSVP:
+        if (sib >= kJitMaxData) return kJitErrSlot;
+        if (code == MTGP_OP_SINVP || code == MTGP_OP_COSVP) ok = push();
+        jit_trig(o, code == MTGP_OP_SINV || code == MTGP_OP_SINVP, vib);
+        break;
+#define MTGP_JIT_FAM(F, I)                                                  \
+      case MTGP_OP_##F##C: fam = I; kind = 0; break;                        \
+      case MTGP_OP_##F##V: fam = I; kind = 1; uses_ib_slot = true; break;   \
+      case MTGP_OP_##F##S: fam = I; kind = 2; break;
+      MTGP_JIT_FAM(ADD, 0)
+      MTGP_JIT_FAM(SUB, 1)
+      MTGP_JIT_FAM(RSUB, 2)
+      MTGP_JIT_FAM(MUL, 3)
+      MTGP_JIT_FAM(DIV, 4)
+      MTGP_JIT_FAM(RDIV, 5)
+#undef MTGP_JIT_FAM
+#define MTGP_JIT_VC(F, I) \
+      case MTGP_OP_VC_##F: fam = I; kind = 3; uses_ax_slot = true; break; \
+      case MTGP_OP_VCP_##F: fam = I; kind = 4; uses_ax_slot = true; break;
+      MTGP_JIT_VC(ADD, 0)
+      MTGP_JIT_VC(SUB, 1)
+      MTGP_JIT_VC(RSUB, 2)
+      MTGP_JIT_VC(MUL, 3)
+      MTGP_JIT_VC(DIV, 4)
+      MTGP_JIT_VC(RDIV, 5)
+#undef MTGP_JIT_VC
+#define MTGP_JIT_VV(F, I) \
+      case MTGP_OP_VV_##F: fam = I; kind = 5; uses_ib_slot = uses_ax_slot = true; break; \
+      case MTGP_OP_VVP_##F: fam = I; kind = 6; uses_ib_slot = uses_ax_slot = true; break;
+      MTGP_JIT_VV(ADD, 0)
+      MTGP_JIT_VV(SUB, 1)
+      MTGP_JIT_VV(MUL, 3)
+      MTGP_JIT_VV(DIV, 4)
+#undef MTGP_JIT_VV
+      default:
+        return kJitErrOpcode;
+    }
+    if (!ok) return kJitErrStack;
+    if (fam < 0) continue;  // handled above
+    if ((uses_ib_slot && sib >= kJitMaxData) || (uses_ax_slot && sax >= kJitMaxData)) return kJitErrSlot;
+    // family f in (ADD, SUB, RSUB, MUL, DIV, RDIV): R* forms swap the operands
+    const int base_fn = fam == 0 ? MTGP_FN_ADD : fam <= 2 ? MTGP_FN_SUB : fam == 3 ? MTGP_FN_MUL : MTGP_FN_DIV;
+    const bool rev = fam == 2 || fam == 5;
+    JitSrc x, y;
+    if (kind <= 2) {  // acc OP {c, V(ib), pop}
+      x = acc;
+      if (kind == 0) y = c;
+      else if (kind == 1) y = vib;
+      else {
+        if (sp <= 0) return kJitErrStack;
+        --sp;
+        y = jit_reg(kJitStack + sp);
+      }
+    } else if (kind <= 4) {  // V(ax) OP c, optional push first
+      if (kind == 4 && !push()) return kJitErrStack;
+      x = vax;
+      y = c;
+    } else {  // V(ib) OP V(ax)
+      if (kind == 6 && !push()) return kJitErrStack;
+      x = vib;
+      y = vax;
+    }
+    if (rev) { const JitSrc t = x; x = y; y = t; }
+    jit_binop(o, base_fn, x, y);
+  }
+  return kJitErrNoEnd;
+}
+
+}  // namespace mtgp
+
+#endif  // MTGP_JIT_H

@@ -17,11 +17,14 @@
 // 403-433; dynamic_evaluate.py:37-118; feedforward_evaluate.py:36-110;
 // SR_evaluator.py:30-94; acrobot.py:29-87).
 #include <hip/hip_runtime.h>
+#include <hsa/hsa.h>
+#include <hsa/hsa_ext_amd.h>
 #include <stdint.h>
 #include "mtgp.h"
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_flatten.h"
+#include "mtgp_jit.h"
 
 namespace {
 
@@ -201,6 +204,8 @@ struct KArgs {
   int32_t P;
   MtgpRollouts ro;
   MtgpOutputs out;
+  uint64_t jit_base;        // JIT code (executable device memory) or 0: interpreter only
+  const uint32_t* jit_off;  // [P, n_prog] byte offset of each program's code
 };
 
 // per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
@@ -250,6 +255,8 @@ struct Lane {
   int wave, lane, Rp, G, q0, g, r, p, rr;
   bool active;
   uint32_t ptab;  // lane gi (< G): byte offset of group gi's program block in A.prog
+  uint32_t jtab;  // lane gi * n_prog + j (< 64): JIT code offset of program j of group gi
+  bool jn;        // jtab holds every (group, program) pair of the wave
 };
 
 #ifndef MTGP_V_PTAB
@@ -281,6 +288,12 @@ __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
   L.ptab = prog_table(A, L);
+  L.jn = L.G * A.n_prog <= kWave;
+  L.jtab = 0;
+  if (A.jit_off && L.jn && L.lane < L.G * A.n_prog) {
+    const int gi = L.lane / A.n_prog, j = L.lane - gi * A.n_prog;
+    if (L.q0 + gi < A.P) L.jtab = A.jit_off[(size_t)sched_ind(A, L.q0 + gi) * A.n_prog + j];
+  }
   return true;
 }
 
@@ -305,9 +318,47 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 }
 
 // --------------------------------------------------------------------------------------
+// The data vector a tree reads and its operand stack.  Interpreter: one LDS column per slot
+// (dcol, st).  JIT: the slots live in VGPRs v[] that the call site pins to v0-v7
+// (mtgp_jit.h register ABI); the LDS columns are only filled for an interpreter fallback.
+template <bool JIT>
+struct DataVec {
+  float* dcol;
+  float* st;
+  float v[kDMax];
+  __device__ __forceinline__ DataVec(float* d, float* s) : dcol(d), st(s) {
+#pragma unroll
+    for (int k = 0; k < kDMax; ++k) v[k] = 0.0f;
+  }
+  __device__ __forceinline__ void put(int slot, float x) {
+    v[slot] = x;
+    if (!JIT) dcol[slot * kWave] = x;
+  }
+  __device__ __forceinline__ void spill() {
+#pragma unroll
+    for (int k = 0; k < kDMax; ++k) dcol[k * kWave] = v[k];
+  }
+};
+
+// Call JIT code at `addr` (mtgp_jit.h ABI): data in v0-v7, result in v8, s[32:33] collects
+// lanes that need the interpreter (slow sin/cos reduction).
+__device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], uint64_t& flag) {
+  // the target must sit in SGPRs: make its uniformity explicit to the compiler
+  const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr_ >> 32)) << 32;
+  float acc;
+  asm volatile("s_swappc_b64 s[30:31], %[tgt]"
+               : "={v8}"(acc), "+{s[32:33]}"(flag)
+               : [tgt] "s"(addr), "{v0}"(d[0]), "{v1}"(d[1]), "{v2}"(d[2]), "{v3}"(d[3]), "{v4}"(d[4]),
+                 "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
+               : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
+                 "v22", "v23", "v24", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "vcc", "memory");
+  return acc;
+}
+
 // Run program `slot` of group gi (its individual's program, wave-uniform).
-__device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
-                                         float* st) {
+__device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
+                                                float* st) {
 #if MTGP_V_PTAB
   const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.ptab, gi) +
                        (uint32_t)slot * (uint32_t)A.L * (uint32_t)sizeof(MtgpInstr);
@@ -318,6 +369,23 @@ __device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, 
 #endif
 }
 
+template <bool JIT>
+__device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, DataVec<JIT>& D) {
+  if (!JIT) return run_one_interp(A, L, gi, slot, D.dcol, D.st);
+  const uint32_t off = L.jn ? (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, gi * A.n_prog + slot)
+                            : (uint32_t)uni((int)A.jit_off[(size_t)group_ind(A, L, gi) * A.n_prog + slot]);
+  uint64_t fl = 0;
+  float r = jit_call(A.jit_base + off, D.v, fl);
+  if (__builtin_expect(fl != 0, 0)) {  // some lane needs the slow sin/cos reduction
+    const uint64_t gm = __ballot(L.g == gi && L.active);
+    if (fl & gm) {
+      D.spill();
+      r = run_one_interp(A, L, gi, slot, D.dcol, D.st);
+    }
+  }
+  return r;
+}
+
 #ifndef MTGP_V_NOINTERP
 #define MTGP_V_NOINTERP 0  // diagnostic only: skip interpretation (cost attribution), never shipped
 #endif
@@ -326,14 +394,26 @@ __device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, 
 // The program runs with the FULL exec mask (lanes of other groups compute a discarded value
 // on their own data/stack columns): inside a divergent `if` the CFG structurizer would turn
 // the uniform opcode switch into exec-masked flow blocks (~2x the scalar dispatch cost).
-__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, int ng, int slot, const float* dcol,
-                                            float* st, float dflt) {
+template <bool JIT>
+__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, int ng, int slot, DataVec<JIT>& D,
+                                            float dflt) {
 #if MTGP_V_NOINTERP
-  return 0.01f * (float)(slot + 1) + 0.001f * dcol[4 * kWave];
+  return 0.01f * (float)(slot + 1) + 0.001f * D.v[4];
 #endif
   float v = dflt;
   for (int gi = 0; gi < ng; ++gi) {
-    const float t = run_one(A, L, gi, slot, dcol, st);
+    const float t = run_one<JIT>(A, L, gi, slot, D);
+    v = (L.g == gi) ? t : v;
+  }
+  return v;
+}
+
+// interpreter-only variant on explicit LDS columns (wide-state SR kernel)
+__device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L, int ng, int slot, const float* dcol,
+                                                   float* st, float dflt) {
+  float v = dflt;
+  for (int gi = 0; gi < ng; ++gi) {
+    const float t = run_one_interp(A, L, gi, slot, dcol, st);
     v = (L.g == gi) ? t : v;
   }
   return v;
@@ -359,7 +439,7 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
 // state equations; at save points the save-time readout (dyn.py:101) is appended.
 // NOISE: observation noise on; the save-point observation uses ts[k] (dyn.py:99), which is
 // recomputed when it differs from the stage-0 time of that step.
-template <int NA, bool TRAJ, bool NOISE>
+template <int NA, bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
@@ -369,6 +449,8 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  DataVec<JIT> D(dcol, st);
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
 
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
@@ -382,7 +464,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
   const int loff = Ln.p * R + r;  // element offset of this (individual, rollout) in a save row
 #pragma unroll
   for (int t = 0; t < kDMax - uslot - 1; ++t)
-    if (t < A.m.n_targets) dset(dcol, uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
+    if (t < A.m.n_targets) D.put(uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   // groups whose save-time readout differs from the drift readout (it reads y): bit per group
   uint64_t diff_mask = 0;
@@ -432,17 +514,17 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 #pragma unroll
       for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
 #pragma unroll
-      for (int j = 0; j < NA; ++j) dset(dcol, 4 + j, at[j]);
-      const float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);
+      for (int j = 0; j < NA; ++j) D.put(4 + j, at[j]);
+      const float u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);
       acro_drift(K, xt, u, kx);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
       acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
-      dset(dcol, uslot, u);
+      for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+      D.put(uslot, u);
 #pragma unroll 1
       for (int q = 0; q < NA; ++q) {
-        const float v = run_groups(A, Ln, ng, A.m.prog_state + q, dcol, st, 0.0f);
+        const float v = run_groups<JIT>(A, Ln, ng, A.m.prog_state + q, D, 0.0f);
 #pragma unroll
         for (int j = 0; j < NA; ++j) ka[j] = (q == j) ? v : ka[j];
       }
@@ -455,13 +537,13 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
             if (__float_as_uint(tsk) != __float_as_uint(t0 + (float)step * h)) {
               acro_obs<true>(nzc, tsk, x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
 #pragma unroll
-              for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
+              for (int i = 0; i < 4; ++i) D.put(i, y[i]);
             }
           }
           if (diff_mask != 0) {
             for (int gi = 0; gi < ng; ++gi) {
               if (!((diff_mask >> gi) & 1ull)) continue;
-              const float t = run_one(A, Ln, gi, A.m.prog_readout_save, dcol, st);
+              const float t = run_one<JIT>(A, Ln, gi, A.m.prog_readout_save, D);
               us = (Ln.g == gi) ? t : us;
             }
           }
@@ -516,7 +598,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 
 // --------------------------------------------------------------------------------------
 // Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
-template <bool TRAJ, bool NOISE>
+template <bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
@@ -526,6 +608,8 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  DataVec<JIT> D(dcol, st);
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
@@ -537,7 +621,7 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
   const int loff = Ln.p * R + r;
 #pragma unroll
   for (int t = 0; t < kDMax - 4; ++t)
-    if (t < A.m.n_targets) dset(dcol, 4 + t, A.ro.targets[rr * A.m.n_targets + t]);
+    if (t < A.m.n_targets) D.put(4 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   float x[4], kx[4], ax[4];
 #pragma unroll
@@ -558,8 +642,8 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
       acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
-      float u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);  // ff.py:106-107 (:97 at saves)
+      for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+      float u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);  // ff.py:106-107 (:97 at saves)
       acro_drift(K, xt, u, kx);
       if (stage == 0) {
         if (is_save) {
@@ -569,8 +653,8 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
             if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
               acro_obs<true>(nzc, tsk, x, y);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) dset(dcol, i, y[i]);
-              u = run_groups(A, Ln, ng, A.m.prog_readout, dcol, st, 0.0f);
+              for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+              u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);
             }
           }
           if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), u, x[0], x[1]);
@@ -613,7 +697,7 @@ __global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
 
 // --------------------------------------------------------------------------------------
 // Symbolic regression of an ODE (SR_evaluator.py:57-94): dx_i = tree_i(x); MSE vs ys_true.
-template <int NV, bool TRAJ>
+template <int NV, bool TRAJ, bool JIT>
 __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
@@ -623,6 +707,8 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  DataVec<JIT> D(dcol, st);
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const size_t PR = (size_t)A.P * R;
@@ -667,10 +753,10 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) dset(dcol, i, stage_in(stage, x[i], kx[i], h, h2));
+      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], h, h2));
 #pragma unroll 1
       for (int q = 0; q < NV; ++q) {
-        const float v = run_groups(A, Ln, ng, A.m.prog_state + q, dcol, st, 0.0f);
+        const float v = run_groups<JIT>(A, Ln, ng, A.m.prog_state + q, D, 0.0f);
 #pragma unroll
         for (int j = 0; j < NV; ++j) kx[j] = (q == j) ? v : kx[j];
       }
@@ -804,7 +890,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       for (int t = 0; t < kWideComp; ++t) {
         const int c = c0 + t;
         if (c >= NV) break;
-        nxt[c * kWave] = run_groups(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+        nxt[c * kWave] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
       }
 #pragma unroll
       for (int t = 0; t < kWideComp; ++t) {
@@ -946,6 +1032,100 @@ __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict
 }
 
 hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+// --------------------------------------------------------------------------------------
+// Program JIT build (mtgp_jit.h): pass 1 sizes every program's code, one block scans the sizes
+// into byte offsets, pass 2 writes the code (vector stores) into executable device memory.
+__global__ void __launch_bounds__(256) k_jit_count(const MtgpInstr* __restrict__ prog, int total, int L,
+                                                   uint32_t* __restrict__ offs, int32_t* __restrict__ info) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int n = mtgp::jit_translate(prog + (size_t)i * L, L, nullptr);
+  offs[i] = n > 0 ? (uint32_t)n * 4u : 0u;
+  if (n < 0) atomicMin(&info[0], n);
+}
+
+// exclusive scan of offs[0..total) in place, offs[total] = total bytes, info[1] = total bytes
+// (saturated to INT32_MAX for the host check)
+__global__ void __launch_bounds__(1024) k_jit_scan(uint32_t* __restrict__ offs, int total, int32_t* __restrict__ info) {
+  __shared__ uint64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (total + 1023) / 1024;
+  const int b = t * per, e = b + per < total ? b + per : total;
+  uint64_t sum = 0;
+  for (int i = b; i < e; ++i) sum += offs[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  uint64_t run = part[t] - sum;
+  for (int i = b; i < e; ++i) {
+    const uint64_t w = offs[i];
+    offs[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+    run += w;
+  }
+  if (t == 1023) {
+    const uint64_t tot = part[1023];
+    offs[total] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+    info[1] = (int32_t)(tot < 0x7fffffffull ? tot : 0x7fffffffull);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_jit_emit(const MtgpInstr* __restrict__ prog, int total, int L,
+                                                  const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
+                                                  uint64_t code_bytes) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const uint32_t b = offs[i], e = offs[i + 1];
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable program or short buffer (host-checked)
+  mtgp::jit_translate(prog + (size_t)i * L, L, code + b / 4);
+}
+
+// Executable device memory for the JIT (HSA pool allocation with the executable flag on the
+// coarse-grained pool of the agent that backs HIP device `dev`, matched by PCI location).
+struct JitAgentQuery {
+  uint32_t domain, bdf;
+  bool found;
+  hsa_agent_t agent;
+  hsa_amd_memory_pool_t pool;
+  bool have_pool;
+};
+
+hsa_status_t jit_find_agent(hsa_agent_t a, void* data) {
+  JitAgentQuery* q = (JitAgentQuery*)data;
+  hsa_device_type_t t;
+  if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) != HSA_STATUS_SUCCESS || t != HSA_DEVICE_TYPE_GPU)
+    return HSA_STATUS_SUCCESS;
+  uint32_t bdf = 0, dom = 0;
+  hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_BDFID, &bdf);
+  hsa_agent_get_info(a, (hsa_agent_info_t)HSA_AMD_AGENT_INFO_DOMAIN, &dom);
+  if ((bdf >> 3) == (q->bdf >> 3) && dom == q->domain) {
+    q->agent = a;
+    q->found = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
+hsa_status_t jit_find_pool(hsa_amd_memory_pool_t p, void* data) {
+  JitAgentQuery* q = (JitAgentQuery*)data;
+  hsa_amd_segment_t seg;
+  if (hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_SEGMENT, &seg) != HSA_STATUS_SUCCESS ||
+      seg != HSA_AMD_SEGMENT_GLOBAL)
+    return HSA_STATUS_SUCCESS;
+  uint32_t fl = 0;
+  hsa_amd_memory_pool_get_info(p, HSA_AMD_MEMORY_POOL_INFO_GLOBAL_FLAGS, &fl);
+  if (fl & HSA_AMD_MEMORY_POOL_GLOBAL_FLAG_COARSE_GRAINED) {
+    q->pool = p;
+    q->have_pool = true;
+    return HSA_STATUS_INFO_BREAK;
+  }
+  return HSA_STATUS_SUCCESS;
+}
+
 bool g_timing = false;
 bool g_have_timing = false;
 
@@ -966,6 +1146,71 @@ int launch_timed(F&& launch, hipStream_t s) {
 extern "C" {
 
 int mtgp_abi_version(void) { return MTGP_ABI_VERSION; }
+
+int mtgp_jit_alloc(int32_t device, size_t bytes, void** code) {
+  if (!code || bytes == 0) return MTGP_ERR_ARG;
+  *code = nullptr;
+  static bool hsa_ready = false;
+  if (!hsa_ready) {
+    if (hsa_init() != HSA_STATUS_SUCCESS) return MTGP_ERR_LAUNCH;
+    hsa_ready = true;
+  }
+  int bus = 0, dev = 0, dom = 0;
+  if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
+      hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, device) != hipSuccess)
+    return MTGP_ERR_ARG;
+  JitAgentQuery q{(uint32_t)dom, (uint32_t)(bus << 8 | dev << 3), false, {}, {}, false};
+  hsa_iterate_agents(jit_find_agent, &q);
+  if (!q.found) return MTGP_ERR_ARG;
+  hsa_amd_agent_iterate_memory_pools(q.agent, jit_find_pool, &q);
+  if (!q.have_pool) return MTGP_ERR_ARG;
+  if (hsa_amd_memory_pool_allocate(q.pool, bytes, HSA_AMD_MEMORY_POOL_EXECUTABLE_FLAG, code) != HSA_STATUS_SUCCESS) {
+    *code = nullptr;
+    return MTGP_ERR_LAUNCH;
+  }
+  return MTGP_OK;
+}
+
+int mtgp_jit_free(void* code) {
+  if (!code) return MTGP_OK;
+  return hsa_amd_memory_pool_free(code) == HSA_STATUS_SUCCESS ? MTGP_OK : MTGP_ERR_ARG;
+}
+
+int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, uint32_t* offsets_out,
+                  int32_t* info_out, void* stream) {
+  if (!prog || !offsets_out || !info_out || P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+  const long total = (long)P * n_prog;
+  if (total > INT32_MAX - 1) return MTGP_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+  if (total == 0) return hipMemsetAsync(offsets_out, 0, sizeof(uint32_t), s) == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_jit_count, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, prog, (int)total, L,
+                     offsets_out, info_out);
+  hipLaunchKernelGGL(k_jit_scan, dim3(1), dim3(1024), 0, s, offsets_out, (int)total, info_out);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, const uint32_t* offsets, void* code,
+                  size_t code_bytes, void* stream) {
+  if (!prog || !offsets || !code || P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+  const long total = (long)P * n_prog;
+  if (total == 0) return MTGP_OK;
+  hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, prog,
+                     (int)total, L, offsets, (uint32_t*)code, (uint64_t)code_bytes);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words) {
+  if (!prog || L <= 0) return MTGP_ERR_ARG;
+  const int n = mtgp::jit_translate(prog, L, nullptr);
+  if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;  /* translation errors: -101 .. -104 */
+  if (out) {
+    if (n > max_words) return MTGP_ERR_ARG;
+    mtgp::jit_translate(prog, L, out);
+  }
+  return n;
+}
 
 int mtgp_set_timing(int enabled) {
   g_timing = enabled != 0;
@@ -1053,6 +1298,12 @@ int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_pro
 int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L,
                   const int32_t* nodes, int32_t P, const MtgpRollouts* rollouts, const MtgpOutputs* out,
                   void* stream) {
+  return mtgp_eval_rk4_jit(model, prog, plen, n_prog, L, nodes, P, rollouts, out, nullptr, stream);
+}
+
+int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen, int32_t n_prog,
+                      int32_t L, const int32_t* nodes, int32_t P, const MtgpRollouts* rollouts,
+                      const MtgpOutputs* out, const MtgpJitCode* jitc, void* stream) {
   if (!model || !prog || !plen || !nodes || !rollouts || !out || !out->fitness) return MTGP_ERR_ARG;
   if (P < 0 || n_prog <= 0 || L <= 0 || (L & 3) != 0) return MTGP_ERR_ARG;
   if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
@@ -1072,6 +1323,10 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
   A.P = P;
   A.ro = *rollouts;
   A.out = *out;
+  const bool jit = jitc && jitc->code && jitc->offsets && !(model->model == MTGP_MODEL_SR && model->n_var > 4);
+  A.jit_base = jit ? (uint64_t)(uintptr_t)jitc->code : 0;
+  A.jit_off = jit ? jitc->offsets : nullptr;
+  // (the wide-state SR kernel keeps its data vector in LDS: interpreter only)
   hipStream_t s = (hipStream_t)stream;
   int Rp = 1;
   while (Rp < rollouts->R) Rp <<= 1;
@@ -1090,12 +1345,20 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
 #define MTGP_DYN(NA)                                                                                      \
   case NA:                                                                                                \
     return launch_timed([&] {                                                                             \
-      if (noise) {                                                                                        \
-        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true>), grid, block, 0, s, A);             \
-        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true>), grid, block, 0, s, A);                 \
+      if (jit) {                                                                                          \
+        if (noise) {                                                                                      \
+          if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true, true>), grid, block, 0, s, A);     \
+          else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true, true>), grid, block, 0, s, A);         \
+        } else {                                                                                          \
+          if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false, true>), grid, block, 0, s, A);    \
+          else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false, true>), grid, block, 0, s, A);        \
+        }                                                                                                 \
+      } else if (noise) {                                                                                 \
+        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true, false>), grid, block, 0, s, A);      \
+        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true, false>), grid, block, 0, s, A);          \
       } else {                                                                                            \
-        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false>), grid, block, 0, s, A);            \
-        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false>), grid, block, 0, s, A);                \
+        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false, false>), grid, block, 0, s, A);     \
+        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false, false>), grid, block, 0, s, A);         \
       }                                                                                                   \
     }, s);
     switch (model->state_size) {
@@ -1110,12 +1373,20 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
     if (model->n_targets < 0 || 4 + model->n_targets > kDMax) return MTGP_ERR_ARG;
     if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
     return launch_timed([&] {
-      if (noise) {
-        if (traj) hipLaunchKernelGGL((k_acro_static<true, true>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_acro_static<false, true>), grid, block, 0, s, A);
+      if (jit) {
+        if (noise) {
+          if (traj) hipLaunchKernelGGL((k_acro_static<true, true, true>), grid, block, 0, s, A);
+          else hipLaunchKernelGGL((k_acro_static<false, true, true>), grid, block, 0, s, A);
+        } else {
+          if (traj) hipLaunchKernelGGL((k_acro_static<true, false, true>), grid, block, 0, s, A);
+          else hipLaunchKernelGGL((k_acro_static<false, false, true>), grid, block, 0, s, A);
+        }
+      } else if (noise) {
+        if (traj) hipLaunchKernelGGL((k_acro_static<true, true, false>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_acro_static<false, true, false>), grid, block, 0, s, A);
       } else {
-        if (traj) hipLaunchKernelGGL((k_acro_static<true, false>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_acro_static<false, false>), grid, block, 0, s, A);
+        if (traj) hipLaunchKernelGGL((k_acro_static<true, false, false>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_acro_static<false, false, false>), grid, block, 0, s, A);
       }
     }, s);
   } else if (model->model == MTGP_MODEL_SR) {
@@ -1133,8 +1404,11 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
 #define MTGP_SR(NV)                                                                                       \
   case NV:                                                                                                \
     return launch_timed([&] {                                                                             \
-      if (traj) hipLaunchKernelGGL((k_sr<NV, true>), grid, block, 0, s, A);                               \
-      else hipLaunchKernelGGL((k_sr<NV, false>), grid, block, 0, s, A);                                   \
+      if (jit) {                                                                                          \
+        if (traj) hipLaunchKernelGGL((k_sr<NV, true, true>), grid, block, 0, s, A);                       \
+        else hipLaunchKernelGGL((k_sr<NV, false, true>), grid, block, 0, s, A);                           \
+      } else if (traj) hipLaunchKernelGGL((k_sr<NV, true, false>), grid, block, 0, s, A);                 \
+      else hipLaunchKernelGGL((k_sr<NV, false, false>), grid, block, 0, s, A);                            \
     }, s);
     switch (model->n_var) {
       MTGP_SR(1)

@@ -8,6 +8,7 @@ evaluator calls.
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -40,13 +41,15 @@ class Flattened:
     L: int
     n_prog: int
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
+    jit: Optional[tuple] = None           # (code pointer, offsets [P*n_prog+1]) from the program JIT
+    jit_tried: bool = False
 
 
 class DeviceEngine:
     """Binds one fitness-function config + node library to the HIP kernels."""
 
     def __init__(self, fitness_function, library: NodeLibrary, size_parsinomy: float = 0.0, device=None,
-                 native=None):
+                 native=None, jit: Optional[bool] = None):
         self.ff = fitness_function
         self.lib = library
         self.parsimony = float(size_parsinomy)
@@ -57,6 +60,67 @@ class DeviceEngine:
         self._data = None
         self._specs_dev = None
         self._specs_key = None
+        # program JIT (csrc/mtgp_jit.h): on unless disabled here or by MTGP_JIT=0
+        self.use_jit = (os.environ.get("MTGP_JIT", "1") != "0") if jit is None else bool(jit)
+        self._arenas = [None, None]  # (pointer, bytes): a ring of two executable code buffers
+        self._arena_i = 0
+
+    def __del__(self):
+        try:
+            if any(a is not None for a in self._arenas):
+                torch.cuda.synchronize(self.device)
+                for a in self._arenas:
+                    if a is not None:
+                        self.native.mtgp_jit_free(a[0])
+                self._arenas = [None, None]
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ jit
+    def _arena(self, nbytes: int):
+        """Next buffer of the executable ring, grown when needed.  Alternating buffers keeps the code
+        of the previous population untouched while a new one is written (stream-ordered)."""
+        self._arena_i ^= 1
+        a = self._arenas[self._arena_i]
+        if a is None or a[1] < nbytes:
+            if a is not None:
+                torch.cuda.synchronize(self.device)
+                self.native.mtgp_jit_free(a[0])
+                self._arenas[self._arena_i] = None
+            size = max(int(nbytes * 1.25) + 4096, 1 << 20)
+            ptr = ctypes.c_void_p()
+            rc = self.native.mtgp_jit_alloc(self.device.index or 0, size, ctypes.byref(ptr))
+            if rc != nat.OK or not ptr.value:
+                raise RuntimeError(f"mtgp_jit_alloc({size}) failed: {rc}")
+            a = (ptr.value, size)
+            self._arenas[self._arena_i] = a
+        return a
+
+    def jit_build(self, fl: Flattened) -> Optional[tuple]:
+        """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit).
+        Returns None (interpreter) when disabled or when a program cannot be translated."""
+        if fl.jit_tried:
+            return fl.jit
+        fl.jit_tried = True
+        if not self.use_jit or self.ff.n_data() > 8:
+            return None
+        P = fl.prog.shape[0]
+        offs = torch.empty((P * fl.n_prog + 1,), dtype=torch.int32, device=self.device)
+        info = torch.empty((2,), dtype=torch.int32, device=self.device)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), info.data_ptr(),
+                                       stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_jit_plan failed: {rc}")
+        err, total = (int(v) for v in info.cpu().tolist())
+        if err < 0 or total <= 0 or total >= 0x7FFFFFFF:
+            return None
+        ptr, size = self._arena(total)
+        rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), ptr, size, stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
+        fl.jit = (ptr, offs)
+        return fl.jit
 
     # ------------------------------------------------------------------ data
     def prepare_data(self, data) -> dict:
@@ -204,8 +268,13 @@ class DeviceEngine:
                         res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
                         setattr(out, name, res[name].data_ptr())
         stream = torch.cuda.current_stream(dev).cuda_stream
-        rc = self.native.mtgp_eval_rk4(ctypes.byref(m), fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L,
-                                       fl.nodes.data_ptr(), P, ctypes.byref(ro), ctypes.byref(out), stream)
+        jit = self.jit_build(fl)
+        jc = nat.MtgpJitCode()
+        if jit is not None:
+            jc.code, jc.offsets = jit[0], jit[1].data_ptr()
+        rc = self.native.mtgp_eval_rk4_jit(ctypes.byref(m), fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L,
+                                           fl.nodes.data_ptr(), P, ctypes.byref(ro), ctypes.byref(out),
+                                           ctypes.byref(jc), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_eval_rk4 rejected the configuration (code {rc})")
         if check:

@@ -182,3 +182,43 @@ def test_obs_noise_save_time_differs_from_step_time(kind):
     res, ref, d = _run(ff, lib, data, pop)
     assert d["save_every"] == 3
     _check(res, ref, pop.shape[0], 16, names)
+
+
+def _run_engine(ff, lib, data, pop, jit):
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=jit)
+    res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=True,
+                       rollout_fitness=True)
+    torch.cuda.synchronize()
+    assert (res["_flat"].jit is not None) == jit
+    return {k: v.cpu().numpy() for k, v in res.items() if isinstance(v, torch.Tensor)}
+
+
+@pytest.mark.parametrize("kind", ["dynamic_noise", "static", "sr"])
+def test_jit_matches_interpreter(kind):
+    """The program JIT (csrc/mtgp_jit.h) and the interpreter give bit-identical results."""
+    if kind == "dynamic_noise":
+        env, lib, ff, data, pop = dynamic_setup(P=48, R=32, n_steps=60, obs_noise=0.1, seed=6)
+    elif kind == "static":
+        env, lib, ff, data, pop = static_setup(P=48, R=16, n_steps=60, seed=6)
+    else:
+        env, lib, ff, data, pop = sr_setup(P=48, R=16, seed=6)
+    a = _run_engine(ff, lib, data, pop, True)
+    b = _run_engine(ff, lib, data, pop, False)
+    for k in a:
+        assert bits_equal(a[k], b[k]), mismatch_report(a[k], b[k], k)
+
+
+def test_jit_slow_sin_cos_lanes_fall_back_to_interpreter():
+    """Coefficients scaled by 1e6: sin/cos arguments beyond 2^17 take the spec's slow
+    reduction, which the JIT code reports and the evaluator re-runs with the interpreter."""
+    env, lib, ff, data, pop = dynamic_setup(P=40, R=16, n_steps=30, seed=9)
+    coef = pop[..., 0] == 1.0
+    pop = pop.copy()
+    pop[..., 3] = np.where(coef, pop[..., 3] * 1e6, pop[..., 3])
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=True)
+    res = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=True, rollout_fitness=True)
+    torch.cuda.synchronize()
+    assert res["_flat"].jit is not None
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])

@@ -1,0 +1,211 @@
+"""Program JIT (multitreegp_amd/csrc/mtgp_jit.h) checked on the CPU before any GPU runs it.
+
+* the committed templates (mtgp_jit_blobs.h) are what scripts/gen_jit_templates.py assembles;
+* every translated program disassembles cleanly with llvm-mc (gfx950), ends in
+  s_setpc_b64 s[30:31] and writes only the registers the call-site ABI allows
+  (v8-v24, s[32:39], vcc; never v0-v7, exec or other SGPRs);
+* a word-level emulator of the emitted subset (v_mov / v_add / v_sub / v_subrev / v_mul, the
+  sin / cos / div templates as black boxes) reproduces the row-order oracle bit for bit on
+  random trees and data, which pins operand order and the compile-time operand stack."""
+import os
+import re
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM_MC = "/opt/rocm/lib/llvm/bin/llvm-mc"
+
+from multitreegp_amd import _native as nat  # noqa: E402
+from multitreegp_amd.sampling import sample_population  # noqa: E402
+from oracle import oracle as orc  # noqa: E402
+from helpers import CONTROL_OPS, SR_OPS  # noqa: E402
+import multitreegp_amd as mt  # noqa: E402
+
+pytestmark = pytest.mark.skipif(not os.path.exists(nat.LIB_PATH), reason="libmtgp_hip.so not built")
+
+
+def _blobs():
+    text = open(os.path.join(ROOT, "multitreegp_amd", "csrc", "mtgp_jit_blobs.h")).read()
+    out = {}
+    for name, body in re.findall(r"mtgp_jit_(\w+)_blob\[\d+\] = \{(.*?)\};", text):
+        out[name.upper()] = [int(x.rstrip("u"), 16) for x in body.split(",")]
+    return out
+
+
+BLOBS = _blobs()
+SETPC = 0xBE801D1E
+
+
+def test_templates_up_to_date():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "gen_jit_templates.py"), "--check"])
+    assert r.returncode == 0, "mtgp_jit_blobs.h is stale: rerun scripts/gen_jit_templates.py"
+
+
+def _programs(lib, pop, n_data, masks):
+    nl = lib.native()
+    progs = []
+    for p in range(pop.shape[0]):
+        for t in range(pop.shape[1]):
+            for zm in masks:
+                instrs, _ = nat.flatten_tree_host(pop[p, t], nl, n_data, zm)
+                raw = _raw_program(pop[p, t], nl, n_data, zm)
+                progs.append((p, t, zm, raw))
+    return progs
+
+
+def _raw_program(tree, nl, n_data, zm):
+    import ctypes
+    lib = nat.load()
+    t = np.ascontiguousarray(tree, np.float32)
+    L = 2 * t.shape[0] + 8
+    out = (nat.MtgpInstr * L)()
+    need = ctypes.c_int32(0)
+    n = lib.mtgp_flatten_tree_host(t.ctypes.data, t.shape[0], ctypes.byref(nl), n_data, zm, L, ctypes.addressof(out),
+                                   ctypes.byref(need))
+    assert n > 0
+    return np.frombuffer(bytes(out), dtype=np.uint32).reshape(-1, 2)[: n + 1].copy()
+
+
+def _disassemble(words):
+    text = " ".join(f"0x{(w >> (8 * b)) & 0xff:02x}" for w in words for b in range(4))
+    r = subprocess.run([LLVM_MC, "-arch=amdgcn", "-mcpu=gfx950", "--disassemble"], input=text.encode(),
+                       capture_output=True)
+    assert r.returncode == 0 and not r.stderr.strip(), r.stderr.decode()[:500]
+    return [ln.strip() for ln in r.stdout.decode().splitlines() if ln.strip()]
+
+
+ALLOWED_V = set(range(8, 25))
+ALLOWED_S = set(range(30, 40))
+
+
+def _check_abi(lines):
+    assert lines[-1] == "s_setpc_b64 s[30:31]", lines[-1]
+    for ln in lines[:-1]:
+        assert "exec" not in ln and "invalid" not in ln.lower(), ln
+        op, _, rest = ln.partition(" ")
+        dst = rest.split(",")[0].strip()
+        if op.startswith("s_nop"):
+            continue
+        if op.startswith("v_cmp") and op.endswith("_e32"):
+            assert dst == "vcc", ln
+            continue
+        m = re.fullmatch(r"v(\d+)", dst)
+        if m:
+            assert int(m.group(1)) in ALLOWED_V, ln
+            # the vcc / sgpr written by v_div_scale / v_cmp_e64 (second operand) is checked below
+            if op.startswith("v_div_scale"):
+                sd = rest.split(",")[1].strip()
+                assert sd == "vcc" or re.fullmatch(r"s\[(\d+):(\d+)\]", sd) and \
+                    all(int(x) in ALLOWED_S for x in re.findall(r"\d+", sd)), ln
+            continue
+        m = re.fullmatch(r"s\[(\d+):(\d+)\]|s(\d+)", dst)
+        assert m, ln
+        regs = [int(x) for x in m.groups() if x is not None]
+        assert all(r in ALLOWED_S for r in regs), ln
+
+
+def _setup(kind):
+    if kind == "dynamic":
+        lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
+        pop = sample_population(5, lib, 40, 1, max_init_depth=8, max_nodes=64)[0]
+        return lib, pop, 7, [0, 0b1001111]
+    if kind == "sr":
+        lib = mt.NodeLibrary(SR_OPS, [["x0", "x1", "x2", "x3"]], [4])
+        pop = sample_population(6, lib, 30, 1, max_init_depth=7, max_nodes=64)[0]
+        return lib, pop, 4, [0]
+    lib = mt.NodeLibrary(CONTROL_OPS + [("/", None, 2, 0.1)], [["y1", "y2", "y3", "y4"]], [1])
+    pop = sample_population(7, lib, 60, 1, max_init_depth=6, max_nodes=40)[0]
+    return lib, pop, 4, [0]
+
+
+def _emulate(words, data):
+    """Run emitted code on data [n_data, M] (float32 lanes); returns v8."""
+    M = data.shape[1]
+    v = np.zeros((32, M), np.float32)
+    v[: data.shape[0]] = data
+    i = 0
+    lit = lambda k: np.full(M, np.array(words[k], np.uint32).view(np.float32), np.float32)  # noqa: E731
+    while True:
+        w = words[i]
+        if w == SETPC:
+            return v[8]
+        hit = None
+        for name, b in BLOBS.items():
+            if words[i:i + len(b)] == b:
+                hit = name
+                break
+        if hit == "DIV":
+            with np.errstate(all="ignore"):
+                v[8] = v[17] / v[18]
+            i += len(BLOBS["DIV"])
+            continue
+        if hit in ("SIN", "COS"):
+            s, c = orc.sincos(v[17])
+            v[8] = s if hit == "SIN" else c
+            i += len(BLOBS[hit])
+            continue
+        src0 = w & 0x1FF
+        if src0 == 255:
+            a = lit(i + 1)
+            step = 2
+        else:
+            assert src0 >= 256, hex(w)
+            a = v[src0 - 256].copy()
+            step = 1
+        vdst = (w >> 17) & 0xFF
+        if (w >> 25) == 0x3F:  # VOP1
+            assert ((w >> 9) & 0xFF) == 1, hex(w)  # v_mov_b32
+            v[vdst] = a
+        else:
+            assert (w >> 31) == 0, hex(w)
+            b = v[(w >> 9) & 0xFF]
+            op = w >> 25
+            with np.errstate(all="ignore"):
+                v[vdst] = {1: lambda: a + b, 2: lambda: a - b, 3: lambda: b - a, 5: lambda: a * b}[op]()
+        i += step
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr"])
+def test_translation_disassembles_and_respects_abi(kind):
+    lib, pop, n_data, masks = _setup(kind)
+    progs = _programs(lib, pop[:12], n_data, masks)
+    words_all = []
+    for (_, _, _, raw) in progs:
+        words = nat.jit_translate_host(raw)
+        words_all.append(words)
+        lines = _disassemble([int(w) for w in words])
+        _check_abi(lines)
+    assert len(words_all) >= 12
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr"])
+def test_emulated_code_matches_row_order_oracle(kind):
+    lib, pop, n_data, masks = _setup(kind)
+    rng = np.random.default_rng(3)
+    data = (rng.standard_normal((n_data, 33)) * 2.5).astype(np.float32)
+    data[:, 0] = 0.0
+    data[:, 1] = [1e6, -3e5, 2.0, 0.5, -0.0, 7.0, 1e-30][:n_data]  # large / tiny / signed-zero lanes
+    checked = 0
+    for (p, t, zm, raw) in _programs(lib, pop, n_data, masks):
+        words = [int(w) for w in nat.jit_translate_host(raw)]
+        got = _emulate(words, data)
+        d = data.copy()
+        for k in range(n_data):
+            if zm >> k & 1:
+                d[k] = 0.0
+        want = np.array([orc.eval_tree(pop[p, t], lib.fn_codes, lib.n_funcs, lib.var_start, d[:, m])
+                         for m in range(d.shape[1])], np.float32)
+        same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+        assert same.all(), (p, t, zm, got[~same][:4], want[~same][:4])
+        checked += 1
+    assert checked >= 30
+
+
+def test_translation_rejects_wide_slots():
+    raw = np.array([[nat.OP_NAMES.index("LDV") << nat.OP_SHIFT, 9 * nat.SLOT_BYTES],
+                    [nat.OP_NAMES.index("END") << nat.OP_SHIFT, 0]], np.uint32)
+    with pytest.raises(ValueError):
+        nat.jit_translate_host(raw)
