@@ -207,13 +207,17 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  *   mtgp_jit_plan   -> offsets[P*n_prog + 1] (byte offset of each program's code, last =
  *                      total) and info[2] = {0 or a negative code if some program cannot be
  *                      translated (data slot >= 8), total bytes}   (device, stream-ordered)
- *   (host reads info, sizes an executable buffer from mtgp_jit_alloc)
+ *   (host sizes an executable buffer from mtgp_jit_alloc -- from info, or from an
+ *    estimate when info is passed on to the evaluator, which then checks it on the device)
  *   mtgp_jit_emit   -> writes the code
  *   mtgp_eval_rk4_jit with MtgpJitCode{code, offsets}.
  * The acrobot evaluators and SR with n_var <= 4 use the code; other models ignore it. */
 typedef struct {
-  const void* code;         /* executable device memory from mtgp_jit_alloc */
-  const uint32_t* offsets;  /* [P*n_prog + 1] from mtgp_jit_plan            */
+  const void* code;         /* executable device memory from mtgp_jit_alloc           */
+  const uint32_t* offsets;  /* [P*n_prog + 1] from mtgp_jit_plan                      */
+  const int32_t* info;      /* info[2] of mtgp_jit_plan, or NULL if the host checked it */
+  uint64_t capacity;        /* bytes of `code`; the kernel interprets when info says the */
+                            /* plan failed or the code did not fit (no host round trip) */
 } MtgpJitCode;
 
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code);

@@ -206,6 +206,8 @@ struct KArgs {
   MtgpOutputs out;
   uint64_t jit_base;        // JIT code (executable device memory) or 0: interpreter only
   const uint32_t* jit_off;  // [P, n_prog] byte offset of each program's code
+  const int32_t* jit_info;  // mtgp_jit_plan info {status, total bytes} (device) or NULL
+  uint64_t jit_cap;         // bytes of the code buffer
 };
 
 // per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
@@ -257,6 +259,7 @@ struct Lane {
   uint32_t ptab;  // lane gi (< G): byte offset of group gi's program block in A.prog
   uint32_t jtab;  // lane gi * n_prog + j (< 64): JIT code offset of program j of group gi
   bool jn;        // jtab holds every (group, program) pair of the wave
+  bool jok;       // the JIT code of this launch is complete (plan status 0, fits the buffer)
 };
 
 #ifndef MTGP_V_PTAB
@@ -289,6 +292,9 @@ __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.rr = L.active ? L.r : 0;
   L.ptab = prog_table(A, L);
   L.jn = L.G * A.n_prog <= kWave;
+  L.jok = true;
+  if (A.jit_info)  // checked on the device, so the host never waits for the plan
+    L.jok = uni((int)(A.jit_info[0] == 0 && (uint64_t)(uint32_t)A.jit_info[1] <= A.jit_cap)) != 0;
   L.jtab = 0;
   if (A.jit_off && L.jn && L.lane < L.G * A.n_prog) {
     const int gi = L.lane / A.n_prog, j = L.lane - gi * A.n_prog;
@@ -372,8 +378,16 @@ __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, i
 template <bool JIT>
 __device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, DataVec<JIT>& D) {
   if (!JIT) return run_one_interp(A, L, gi, slot, D.dcol, D.st);
-  const uint32_t off = L.jn ? (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, gi * A.n_prog + slot)
-                            : (uint32_t)uni((int)A.jit_off[(size_t)group_ind(A, L, gi) * A.n_prog + slot]);
+  if (__builtin_expect(!L.jok, 0)) {  // no usable code for this launch: interpret
+    D.spill();
+    return run_one_interp(A, L, gi, slot, D.dcol, D.st);
+  }
+  uint32_t off;
+  if (__builtin_expect(uni((int)L.jn), 1)) {  // wave-uniform: every (group, program) offset is in jtab
+    off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, gi * A.n_prog + slot);
+  } else {
+    off = (uint32_t)uni((int)A.jit_off[(size_t)group_ind(A, L, gi) * A.n_prog + slot]);
+  }
   uint64_t fl = 0;
   float r = jit_call(A.jit_base + off, D.v, fl);
   if (__builtin_expect(fl != 0, 0)) {  // some lane needs the slow sin/cos reduction
@@ -1326,6 +1340,8 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const bool jit = jitc && jitc->code && jitc->offsets && !(model->model == MTGP_MODEL_SR && model->n_var > 4);
   A.jit_base = jit ? (uint64_t)(uintptr_t)jitc->code : 0;
   A.jit_off = jit ? jitc->offsets : nullptr;
+  A.jit_info = jit ? jitc->info : nullptr;
+  A.jit_cap = jit ? jitc->capacity : 0;
   // (the wide-state SR kernel keeps its data vector in LDS: interpreter only)
   hipStream_t s = (hipStream_t)stream;
   int Rp = 1;

@@ -41,7 +41,7 @@ class Flattened:
     L: int
     n_prog: int
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
-    jit: Optional[tuple] = None           # (code pointer, offsets [P*n_prog+1]) from the program JIT
+    jit: Optional[tuple] = None           # (code ptr, offsets [P*n_prog+1], info [2], capacity) of the JIT
     jit_tried: bool = False
 
 
@@ -64,6 +64,8 @@ class DeviceEngine:
         self.use_jit = (os.environ.get("MTGP_JIT", "1") != "0") if jit is None else bool(jit)
         self._arenas = [None, None]  # (pointer, bytes): a ring of two executable code buffers
         self._arena_i = 0
+        self._jit_last = None        # (pinned host info, event) of the previous build: capacity hint
+        self._jit_bytes_per_prog = 1024.0
 
     def __del__(self):
         try:
@@ -97,30 +99,48 @@ class DeviceEngine:
         return a
 
     def jit_build(self, fl: Flattened) -> Optional[tuple]:
-        """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit).
-        Returns None (interpreter) when disabled or when a program cannot be translated."""
+        """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit),
+        without a host round trip: the buffer is sized from the code size per program seen in
+        earlier builds (read back asynchronously), and the evaluator checks the plan's status and
+        size on the device, interpreting when the code is unusable.  Returns None when disabled."""
         if fl.jit_tried:
             return fl.jit
         fl.jit_tried = True
         if not self.use_jit or self.ff.n_data() > 8:
             return None
         P = fl.prog.shape[0]
-        offs = torch.empty((P * fl.n_prog + 1,), dtype=torch.int32, device=self.device)
-        info = torch.empty((2,), dtype=torch.int32, device=self.device)
+        n = P * fl.n_prog
+        if self._jit_last is not None and self._jit_last[1].query():  # previous plan done: learn its size
+            err, total, n_prev = (int(v) for v in self._jit_last[0].tolist())
+            if err == 0 and n_prev > 0:
+                self._jit_bytes_per_prog = max(self._jit_bytes_per_prog * 0.5, total / n_prev * 1.5)
+        offs = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
+        info = torch.empty((3,), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), info.data_ptr(),
                                        stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_plan failed: {rc}")
-        err, total = (int(v) for v in info.cpu().tolist())
-        if err < 0 or total <= 0 or total >= 0x7FFFFFFF:
-            return None
-        ptr, size = self._arena(total)
+        info[2].fill_(n)
+        host = torch.empty((3,), dtype=torch.int32, pin_memory=True)
+        host.copy_(info, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        self._jit_last = (host, ev)
+        ptr, size = self._arena(int(n * self._jit_bytes_per_prog) + 4096)
         rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), ptr, size, stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
-        fl.jit = (ptr, offs)
+        fl.jit = (ptr, offs, info, size)
         return fl.jit
+
+    @staticmethod
+    def jit_ok(fl: Flattened) -> bool:
+        """Whether the evaluations of `fl` ran JIT code (synchronises; tests and tooling)."""
+        if fl.jit is None:
+            return False
+        err, total = (int(v) for v in fl.jit[2][:2].cpu().tolist())
+        return err == 0 and 0 < total <= fl.jit[3]
 
     # ------------------------------------------------------------------ data
     def prepare_data(self, data) -> dict:
@@ -271,7 +291,7 @@ class DeviceEngine:
         jit = self.jit_build(fl)
         jc = nat.MtgpJitCode()
         if jit is not None:
-            jc.code, jc.offsets = jit[0], jit[1].data_ptr()
+            jc.code, jc.offsets, jc.info, jc.capacity = jit[0], jit[1].data_ptr(), jit[2].data_ptr(), jit[3]
         rc = self.native.mtgp_eval_rk4_jit(ctypes.byref(m), fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L,
                                            fl.nodes.data_ptr(), P, ctypes.byref(ro), ctypes.byref(out),
                                            ctypes.byref(jc), stream)

@@ -189,7 +189,7 @@ def _run_engine(ff, lib, data, pop, jit):
     res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=True,
                        rollout_fitness=True)
     torch.cuda.synchronize()
-    assert (res["_flat"].jit is not None) == jit
+    assert DeviceEngine.jit_ok(res["_flat"]) == jit
     return {k: v.cpu().numpy() for k, v in res.items() if isinstance(v, torch.Tensor)}
 
 
@@ -218,7 +218,25 @@ def test_jit_slow_sin_cos_lanes_fall_back_to_interpreter():
     eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=True)
     res = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=True, rollout_fitness=True)
     torch.cuda.synchronize()
-    assert res["_flat"].jit is not None
+    assert DeviceEngine.jit_ok(res["_flat"])
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
+
+
+def test_jit_code_that_does_not_fit_is_interpreted():
+    """The host never waits for the JIT plan: when the code is larger than the buffer the
+    evaluator sees it on the device and interprets (results unchanged)."""
+    env, lib, ff, data, pop = dynamic_setup(P=24, R=16, n_steps=30, seed=12)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=True)
+    pd = torch.from_numpy(pop).cuda()
+    fl = eng.flatten(pd)
+    eng.schedule(fl, 16)
+    ptr, offs, info, cap = eng.jit_build(fl)
+    fl.jit = (ptr, offs, info, 16)  # claim a 16-byte buffer: every launch must fall back
+    assert not DeviceEngine.jit_ok(fl)
+    res = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True, flattened=fl)
+    torch.cuda.synchronize()
     d = eng.prepare_data(data)
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
     _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
