@@ -454,7 +454,7 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
 // NOISE: observation noise on; the save-point observation uses ts[k] (dyn.py:99), which is
 // recomputed when it differs from the stage-0 time of that step.
 template <int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_acro_dynamic(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(256) k_acro_dynamic(KArgs A) {
 // --------------------------------------------------------------------------------------
 // Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
 template <bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) k_acro_static(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_acro_static(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
