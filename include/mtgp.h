@@ -203,10 +203,14 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  * of every rollout runs them), so they can be translated once into gfx950 machine code that
  * the evaluator calls directly instead of interpreting (multitreegp_amd/csrc/mtgp_jit.h; no
  * reference counterpart -- this replaces XLA's compile of the vmapped tree evaluator).
- * Results are bit-identical to the interpreter.  Usage per flattened population:
- *   mtgp_jit_plan   -> offsets[P*n_prog + 1] (byte offset of each program's code, last =
- *                      total) and info[2] = {0 or a negative code if some program cannot be
- *                      translated (data slot >= 8), total bytes}   (device, stream-ordered)
+ * Code is emitted per (wave, program) unit: the code the evaluator calls to run program j for
+ * all G = 64 / pow2ceil(R) individuals packed in one wave, so it depends on R and on the
+ * schedule (order) the evaluation will use.
+ * Results are bit-identical to the interpreter.  Usage per flattened population + schedule:
+ *   mtgp_jit_units  -> number of units U = ceil(P / G) * n_prog
+ *   mtgp_jit_plan   -> offsets[U + 1] (byte offset of each unit's code, last = total) and
+ *                      info[2] = {0 or a negative code if some program cannot be translated
+ *                      (data slot >= 8), total bytes}   (device, stream-ordered)
  *   (host sizes an executable buffer from mtgp_jit_alloc -- from info, or from an
  *    estimate when info is passed on to the evaluator, which then checks it on the device)
  *   mtgp_jit_emit   -> writes the code
@@ -214,7 +218,7 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  * The acrobot evaluators and SR with n_var <= 4 use the code; other models ignore it. */
 typedef struct {
   const void* code;         /* executable device memory from mtgp_jit_alloc           */
-  const uint32_t* offsets;  /* [P*n_prog + 1] from mtgp_jit_plan                      */
+  const uint32_t* offsets;  /* [units + 1] from mtgp_jit_plan (same model, R, order)   */
   const int32_t* info;      /* info[2] of mtgp_jit_plan, or NULL if the host checked it */
   uint64_t capacity;        /* bytes of `code`; the kernel interprets when info says the */
                             /* plan failed or the code did not fit (no host round trip) */
@@ -222,12 +226,21 @@ typedef struct {
 
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code);
 int mtgp_jit_free(void* code);
-int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, uint32_t* offsets_out,
-                  int32_t* info_out, void* stream);
-int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, const uint32_t* offsets,
-                  void* code, size_t code_bytes, void* stream);
+int mtgp_jit_units(int32_t P, int32_t n_prog, int32_t R);
+int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                  const int32_t* order, uint32_t* offsets_out, int32_t* info_out, void* stream);
+int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                  const int32_t* order, const uint32_t* offsets, void* code, size_t code_bytes,
+                  void* stream);
 /* host translation of one program (tests/tooling): number of code words, or < 0 */
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
+/* Schedule weights for JIT code: cost_out[P*n_prog] = executed code words / 4 of each program
+ * (plen where a program cannot be translated); pass it to mtgp_schedule instead of plen. */
+int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t n_prog, int32_t L,
+                  int32_t* cost_out, void* stream);
+/* host emission of one (wave, program) unit over HOST arrays prog/order (tests/tooling) */
+int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                       const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words);
 int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,
                       int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
                       const MtgpRollouts* rollouts, const MtgpOutputs* out, const MtgpJitCode* jit,

@@ -45,6 +45,7 @@ constexpr int kJitMaxWordsPerInstr = 1 + 4 + MTGP_JIT_SIN_WORDS;
 struct JitOut {
   uint32_t* out;  // nullptr: count only
   int n;
+  int trig = 0;   // sin/cos templates emitted (their double-precision block is normally skipped)
   MTGP_JIT_HD void w(uint32_t v) {
     if (out) out[n] = v;
     ++n;
@@ -101,6 +102,7 @@ MTGP_JIT_HD inline void jit_binop(JitOut& o, int fn, JitSrc x, JitSrc y) {
 }
 
 MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
+  ++o.trig;
   if (x.lit) o.movc(kJitT0, x.bits); else o.movv(kJitT0, x.reg);
   if (is_sin) o.blob(mtgp_jit_sin_blob, MTGP_JIT_SIN_WORDS);
   else o.blob(mtgp_jit_cos_blob, MTGP_JIT_COS_WORDS);
@@ -108,10 +110,10 @@ MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
 
 enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJitErrNoEnd = -4 };
 
-// Translate one END-terminated program (at most L instructions).  Returns the number of
-// 32-bit code words (out == nullptr: count only) or a negative kJitErr* code.
-MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out) {
-  JitOut o{out, 0};
+// Translate one END-terminated program (at most L instructions) into o; with `ret` the END
+// becomes s_setpc_b64 s[30:31], otherwise nothing (the code falls through).  Returns kJitOk
+// or a negative kJitErr* code.
+MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret) {
   int sp = 0;
   for (int i = 0; i < L; ++i) {
     const uint32_t w = prog[i].op;
@@ -133,8 +135,8 @@ MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out
     int fam = -1, kind = -1;  // family ADD SUB RSUB MUL DIV RDIV; kind 0 C, 1 V, 2 S
     switch (code) {
       case MTGP_OP_END:
-        o.w(kSetpcS30);
-        return o.n;
+        if (ret) o.w(kSetpcS30);
+        return kJitOk;
       case MTGP_OP_LDC: o.movc(kJitAcc, ib); continue;
       case MTGP_OP_LDCP: ok = push(); o.movc(kJitAcc, ib); break;
       case MTGP_OP_LDV: uses_ib_slot = true; if (sib >= kJitMaxData) return kJitErrSlot; o.movv(kJitAcc, kJitData + sib); continue;
@@ -207,6 +209,62 @@ MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out
     jit_binop(o, base_fn, x, y);
   }
   return kJitErrNoEnd;
+}
+
+// One callable program: number of 32-bit code words (out == nullptr: count only) or < 0.
+MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out) {
+  JitOut o{out, 0};
+  const int rc = jit_program(o, prog, L, true);
+  return rc < 0 ? rc : o.n;
+}
+
+// Estimated issue cost of one program (schedule weight): code words actually executed, i.e.
+// without the slow-reduction blocks of the sin/cos templates (skipped unless |x| >= 2^17).
+constexpr int kJitTrigSkipped = MTGP_JIT_SIN_SKIPPABLE_WORDS;
+MTGP_JIT_HD inline int jit_cost(const MtgpInstr* prog, int L) {
+  JitOut o{nullptr, 0};
+  const int rc = jit_program(o, prog, L, true);
+  if (rc < 0) return rc;
+  const int w = o.n - kJitTrigSkipped * o.trig;
+  return w > 1 ? w : 1;
+}
+
+// ---- per-wave units ------------------------------------------------------------------
+// The evaluator calls program j for all G individuals of its wave at once: one unit of code per
+// (wave, program) runs the G individuals' programs back to back with full exec; after group
+// g > 0 a v_cndmask keeps group g's lanes (g*Rp .. g*Rp+Rp-1) from the new value and the
+// other lanes from the running result (v25), so v8 ends with every lane's own individual's
+// value -- one call instead of G, no selects at the call site.  (Variants that switched exec
+// per group, or returned several programs' results in v25-v28, measured slower: DESIGN.md.)
+constexpr int kJitKeep = 25;
+constexpr uint32_t kMovS42 = 0xbeaa00ffu;   // s_mov_b32 s42, literal
+constexpr uint32_t kMovS43 = 0xbeab00ffu;   // s_mov_b32 s43, literal
+constexpr uint32_t kSelLo = 0xd1000008u;    // v_cndmask_b32_e64 v8, v25, v8, s[42:43]
+constexpr uint32_t kSelHi = 0x00aa1119u;
+
+// Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
+MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
+                                int wave, int j, uint32_t* out) {
+  JitOut o{out, 0};
+  for (int g = 0; g < G; ++g) {
+    const int q = wave * G + g;
+    if (q >= P) break;
+    const int ind = order ? order[q] : q;
+    if (g > 0) o.movv(kJitKeep, kJitAcc);
+    const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false);
+    if (rc < 0) return rc;
+    if (g > 0) {
+      const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);  // g > 0 implies Rp < 64
+      o.w(kMovS42);
+      o.w((uint32_t)mask);
+      o.w(kMovS43);
+      o.w((uint32_t)(mask >> 32));
+      o.w(kSelLo);
+      o.w(kSelHi);
+    }
+  }
+  o.w(kSetpcS30);
+  return o.n;
 }
 
 }  // namespace mtgp

@@ -205,7 +205,7 @@ struct KArgs {
   MtgpRollouts ro;
   MtgpOutputs out;
   uint64_t jit_base;        // JIT code (executable device memory) or 0: interpreter only
-  const uint32_t* jit_off;  // [P, n_prog] byte offset of each program's code
+  const uint32_t* jit_off;  // [n_waves, n_prog] byte offset of each (wave, program) unit's code
   const int32_t* jit_info;  // mtgp_jit_plan info {status, total bytes} (device) or NULL
   uint64_t jit_cap;         // bytes of the code buffer
 };
@@ -257,8 +257,7 @@ struct Lane {
   int wave, lane, Rp, G, q0, g, r, p, rr;
   bool active;
   uint32_t ptab;  // lane gi (< G): byte offset of group gi's program block in A.prog
-  uint32_t jtab;  // lane gi * n_prog + j (< 64): JIT code offset of program j of group gi
-  bool jn;        // jtab holds every (group, program) pair of the wave
+  uint32_t jtab;  // lane j < n_prog: JIT code offset of this wave's program-j unit
   bool jok;       // the JIT code of this launch is complete (plan status 0, fits the buffer)
 };
 
@@ -291,15 +290,11 @@ __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
   L.ptab = prog_table(A, L);
-  L.jn = L.G * A.n_prog <= kWave;
   L.jok = true;
   if (A.jit_info)  // checked on the device, so the host never waits for the plan
     L.jok = uni((int)(A.jit_info[0] == 0 && (uint64_t)(uint32_t)A.jit_info[1] <= A.jit_cap)) != 0;
   L.jtab = 0;
-  if (A.jit_off && L.jn && L.lane < L.G * A.n_prog) {
-    const int gi = L.lane / A.n_prog, j = L.lane - gi * A.n_prog;
-    if (L.q0 + gi < A.P) L.jtab = A.jit_off[(size_t)sched_ind(A, L.q0 + gi) * A.n_prog + j];
-  }
+  if (A.jit_off && L.lane < A.n_prog) L.jtab = A.jit_off[(size_t)(L.q0 / L.G) * A.n_prog + L.lane];
   return true;
 }
 
@@ -346,8 +341,9 @@ struct DataVec {
   }
 };
 
-// Call JIT code at `addr` (mtgp_jit.h ABI): data in v0-v7, result in v8, s[32:33] collects
-// lanes that need the interpreter (slow sin/cos reduction).
+// Call a JIT unit at `addr` (mtgp_jit.h ABI): data in v0-v7; a single-program role returns in
+// v8, a multi-program role in v25.. ; s[32:33] collects lanes that need the interpreter (slow
+// sin/cos reduction).
 __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], uint64_t& flag) {
   // the target must sit in SGPRs: make its uniformity explicit to the compiler
   const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
@@ -358,9 +354,27 @@ __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], 
                : [tgt] "s"(addr), "{v0}"(d[0]), "{v1}"(d[1]), "{v2}"(d[2]), "{v3}"(d[3]), "{v4}"(d[4]),
                  "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
                : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
-                 "v22", "v23", "v24", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "vcc", "memory");
+                 "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s42", "s43",
+                 "vcc", "memory");
   return acc;
 }
+
+#ifndef MTGP_V_TIMING
+#define MTGP_V_TIMING 0  // diagnostic only: per-wave start/end clock + HW_ID (residency study), never shipped
+#endif
+#if MTGP_V_TIMING
+__device__ uint64_t g_wave_probe[65536 * 4];
+__device__ __forceinline__ void probe(const Lane& L, int what) {
+  const int w = uni((int)(blockIdx.x * kWavesPerBlock + L.wave));
+  if (L.lane == 0 && w < 65536) {
+    g_wave_probe[w * 4 + what] = __builtin_amdgcn_s_memrealtime();
+    if (what == 0) g_wave_probe[w * 4 + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
+  }
+}
+#define MTGP_PROBE(L, w) probe(L, w)
+#else
+#define MTGP_PROBE(L, w)
+#endif
 
 // Run program `slot` of group gi (its individual's program, wave-uniform).
 __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
@@ -375,54 +389,7 @@ __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, i
 #endif
 }
 
-template <bool JIT>
-__device__ __forceinline__ float run_one(const KArgs& A, const Lane& L, int gi, int slot, DataVec<JIT>& D) {
-  if (!JIT) return run_one_interp(A, L, gi, slot, D.dcol, D.st);
-  if (__builtin_expect(!L.jok, 0)) {  // no usable code for this launch: interpret
-    D.spill();
-    return run_one_interp(A, L, gi, slot, D.dcol, D.st);
-  }
-  uint32_t off;
-  if (__builtin_expect(uni((int)L.jn), 1)) {  // wave-uniform: every (group, program) offset is in jtab
-    off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, gi * A.n_prog + slot);
-  } else {
-    off = (uint32_t)uni((int)A.jit_off[(size_t)group_ind(A, L, gi) * A.n_prog + slot]);
-  }
-  uint64_t fl = 0;
-  float r = jit_call(A.jit_base + off, D.v, fl);
-  if (__builtin_expect(fl != 0, 0)) {  // some lane needs the slow sin/cos reduction
-    const uint64_t gm = __ballot(L.g == gi && L.active);
-    if (fl & gm) {
-      D.spill();
-      r = run_one_interp(A, L, gi, slot, D.dcol, D.st);
-    }
-  }
-  return r;
-}
-
-#ifndef MTGP_V_NOINTERP
-#define MTGP_V_NOINTERP 0  // diagnostic only: skip interpretation (cost attribution), never shipped
-#endif
-
-// Run program `slot` of every live group; each lane keeps its own individual's value.
-// The program runs with the FULL exec mask (lanes of other groups compute a discarded value
-// on their own data/stack columns): inside a divergent `if` the CFG structurizer would turn
-// the uniform opcode switch into exec-masked flow blocks (~2x the scalar dispatch cost).
-template <bool JIT>
-__device__ __forceinline__ float run_groups(const KArgs& A, const Lane& L, int ng, int slot, DataVec<JIT>& D,
-                                            float dflt) {
-#if MTGP_V_NOINTERP
-  return 0.01f * (float)(slot + 1) + 0.001f * D.v[4];
-#endif
-  float v = dflt;
-  for (int gi = 0; gi < ng; ++gi) {
-    const float t = run_one<JIT>(A, L, gi, slot, D);
-    v = (L.g == gi) ? t : v;
-  }
-  return v;
-}
-
-// interpreter-only variant on explicit LDS columns (wide-state SR kernel)
+// interpreter: program `slot` of every live group on explicit LDS columns
 __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L, int ng, int slot, const float* dcol,
                                                    float* st, float dflt) {
   float v = dflt;
@@ -433,7 +400,58 @@ __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L
   return v;
 }
 
+// Programs first .. first+M-1 of every live group -> out[0..M-1], each lane its own
+// individual's values.  JIT: one call per program to the wave's unit (mtgp_jit.h jit_unit);
+// the interpreter runs when there is no usable code or when a lane needs the slow sin/cos path.
+template <bool JIT, int M>
+__device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, int role, int first, DataVec<JIT>& D,
+                                         float (&out)[M]) {
+  (void)role;
+  bool interp = !JIT;
+  if (JIT) {
+    if (__builtin_expect(L.jok, 1)) {
+#pragma unroll 1
+      for (int q = 0; q < M; ++q) {
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first + q);
+        uint64_t fl = 0;
+        float v = jit_call(A.jit_base + off, D.v, fl);
+        if (__builtin_expect(fl != 0, 0)) {  // lanes that need the Payne-Hanek sin/cos: re-run only
+          bool spilled = false;               // this program, only for the groups concerned
+          for (int gi = 0; gi < ng; ++gi) {
+            if (!(fl & __ballot(L.g == gi && L.active))) continue;
+            if (!spilled) { D.spill(); spilled = true; }
+            const float t = run_one_interp(A, L, gi, first + q, D.dcol, D.st);
+            v = (L.g == gi) ? t : v;
+          }
+#if MTGP_V_TIMING
+          if (spilled && L.lane == 0) {
+            const int w = (int)(blockIdx.x * kWavesPerBlock + L.wave);
+            if (w < 65536) g_wave_probe[w * 4 + 3] += 1;
+          }
+#endif
+        }
+#pragma unroll
+        for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
+      }
+    } else {
+      interp = true;
+    }
+    if (interp) D.spill();
+  }
+  if (interp) {
+#pragma unroll 1
+    for (int q = 0; q < M; ++q) {
+      const float v = run_groups_interp(A, L, ng, first + q, D.dcol, D.st, 0.0f);
+#pragma unroll
+      for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
+    }
+  }
+}
+
+
+
 __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, float F) {
+  MTGP_PROBE(L, 1);
   const float mx = A.m.max_fitness;
   if (A.out.rollout_fitness && L.active) A.out.rollout_fitness[(size_t)L.p * A.ro.R + L.r] = F;
   float v = L.active ? (mtgp_isfinite(F) ? F : mx) : 0.0f;
@@ -458,6 +476,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
+  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -529,19 +548,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
 #pragma unroll
       for (int j = 0; j < NA; ++j) D.put(4 + j, at[j]);
-      const float u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);
+      float ur[1];
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+      const float u = ur[0];
       acro_drift(K, xt, u, kx);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
       acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
       for (int i = 0; i < 4; ++i) D.put(i, y[i]);
       D.put(uslot, u);
-#pragma unroll 1
-      for (int q = 0; q < NA; ++q) {
-        const float v = run_groups<JIT>(A, Ln, ng, A.m.prog_state + q, D, 0.0f);
-#pragma unroll
-        for (int j = 0; j < NA; ++j) ka[j] = (q == j) ? v : ka[j];
-      }
+      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka);
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
@@ -554,10 +570,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               for (int i = 0; i < 4; ++i) D.put(i, y[i]);
             }
           }
-          if (diff_mask != 0) {
+          if (JIT && diff_mask != 0) {  // the save-readout unit covers every group (equal programs give u again)
+            float sr[1];
+            run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
+            us = sr[0];
+          } else if (!JIT && diff_mask != 0) {
             for (int gi = 0; gi < ng; ++gi) {
               if (!((diff_mask >> gi) & 1ull)) continue;
-              const float t = run_one<JIT>(A, Ln, gi, A.m.prog_readout_save, D);
+              const float t = run_one_interp(A, Ln, gi, A.m.prog_readout_save, D.dcol, D.st);
               us = (Ln.g == gi) ? t : us;
             }
           }
@@ -617,6 +637,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
+  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -657,7 +678,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
 #pragma unroll
       for (int i = 0; i < 4; ++i) D.put(i, y[i]);
-      float u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);  // ff.py:106-107 (:97 at saves)
+      float ur[1];
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // ff.py:106-107 (:97 at saves)
+      float u = ur[0];
       acro_drift(K, xt, u, kx);
       if (stage == 0) {
         if (is_save) {
@@ -668,7 +691,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               acro_obs<true>(nzc, tsk, x, y);
 #pragma unroll
               for (int i = 0; i < 4; ++i) D.put(i, y[i]);
-              u = run_groups<JIT>(A, Ln, ng, A.m.prog_readout, D, 0.0f);
+              run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+              u = ur[0];
             }
           }
           if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), u, x[0], x[1]);
@@ -716,6 +740,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
+  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -768,12 +793,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
     for (int stage = 0; stage < 4; ++stage) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], h, h2));
-#pragma unroll 1
-      for (int q = 0; q < NV; ++q) {
-        const float v = run_groups<JIT>(A, Ln, ng, A.m.prog_state + q, D, 0.0f);
-#pragma unroll
-        for (int j = 0; j < NV; ++j) kx[j] = (q == j) ? v : kx[j];
-      }
+      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
 #pragma unroll
       for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
@@ -1047,19 +1067,44 @@ __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict
 
 hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 // --------------------------------------------------------------------------------------
-// Program JIT build (mtgp_jit.h): pass 1 sizes every program's code, one block scans the sizes
-// into byte offsets, pass 2 writes the code (vector stores) into executable device memory.
-__global__ void __launch_bounds__(256) k_jit_count(const MtgpInstr* __restrict__ prog, int total, int L,
-                                                   uint32_t* __restrict__ offs, int32_t* __restrict__ info) {
+// Program JIT build (mtgp_jit.h): one unit of code per (wave, role).  Pass 1 sizes every
+// unit, one block scans the sizes into byte offsets, pass 2 writes the code (vector stores)
+// into executable device memory.
+constexpr uint32_t kJitAlign = 64u;
+
+struct JitUnitArgs {
+  const MtgpInstr* prog;
+  int n_prog, L, P, G, Rp, n_units;
+  const int32_t* order;
+};
+
+__device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out) {
+  const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out);
+}
+
+__global__ void __launch_bounds__(256) k_jit_count(JitUnitArgs U, uint32_t* __restrict__ offs,
+                                                   int32_t* __restrict__ info) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int n = mtgp::jit_translate(prog + (size_t)i * L, L, nullptr);
-  offs[i] = n > 0 ? (uint32_t)n * 4u : 0u;
+  if (i >= U.n_units) return;
+  const int n = jit_unit_words(U, i, nullptr);
+  // units start on 64-byte instruction-cache lines (measured: unaligned call targets made some
+  // code shapes 2x slower, scripts/dispatch_cost.py k = 4)
+  offs[i] = n > 0 ? ((uint32_t)n * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u) : 0u;
   if (n < 0) atomicMin(&info[0], n);
 }
 
 // exclusive scan of offs[0..total) in place, offs[total] = total bytes, info[1] = total bytes
 // (saturated to INT32_MAX for the host check)
+// per-program JIT cost for the schedule: executed code words / 4 (>= 1; untranslatable -> plen)
+__global__ void __launch_bounds__(256) k_jit_cost(const MtgpInstr* __restrict__ prog, int total, int L,
+                                                  const int32_t* __restrict__ plen, int32_t* __restrict__ cost) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int c = mtgp::jit_cost(prog + (size_t)i * L, L);
+  cost[i] = c > 0 ? (c + 3) / 4 : plen[i];
+}
+
 __global__ void __launch_bounds__(1024) k_jit_scan(uint32_t* __restrict__ offs, int total, int32_t* __restrict__ info) {
   __shared__ uint64_t part[1024];
   const int t = threadIdx.x;
@@ -1088,14 +1133,31 @@ __global__ void __launch_bounds__(1024) k_jit_scan(uint32_t* __restrict__ offs, 
   }
 }
 
-__global__ void __launch_bounds__(256) k_jit_emit(const MtgpInstr* __restrict__ prog, int total, int L,
-                                                  const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
-                                                  uint64_t code_bytes) {
+__global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t* __restrict__ offs,
+                                                  uint32_t* __restrict__ code, uint64_t code_bytes) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
+  if (i >= U.n_units) return;
   const uint32_t b = offs[i], e = offs[i + 1];
-  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable program or short buffer (host-checked)
-  mtgp::jit_translate(prog + (size_t)i * L, L, code + b / 4);
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
+  jit_unit_words(U, i, code + b / 4);
+}
+
+bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                   JitUnitArgs& U) {
+  if (!prog || P < 0 || n_prog <= 0 || n_prog > MTGP_MAX_PROGRAMS || L <= 0 || R <= 0 || R > kWave) return false;
+  int Rp = 1;
+  while (Rp < R) Rp <<= 1;
+  U.prog = prog;
+  U.n_prog = n_prog;
+  U.L = L;
+  U.P = P;
+  U.Rp = Rp;
+  U.G = kWave / Rp;
+  U.order = order;
+  const long waves = ((long)P + U.G - 1) / U.G;
+  if (waves * n_prog > INT32_MAX - 1) return false;
+  U.n_units = (int)(waves * n_prog);
+  return true;
 }
 
 // Executable device memory for the JIT (HSA pool allocation with the executable flag on the
@@ -1161,6 +1223,12 @@ extern "C" {
 
 int mtgp_abi_version(void) { return MTGP_ABI_VERSION; }
 
+#if MTGP_V_TIMING
+int mtgp_debug_probe(uint64_t* host, size_t n) {  // diagnostic variant only
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_probe), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif
+
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code) {
   if (!code || bytes == 0) return MTGP_ERR_ARG;
   *code = nullptr;
@@ -1191,28 +1259,58 @@ int mtgp_jit_free(void* code) {
   return hsa_amd_memory_pool_free(code) == HSA_STATUS_SUCCESS ? MTGP_OK : MTGP_ERR_ARG;
 }
 
-int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, uint32_t* offsets_out,
-                  int32_t* info_out, void* stream) {
-  if (!prog || !offsets_out || !info_out || P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
-  const long total = (long)P * n_prog;
-  if (total > INT32_MAX - 1) return MTGP_ERR_ARG;
+int mtgp_jit_units(int32_t P, int32_t n_prog, int32_t R) {
+  JitUnitArgs U;
+  static const MtgpInstr dummy = {0u, 0.0f};
+  if (!jit_unit_args(&dummy, P, n_prog, 1, R, nullptr, U)) return MTGP_ERR_ARG;
+  return U.n_units;
+}
+
+int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                  uint32_t* offsets_out, int32_t* info_out, void* stream) {
+  JitUnitArgs U;
+  if (!offsets_out || !info_out || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
   hipStream_t s = (hipStream_t)stream;
   if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
-  if (total == 0) return hipMemsetAsync(offsets_out, 0, sizeof(uint32_t), s) == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
-  hipLaunchKernelGGL(k_jit_count, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, prog, (int)total, L,
-                     offsets_out, info_out);
-  hipLaunchKernelGGL(k_jit_scan, dim3(1), dim3(1024), 0, s, offsets_out, (int)total, info_out);
+  if (U.n_units == 0) return hipMemsetAsync(offsets_out, 0, sizeof(uint32_t), s) == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_jit_count, dim3((unsigned)((U.n_units + 255) / 256)), dim3(256), 0, s, U, offsets_out,
+                     info_out);
+  hipLaunchKernelGGL(k_jit_scan, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
-int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, const uint32_t* offsets, void* code,
-                  size_t code_bytes, void* stream) {
-  if (!prog || !offsets || !code || P < 0 || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
+int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                  const uint32_t* offsets, void* code, size_t code_bytes, void* stream) {
+  JitUnitArgs U;
+  if (!offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
+  if (U.n_units == 0) return MTGP_OK;
+  hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((U.n_units + 255) / 256)), dim3(256), 0, (hipStream_t)stream, U,
+                     offsets, (uint32_t*)code, (uint64_t)code_bytes);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t n_prog, int32_t L, int32_t* cost_out,
+                  void* stream) {
+  if (!prog || !plen || !cost_out || P < 0 || n_prog <= 0 || L <= 0 || (long)P * n_prog > INT32_MAX) return MTGP_ERR_ARG;
   const long total = (long)P * n_prog;
   if (total == 0) return MTGP_OK;
-  hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, prog,
-                     (int)total, L, offsets, (uint32_t*)code, (uint64_t)code_bytes);
+  hipLaunchKernelGGL(k_jit_cost, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, (hipStream_t)stream, prog,
+                     (int)total, L, plen, cost_out);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                       int32_t unit, uint32_t* out, int32_t max_words) {
+  JitUnitArgs U;
+  if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
+  const int wave = unit / n_prog, j = unit - wave * n_prog;
+  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr);
+  if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
+  if (out) {
+    if (n > max_words) return MTGP_ERR_ARG;
+    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out);
+  }
+  return n;
 }
 
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words) {

@@ -41,8 +41,8 @@ class Flattened:
     L: int
     n_prog: int
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
-    jit: Optional[tuple] = None           # (code ptr, offsets [P*n_prog+1], info [2], capacity) of the JIT
-    jit_tried: bool = False
+    jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity) of the JIT
+    jit_key: Optional[tuple] = None       # (R, roles, order) the JIT units were built for
 
 
 class DeviceEngine:
@@ -65,7 +65,7 @@ class DeviceEngine:
         self._arenas = [None, None]  # (pointer, bytes): a ring of two executable code buffers
         self._arena_i = 0
         self._jit_last = None        # (pinned host info, event) of the previous build: capacity hint
-        self._jit_bytes_per_prog = 1024.0
+        self._jit_bytes_per_unit = None  # learnt from earlier plans (None: estimate from G)
 
     def __del__(self):
         try:
@@ -98,27 +98,31 @@ class DeviceEngine:
             self._arenas[self._arena_i] = a
         return a
 
-    def jit_build(self, fl: Flattened) -> Optional[tuple]:
+    def jit_build(self, fl: Flattened, m, R: int, order: Optional[torch.Tensor]) -> Optional[tuple]:
         """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit),
         without a host round trip: the buffer is sized from the code size per program seen in
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
-        if fl.jit_tried:
+        key = (R, None if order is None else order.data_ptr())
+        if fl.jit_key == key:
             return fl.jit
-        fl.jit_tried = True
-        if not self.use_jit or self.ff.n_data() > 8:
+        fl.jit_key, fl.jit = key, None
+        if not self.use_jit or self.ff.n_data() > 8 or (m.model == nat.MODEL_SR and m.n_var > 4):
             return None
         P = fl.prog.shape[0]
-        n = P * fl.n_prog
+        n = self.native.mtgp_jit_units(P, fl.n_prog, R)
+        if n < 0:
+            return None
+        optr = None if order is None else order.data_ptr()
         if self._jit_last is not None and self._jit_last[1].query():  # previous plan done: learn its size
             err, total, n_prev = (int(v) for v in self._jit_last[0].tolist())
             if err == 0 and n_prev > 0:
-                self._jit_bytes_per_prog = max(self._jit_bytes_per_prog * 0.5, total / n_prev * 1.5)
+                self._jit_bytes_per_unit = total / n_prev * 1.5
         offs = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
         info = torch.empty((3,), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), info.data_ptr(),
-                                       stream)
+        rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(),
+                                       info.data_ptr(), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_plan failed: {rc}")
         info[2].fill_(n)
@@ -127,8 +131,11 @@ class DeviceEngine:
         ev = torch.cuda.Event()
         ev.record()
         self._jit_last = (host, ev)
-        ptr, size = self._arena(int(n * self._jit_bytes_per_prog) + 4096)
-        rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, offs.data_ptr(), ptr, size, stream)
+        G = 64 // (1 << max(R - 1, 0).bit_length())
+        per_unit = self._jit_bytes_per_unit or 1024.0 * G
+        ptr, size = self._arena(int(n * per_unit) + 4096)
+        rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(), ptr,
+                                       size, stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
         fl.jit = (ptr, offs, info, size)
@@ -223,8 +230,22 @@ class DeviceEngine:
             w[roles["prog_readout_save"]] = 1  # once per save point
         return w
 
+    def schedule_cost(self, fl: Flattened) -> torch.Tensor:
+        """Per-program cost [P, n_prog] the schedule balances: the executed JIT code size when the
+        programs run as JIT code (sin/cos dominate there), the program length otherwise."""
+        if not (self.use_jit and self.ff.n_data() <= 8):
+            return fl.plen
+        P = fl.plen.shape[0]
+        cost = torch.empty_like(fl.plen)
+        stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = self.native.mtgp_jit_cost(fl.prog.data_ptr(), fl.plen.data_ptr(), P, fl.n_prog, fl.L, cost.data_ptr(),
+                                       stream)
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_jit_cost failed: {rc}")
+        return cost
+
     def schedule(self, fl: Flattened, R: int) -> torch.Tensor:
-        """Build (once per flattened population) the wave schedule that balances interpreter work."""
+        """Build (once per flattened population) the wave schedule that balances per-wave work."""
         if fl.order is None:
             P = fl.plen.shape[0]
             order = torch.empty((P,), dtype=torch.int32, device=self.device)
@@ -232,7 +253,8 @@ class DeviceEngine:
             w = self.schedule_weights()
             wts = (ctypes.c_int32 * len(w))(*w)
             stream = torch.cuda.current_stream(self.device).cuda_stream
-            rc = self.native.mtgp_schedule(fl.plen.data_ptr(), P, fl.n_prog, wts, R, order.data_ptr(),
+            cost = self.schedule_cost(fl)
+            rc = self.native.mtgp_schedule(cost.data_ptr(), P, fl.n_prog, wts, R, order.data_ptr(),
                                            scratch.data_ptr(), stream)
             if rc != nat.OK:
                 raise RuntimeError(f"mtgp_schedule failed: {rc}")
@@ -268,7 +290,8 @@ class DeviceEngine:
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
-        ro.order = _ptr(self.schedule(fl, R)) if schedule and P > 1 else None
+        ro_order = self.schedule(fl, R) if schedule and P > 1 else None
+        ro.order = _ptr(ro_order)
         ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
         dev = self.device
         res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
@@ -288,7 +311,7 @@ class DeviceEngine:
                         res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
                         setattr(out, name, res[name].data_ptr())
         stream = torch.cuda.current_stream(dev).cuda_stream
-        jit = self.jit_build(fl)
+        jit = self.jit_build(fl, m, R, ro_order)
         jc = nat.MtgpJitCode()
         if jit is not None:
             jc.code, jc.offsets, jc.info, jc.capacity = jit[0], jit[1].data_ptr(), jit[2].data_ptr(), jit[3]

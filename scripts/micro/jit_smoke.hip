@@ -58,6 +58,22 @@ __global__ void k_run(uint64_t base, const uint32_t* offs, int nprog, const floa
   }
 }
 
+// sweep: sin and cos JIT programs over many arguments (all magnitudes incl. the double path)
+__global__ void k_sweep(uint64_t base, uint32_t off_sin, uint32_t off_cos, const float* xs, int n, float* os, float* oc,
+                        uint32_t* flags) {
+  asm volatile("s_icache_inv");
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    float d[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int i = i0 + (int)threadIdx.x;
+    d[2] = i < n ? xs[i] : 0.0f;
+    uint64_t fl = 0;
+    const float s = jit_call(base + off_sin, d, fl);
+    const float c = jit_call(base + off_cos, d, fl);
+    if (i < n) { os[i] = s; oc[i] = c; }
+    if (fl && threadIdx.x == 0) atomicAdd(flags, 1u);
+  }
+}
+
 static MtgpInstr I(int op, uint32_t aux, float imm) { MtgpInstr x; x.op = (uint32_t)op << MTGP_OP_SHIFT | aux; x.imm = imm; return x; }
 static MtgpInstr IS(int op, uint32_t aux, uint32_t slot) { MtgpInstr x; x.op = (uint32_t)op << MTGP_OP_SHIFT | aux; memcpy(&x.imm, &slot, 4); return x; }
 
@@ -77,6 +93,7 @@ int main() {
       {IS(MTGP_OP_SINV, 0, 2 * SB), I(MTGP_OP_END, 0, 0)},                                   // sin d2
       {IS(MTGP_OP_COSV, 0, 3 * SB), I(MTGP_OP_MULC, 0, 3.0f), I(MTGP_OP_END, 0, 0)},         // cos(d3) * 3
       {IS(MTGP_OP_VV_DIV, 5 * SB, 4 * SB), IS(MTGP_OP_LDVP, 0, 0), I(MTGP_OP_RSUBS, 0, 0), I(MTGP_OP_END, 0, 0)},  // RSUBS: d4/d5 - d0
+      {IS(MTGP_OP_COSV, 0, 2 * SB), I(MTGP_OP_END, 0, 0)},                                   // cos d2 (sweep)
   };
   std::vector<uint32_t> words, offs;
   for (auto& p : progs) {
@@ -98,7 +115,7 @@ int main() {
   hipMemcpy(doffs, offs.data(), offs.size() * 4, hipMemcpyHostToDevice);
   float hin[8 * 64];
   for (int i = 0; i < 8 * 64; ++i) hin[i] = 0.37f * (float)(i % 64) - 5.0f + (float)(i / 64);
-  hin[2 * 64 + 7] = 3.0e5f;  // a slow-path sin argument in lane 7
+  hin[2 * 64 + 7] = 3.0e5f;  // a double-path sin argument in lane 7 (2^17 <= |x| < 2^28)
   hipMemcpy(din, hin, sizeof(hin), hipMemcpyHostToDevice);
   hipLaunchKernelGGL(k_copy, dim3((words.size() + 255) / 256), dim3(256), 0, 0, dw, (uint32_t*)code, (int)words.size());
   hipDeviceSynchronize();
@@ -116,14 +133,55 @@ int main() {
     for (int i = 0; i < 8; ++i) d[i] = hin[i * 64 + l];
     const float want[5] = {2.5f, d[1] + 0.75f, mtgp_sinf(d[2]), mtgp_cosf(d[3]) * 3.0f, d[4] / d[5] - d[0]};
     for (int p = 0; p < 5; ++p) {
-      if (p == 2 && l == 7) continue;  // slow lane: flagged, interpreter re-runs it
       uint32_t a, b;
       memcpy(&a, &hout[p * 64 + l], 4);
       memcpy(&b, &want[p], 4);
       if (a != b) { if (bad < 10) printf("mismatch prog %d lane %d: %g vs %g\n", p, l, hout[p * 64 + l], want[p]); ++bad; }
     }
   }
-  printf("flags: %u %u %u %u %u (expect 0 0 1 0 0)\n", hfl[0], hfl[1], hfl[2], hfl[3], hfl[4]);
+  printf("flags: %u %u %u %u %u (expect 0 0 0 0 0: 3e5 now takes the double path)\n", hfl[0], hfl[1], hfl[2], hfl[3], hfl[4]);
+  // sweep
+  {
+    const int n = 1 << 20;
+    std::vector<float> xs(n);
+    uint32_t st = 12345u;
+    for (int i = 0; i < n; ++i) {
+      st = st * 1664525u + 1013904223u;
+      const float u = (float)(st >> 8) / 16777216.0f;
+      const int band = i % 10;
+      const float mag = band == 0 ? 4.0f : band == 1 ? 2.0e5f : band == 2 ? 1.5e8f : band == 3 ? 1.0e7f
+                      : band == 4 ? 131072.0f * (1.0f + u) : band == 5 ? 268435456.0f * 0.999f
+                      : band == 6 ? 268435456.0f * (1.0f + 3.0f * u) : band == 7 ? 1.0e12f
+                      : band == 8 ? 1.0e25f : 3.0e38f;
+      xs[i] = (u * 2.0f - 1.0f) * mag;
+    }
+    xs[0] = 131072.0f; xs[1] = -131072.0f; xs[2] = 268435440.0f; xs[3] = 1e-30f; xs[4] = -0.0f;
+    xs[5] = 268435456.0f; xs[6] = -268435456.0f; xs[7] = 3.4028235e38f; xs[8] = -3.4028235e38f;
+    xs[9] = 1.0f / 0.0f; xs[10] = -1.0f / 0.0f; xs[11] = __builtin_nanf("");
+    float *dx, *ds, *dc;
+    uint32_t* dfl;
+    hipMalloc(&dx, n * 4); hipMalloc(&ds, n * 4); hipMalloc(&dc, n * 4); hipMalloc(&dfl, 4);
+    hipMemcpy(dx, xs.data(), n * 4, hipMemcpyHostToDevice);
+    hipMemset(dfl, 0, 4);
+    hipLaunchKernelGGL(k_sweep, dim3(1), dim3(64), 0, 0, (uint64_t)code, offs[2], offs[5], dx, n, ds, dc, dfl);
+    hipError_t e2 = hipDeviceSynchronize();
+    printf("sweep: %s\n", hipGetErrorString(e2));
+    std::vector<float> hs(n), hc(n);
+    uint32_t nfl = 0;
+    hipMemcpy(hs.data(), ds, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(hc.data(), dc, n * 4, hipMemcpyDeviceToHost);
+    hipMemcpy(&nfl, dfl, 4, hipMemcpyDeviceToHost);
+    int sb = 0;
+    for (int i = 0; i < n; ++i) {
+      const float ws = mtgp_sinf(xs[i]), wc = mtgp_cosf(xs[i]);
+      uint32_t a, b, c2, d2;
+      memcpy(&a, &hs[i], 4); memcpy(&b, &ws, 4); memcpy(&c2, &hc[i], 4); memcpy(&d2, &wc, 4);
+      const bool nan_ok = (hs[i] != hs[i] && ws != ws) && (hc[i] != hc[i] && wc != wc);
+      if ((a != b || c2 != d2) && !nan_ok) { if (sb < 5) printf("sweep mismatch x=%.9g sin %.9g/%.9g cos %.9g/%.9g\n", xs[i], hs[i], ws, hc[i], wc); ++sb; }
+    }
+    printf("sweep: %d mismatches of %d, fallback flags %u (expect 0)\n", sb, n, nfl);
+    bad += sb + (int)nfl;
+  }
   printf("%s: %d mismatches\n", bad ? "FAIL" : "OK", bad);
   hsa_amd_memory_pool_free(code);
   return bad ? 5 : 0;

@@ -229,13 +229,11 @@ def test_jit_code_that_does_not_fit_is_interpreted():
     evaluator sees it on the device and interprets (results unchanged)."""
     env, lib, ff, data, pop = dynamic_setup(P=24, R=16, n_steps=30, seed=12)
     eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=True)
+    real_arena = eng._arena
+    eng._arena = lambda nbytes: (real_arena(nbytes)[0], 16)  # claim a 16-byte buffer: every launch falls back
     pd = torch.from_numpy(pop).cuda()
-    fl = eng.flatten(pd)
-    eng.schedule(fl, 16)
-    ptr, offs, info, cap = eng.jit_build(fl)
-    fl.jit = (ptr, offs, info, 16)  # claim a 16-byte buffer: every launch must fall back
-    assert not DeviceEngine.jit_ok(fl)
-    res = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True, flattened=fl)
+    res = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True)
+    assert res["_flat"].jit is not None and not DeviceEngine.jit_ok(res["_flat"])
     torch.cuda.synchronize()
     d = eng.prepare_data(data)
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)

@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 
 def _costs(eng, fl):
     w = np.array(eng.schedule_weights(), dtype=np.int64)
-    c = (fl.plen.cpu().numpy().astype(np.int64) * w[None, :]).sum(axis=1)
+    c = (eng.schedule_cost(fl).cpu().numpy().astype(np.int64) * w[None, :]).sum(axis=1)
     return np.clip(c, 0, nat.SCHED_BINS - 1)
 
 

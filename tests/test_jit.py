@@ -77,13 +77,17 @@ def _disassemble(words):
     return [ln.strip() for ln in r.stdout.decode().splitlines() if ln.strip()]
 
 
-ALLOWED_V = set(range(8, 25))
-ALLOWED_S = set(range(30, 40))
+ALLOWED_V = set(range(8, 26))
+ALLOWED_S = set(range(30, 44))
+EXEC_OK = ("s_mov_b64 s[40:41], exec", "s_mov_b64 exec, s[40:41]", "s_mov_b64 exec, s[36:37]")
 
 
 def _check_abi(lines):
     assert lines[-1] == "s_setpc_b64 s[30:31]", lines[-1]
     for ln in lines[:-1]:
+        if ln in EXEC_OK or ln.startswith("s_mov_b32 exec_lo, ") or ln.startswith("s_mov_b32 exec_hi, ") or \
+                ln.startswith("s_and_saveexec_b64 s[36:37]") or ln.startswith("s_cbranch_execz"):
+            continue
         assert "exec" not in ln and "invalid" not in ln.lower(), ln
         op, _, rest = ln.partition(" ")
         dst = rest.split(",")[0].strip()
@@ -92,9 +96,9 @@ def _check_abi(lines):
         if op.startswith("v_cmp") and op.endswith("_e32"):
             assert dst == "vcc", ln
             continue
-        m = re.fullmatch(r"v(\d+)", dst)
+        m = re.fullmatch(r"v(\d+)|v\[(\d+):(\d+)\]", dst)
         if m:
-            assert int(m.group(1)) in ALLOWED_V, ln
+            assert all(int(x) in ALLOWED_V for x in m.groups() if x is not None), ln
             # the vcc / sgpr written by v_div_scale / v_cmp_e64 (second operand) is checked below
             if op.startswith("v_div_scale"):
                 sd = rest.split(",")[1].strip()
@@ -121,17 +125,51 @@ def _setup(kind):
     return lib, pop, 4, [0]
 
 
-def _emulate(words, data):
-    """Run emitted code on data [n_data, M] (float32 lanes); returns v8."""
+def _emulate(words, data, full=False):
+    """Run emitted code on data [n_data, M] (float32 lanes, M <= 64); returns v8 (or all VGPRs).
+    Honours the exec moves of per-wave units (VALU results only land in exec lanes)."""
     M = data.shape[1]
     v = np.zeros((32, M), np.float32)
     v[: data.shape[0]] = data
     i = 0
     lit = lambda k: np.full(M, np.array(words[k], np.uint32).view(np.float32), np.float32)  # noqa: E731
+    exec_ = np.ones(M, bool)
+    saved = None
+    sel = [0, 0]
+
+    def put(dst, val):
+        v[dst] = np.where(exec_, val, v[dst])
+
     while True:
         w = words[i]
         if w == SETPC:
-            return v[8]
+            return v if full else v[8]
+        if (w >> 23) == 0x17D:  # SOP1: the exec save / restore / set of per-wave units
+            sdst, op, ssrc = (w >> 16) & 0x7F, (w >> 8) & 0xFF, w & 0xFF
+            if (sdst, op, ssrc) == (40, 1, 126):
+                saved = exec_.copy()
+                i += 1
+            elif (sdst, op, ssrc) == (126, 1, 40):
+                exec_ = saved.copy()
+                i += 1
+            elif op == 0 and ssrc == 255 and sdst in (126, 127):
+                bits = words[i + 1]
+                lo = 0 if sdst == 126 else 32
+                for lane in range(lo, min(lo + 32, M)):
+                    exec_[lane] = bool(bits >> (lane - lo) & 1)
+                i += 2
+            elif op == 0 and ssrc == 255 and sdst in (42, 43):  # lane mask of a wave unit's select
+                sel[sdst - 42] = words[i + 1]
+                i += 2
+            else:
+                raise AssertionError(hex(w))
+            continue
+        if words[i:i + 2] == [0xD1000008, 0x00AA1119]:  # v_cndmask_b32_e64 v8, v25, v8, s[42:43]
+            m64 = sel[0] | sel[1] << 32
+            lanes = np.array([bool(m64 >> lane & 1) for lane in range(M)])
+            put(8, np.where(lanes, v[8], v[25]))
+            i += 2
+            continue
         hit = None
         for name, b in BLOBS.items():
             if words[i:i + len(b)] == b:
@@ -139,12 +177,12 @@ def _emulate(words, data):
                 break
         if hit == "DIV":
             with np.errstate(all="ignore"):
-                v[8] = v[17] / v[18]
+                put(8, v[17] / v[18])
             i += len(BLOBS["DIV"])
             continue
         if hit in ("SIN", "COS"):
             s, c = orc.sincos(v[17])
-            v[8] = s if hit == "SIN" else c
+            put(8, s if hit == "SIN" else c)
             i += len(BLOBS[hit])
             continue
         src0 = w & 0x1FF
@@ -158,13 +196,13 @@ def _emulate(words, data):
         vdst = (w >> 17) & 0xFF
         if (w >> 25) == 0x3F:  # VOP1
             assert ((w >> 9) & 0xFF) == 1, hex(w)  # v_mov_b32
-            v[vdst] = a
+            put(vdst, a)
         else:
             assert (w >> 31) == 0, hex(w)
             b = v[(w >> 9) & 0xFF]
             op = w >> 25
             with np.errstate(all="ignore"):
-                v[vdst] = {1: lambda: a + b, 2: lambda: a - b, 3: lambda: b - a, 5: lambda: a * b}[op]()
+                put(vdst, {1: lambda: a + b, 2: lambda: a - b, 3: lambda: b - a, 5: lambda: a * b}[op]())
         i += step
 
 
@@ -209,3 +247,83 @@ def test_translation_rejects_wide_slots():
                     [nat.OP_NAMES.index("END") << nat.OP_SHIFT, 0]], np.uint32)
     with pytest.raises(ValueError):
         nat.jit_translate_host(raw)
+
+
+def _host_flatten(ff, lib, pop):
+    """Programs [P, n_prog, L, 2] of a population as the device flattener lays them out."""
+    specs, roles = ff.program_specs()
+    nl = lib.native()
+    P, T, N, _ = pop.shape
+    L = (2 * N + 8 + 3) // 4 * 4
+    prog = np.zeros((P, len(specs), L, 2), np.uint32)
+    for p in range(P):
+        for j, (t, nd, zm) in enumerate(specs):
+            raw = _raw_program(pop[p, t], nl, nd, zm)
+            prog[p, j, : raw.shape[0]] = raw
+    return prog, specs, roles, L
+
+
+@pytest.mark.parametrize("kind,R", [("dynamic", 32), ("dynamic", 8), ("static", 16), ("sr", 16), ("sr", 64)])
+def test_wave_units_emulate_to_oracle(kind, R):
+    """(wave, program) units: the G individuals' programs back to back, merged per lane group
+    with v_cndmask, checked lane by lane against the oracle of each lane's own individual."""
+    import ctypes
+    if kind == "dynamic":
+        lib, pop, n_data, _ = _setup("dynamic")
+        ff = mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05)
+    elif kind == "static":
+        lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1])
+        pop = sample_population(8, lib, 40, 1, max_init_depth=6, max_nodes=40)[0]
+        ff = mt.FeedforwardEvaluator(mt.Acrobot(0, 0), 0.05)
+        n_data = 4
+    else:
+        lib, pop, n_data, _ = _setup("sr")
+        ff = mt.SREvaluator(dt0=0.05)
+        ff._n_var = 4
+    prog, specs, roles, L = _host_flatten(ff, lib, pop)
+    P, n_prog = prog.shape[:2]
+    order = np.random.default_rng(1).permutation(P).astype(np.int32)
+    lib_n = nat.load()
+    units = lib_n.mtgp_jit_units(P, n_prog, R)
+    Rp = 1 << max(R - 1, 0).bit_length()
+    G = 64 // Rp
+    assert units == -(-P // G) * n_prog
+    rng = np.random.default_rng(2)
+    out = np.zeros(1 << 16, np.uint32)
+    for u in range(units):
+        n = lib_n.mtgp_jit_unit_host(prog.ctypes.data, P, n_prog, L, R, order.ctypes.data, u, out.ctypes.data,
+                                     out.size)
+        assert n > 0, n
+        words = [int(x) for x in out[:n]]
+        _check_abi(_disassemble(words))
+        data = (rng.standard_normal((8, 64)) * 2).astype(np.float32)
+        regs = _emulate(words, data, full=True)
+        wave, j = divmod(u, n_prog)
+        t, nd, zm = specs[j]
+        for lane in range(64):
+            g = lane // Rp
+            q = wave * G + g
+            if q >= P:
+                continue
+            d = data[:n_data, lane].copy()
+            for b in range(nd):
+                if zm >> b & 1:
+                    d[b] = 0.0
+            want = orc.eval_tree(pop[order[q], t], lib.fn_codes, lib.n_funcs, lib.var_start, d)
+            got = regs[8, lane]
+            assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
+                (np.isnan(got) and np.isnan(want)), (u, lane, got, want)
+
+
+def test_template_branch_targets_resolved():
+    """The sin/cos templates branch over their double-precision block: the assembled offset
+    must land on the exec restore (assembled from an object file, not the unresolved fixup)."""
+    for name in ("SIN", "COS"):
+        w = BLOBS[name]
+        br = [i for i, x in enumerate(w) if (x >> 16) == 0xBF88]  # s_cbranch_execz
+        assert len(br) == 2  # the Payne-Hanek block and the double Cody-Waite block
+        for b in br:
+            target = b + 1 + (w[b] & 0xFFFF)
+            assert w[target] == 0xBEFE0124, hex(w[target])  # s_mov_b64 exec, s[36:37]
+        lines = _disassemble(w + [SETPC])
+        assert any(ln.startswith("s_and_saveexec_b64 s[36:37]") for ln in lines)
