@@ -238,7 +238,8 @@ int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int
  * (plen where a program cannot be translated); pass it to mtgp_schedule instead of plen. */
 int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t n_prog, int32_t L,
                   int32_t* cost_out, void* stream);
-/* host emission of one (wave, program) unit over HOST arrays prog/order (tests/tooling) */
+/* host emission of one (wave, program) unit over HOST arrays prog/order (tests/tooling), laid
+ * out as if it started right after the shared sin/cos subroutines (PC-relative calls) */
 int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                        const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words);
 int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,

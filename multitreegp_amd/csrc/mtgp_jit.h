@@ -14,9 +14,11 @@
 //
 // Register ABI of a generated program (the evaluator's call site pins these):
 //   v0-v7    data slots 0-7 (read only)          v8      accumulator = result
-//   v9-v16   operand stack (depth <= 8)          v17-v24 template temporaries
+//   v9-v16   operand stack (depth <= 8)          v17-v25 template / unit temporaries
 //   s[30:31] return address (s_swappc_b64)       s[32:33] fallback lanes (OR-accumulated)
-//   s[34:39] template temporaries, vcc           exec    never written
+//   s[34:45] template temporaries, the sin/cos subroutine return address s[40:41] and
+//            target s[44:45], the unit's lane mask s[42:43]; vcc
+//   exec     restored (the sin/cos subroutines mask their slow-reduction blocks)
 // The host ABI (mtgp.h mtgp_jit_*) places the code in executable device memory.
 #ifndef MTGP_JIT_H
 #define MTGP_JIT_H
@@ -42,10 +44,24 @@ constexpr uint32_t kSetpcS30 = 0xbe801d1eu;  // s_setpc_b64 s[30:31]
 // largest translation of one program instruction (push + two moves + the sin template)
 constexpr int kJitMaxWordsPerInstr = 1 + 4 + MTGP_JIT_SIN_WORDS;
 
+// The sin/cos templates are shared subroutines at the start of the code buffer (one copy,
+// hot in the instruction cache); generated code calls them with a PC-relative address.
+constexpr uint32_t kJitAlignBytes = 64u;
+constexpr uint32_t kJitSinOffset = 0u;
+constexpr uint32_t kJitCosOffset = (MTGP_JIT_SIN_WORDS * 4u + kJitAlignBytes - 1u) & ~(kJitAlignBytes - 1u);
+constexpr uint32_t kJitTemplateBytes =
+    (kJitCosOffset + MTGP_JIT_COS_WORDS * 4u + kJitAlignBytes - 1u) & ~(kJitAlignBytes - 1u);
+constexpr uint32_t kGetpcS44 = 0xbeac1c00u;     // s_getpc_b64 s[44:45]
+constexpr uint32_t kAddS44 = 0x802cff2cu;       // s_add_u32 s44, s44, literal
+constexpr uint32_t kAddcS45M1 = 0x822dc12du;    // s_addc_u32 s45, s45, -1
+constexpr uint32_t kAddcS45Z = 0x822d802du;     // s_addc_u32 s45, s45, 0
+constexpr uint32_t kSwappcS40 = 0xbea81e2cu;    // s_swappc_b64 s[40:41], s[44:45]
+
 struct JitOut {
   uint32_t* out;  // nullptr: count only
   int n;
-  int trig = 0;   // sin/cos templates emitted (their double-precision block is normally skipped)
+  int trig = 0;       // sin/cos subroutine calls emitted
+  uint32_t base = 0;  // byte offset of out[0] in the code buffer (for PC-relative calls)
   MTGP_JIT_HD void w(uint32_t v) {
     if (out) out[n] = v;
     ++n;
@@ -104,8 +120,15 @@ MTGP_JIT_HD inline void jit_binop(JitOut& o, int fn, JitSrc x, JitSrc y) {
 MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
   ++o.trig;
   if (x.lit) o.movc(kJitT0, x.bits); else o.movv(kJitT0, x.reg);
-  if (is_sin) o.blob(mtgp_jit_sin_blob, MTGP_JIT_SIN_WORDS);
-  else o.blob(mtgp_jit_cos_blob, MTGP_JIT_COS_WORDS);
+  // s_getpc_b64 yields the address of the next instruction: target = that + rel
+  const uint32_t pc_next = o.base + (uint32_t)(o.n + 1) * 4u;
+  const uint32_t target = is_sin ? kJitSinOffset : kJitCosOffset;
+  const int64_t rel = (int64_t)target - (int64_t)pc_next;
+  o.w(kGetpcS44);
+  o.w(kAddS44);
+  o.w((uint32_t)(int32_t)rel);
+  o.w(rel < 0 ? kAddcS45M1 : kAddcS45Z);
+  o.w(kSwappcS40);
 }
 
 enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJitErrNoEnd = -4 };
@@ -212,20 +235,21 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
 }
 
 // One callable program: number of 32-bit code words (out == nullptr: count only) or < 0.
-MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out) {
+MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out, uint32_t base = kJitTemplateBytes) {
   JitOut o{out, 0};
+  o.base = base;
   const int rc = jit_program(o, prog, L, true);
   return rc < 0 ? rc : o.n;
 }
 
 // Estimated issue cost of one program (schedule weight): code words actually executed, i.e.
 // without the slow-reduction blocks of the sin/cos templates (skipped unless |x| >= 2^17).
-constexpr int kJitTrigSkipped = MTGP_JIT_SIN_SKIPPABLE_WORDS;
+constexpr int kJitTrigExecuted = MTGP_JIT_SIN_WORDS - MTGP_JIT_SIN_SKIPPABLE_WORDS;
 MTGP_JIT_HD inline int jit_cost(const MtgpInstr* prog, int L) {
   JitOut o{nullptr, 0};
   const int rc = jit_program(o, prog, L, true);
   if (rc < 0) return rc;
-  const int w = o.n - kJitTrigSkipped * o.trig;
+  const int w = o.n + kJitTrigExecuted * o.trig;
   return w > 1 ? w : 1;
 }
 
@@ -244,8 +268,9 @@ constexpr uint32_t kSelHi = 0x00aa1119u;
 
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
-                                int wave, int j, uint32_t* out) {
+                                int wave, int j, uint32_t* out, uint32_t base) {
   JitOut o{out, 0};
+  o.base = base;
   for (int g = 0; g < G; ++g) {
     const int q = wave * G + g;
     if (q >= P) break;

@@ -354,8 +354,8 @@ __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], 
                : [tgt] "s"(addr), "{v0}"(d[0]), "{v1}"(d[1]), "{v2}"(d[2]), "{v3}"(d[3]), "{v4}"(d[4]),
                  "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
                : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
-                 "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s42", "s43",
-                 "vcc", "memory");
+                 "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41",
+                 "s42", "s43", "s44", "s45", "vcc", "memory");
   return acc;
 }
 
@@ -1078,16 +1078,16 @@ struct JitUnitArgs {
   const int32_t* order;
 };
 
-__device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out) {
+__device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
-  return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out);
+  return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out, base);
 }
 
 __global__ void __launch_bounds__(256) k_jit_count(JitUnitArgs U, uint32_t* __restrict__ offs,
                                                    int32_t* __restrict__ info) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= U.n_units) return;
-  const int n = jit_unit_words(U, i, nullptr);
+  const int n = jit_unit_words(U, i, nullptr, 0u);
   // units start on 64-byte instruction-cache lines (measured: unaligned call targets made some
   // code shapes 2x slower, scripts/dispatch_cost.py k = 4)
   offs[i] = n > 0 ? ((uint32_t)n * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u) : 0u;
@@ -1120,14 +1120,14 @@ __global__ void __launch_bounds__(1024) k_jit_scan(uint32_t* __restrict__ offs, 
     part[t] += v;
     __syncthreads();
   }
-  uint64_t run = part[t] - sum;
+  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
   for (int i = b; i < e; ++i) {
     const uint64_t w = offs[i];
     offs[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
     run += w;
   }
   if (t == 1023) {
-    const uint64_t tot = part[1023];
+    const uint64_t tot = part[1023] + mtgp::kJitTemplateBytes;
     offs[total] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
     info[1] = (int32_t)(tot < 0x7fffffffull ? tot : 0x7fffffffull);
   }
@@ -1139,7 +1139,14 @@ __global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t*
   if (i >= U.n_units) return;
   const uint32_t b = offs[i], e = offs[i + 1];
   if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
-  jit_unit_words(U, i, code + b / 4);
+  jit_unit_words(U, i, code + b / 4, b);
+}
+
+// the shared sin/cos subroutines at the start of the code buffer
+__global__ void __launch_bounds__(256) k_jit_templates(uint32_t* __restrict__ code, uint64_t code_bytes) {
+  if (code_bytes < mtgp::kJitTemplateBytes) return;
+  for (int i = threadIdx.x; i < MTGP_JIT_SIN_WORDS; i += blockDim.x) code[mtgp::kJitSinOffset / 4 + i] = mtgp_jit_sin_blob[i];
+  for (int i = threadIdx.x; i < MTGP_JIT_COS_WORDS; i += blockDim.x) code[mtgp::kJitCosOffset / 4 + i] = mtgp_jit_cos_blob[i];
 }
 
 bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
@@ -1284,6 +1291,8 @@ int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, i
   JitUnitArgs U;
   if (!offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
   if (U.n_units == 0) return MTGP_OK;
+  hipLaunchKernelGGL(k_jit_templates, dim3(1), dim3(256), 0, (hipStream_t)stream, (uint32_t*)code,
+                     (uint64_t)code_bytes);
   hipLaunchKernelGGL(k_jit_emit, dim3((unsigned)((U.n_units + 255) / 256)), dim3(256), 0, (hipStream_t)stream, U,
                      offsets, (uint32_t*)code, (uint64_t)code_bytes);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
@@ -1304,11 +1313,11 @@ int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t
   JitUnitArgs U;
   if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
   const int wave = unit / n_prog, j = unit - wave * n_prog;
-  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr);
+  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes);
   if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
   if (out) {
     if (n > max_words) return MTGP_ERR_ARG;
-    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out);
+    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes);
   }
   return n;
 }

@@ -9,7 +9,8 @@ division are copied from the templates below.  Register ABI of the generated cod
 v17-v24 template temporaries, s[30:31] return address, s[32:33] fallback lane mask
 (OR-accumulated), s[34:39] template temporaries, vcc clobbered, exec never written.
 
-  SIN / COS  : x in v17 -> v8.  include/mtgp_f32math.h mtgp_sinf/mtgp_cosf op for op: float
+  SIN / COS  : subroutines (one shared copy at the start of the code buffer, called with
+               s_swappc_b64 s[40:41], returning with s_setpc_b64 s[40:41]): x in v17 -> v8.  include/mtgp_f32math.h mtgp_sinf/mtgp_cosf op for op: float
                Cody-Waite for |x| < 2^17; for finite |x| >= 2^28 the spec's Payne-Hanek
                reduction (96-bit window of 2/pi selected per lane, three 32x32->64 products,
                int64 -> double, times pi/2), for 2^17 <= |x| < 2^28 the spec's double
@@ -190,6 +191,7 @@ v_xor_b32 v23, v23, v18
 v_cmp_gt_f32_e32 vcc, 0x39800000, v24
 s_nop 1
 v_cndmask_b32_e32 v8, v23, v17, vcc
+s_setpc_b64 s[40:41]
 """,
     "COS": REDUCE + """
 v_cndmask_b32_e32 v23, v22, v21, vcc
@@ -200,6 +202,7 @@ v_xor_b32 v23, v23, v18
 v_cmp_ngt_f32_e32 vcc, 0x39800000, v24
 s_nop 1
 v_cndmask_b32_e32 v8, 1.0, v23, vcc
+s_setpc_b64 s[40:41]
 """,
     "DIV": """
 v_div_scale_f32 v19, s[34:35], v18, v18, v17

@@ -37,7 +37,8 @@ __device__ __forceinline__ float jit_call(uint64_t addr, const float d[8], uint6
                : [tgt] "s"(addr), "{v0}"(d[0]), "{v1}"(d[1]), "{v2}"(d[2]), "{v3}"(d[3]), "{v4}"(d[4]),
                  "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
                : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
-                 "v22", "v23", "v24", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "vcc", "memory");
+                 "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41",
+                 "s42", "s43", "s44", "s45", "vcc", "memory");
   return acc;
 }
 
@@ -95,13 +96,17 @@ int main() {
       {IS(MTGP_OP_VV_DIV, 5 * SB, 4 * SB), IS(MTGP_OP_LDVP, 0, 0), I(MTGP_OP_RSUBS, 0, 0), I(MTGP_OP_END, 0, 0)},  // RSUBS: d4/d5 - d0
       {IS(MTGP_OP_COSV, 0, 2 * SB), I(MTGP_OP_END, 0, 0)},                                   // cos d2 (sweep)
   };
-  std::vector<uint32_t> words, offs;
+  // shared sin/cos subroutines first (mtgp_jit.h layout), then the programs
+  std::vector<uint32_t> words(mtgp::kJitTemplateBytes / 4, 0xbf800000u), offs;
+  for (int i = 0; i < MTGP_JIT_SIN_WORDS; ++i) words[mtgp::kJitSinOffset / 4 + i] = mtgp_jit_sin_blob[i];
+  for (int i = 0; i < MTGP_JIT_COS_WORDS; ++i) words[mtgp::kJitCosOffset / 4 + i] = mtgp_jit_cos_blob[i];
   for (auto& p : progs) {
-    offs.push_back((uint32_t)(words.size() * 4));
-    const int n = mtgp::jit_translate(p.data(), (int)p.size(), nullptr);
+    const uint32_t base = (uint32_t)(words.size() * 4);
+    offs.push_back(base);
+    const int n = mtgp::jit_translate(p.data(), (int)p.size(), nullptr, base);
     if (n < 0) { printf("translate error %d\n", n); return 3; }
     words.resize(words.size() + n);
-    mtgp::jit_translate(p.data(), (int)p.size(), words.data() + words.size() - n);
+    mtgp::jit_translate(p.data(), (int)p.size(), words.data() + words.size() - n, base);
     while (words.size() % 16) words.push_back(0xbf800000u);  // s_nop 0 padding to 64 B
   }
   uint32_t *dw, *doffs, *dflags;

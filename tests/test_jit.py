@@ -37,6 +37,10 @@ def _blobs():
 
 BLOBS = _blobs()
 SETPC = 0xBE801D1E
+GETPC_S44 = 0xBEAC1C00  # s_getpc_b64 s[44:45] -- starts a call of a shared sin/cos subroutine
+_up = lambda x: (x + 63) // 64 * 64  # noqa: E731
+COS_OFF = _up(len(BLOBS["SIN"]) * 4)
+TEMPLATE_BYTES = _up(COS_OFF + len(BLOBS["COS"]) * 4)  # host translations start right after them
 
 
 def test_templates_up_to_date():
@@ -78,7 +82,7 @@ def _disassemble(words):
 
 
 ALLOWED_V = set(range(8, 26))
-ALLOWED_S = set(range(30, 44))
+ALLOWED_S = set(range(30, 46))
 EXEC_OK = ("s_mov_b64 s[40:41], exec", "s_mov_b64 exec, s[40:41]", "s_mov_b64 exec, s[36:37]")
 
 
@@ -144,6 +148,15 @@ def _emulate(words, data, full=False):
         w = words[i]
         if w == SETPC:
             return v if full else v[8]
+        if w == GETPC_S44:  # getpc; s_add_u32 s44, lit; s_addc_u32 s45; s_swappc_b64 s[40:41], s[44:45]
+            assert words[i + 1] == 0x802CFF2C and words[i + 4] == 0xBEA81E2C, [hex(x) for x in words[i:i + 5]]
+            rel = int(np.array(words[i + 2], np.uint32).view(np.int32))
+            target = TEMPLATE_BYTES + 4 * (i + 1) + rel
+            assert target in (0, COS_OFF), target
+            s_, c_ = orc.sincos(v[17])
+            put(8, s_ if target == 0 else c_)
+            i += 5
+            continue
         if (w >> 23) == 0x17D:  # SOP1: the exec save / restore / set of per-wave units
             sdst, op, ssrc = (w >> 16) & 0x7F, (w >> 8) & 0xFF, w & 0xFF
             if (sdst, op, ssrc) == (40, 1, 126):
