@@ -148,18 +148,59 @@ __device__ __forceinline__ void acro_f_obs(const float x[4], float y[4]) {
 // shared.  C@x and the noise product are summed in index order exactly like the oracle.
 struct ObsNoise {
   uint32_t k0, k1;  // this lane's rollout key
-  float W[16];      // [n_obs, n_obs] row-major, wave-uniform
+  const float* W;   // [n_obs, n_obs] row-major (read with scalar loads when used: no registers held)
   int impl;         // MTGP_PRNG_* random-bits layout
+  bool diag;        // W diagonal with a non-zero diagonal (obs_noise * I): noise_j = n_j * W_jj exactly
 };
 
 __device__ __forceinline__ ObsNoise obs_noise_setup(const MtgpModel& m, const MtgpRollouts& ro, int rr) {
   ObsNoise z;
   z.k0 = ro.obs_keys[2 * rr + 0];
   z.k1 = ro.obs_keys[2 * rr + 1];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) z.W[i] = ro.obs_w[i];
+  z.W = ro.obs_w;
   z.impl = m.prng_impl;
+  bool diag = true;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) diag = diag && ((i == j) ? (z.W[i * 4 + j] != 0.0f) : (z.W[i * 4 + j] == 0.0f));
+  z.diag = uni((int)diag) != 0;
   return z;
+}
+
+// noise vector normal(fold_in(key, bitcast(t)), (4,)) @ W (summed in index order).  With W
+// diagonal and non-zero on the diagonal, the off-diagonal products are +-0 and the sum is
+// exactly n_j * W_jj (n_j is never 0: |u| > 0 always), so the product is skipped.
+__device__ __forceinline__ void obs_noise_vec(const ObsNoise& z, float t, float nz[4]) {
+  float n[4];
+  mtgp_obs_normals(z.k0, z.k1, t, 4, z.impl, n);
+  if (z.diag) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) nz[j] = n[j] * z.W[j * 4 + j];
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    float acc = n[0] * z.W[j];
+#pragma unroll
+    for (int i = 1; i < 4; ++i) acc = acc + n[i] * z.W[i * 4 + j];
+    nz[j] = acc;
+  }
+}
+
+// y = C@x + nz with C = I: (C@x)_i + nz_i equals x_i + nz_i when every x_j is finite (the +-0
+// terms 0*x_j cannot change a sum with the non-zero nz_i), NaN otherwise (0*inf), then the
+// Acrobot angle wrap (acrobot.py:29-32).
+__device__ __forceinline__ void acro_obs_apply(const float x[4], const float nz[4], float y[4]) {
+  const bool f0 = mtgp_isfinite(x[0]), f1 = mtgp_isfinite(x[1]), f2 = mtgp_isfinite(x[2]),
+             f3 = mtgp_isfinite(x[3]);
+  const float qn = mtgp_qnan();
+  y[0] = (f1 && f2 && f3) ? x[0] + nz[0] : qn;
+  y[1] = (f0 && f2 && f3) ? x[1] + nz[1] : qn;
+  y[2] = (f0 && f1 && f3) ? x[2] + nz[2] : qn;
+  y[3] = (f0 && f1 && f2) ? x[3] + nz[3] : qn;
+  y[0] = mtgp_wrap_angle(y[0]);
+  y[1] = mtgp_wrap_angle(y[1]);
 }
 
 template <bool NOISE>
@@ -168,24 +209,9 @@ __device__ __forceinline__ void acro_obs(const ObsNoise& z, float t, const float
     acro_f_obs(x, y);
     return;
   }
-  float n[4], nz[4];
-  mtgp_obs_normals(z.k0, z.k1, t, 4, z.impl, n);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    float acc = n[0] * z.W[j];
-#pragma unroll
-    for (int i = 1; i < 4; ++i) acc = acc + n[i] * z.W[i * 4 + j];
-    nz[j] = acc;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    float cx = (i == 0) ? x[0] : 0.0f * x[0];
-#pragma unroll
-    for (int j = 1; j < 4; ++j) cx = cx + ((i == j) ? x[j] : 0.0f * x[j]);
-    y[i] = cx + nz[i];
-  }
-  y[0] = mtgp_wrap_angle(y[0]);
-  y[1] = mtgp_wrap_angle(y[1]);
+  float nz[4];
+  obs_noise_vec(z, t, nz);
+  acro_obs_apply(x, nz, y);
 }
 
 __device__ __forceinline__ bool acro_bad(const float* s, int n) {
@@ -489,10 +515,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
   ObsNoise nzc;
+  float nzv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
   constexpr int uslot = 4 + NA;
-  const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
-                                 A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
+  // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
+  // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
+  const float pl1 = A.ro.params[4 * rr + 0], pl2 = A.ro.params[4 * rr + 1], pm1 = A.ro.params[4 * rr + 2],
+              pm2 = A.ro.params[4 * rr + 3];
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;  // element offset of this (individual, rollout) in a save row
 #pragma unroll
@@ -551,9 +580,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       float ur[1];
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       const float u = ur[0];
-      acro_drift(K, xt, u, kx);
+      acro_drift(acro_const(pl1, pl2, pm1, pm2), xt, u, kx);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
+      if (NOISE) {  // stages 1 and 2 share the time t + h/2, hence the noise draw
+        if (stage != 2) obs_noise_vec(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+        acro_obs_apply(xt, nzv, y);
+      } else {
+        acro_f_obs(xt, y);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) D.put(i, y[i]);
       D.put(uslot, u);
@@ -649,9 +683,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
   ObsNoise nzc;
+  float nzv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
-  const AcroConst K = acro_const(A.ro.params[4 * rr + 0], A.ro.params[4 * rr + 1],
-                                 A.ro.params[4 * rr + 2], A.ro.params[4 * rr + 3]);
+  // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
+  // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
+  const float pl1 = A.ro.params[4 * rr + 0], pl2 = A.ro.params[4 * rr + 1], pm1 = A.ro.params[4 * rr + 2],
+              pm2 = A.ro.params[4 * rr + 3];
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;
 #pragma unroll
@@ -675,13 +712,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
       for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      acro_obs<NOISE>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), xt, y);
+      if (NOISE) {  // stages 1 and 2 share the time t + h/2, hence the noise draw
+        if (stage != 2) obs_noise_vec(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+        acro_obs_apply(xt, nzv, y);
+      } else {
+        acro_f_obs(xt, y);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) D.put(i, y[i]);
       float ur[1];
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // ff.py:106-107 (:97 at saves)
       float u = ur[0];
-      acro_drift(K, xt, u, kx);
+      acro_drift(acro_const(pl1, pl2, pm1, pm2), xt, u, kx);
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
@@ -986,17 +1028,18 @@ __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, i
                                                 MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                 int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                 int32_t* nodes_out, int32_t* status_out) {
-  constexpr int TPB = (NMAX <= 64) ? 64 : (NMAX <= 128 ? 32 : 16);
-  __shared__ mtgp::RowInfo info_all[TPB * NMAX];
+  // per-lane row table in private memory: an LDS table (28 B x NMAX x 64 lanes = 112 KB at
+  // NMAX = 64) allowed one wave per CU; private arrays let the flatten run at full occupancy
+  constexpr int TPB = 64;
+  mtgp::RowInfo info_priv[NMAX];
   const int t_in = threadIdx.x;
-  if (t_in >= TPB) return;
   const long gid = (long)blockIdx.x * TPB + t_in;
   const long total = (long)P * n_prog;
   if (gid >= total) return;
   const int p = (int)(gid / n_prog), j = (int)(gid % n_prog);
   const MtgpProgramSpec sp = specs[j];
   const float* tree = pop + ((size_t)p * T + sp.tree) * N * 4;
-  mtgp::RowInfo* info = &info_all[t_in * NMAX];
+  mtgp::RowInfo* info = info_priv;
   MtgpInstr* out = prog_out + ((size_t)p * n_prog + j) * L;
   int need = 0;
   const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
@@ -1357,15 +1400,15 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const
   const long total = (long)P * n_prog;
   MtgpNodeLibrary libv = *lib;
   if (N <= 64) {
-    const int tpb = 64;
+    const int tpb = 64;  // one lane per program (k_flatten TPB)
     hipLaunchKernelGGL(k_flatten<64>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T, N,
                        libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
   } else if (N <= 128) {
-    const int tpb = 32;
+    const int tpb = 64;
     hipLaunchKernelGGL(k_flatten<128>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
                        N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
   } else {
-    const int tpb = 16;
+    const int tpb = 64;
     hipLaunchKernelGGL(k_flatten<256>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
                        N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
   }

@@ -238,3 +238,17 @@ def test_jit_code_that_does_not_fit_is_interpreted():
     d = eng.prepare_data(data)
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
     _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
+
+
+def test_obs_noise_dense_w_bitexact():
+    """A general (non-diagonal) noise matrix W: noise = normal @ W summed in index order."""
+    env, lib, ff, data, pop = dynamic_setup(P=24, R=16, n_steps=40, obs_noise=0.1, seed=8)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    d = eng.prepare_data(data)
+    W = (np.random.default_rng(4).standard_normal((4, 4)) * 0.05).astype(np.float32)
+    d["obs_w"] = W
+    d["obs_w_dev"] = torch.from_numpy(W).cuda()
+    res = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=True, rollout_fitness=True)
+    torch.cuda.synchronize()
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
