@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 6
+#define MTGP_ABI_VERSION 7
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -102,6 +102,18 @@ enum {
   MTGP_MODEL_ACROBOT_STATIC = 2,  /* feedforward_evaluate.Evaluator + Acrobot ff.py:10-110 */
   MTGP_MODEL_SR = 3               /* SR_evaluator.Evaluator             sr.py:9-94       */
 };
+/* The two control models run any of these environments (MtgpModel.env); the enum names above
+ * keep their round-1 spelling: MTGP_MODEL_ACROBOT_DYNAMIC is the dynamic evaluator, whatever
+ * the environment. */
+#define MTGP_MODEL_DYNAMIC MTGP_MODEL_ACROBOT_DYNAMIC
+#define MTGP_MODEL_STATIC MTGP_MODEL_ACROBOT_STATIC
+enum {
+  MTGP_ENV_ACROBOT = 0,              /* acrobot.py:7-87:  n_var 4, n_obs 4, params [R, 4] l1 l2 m1 m2 */
+  MTGP_ENV_HARMONIC_OSCILLATOR = 1,  /* harmonic_oscillator.py:8-80: n_var 2, n_obs 2, n_targets 1,  */
+                                     /*   params [R, 2] omega zeta                                     */
+  MTGP_ENV_STIRRED_TANK_REACTOR = 2  /* reactor.py:7-81: n_var 3, n_obs 3, n_targets 1,              */
+                                     /*   params [R, 8] Vol Cp dHr UA q Tf Tcf Volc                    */
+};
 
 typedef struct {
   int32_t model;
@@ -124,11 +136,12 @@ typedef struct {
   int32_t prng_impl;         /* observation-noise random-bits layout (mtgp_prng.h): */
                              /* 0 threefry original (JAX <= 0.4.x default),        */
                              /* 1 threefry partitionable (JAX >= 0.5 default)      */
+  int32_t env;               /* control models: MTGP_ENV_* (0 = Acrobot)            */
 } MtgpModel;
 
 typedef struct {
   const float* x0;      /* [R, n_var]                                       */
-  const float* params;  /* [R, 4] Acrobot (l1, l2, m1, m2) acrobot.py:34-49   */
+  const float* params;  /* [R, n_params] per MTGP_ENV_* (Acrobot: l1 l2 m1 m2) */
   const float* targets; /* [R, n_targets] (may be NULL when n_targets == 0)  */
   const float* ts;      /* [n_save] save times (fitness mask acrobot.py:82)  */
   const float* ys_true; /* SR: [n_save, n_var, R] ground truth, time-major   */
@@ -141,7 +154,8 @@ typedef struct {
   /*   y = C@x + normal(fold_in(obs_keys[r], bitcast(t)), (n_obs,)) @ obs_w       */
   /* at every RK4 stage time t = ts[0] + n*h + c_i*h and at every save time ts[k]. */
   const uint32_t* obs_keys; /* [R, 2] obs_noise_keys (dyn.py:65) or NULL = noise-free */
-  const float* obs_w;       /* [n_obs, n_obs] W = obs_noise * I (acrobot.py:49)        */
+  const float* obs_w;       /* [n_obs, n_obs] W (acrobot.py:49: obs_noise * I;          */
+                            /*  reactor.py:43: obs_noise * I * [15, 15, 0.1])          */
 } MtgpRollouts;
 
 /* Outputs.  Trajectories are time-major structure-of-arrays so that every save point

@@ -262,4 +262,34 @@ MTGP_INLINE MTGP_HD float mtgp_clip1(float u) {
   return u < -1.0f ? -1.0f : (u > 1.0f ? 1.0f : u);
 }
 
+/* jnp.clip(u, lo, hi) = minimum(maximum(u, lo), hi), NaN-propagating (reactor.py:63). */
+MTGP_INLINE MTGP_HD float mtgp_clip(float u, float lo, float hi) {
+  if (mtgp_isnan(u)) return u;
+  return u < lo ? lo : (u > hi ? hi : u);
+}
+
+/* exp(x) (StirredTankReactor.k, reactor.py:40: k0 * exp(-Ea/R/T)).  n = rint(x / ln2),
+ * r = x - n ln2 by a two-constant fma Cody-Waite step, exp(r) by the degree-6 Cephes expf
+ * polynomial, then y * 2^n as two exact power-of-two scalings (one rounding, gradual
+ * underflow).  NaN -> NaN, x > 88.7228394 -> +inf, x < -103.972084 -> +0.  Max error
+ * ~1 ulp vs float64 exp (tests/test_f32math.py). */
+MTGP_INLINE MTGP_HD float mtgp_expf(float x) {
+  if (mtgp_isnan(x)) return x;
+  if (x > 88.7228394f) return mtgp_u2f(0x7f800000u);
+  if (x < -103.972084f) return 0.0f;
+  const float n = MTGP_RINTF(x * 1.44269502162933350e+00f);
+  float r = MTGP_FMAF(-n, 6.93147182464599609e-01f, x);
+  r = MTGP_FMAF(-n, -1.90465429995776804e-09f, r);
+  float p = 1.9875691500e-4f;
+  p = MTGP_FMAF(p, r, 1.3981999507e-3f);
+  p = MTGP_FMAF(p, r, 8.3334519073e-3f);
+  p = MTGP_FMAF(p, r, 4.1665795894e-2f);
+  p = MTGP_FMAF(p, r, 1.6666665459e-1f);
+  p = MTGP_FMAF(p, r, 5.0000001201e-1f);
+  float y = MTGP_FMAF(p, r * r, r) + 1.0f;
+  const int ni = (int)n, n1 = ni / 2, n2 = ni - n1; /* |n1|, |n2| <= 75: normal powers of two */
+  y = y * mtgp_u2f((uint32_t)(n1 + 127) << 23);
+  return y * mtgp_u2f((uint32_t)(n2 + 127) << 23);
+}
+
 #endif /* MTGP_F32MATH_H */

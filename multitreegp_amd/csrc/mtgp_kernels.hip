@@ -129,89 +129,84 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
   dx[3] = a2;
 }
 
-// f_obs with C = I and zero observation noise (cbase.py:43-48): y = C@x + 0, i.e. x_i + 0
-// when every component is finite; C@x propagates NaN from any non-finite x_j (0*inf).
-__device__ __forceinline__ void acro_f_obs(const float x[4], float y[4]) {
-  const bool f0 = mtgp_isfinite(x[0]), f1 = mtgp_isfinite(x[1]), f2 = mtgp_isfinite(x[2]),
-             f3 = mtgp_isfinite(x[3]);
-  const float qn = mtgp_qnan();
-  y[0] = (f1 && f2 && f3) ? x[0] + 0.0f : qn;
-  y[1] = (f0 && f2 && f3) ? x[1] + 0.0f : qn;
-  y[2] = (f0 && f1 && f3) ? x[2] + 0.0f : qn;
-  y[3] = (f0 && f1 && f2) ? x[3] + 0.0f : qn;
-  y[0] = mtgp_wrap_angle(y[0]);
-  y[1] = mtgp_wrap_angle(y[1]);
-}
-
-// Observation noise (cbase.py:43-48): out = C@x + normal(fold_in(key, bitcast(t)), (4,)) @ W.
-// The key is per rollout (obs_noise_keys, dyn.py:65), W (= obs_noise * I, acrobot.py:49) is
-// shared.  C@x and the noise product are summed in index order exactly like the oracle.
+// Observation noise (cbase.py:43-48): out = C@x + normal(fold_in(key, bitcast(t)), (NO,)) @ W.
+// The key is per rollout (obs_noise_keys, dyn.py:65), W (acrobot.py:49: obs_noise * I;
+// reactor.py:43: obs_noise * I * [15, 15, 0.1]) is shared.  C@x and the noise product are
+// summed in index order exactly like the oracle.
+template <int NO>
 struct ObsNoise {
   uint32_t k0, k1;  // this lane's rollout key
-  const float* W;   // [n_obs, n_obs] row-major (read with scalar loads when used: no registers held)
+  const float* W;   // [NO, NO] row-major (read with scalar loads when used: no registers held)
   int impl;         // MTGP_PRNG_* random-bits layout
-  bool diag;        // W diagonal with a non-zero diagonal (obs_noise * I): noise_j = n_j * W_jj exactly
+  bool diag;        // W diagonal with a non-zero diagonal: noise_j = n_j * W_jj exactly
 };
 
-__device__ __forceinline__ ObsNoise obs_noise_setup(const MtgpModel& m, const MtgpRollouts& ro, int rr) {
-  ObsNoise z;
+template <int NO>
+__device__ __forceinline__ ObsNoise<NO> obs_noise_setup(const MtgpModel& m, const MtgpRollouts& ro, int rr) {
+  ObsNoise<NO> z;
   z.k0 = ro.obs_keys[2 * rr + 0];
   z.k1 = ro.obs_keys[2 * rr + 1];
   z.W = ro.obs_w;
   z.impl = m.prng_impl;
   bool diag = true;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NO; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) diag = diag && ((i == j) ? (z.W[i * 4 + j] != 0.0f) : (z.W[i * 4 + j] == 0.0f));
+    for (int j = 0; j < NO; ++j) diag = diag && ((i == j) ? (z.W[i * NO + j] != 0.0f) : (z.W[i * NO + j] == 0.0f));
   z.diag = uni((int)diag) != 0;
   return z;
 }
 
-// noise vector normal(fold_in(key, bitcast(t)), (4,)) @ W (summed in index order).  With W
+// noise vector normal(fold_in(key, bitcast(t)), (NO,)) @ W (summed in index order).  With W
 // diagonal and non-zero on the diagonal, the off-diagonal products are +-0 and the sum is
 // exactly n_j * W_jj (n_j is never 0: |u| > 0 always), so the product is skipped.
-__device__ __forceinline__ void obs_noise_vec(const ObsNoise& z, float t, float nz[4]) {
-  float n[4];
-  mtgp_obs_normals(z.k0, z.k1, t, 4, z.impl, n);
+template <int NO>
+__device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, float nz[NO]) {
+  float n[NO];
+  mtgp_obs_normals(z.k0, z.k1, t, NO, z.impl, n);
   if (z.diag) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) nz[j] = n[j] * z.W[j * 4 + j];
+    for (int j = 0; j < NO; ++j) nz[j] = n[j] * z.W[j * NO + j];
     return;
   }
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
+  for (int j = 0; j < NO; ++j) {
     float acc = n[0] * z.W[j];
 #pragma unroll
-    for (int i = 1; i < 4; ++i) acc = acc + n[i] * z.W[i * 4 + j];
+    for (int i = 1; i < NO; ++i) acc = acc + n[i] * z.W[i * NO + j];
     nz[j] = acc;
   }
 }
 
-// y = C@x + nz with C = I: (C@x)_i + nz_i equals x_i + nz_i when every x_j is finite (the +-0
-// terms 0*x_j cannot change a sum with the non-zero nz_i), NaN otherwise (0*inf), then the
-// Acrobot angle wrap (acrobot.py:29-32).
-__device__ __forceinline__ void acro_obs_apply(const float x[4], const float nz[4], float y[4]) {
-  const bool f0 = mtgp_isfinite(x[0]), f1 = mtgp_isfinite(x[1]), f2 = mtgp_isfinite(x[2]),
-             f3 = mtgp_isfinite(x[3]);
+// y = C@x + nz with C = I (n_obs = n_var for every environment on this path): (C@x)_i + nz_i
+// equals x_i + nz_i when every x_j is finite (the +-0 terms 0*x_j cannot change the sum; with
+// nz = +0 a -0 becomes +0 either way), NaN otherwise (0*inf), then the environment's own
+// observation transform (Acrobot: angle wrap, acrobot.py:29-32).
+template <class Env>
+__device__ __forceinline__ void ctl_obs_apply(const float x[Env::NV], const float nz[Env::NV], float y[Env::NV]) {
+  constexpr int NV = Env::NV;
+  bool fin[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) fin[j] = mtgp_isfinite(x[j]);
   const float qn = mtgp_qnan();
-  y[0] = (f1 && f2 && f3) ? x[0] + nz[0] : qn;
-  y[1] = (f0 && f2 && f3) ? x[1] + nz[1] : qn;
-  y[2] = (f0 && f1 && f3) ? x[2] + nz[2] : qn;
-  y[3] = (f0 && f1 && f2) ? x[3] + nz[3] : qn;
-  y[0] = mtgp_wrap_angle(y[0]);
-  y[1] = mtgp_wrap_angle(y[1]);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    bool ok = true;
+#pragma unroll
+    for (int j = 0; j < NV; ++j)
+      if (j != i) ok = ok && fin[j];
+    y[i] = ok ? x[i] + nz[i] : qn;
+  }
+  Env::obs_transform(y);
 }
 
-template <bool NOISE>
-__device__ __forceinline__ void acro_obs(const ObsNoise& z, float t, const float x[4], float y[4]) {
-  if (!NOISE) {
-    acro_f_obs(x, y);
-    return;
-  }
-  float nz[4];
-  obs_noise_vec(z, t, nz);
-  acro_obs_apply(x, nz, y);
+template <class Env, bool NOISE>
+__device__ __forceinline__ void ctl_obs(const ObsNoise<Env::NV>& z, float t, const float x[Env::NV], float y[Env::NV]) {
+  float nz[Env::NV];
+#pragma unroll
+  for (int j = 0; j < Env::NV; ++j) nz[j] = 0.0f;
+  if (NOISE) obs_noise_vec<Env::NV>(z, t, nz);
+  ctl_obs_apply<Env>(x, nz, y);
 }
 
 __device__ __forceinline__ bool acro_bad(const float* s, int n) {
@@ -259,16 +254,165 @@ __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool i
   }
 }
 
+__device__ __forceinline__ bool save_incl(const float* ts, int k) {
+  const float dts = ts[1] - ts[0];
+  return !((ts[k] / dts) > (float)k);
+}
+
+// --------------------------------------------------------------------------------------
+// Environments (control_environments/*.py).  Each is a per-lane struct: its parameters and
+// target live in registers for the whole rollout; drift, observation transform, termination
+// test and an online (single-pass) fitness accumulator, each restating the reference's
+// expression with the same operations and operand order as the oracle (bit-identical).
+//   NV          latent state size (= n_obs: C = I on this path)
+//   load        per-rollout constants (initialize_parameters) and the target
+//   drift       EnvironmentBase.drift(t, x, u) (autonomous: t unused by all three)
+//   bad         the cond_fn_nan event (true = terminate)
+//   fit_*       fitness_function over the saved points, accumulated at each save; fit_kill marks
+//               a rollout whose remaining save points are the +inf fill (its fitness is then
+//               fixed: Acrobot ignores them, the quadratic costs become NaN).
+
+// Acrobot (acrobot.py:7-87)
+struct EnvAcrobot {
+  static constexpr int NV = 4;
+  // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
+  // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
+  float l1, l2, m1, m2;
+  typedef AcroFit Fit;
+  __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
+    (void)nt;
+    l1 = ro.params[4 * rr + 0];
+    l2 = ro.params[4 * rr + 1];
+    m1 = ro.params[4 * rr + 2];
+    m2 = ro.params[4 * rr + 3];
+  }
+  __device__ __forceinline__ void drift(const float x[4], float u, float dx[4]) const {
+    acro_drift(acro_const(l1, l2, m1, m2), x, u, dx);
+  }
+  __device__ __forceinline__ static void obs_transform(float y[4]) {
+    y[0] = mtgp_wrap_angle(y[0]);
+    y[1] = mtgp_wrap_angle(y[1]);
+  }
+  __device__ __forceinline__ static bool bad(const float* s, int n) { return acro_bad(s, n); }
+  __device__ __forceinline__ static Fit fit_init(bool active) { return Fit{!active, 0.0f, 0.0f, 0.0f}; }
+  __device__ __forceinline__ void fit_update(Fit& f, int k, int S, const float* ts, float u, const float x[4]) const {
+    acro_fit_update(f, k, S, save_incl(ts, k), u, x[0], x[1]);
+  }
+  __device__ __forceinline__ static void fit_kill(Fit& f) { (void)f; }  // fs/cost mask ignore the fill
+  __device__ __forceinline__ static float fit_final(Fit& f, int S) {
+    if (!f.settled) { f.settled = true; f.F = (float)S + f.c0incl; }
+    return f.F;
+  }
+};
+
+__device__ __forceinline__ bool any_nonfinite(const float* s, int n) {
+  bool bad = false;
+  for (int i = 0; i < n; ++i) bad = bad || !mtgp_isfinite(s[i]);
+  return bad;
+}
+
+// (e^T Q) e with every product summed left to right over the full matrix (zeros included), the
+// literal `(x - x_d).T @ Q @ (x - x_d)` of harmonic_oscillator.py:76 / reactor.py:77
+template <int N>
+__device__ __forceinline__ float quad_form(const float e[N], const float (&Q)[N * N]) {
+  float out = 0.0f;
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    float v = e[0] * Q[j];
+#pragma unroll
+    for (int i = 1; i < N; ++i) v = v + e[i] * Q[i * N + j];
+    out = (j == 0) ? v * e[0] : out + v * e[j];
+  }
+  return out;
+}
+
+// running sum of per-save quadratic costs (jnp.sum(costs), summed in time order)
+struct QuadFit {
+  bool settled;
+  float F;
+};
+
+// HarmonicOscillator (harmonic_oscillator.py:8-80): dx = A x + b u, A = [[0, 1], [-omega, -zeta]],
+// b = [0, 1]^T; cost (x - x_d)^T Q (x - x_d) + (u - u_d) R (u - u_d), x_d = [target, 0],
+// u_d = -pinv(b) A x_d with pinv(b) = [[0, 1]] exactly, Q = [[0.5, 0], [0, 0]], R = [[0.5]].
+struct EnvHarmonic {
+  static constexpr int NV = 2;
+  float a10, a11, tg, ud;
+  typedef QuadFit Fit;
+  __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
+    a10 = -ro.params[2 * rr + 0];
+    a11 = -ro.params[2 * rr + 1];
+    tg = ro.targets[rr * nt];
+    const float M0 = (-0.0f) * 0.0f + (-1.0f) * a10, M1 = (-0.0f) * 1.0f + (-1.0f) * a11;  // -pinv(b) @ A
+    ud = M0 * tg + M1 * 0.0f;
+  }
+  __device__ __forceinline__ void drift(const float x[2], float u, float dx[2]) const {
+    dx[0] = (0.0f * x[0] + 1.0f * x[1]) + 0.0f * u;
+    dx[1] = (a10 * x[0] + a11 * x[1]) + 1.0f * u;
+  }
+  __device__ __forceinline__ static void obs_transform(float y[2]) { (void)y; }
+  __device__ __forceinline__ static bool bad(const float* s, int n) { return any_nonfinite(s, n); }
+  __device__ __forceinline__ static Fit fit_init(bool active) { return Fit{!active, 0.0f}; }
+  __device__ __forceinline__ void fit_update(Fit& f, int k, int S, const float* ts, float u, const float x[2]) const {
+    (void)k; (void)S; (void)ts;
+    const float Q[4] = {0.5f, 0.0f, 0.0f, 0.0f};
+    const float e[2] = {x[0] - tg, x[1] - 0.0f};
+    const float du = u - ud;
+    f.F = f.F + (quad_form<2>(e, Q) + (du * 0.5f) * du);
+  }
+  __device__ __forceinline__ static void fit_kill(Fit& f) { f.settled = true; f.F = mtgp_qnan(); }
+  __device__ __forceinline__ static float fit_final(Fit& f, int S) { (void)S; return f.F; }
+};
+
+// StirredTankReactor (reactor.py:7-81), state (Tc, T, c): k(T) = k0 exp(-Ea/R/T) with -Ea/R a
+// Python float64 quotient rounded to f32, k0 = f32(7.2e10); control clipped to [0, 300]; the
+// per-rollout quotients q/Vol, -dHr/Cp, UA/Vol/Cp, UA/Volc/Cp are formed once (same operations).
+// Cost: x_d = [0, target, 0], Q = diag(0, 0.01, 0) (full 3x3), r = [[1e-4]].
+struct EnvReactor {
+  static constexpr int NV = 3;
+  float qV, Tf, mdHrCp, UAVCp, Volc, Tcf, UAVcCp, tg;
+  typedef QuadFit Fit;
+  __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
+    const float* p = ro.params + 8 * rr;
+    const float Vol = p[0], Cp = p[1], dHr = p[2], UA = p[3], q = p[4];
+    Tf = p[5];
+    Tcf = p[6];
+    Volc = p[7];
+    qV = q / Vol;
+    mdHrCp = (-dHr) / Cp;
+    UAVCp = (UA / Vol) / Cp;
+    UAVcCp = (UA / Volc) / Cp;
+    tg = ro.targets[rr * nt];
+  }
+  __device__ __forceinline__ void drift(const float x[3], float u, float dx[3]) const {
+    const float Tc = x[0], T = x[1], c = x[2];
+    const float control = mtgp_clip(u, 0.0f, 300.0f);
+    const float kT = 7.2e10f * mtgp_expf((float)(-72750.0 / 8.314) / T);
+    const float dc = qV * (1.0f - c) - kT * c;
+    const float dT = (qV * (Tf - T) + (mdHrCp * kT) * c) + UAVCp * (Tc - T);
+    const float dTc = (control / Volc) * (Tcf - Tc) + UAVcCp * (T - Tc);
+    dx[0] = dTc;
+    dx[1] = dT;
+    dx[2] = dc;
+  }
+  __device__ __forceinline__ static void obs_transform(float y[3]) { (void)y; }
+  __device__ __forceinline__ static bool bad(const float* s, int n) { return any_nonfinite(s, n); }
+  __device__ __forceinline__ static Fit fit_init(bool active) { return Fit{!active, 0.0f}; }
+  __device__ __forceinline__ void fit_update(Fit& f, int k, int S, const float* ts, float u, const float x[3]) const {
+    (void)k; (void)S; (void)ts;
+    const float Q[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.01f, 0.0f, 0.0f, 0.0f, 0.0f};
+    const float e[3] = {x[0] - 0.0f, x[1] - tg, x[2] - 0.0f};
+    f.F = f.F + (quad_form<3>(e, Q) + (u * 0.0001f) * u);
+  }
+  __device__ __forceinline__ static void fit_kill(Fit& f) { f.settled = true; f.F = mtgp_qnan(); }
+  __device__ __forceinline__ static float fit_final(Fit& f, int S) { (void)S; return f.F; }
+};
+
 // store v at row `row` (wave-uniform element offset) + off (per lane): the 64-bit row base
 // stays in SGPRs, only the 32-bit lane offset is a VGPR
 __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
   float* p = arr + row;
   p[off] = v;
-}
-
-__device__ __forceinline__ bool save_incl(const float* ts, int k) {
-  const float dts = ts[1] - ts[0];
-  return !((ts[k] / dts) > (float)k);
 }
 
 // --------------------------------------------------------------------------------------
@@ -491,14 +635,15 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
 }
 
 // --------------------------------------------------------------------------------------
-// Acrobot, dynamic symbolic policy (dynamic_evaluate.py:65-118).  NA = state_size.
-// Data slots: y 0..3 | a 4..4+NA-1 | u 4+NA | targets.  Per stage the programs run in
+// Dynamic symbolic policy (dynamic_evaluate.py:65-118) on environment Env.  NA = state_size.
+// Data slots: y 0..NV-1 | a NV..NV+NA-1 | u NV+NA | targets.  Per stage the programs run in
 // the order of _drift (dyn.py:107-118): readout (y, u folded to 0) -> drift -> f_obs ->
 // state equations; at save points the save-time readout (dyn.py:101) is appended.
 // NOISE: observation noise on; the save-point observation uses ts[k] (dyn.py:99), which is
 // recomputed when it differs from the stage-0 time of that step.
-template <int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_acro_dynamic(KArgs A) {
+template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dynamic(KArgs A) {
+  constexpr int NV = Env::NV;
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
@@ -514,14 +659,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
-  ObsNoise nzc;
-  float nzv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
-  constexpr int uslot = 4 + NA;
-  // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
-  // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
-  const float pl1 = A.ro.params[4 * rr + 0], pl2 = A.ro.params[4 * rr + 1], pm1 = A.ro.params[4 * rr + 2],
-              pm2 = A.ro.params[4 * rr + 3];
+  ObsNoise<NV> nzc;
+  float nzv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+  if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
+  constexpr int uslot = NV + NA;
+  Env env;
+  env.load(A.ro, rr, A.m.n_targets);
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;  // element offset of this (individual, rollout) in a save row
 #pragma unroll
@@ -545,23 +690,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   }
   diff_mask = __builtin_amdgcn_readfirstlane(diff_mask);
 
-  float x[4], a[NA], kx[4], ka[NA], ax[4], aa[NA];
+  float x[NV], a[NA], kx[NV], ka[NA], ax[NV], aa[NA];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = A.ro.x0[rr * 4 + i];
+  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
 #pragma unroll
   for (int j = 0; j < NA; ++j) a[j] = 0.0f;
 
-  AcroFit fit = {!active, 0.0f, 0.0f, 0.0f};
+  typename Env::Fit fit = Env::fit_init(active);
   bool dead = !active;  // state frozen at +inf once the event state has been saved
   bool pending = false; // event fired at the end of the previous step
   bool prev_ok;
   {
-    float s0[4 + NA];
+    float s0[NV + NA];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) s0[i] = x[i];
+    for (int i = 0; i < NV; ++i) s0[i] = x[i];
 #pragma unroll
-    for (int j = 0; j < NA; ++j) s0[4 + j] = a[j];
-    prev_ok = !acro_bad(s0, 4 + NA);
+    for (int j = 0; j < NA; ++j) s0[NV + j] = a[j];
+    prev_ok = !Env::bad(s0, NV + NA);
   }
 
   for (int step = 0;; ++step) {
@@ -570,26 +715,23 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     bool stop = last;
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
-      float xt[4], at[NA], y[4];
+      float xt[NV], at[NA], y[NV];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
+      for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
 #pragma unroll
       for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
 #pragma unroll
-      for (int j = 0; j < NA; ++j) D.put(4 + j, at[j]);
+      for (int j = 0; j < NA; ++j) D.put(NV + j, at[j]);
       float ur[1];
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       const float u = ur[0];
-      acro_drift(acro_const(pl1, pl2, pm1, pm2), xt, u, kx);
+      env.drift(xt, u, kx);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      if (NOISE) {  // stages 1 and 2 share the time t + h/2, hence the noise draw
-        if (stage != 2) obs_noise_vec(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
-        acro_obs_apply(xt, nzv, y);
-      } else {
-        acro_f_obs(xt, y);
-      }
+      // stages 1 and 2 share the time t + h/2, hence the noise draw
+      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+      ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+      for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, u);
       run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka);
       if (stage == 0) {
@@ -599,9 +741,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
           if (NOISE) {
             const float tsk = A.ro.ts[k];
             if (__float_as_uint(tsk) != __float_as_uint(t0 + (float)step * h)) {
-              acro_obs<true>(nzc, tsk, x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
+              ctl_obs<Env, true>(nzc, tsk, x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
 #pragma unroll
-              for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+              for (int i = 0; i < NV; ++i) D.put(i, y[i]);
             }
           }
           if (JIT && diff_mask != 0) {  // the save-readout unit covers every group (equal programs give u again)
@@ -615,15 +757,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               us = (Ln.g == gi) ? t : us;
             }
           }
-          if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), us, x[0], x[1]);
+          if (!dead) env.fit_update(fit, k, S, A.ro.ts, us, x);
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR, loff, x[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR, loff, y[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
             }
             if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us);
             if (A.out.acts) {
@@ -635,8 +777,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (pending) {  // the event state has been saved: freeze at +inf (saveat fill)
           pending = false;
           dead = true;
+          if (!last) Env::fit_kill(fit);  // save points of the +inf fill follow
 #pragma unroll
-          for (int i = 0; i < 4; ++i) x[i] = kInf;
+          for (int i = 0; i < NV; ++i) x[i] = kInf;
 #pragma unroll
           for (int j = 0; j < NA; ++j) a[j] = kInf;
         }
@@ -644,30 +787,31 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (stop) break;
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
 #pragma unroll
       for (int j = 0; j < NA; ++j) aa[j] = stage_acc(stage, aa[j], ka[j]);
     }
     if (stop) break;
     if (!dead) {
-      float sn[4 + NA];
+      float sn[NV + NA];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) { x[i] = MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+      for (int i = 0; i < NV; ++i) { x[i] = MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
 #pragma unroll
-      for (int j = 0; j < NA; ++j) { a[j] = MTGP_FMAF(h6, aa[j], a[j]); sn[4 + j] = a[j]; }
-      const bool ok = !acro_bad(sn, 4 + NA);
+      for (int j = 0; j < NA; ++j) { a[j] = MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
+      const bool ok = !Env::bad(sn, NV + NA);
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
     }
   }
-  if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
-  finish_group(A, Ln, fit.F);
+  finish_group(A, Ln, Env::fit_final(fit, S));
 }
 
 // --------------------------------------------------------------------------------------
-// Acrobot, static policy (feedforward_evaluate.py:64-110).  Data slots: y 0..3 | targets.
-template <bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_acro_static(KArgs A) {
+// Static policy (feedforward_evaluate.py:64-110) on environment Env.  Data slots:
+// y 0..NV-1 | targets.
+template <class Env, bool TRAJ, bool NOISE, bool JIT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_static(KArgs A) {
+  constexpr int NV = Env::NV;
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
@@ -682,25 +826,25 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
-  ObsNoise nzc;
-  float nzv[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  if (NOISE) nzc = obs_noise_setup(A.m, A.ro, rr);
-  // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
-  // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
-  const float pl1 = A.ro.params[4 * rr + 0], pl2 = A.ro.params[4 * rr + 1], pm1 = A.ro.params[4 * rr + 2],
-              pm2 = A.ro.params[4 * rr + 3];
+  ObsNoise<NV> nzc;
+  float nzv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+  if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
+  Env env;
+  env.load(A.ro, rr, A.m.n_targets);
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;
 #pragma unroll
-  for (int t = 0; t < kDMax - 4; ++t)
-    if (t < A.m.n_targets) D.put(4 + t, A.ro.targets[rr * A.m.n_targets + t]);
+  for (int t = 0; t < kDMax - NV; ++t)
+    if (t < A.m.n_targets) D.put(NV + t, A.ro.targets[rr * A.m.n_targets + t]);
 
-  float x[4], kx[4], ax[4];
+  float x[NV], kx[NV], ax[NV];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) x[i] = A.ro.x0[rr * 4 + i];
-  AcroFit fit = {!active, 0.0f, 0.0f, 0.0f};
+  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+  typename Env::Fit fit = Env::fit_init(active);
   bool dead = !active, pending = false;
-  bool prev_ok = !acro_bad(x, 4);
+  bool prev_ok = !Env::bad(x, NV);
 
   for (int step = 0;; ++step) {
     const bool last = step == n_steps;
@@ -708,44 +852,41 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     bool stop = last;
 #pragma unroll 1
     for (int stage = 0; stage < 4; ++stage) {
-      float xt[4], y[4];
+      float xt[NV], y[NV];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
+      for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      if (NOISE) {  // stages 1 and 2 share the time t + h/2, hence the noise draw
-        if (stage != 2) obs_noise_vec(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
-        acro_obs_apply(xt, nzv, y);
-      } else {
-        acro_f_obs(xt, y);
-      }
+      // stages 1 and 2 share the time t + h/2, hence the noise draw
+      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+      ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+      for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       float ur[1];
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // ff.py:106-107 (:97 at saves)
       float u = ur[0];
-      acro_drift(acro_const(pl1, pl2, pm1, pm2), xt, u, kx);
+      env.drift(xt, u, kx);
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
           if (NOISE) {
             const float tsk = A.ro.ts[k];
             if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
-              acro_obs<true>(nzc, tsk, x, y);
+              ctl_obs<Env, true>(nzc, tsk, x, y);
 #pragma unroll
-              for (int i = 0; i < 4; ++i) D.put(i, y[i]);
+              for (int i = 0; i < NV; ++i) D.put(i, y[i]);
               run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
               u = ur[0];
             }
           }
-          if (!dead) acro_fit_update(fit, k, S, save_incl(A.ro.ts, k), u, x[0], x[1]);
+          if (!dead) env.fit_update(fit, k, S, A.ro.ts, u, x);
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.xs, ((size_t)k * 4 + i) * PR, loff, x[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i]);
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < 4; ++i) store_row(A.out.ys, ((size_t)k * 4 + i) * PR, loff, y[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
             }
             if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u);
           }
@@ -753,26 +894,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (pending) {
           pending = false;
           dead = true;
+          if (!last) Env::fit_kill(fit);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) x[i] = kInf;
+          for (int i = 0; i < NV; ++i) x[i] = kInf;
         }
         if (!TRAJ && __all(fit.settled || dead)) stop = true;
         if (stop) break;
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
     if (stop) break;
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
-      const bool ok = !acro_bad(x, 4);
+      for (int i = 0; i < NV; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
+      const bool ok = !Env::bad(x, NV);
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
     }
   }
-  if (!fit.settled) { fit.settled = true; fit.F = (float)S + fit.c0incl; }
-  finish_group(A, Ln, fit.F);
+  finish_group(A, Ln, Env::fit_final(fit, S));
 }
 
 // --------------------------------------------------------------------------------------
@@ -1269,6 +1410,53 @@ int launch_timed(F&& launch, hipStream_t s) {
 
 }  // namespace
 
+// the eight (TRAJ, NOISE, JIT) variants of one control kernel
+#define MTGP_CTL_VARIANTS(KERNEL, ...)                                                                   \
+  do {                                                                                                  \
+    if (jit) {                                                                                          \
+      if (noise) {                                                                                      \
+        if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, true>), grid, block, 0, s, A);    \
+        else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, true>), grid, block, 0, s, A);        \
+      } else {                                                                                          \
+        if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, true>), grid, block, 0, s, A);   \
+        else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, true>), grid, block, 0, s, A);       \
+      }                                                                                                 \
+    } else if (noise) {                                                                                 \
+      if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, false>), grid, block, 0, s, A);     \
+      else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, false>), grid, block, 0, s, A);         \
+    } else {                                                                                            \
+      if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, false>), grid, block, 0, s, A);    \
+      else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, false>), grid, block, 0, s, A);        \
+    }                                                                                                   \
+  } while (0)
+
+template <class Env, int NA>
+int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
+  return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
+}
+
+// dynamic / static evaluator on environment Env: shape checks, then the kernel variant
+template <class Env>
+int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, bool jit, bool noise, bool traj,
+               dim3 grid, dim3 block, hipStream_t s) {
+  constexpr int NV = Env::NV;
+  if (model->n_var != NV || model->n_obs != NV || model->n_control != 1 || !ro->params) return MTGP_ERR_ARG;
+  if (model->n_targets < 0 || (model->n_targets > 0 && !ro->targets)) return MTGP_ERR_ARG;
+  if (model->env != MTGP_ENV_ACROBOT && model->n_targets < 1) return MTGP_ERR_ARG;  // x_d needs the target
+  if (model->model == MTGP_MODEL_STATIC) {
+    if (NV + model->n_targets > kDMax) return MTGP_ERR_ARG;
+    return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_static, Env); }, s);
+  }
+  if (NV + model->state_size + 1 + model->n_targets > kDMax) return MTGP_ERR_ARG;
+  switch (model->state_size) {
+    case 1: return launch_dyn<Env, 1>(A, jit, noise, traj, grid, block, s);
+    case 2: return launch_dyn<Env, 2>(A, jit, noise, traj, grid, block, s);
+    case 3: return launch_dyn<Env, 3>(A, jit, noise, traj, grid, block, s);
+    default: return MTGP_ERR_ARG;
+  }
+}
+
+
 extern "C" {
 
 int mtgp_abi_version(void) { return MTGP_ABI_VERSION; }
@@ -1501,60 +1689,18 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
   const bool noise = rollouts->obs_keys != nullptr;
-  if (noise && (!rollouts->obs_w || model->model == MTGP_MODEL_SR || model->n_obs != 4)) return MTGP_ERR_ARG;
+  if (noise && (!rollouts->obs_w || model->model == MTGP_MODEL_SR)) return MTGP_ERR_ARG;
   if (model->prng_impl != MTGP_PRNG_THREEFRY_ORIGINAL && model->prng_impl != MTGP_PRNG_THREEFRY_PARTITIONABLE)
     return MTGP_ERR_ARG;
-  if (model->model == MTGP_MODEL_ACROBOT_DYNAMIC) {
-    if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;
-    if (model->n_targets < 0 || 4 + model->state_size + 1 + model->n_targets > kDMax) return MTGP_ERR_ARG;
-    if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
-#define MTGP_DYN(NA)                                                                                      \
-  case NA:                                                                                                \
-    return launch_timed([&] {                                                                             \
-      if (jit) {                                                                                          \
-        if (noise) {                                                                                      \
-          if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true, true>), grid, block, 0, s, A);     \
-          else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true, true>), grid, block, 0, s, A);         \
-        } else {                                                                                          \
-          if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false, true>), grid, block, 0, s, A);    \
-          else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false, true>), grid, block, 0, s, A);        \
-        }                                                                                                 \
-      } else if (noise) {                                                                                 \
-        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, true, false>), grid, block, 0, s, A);      \
-        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, true, false>), grid, block, 0, s, A);          \
-      } else {                                                                                            \
-        if (traj) hipLaunchKernelGGL((k_acro_dynamic<NA, true, false, false>), grid, block, 0, s, A);     \
-        else hipLaunchKernelGGL((k_acro_dynamic<NA, false, false, false>), grid, block, 0, s, A);         \
-      }                                                                                                   \
-    }, s);
-    switch (model->state_size) {
-      MTGP_DYN(1)
-      MTGP_DYN(2)
-      MTGP_DYN(3)
+  if (model->model == MTGP_MODEL_DYNAMIC || model->model == MTGP_MODEL_STATIC) {
+    switch (model->env) {
+      case MTGP_ENV_ACROBOT: return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
+      case MTGP_ENV_HARMONIC_OSCILLATOR:
+        return launch_ctl<EnvHarmonic>(A, model, rollouts, jit, noise, traj, grid, block, s);
+      case MTGP_ENV_STIRRED_TANK_REACTOR:
+        return launch_ctl<EnvReactor>(A, model, rollouts, jit, noise, traj, grid, block, s);
       default: return MTGP_ERR_ARG;
     }
-#undef MTGP_DYN
-  } else if (model->model == MTGP_MODEL_ACROBOT_STATIC) {
-    if (model->n_var != 4 || model->n_obs != 4 || model->n_control != 1 || !rollouts->params) return MTGP_ERR_ARG;
-    if (model->n_targets < 0 || 4 + model->n_targets > kDMax) return MTGP_ERR_ARG;
-    if (model->n_targets > 0 && !rollouts->targets) return MTGP_ERR_ARG;
-    return launch_timed([&] {
-      if (jit) {
-        if (noise) {
-          if (traj) hipLaunchKernelGGL((k_acro_static<true, true, true>), grid, block, 0, s, A);
-          else hipLaunchKernelGGL((k_acro_static<false, true, true>), grid, block, 0, s, A);
-        } else {
-          if (traj) hipLaunchKernelGGL((k_acro_static<true, false, true>), grid, block, 0, s, A);
-          else hipLaunchKernelGGL((k_acro_static<false, false, true>), grid, block, 0, s, A);
-        }
-      } else if (noise) {
-        if (traj) hipLaunchKernelGGL((k_acro_static<true, true, false>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_acro_static<false, true, false>), grid, block, 0, s, A);
-      } else {
-        if (traj) hipLaunchKernelGGL((k_acro_static<true, false, false>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_acro_static<false, false, false>), grid, block, 0, s, A);
-      }
-    }, s);
   } else if (model->model == MTGP_MODEL_SR) {
     if (!rollouts->ys_true) return MTGP_ERR_ARG;
     if (model->n_var > 4) {

@@ -287,6 +287,7 @@ class DeviceEngine:
         m.prog_state, m.prog_readout = roles["prog_state"], roles["prog_readout"]
         m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
         m.prng_impl = d.get("prng_impl", 0)
+        m.env = d.get("env", nat.ENV_ACROBOT)
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
@@ -306,7 +307,7 @@ class DeviceEngine:
                 res["xs"] = torch.empty((S, m.n_var, PR), dtype=torch.float32, device=dev)
                 out.xs = res["xs"].data_ptr()
             else:
-                for name, c in (("xs", 4), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size)):
+                for name, c in (("xs", m.n_var), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size)):
                     if c > 0:
                         res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
                         setattr(out, name, res[name].data_ptr())

@@ -41,6 +41,93 @@ class Acrobot:
         one = np.ones(batch_size, dtype=np.float32)
         return one, one.copy(), one.copy(), one.copy()
 
+    def obs_matrix(self) -> np.ndarray:
+        """W = obs_noise * eye(n_obs) (acrobot.py:49), float32."""
+        return (np.float32(self.obs_noise) * np.eye(self.n_obs, dtype=np.float32)).astype(np.float32)
+
+
+class HarmonicOscillator:
+    """harmonic_oscillator.py:8-80.  n_var 2, n_control 1, n_targets 1, n_obs 2 (default).
+
+    The kernel functor (mtgp_kernels.hip EnvHarmonic) restates drift A x + b u,
+    A = [[0, 1], [-omega, -zeta]], the quadratic cost with q = r = 0.5 and cond_fn_nan."""
+
+    def __init__(self, process_noise: float, obs_noise: float, n_obs: int = 2):
+        self.n_dim = 1
+        self.n_var = 2
+        self.n_control = 1
+        self.n_targets = 1
+        self.n_obs = n_obs
+        self.process_noise = process_noise
+        self.obs_noise = obs_noise
+        self.mu0 = np.zeros(self.n_var, np.float32)
+        self.P0 = (np.eye(self.n_var) * np.array([3.0, 1.0])).astype(np.float32)
+        self.q = self.r = 0.5
+
+    def sample_init_states(self, batch_size: int, rng) -> Tuple[np.ndarray, np.ndarray]:
+        """harmonic_oscillator.py:23-27: x0 = mu0 + N(0, 1) @ P0, targets ~ U(-3, 3)."""
+        rng = np.random.default_rng(rng)
+        x0 = (self.mu0 + rng.standard_normal((batch_size, self.n_var)).astype(np.float32) @ self.P0).astype(np.float32)
+        targets = rng.uniform(-3, 3, size=(batch_size, self.n_targets)).astype(np.float32)
+        return x0, targets
+
+    def sample_params(self, batch_size: int, mode, ts, rng) -> Tuple[np.ndarray, np.ndarray]:
+        """harmonic_oscillator.py:29-31 ("Constant": omega 1, zeta 0) and :32-34 ("Different":
+        omega ~ U(0, 2), zeta ~ U(0, 1.5)).  The time-varying modes give [R, S] arrays that the
+        reference's own A = [[0, 1], [-omega, -zeta]] cannot take; they are not supported."""
+        if mode == "Constant":
+            return np.ones(batch_size, np.float32), np.zeros(batch_size, np.float32)
+        if mode == "Different":
+            rng = np.random.default_rng(rng)
+            return (rng.uniform(0.0, 2.0, batch_size).astype(np.float32),
+                    rng.uniform(0.0, 1.5, batch_size).astype(np.float32))
+        raise NotImplementedError(f"mode {mode!r}")
+
+    def obs_matrix(self) -> np.ndarray:
+        """W = obs_noise * eye(n_obs) (harmonic_oscillator.py:66)."""
+        return (np.float32(self.obs_noise) * np.eye(self.n_obs, dtype=np.float32)).astype(np.float32)
+
+
+class StirredTankReactor:
+    """reactor.py:7-81.  State (Tc, T, c), n_control 1 (coolant flow, clipped to [0, 300]),
+    n_targets 1 (reactor temperature), n_obs 3 (default).  Kernel functor: EnvReactor."""
+
+    def __init__(self, process_noise: float, obs_noise: float, n_obs: int = 3, n_targets: int = 1):
+        self.process_noise = process_noise
+        self.obs_noise = obs_noise
+        self.n_var = 3
+        self.n_control = 1
+        self.n_dim = 1
+        self.n_targets = n_targets
+        self.n_obs = n_obs
+        self.init_lower_bounds = np.array([275, 350, 0.5], np.float32)
+        self.init_upper_bounds = np.array([300, 375, 1.0], np.float32)
+
+    def sample_init_states(self, batch_size: int, rng) -> Tuple[np.ndarray, np.ndarray]:
+        """reactor.py:71-75: x0 ~ U(lower, upper), targets ~ U(400, 500)."""
+        rng = np.random.default_rng(rng)
+        x0 = rng.uniform(self.init_lower_bounds, self.init_upper_bounds,
+                         size=(batch_size, self.n_var)).astype(np.float32)
+        targets = rng.uniform(400, 500, size=(batch_size, self.n_targets)).astype(np.float32)
+        return x0, targets
+
+    def sample_params(self, batch_size: int, mode, ts, rng):
+        """reactor.py:46-69 -> (Vol, Cp, dHr, UA, q, Tf, Tcf, Volc), each [batch]."""
+        if mode == "Constant":
+            vals = (100.0, 239.0, -5.0e4, 5.0e4, 100.0, 300.0, 300.0, 20.0)
+            return tuple(np.full(batch_size, v, np.float32) for v in vals)
+        if mode == "Different":
+            rng = np.random.default_rng(rng)
+            bounds = ((75, 150), (200, 350), (-55000, -45000), (25000, 75000), (75, 125), (300, 350), (250, 300),
+                      (10, 30))
+            return tuple(rng.uniform(lo, hi, batch_size).astype(np.float32) for lo, hi in bounds)
+        raise NotImplementedError(f"mode {mode!r}")
+
+    def obs_matrix(self) -> np.ndarray:
+        """W = obs_noise * eye(n_obs) * [15, 15, 0.1][:n_obs] (reactor.py:43), float32 ops."""
+        w = np.float32(self.obs_noise) * np.eye(self.n_obs, dtype=np.float32)
+        return (w * np.array([15, 15, 0.1], np.float32)[: self.n_obs]).astype(np.float32)
+
 
 class VanDerPolOscillator:
     """SR_environments/vd_pol_oscillator.py:6-29 (mu = 1)."""
@@ -104,7 +191,8 @@ def ground_truth(env, x0: np.ndarray, ts: np.ndarray, h: float = 1e-3) -> np.nda
     return out.astype(np.float32)
 
 
-def control_data(env, batch_size: int, dt: float, T: float, seed: int = 1, n_steps: int = None):
+def control_data(env, batch_size: int, dt: float, T: float, seed: int = 1, n_steps: int = None,
+                 mode: str = "Constant"):
     """The notebooks' get_data (DynamicPolicy.ipynb cell 2) with numpy RNG:
     (x0, ts, targets, process_noise_keys, obs_noise_keys, params).  The noise keys are
     distinct JAX-format keys (split of PRNGKey(seed)); see jax_control_data for the
@@ -116,7 +204,7 @@ def control_data(env, batch_size: int, dt: float, T: float, seed: int = 1, n_ste
     else:
         ts = (np.arange(n_steps + 1, dtype=np.float32) * np.float32(dt)).astype(np.float32)
     _, k1, k2 = prng.split(prng.PRNGKey(seed), 3)
-    params = env.sample_params(batch_size, "Constant", ts, rng)
+    params = env.sample_params(batch_size, mode, ts, rng)
     return x0, ts, targets, prng.split(k1, batch_size), prng.split(k2, batch_size), params
 
 

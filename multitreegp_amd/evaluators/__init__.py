@@ -48,11 +48,11 @@ def _check_solver(solver, controller):
             raise NotImplementedError(f"stepsize_controller {controller!r}: only ConstantStepSize is implemented")
 
 
-def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
+def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool = True) -> Tuple[int, int, int]:
     """Map (ts, dt0) to (n_steps, save_every, n_save) for save points on step ends.
 
-    Also checks the Acrobot fitness-mask regularity ts[k]/(ts[1]-ts[0]) in (k-1, k+1] that the
-    kernel's one-pass fitness relies on (acrobot.py:82)."""
+    With acrobot_mask, also checks the Acrobot fitness-mask regularity ts[k]/(ts[1]-ts[0]) in
+    (k-1, k+1] that the kernel's one-pass fitness relies on (acrobot.py:82)."""
     ts = np.asarray(ts, dtype=np.float32)
     S = int(ts.shape[0])
     if S < 2:
@@ -66,7 +66,7 @@ def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, 
         raise ValueError("ts must be uniformly spaced (fixed-step RK4 saves on step ends)")
     ratio = ts / np.float32(ts[1] - ts[0])
     k = np.arange(S, dtype=np.float32)
-    if not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
+    if acrobot_mask and not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
         raise NotImplementedError("ts with an offset start (ts[0] != 0 style masks) is not supported")
     n_steps = (S - 1) * save_every
     if n_steps > max_steps:
@@ -131,15 +131,29 @@ class _TreeOnly:
         return [(t, self._d, 0) for t in range(self._t)], {}
 
 
+# environments with a kernel functor (mtgp.h MTGP_ENV_*): class name -> (env id, n_var, n_params)
+ENVIRONMENTS = {
+    "Acrobot": (nat.ENV_ACROBOT, 4, 4),                          # acrobot.py:7-87
+    "HarmonicOscillator": (nat.ENV_HARMONIC_OSCILLATOR, 2, 2),   # harmonic_oscillator.py:8-80
+    "StirredTankReactor": (nat.ENV_STIRRED_TANK_REACTOR, 3, 8),  # reactor.py:7-81
+}
+
+
 class _ControlEvaluator(_CandidateAPI):
     max_fitness = 1e4
 
     def __init__(self, env, dt0: float, solver=None, max_steps: int = 16 ** 4, stepsize_controller=None):
         _check_solver(solver if solver is not None else RK4(), stepsize_controller)
-        if type(env).__name__ != "Acrobot":
-            raise NotImplementedError(f"environment {type(env).__name__}: only Acrobot is on the MI355X path")
-        if env.n_obs != 4:
-            raise NotImplementedError("Acrobot with n_obs != 4")
+        name = type(env).__name__
+        if name not in ENVIRONMENTS:
+            # CartPole / Acrobot2 / ChangingHarmonicOscillator / HarmonicOscillator2 have no
+            # cond_fn_nan, which the reference evaluators require (dyn.py:94, ff.py:91)
+            raise NotImplementedError(f"environment {name}: the MI355X path runs {sorted(ENVIRONMENTS)}")
+        self.env_id, n_var, self.n_params = ENVIRONMENTS[name]
+        if env.n_obs != n_var:
+            raise NotImplementedError(f"{name} with n_obs != {n_var} (C = I only)")
+        if env.n_control != 1 or (self.env_id != nat.ENV_ACROBOT and env.n_targets != 1):
+            raise NotImplementedError(f"{name}: one control and one target only")
         self.env = env
         self.obs_size = env.n_obs
         self.control_size = env.n_control
@@ -158,12 +172,22 @@ class _ControlEvaluator(_CandidateAPI):
         x0, ts, targets, _pk, obs_keys, params = data
         x0 = _f32(x0)
         R = x0.shape[0]
-        if x0.shape[1] != 4:
-            raise ValueError("Acrobot x0 must be [R, 4]")
-        prm = np.stack([_f32(p).reshape(R) for p in params], axis=1) if params is not None else np.ones((R, 4), np.float32)
+        nv = self.env.n_var
+        if x0.ndim != 2 or x0.shape[1] != nv:
+            raise ValueError(f"{type(self.env).__name__} x0 must be [R, {nv}]")
+        if params is None:
+            raise ValueError("params tuple required (env.sample_params)")
+        if len(params) != self.n_params:
+            raise ValueError(f"{type(self.env).__name__} takes {self.n_params} parameters per rollout")
+        for p in params:
+            if np.asarray(p).size != R:
+                raise NotImplementedError("time-varying parameters ([R, S]: 'Switch'/'Decay' modes) are not supported")
+        prm = np.stack([_f32(p).reshape(R) for p in params], axis=1)
         tg = _f32(targets).reshape(R, -1)
-        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
-        out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R,
+        if tg.shape[1] != self.env.n_targets:
+            raise ValueError(f"targets must be [R, {self.env.n_targets}]")
+        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps, acrobot_mask=self.env_id == nat.ENV_ACROBOT)
+        out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R, n_var=nv, env=self.env_id,
                    n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code())
         obs_noise = float(getattr(self.env, "obs_noise", 0.0))
         if obs_noise != 0.0:
@@ -171,8 +195,9 @@ class _ControlEvaluator(_CandidateAPI):
             if keys.shape != (R, 2):
                 raise ValueError(f"obs_noise_keys must be uint32 [R, 2] key data, got {keys.shape}")
             out["obs_keys"] = keys
-            # W = obs_noise * eye(n_obs) (acrobot.py:49), formed in float32 like the reference
-            out["obs_w"] = (np.float32(obs_noise) * np.eye(self.obs_size, dtype=np.float32)).astype(np.float32)
+            # W = obs_noise * eye(n_obs) (acrobot.py:49, harmonic_oscillator.py:66), times the
+            # per-channel scale for the reactor (reactor.py:43), formed in float32 like the reference
+            out["obs_w"] = self.env.obs_matrix()
         return out
 
 

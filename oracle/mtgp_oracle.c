@@ -100,11 +100,15 @@ typedef struct {
   int32_t n_steps, save_every, n_save;
   float h, max_fitness, parsimony;
   int32_t prng_impl; /* mtgp_prng.h: 0 threefry original layout, 1 partitionable */
+  int32_t env;       /* control models: 0 Acrobot, 1 HarmonicOscillator, 2 StirredTankReactor */
 } OrModel;
+
+enum { ENV_ACROBOT = 0, ENV_HARMONIC = 1, ENV_REACTOR = 2 };
 
 typedef struct {
   const float* x0;      /* [R, n_var] */
-  const float* params;  /* [R, 4] l1 l2 m1 m2 */
+  const float* params;  /* [R, n_params]: Acrobot (l1, l2, m1, m2), HarmonicOscillator (omega,
+                           zeta), StirredTankReactor (Vol, Cp, dHr, UA, q, Tf, Tcf, Volc) */
   const float* targets; /* [R, n_targets] */
   const float* ts;      /* [n_save] */
   const float* ys_true; /* SR: [R, n_save, n_var] (reference layout) */
@@ -119,46 +123,50 @@ typedef struct {
   int N;
   OrLib lib;
   const float* target;
-  float l1, l2, m1, m2;
+  const float* prm;    /* this rollout's environment parameters */
   const uint32_t* key; /* this rollout's obs_noise_key or NULL */
   const float* W;
 } OrCtx;
 
-/* EnvironmentBase.f_obs (cbase.py:43-48) with C = I (acrobot.py:48):
+/* EnvironmentBase.f_obs (cbase.py:43-48) with C = eye(n_var)[:n_obs] (acrobot.py:48,
+ * harmonic_oscillator.py:65, reactor.py:42):
  *   out = C@x + normal(fold_in(key, bitcast_i32(t)), (n_obs,)) @ W
  * matrix products summed in index order; without a key (obs_noise = 0) the noise term is
  * +0.  Then Acrobot wraps out[0:2] (acrobot.py:29-32). */
-static void acro_f_obs(const OrCtx* c, float t, const float* x, float* y) {
-  float nz[4];
+static void ctl_f_obs(const OrCtx* c, float t, const float* x, float* y) {
+  const int nv = c->m->n_var, no = c->m->n_obs;
+  float nz[OR_MAX_D];
   if (c->key) {
-    float n[4];
-    mtgp_obs_normals(c->key[0], c->key[1], t, 4, c->m->prng_impl, n);
-    for (int j = 0; j < 4; ++j) {
-      float s = n[0] * c->W[0 * 4 + j];
-      for (int i = 1; i < 4; ++i) s = s + n[i] * c->W[i * 4 + j];
+    float n[OR_MAX_D];
+    mtgp_obs_normals(c->key[0], c->key[1], t, no, c->m->prng_impl, n);
+    for (int j = 0; j < no; ++j) {
+      float s = n[0] * c->W[0 * no + j];
+      for (int i = 1; i < no; ++i) s = s + n[i] * c->W[i * no + j];
       nz[j] = s;
     }
   } else {
-    for (int j = 0; j < 4; ++j) nz[j] = 0.0f;
+    for (int j = 0; j < no; ++j) nz[j] = 0.0f;
   }
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < no; ++i) {
     float s = 0.0f;
     int first = 1;
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < nv; ++j) {
       const float term = (i == j ? 1.0f : 0.0f) * x[j];
       if (first) { s = term; first = 0; } else s = s + term;
     }
     y[i] = s + nz[i];
   }
-  y[0] = mtgp_wrap_angle(y[0]);
-  y[1] = mtgp_wrap_angle(y[1]);
+  if (c->m->env == ENV_ACROBOT) {
+    y[0] = mtgp_wrap_angle(y[0]);
+    y[1] = mtgp_wrap_angle(y[1]);
+  }
 }
 
 /* Acrobot.drift (acrobot.py:51-72), evaluation order of the Python source. */
 static void acro_drift(const OrCtx* c, const float* st, float u_raw, float* dx) {
   const float control = mtgp_clip1(u_raw);
   const float th1 = st[0], th2 = st[1], thd1 = st[2], thd2 = st[3];
-  const float l1 = c->l1, l2 = c->l2, m1 = c->m1, m2 = c->m2;
+  const float l1 = c->prm[0], l2 = c->prm[1], m1 = c->prm[2], m2 = c->prm[3];
   const float lc1 = 0.5f * l1, lc2 = 0.5f * l2;
   const float moi1 = 1.0f, moi2 = 1.0f, g = 9.81f;
   (void)l2;
@@ -177,6 +185,41 @@ static void acro_drift(const OrCtx* c, const float* st, float u_raw, float* dx) 
   dx[3] = th2acc;
 }
 
+/* HarmonicOscillator.drift (harmonic_oscillator.py:58-69): A@state + b@args with
+ * A = [[0, 1], [-omega, -zeta]], b = [[0], [1]], each product summed in index order. */
+static void ho_drift(const OrCtx* c, const float* x, float u, float* dx) {
+  const float omega = c->prm[0], zeta = c->prm[1];
+  const float A[2][2] = {{0.0f, 1.0f}, {-omega, -zeta}};
+  const float b[2] = {0.0f, 1.0f};
+  for (int i = 0; i < 2; ++i) dx[i] = (A[i][0] * x[0] + A[i][1] * x[1]) + b[i] * u;
+}
+
+/* StirredTankReactor.drift (reactor.py:60-69), evaluation order of the Python source.
+ * k(T) = k0 * exp(-Ea / R / T) with -Ea/R formed in Python float64 (an int over a float)
+ * and rounded to f32 as a weak-typed scalar; k0 = f32(7.2e10).  The clipped `state` of
+ * reactor.py:64 is never read (dc uses the unclipped c). */
+#define REACTOR_MEAR_F ((float)(-72750.0 / 8.314))
+#define REACTOR_K0_F 7.2e10f
+static void reactor_drift(const OrCtx* c, const float* x, float u, float* dx) {
+  const float Vol = c->prm[0], Cp = c->prm[1], dHr = c->prm[2], UA = c->prm[3], q = c->prm[4], Tf = c->prm[5],
+              Tcf = c->prm[6], Volc = c->prm[7];
+  const float Tc = x[0], T = x[1], cc = x[2];
+  const float control = mtgp_clip(u, 0.0f, 300.0f);
+  const float kT = REACTOR_K0_F * mtgp_expf(REACTOR_MEAR_F / T);
+  const float dc = (q / Vol) * (1.0f - cc) - kT * cc;
+  const float dT = (q / Vol) * (Tf - T) + ((-dHr) / Cp) * kT * cc + ((UA / Vol) / Cp) * (Tc - T);
+  const float dTc = (control / Volc) * (Tcf - Tc) + ((UA / Volc) / Cp) * (T - Tc);
+  dx[0] = dTc;
+  dx[1] = dT;
+  dx[2] = dc;
+}
+
+static void env_drift(const OrCtx* c, const float* x, float u, float* dx) {
+  if (c->m->env == ENV_HARMONIC) ho_drift(c, x, u, dx);
+  else if (c->m->env == ENV_REACTOR) reactor_drift(c, x, u, dx);
+  else acro_drift(c, x, u, dx);
+}
+
 static float tree_eval(const OrCtx* c, int t, const float* data, int n_data) {
   return oracle_eval_tree(c->cand + (size_t)t * c->N * 4, c->N, c->lib.n_funcs, c->lib.var_start, c->lib.fn,
                           data, n_data);
@@ -186,31 +229,31 @@ static float tree_eval(const OrCtx* c, int t, const float* data, int n_data) {
 static void dyn_rhs(const OrCtx* c, float t, const float* s, float* ds) {
   const OrModel* m = c->m;
   const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
-  const int D = no + na + nu + nt;
-  float y[4], data[OR_MAX_D], u[8];
-  acro_f_obs(c, t, s, y);
+  const int D = no + na + nu + nt, nv = m->n_var;
+  float y[OR_MAX_D], data[OR_MAX_D], u[8];
+  ctl_f_obs(c, t, s, y);
   /* readout sees [0_obs, a, 0_u, target] */
   for (int i = 0; i < D; ++i) data[i] = 0.0f;
-  for (int i = 0; i < na; ++i) data[no + i] = s[4 + i];
+  for (int i = 0; i < na; ++i) data[no + i] = s[nv + i];
   for (int i = 0; i < nt; ++i) data[no + na + nu + i] = c->target[i];
   for (int j = 0; j < nu; ++j) u[j] = tree_eval(c, na + j, data, D);
-  acro_drift(c, s, u[0], ds);
+  env_drift(c, s, u[0], ds);
   /* state equation sees [y, a, u, target] */
   for (int i = 0; i < no; ++i) data[i] = y[i];
   for (int j = 0; j < nu; ++j) data[no + na + j] = u[j];
-  for (int i = 0; i < na; ++i) ds[4 + i] = tree_eval(c, i, data, D);
+  for (int i = 0; i < na; ++i) ds[nv + i] = tree_eval(c, i, data, D);
 }
 
 /* feedforward_evaluate._drift (ff.py:104-110) */
 static void ff_rhs(const OrCtx* c, float t, const float* s, float* ds) {
   const OrModel* m = c->m;
   const int no = m->n_obs, nt = m->n_targets;
-  float y[4], data[OR_MAX_D];
-  acro_f_obs(c, t, s, y);
+  float y[OR_MAX_D], data[OR_MAX_D];
+  ctl_f_obs(c, t, s, y);
   for (int i = 0; i < no; ++i) data[i] = y[i];
   for (int i = 0; i < nt; ++i) data[no + i] = c->target[i];
   const float u = tree_eval(c, 0, data, no + nt);
-  acro_drift(c, s, u, ds);
+  env_drift(c, s, u, ds);
 }
 
 /* SR_evaluator._drift (sr.py:85-88) */
@@ -225,14 +268,15 @@ static void rhs(const OrCtx* c, float t, const float* s, float* ds) {
   else sr_rhs(c, t, s, ds);
 }
 
-static int state_dim(const OrModel* m) { return m->model == 1 ? 4 + m->state_size : m->n_var; }
+static int state_dim(const OrModel* m) { return m->model == 1 ? m->n_var + m->state_size : m->n_var; }
 
 /* diffrax.Event(cond_fn) with a float condition: +1 valid, -1 terminate. */
 static float cond_fn(const OrModel* m, const float* s) {
   const int n = state_dim(m);
   int bad = 0;
   for (int i = 0; i < n; ++i) bad |= !mtgp_isfinite(s[i]);
-  if (m->model != 3) { /* acrobot.py:86-87 */
+  if (m->model != 3 && m->env == ENV_ACROBOT) { /* acrobot.py:86-87 (the others: any inf/NaN only,
+                                                   harmonic_oscillator.py:79-80, reactor.py:80-81) */
     bad |= (mtgp_isnan(s[2]) ? 0 : (MTGP_FABSF(s[2]) > MTGP_8PI_F));
     bad |= (mtgp_isnan(s[3]) ? 0 : (MTGP_FABSF(s[3]) > MTGP_18PI_F));
   }
@@ -299,6 +343,52 @@ static float acro_fitness(const float* xs, const float* us, const float* ts, int
   return (float)(fs + (fs == 0) * S) + cs;
 }
 
+/* HarmonicOscillator.fitness_function (harmonic_oscillator.py:71-77) on full arrays:
+ * x_d = [target, 0], u_d = -pinv(b) @ A @ x_d with pinv(b) = [[0, 1]] taken exact (XLA's SVD
+ * pinv of b is not restated: parity unpinned), costs (x - x_d)^T Q (x - x_d) + (u - u_d) R
+ * (u - u_d) with Q = [[q, 0], [0, 0]], R = [[r]], q = r = 0.5; every matrix product is the
+ * literal left-to-right index-order sum (zeros included), the sum over time sequential. */
+static float quad_form(const float* e, const float* Q, int n) {
+  float out = 0.0f;
+  for (int j = 0; j < n; ++j) {
+    float v = e[0] * Q[0 * n + j];
+    for (int i = 1; i < n; ++i) v = v + e[i] * Q[i * n + j];
+    out = (j == 0) ? v * e[0] : out + v * e[j];
+  }
+  return out;
+}
+
+static float ho_u_target(const float* prm, float tg) {
+  const float A[2][2] = {{0.0f, 1.0f}, {-prm[0], -prm[1]}};
+  const float nb[2] = {-0.0f, -1.0f}; /* -pinv(b) */
+  const float M0 = nb[0] * A[0][0] + nb[1] * A[1][0], M1 = nb[0] * A[0][1] + nb[1] * A[1][1];
+  return M0 * tg + M1 * 0.0f;
+}
+
+static float ho_fitness(const float* xs, const float* us, const float* prm, float tg, int S) {
+  const float Q[4] = {0.5f, 0.0f, 0.0f, 0.0f}, r = 0.5f;
+  const float ud = ho_u_target(prm, tg);
+  float cs = 0.0f;
+  for (int k = 0; k < S; ++k) {
+    const float e[2] = {xs[2 * k + 0] - tg, xs[2 * k + 1] - 0.0f};
+    const float du = us[k] - ud;
+    cs = cs + (quad_form(e, Q, 2) + (du * r) * du);
+  }
+  return cs;
+}
+
+/* StirredTankReactor.fitness_function (reactor.py:73-78): x_d = [0, target, 0],
+ * Q = diag(0, 0.01, 0) (full 3x3), r = [[0.0001]]. */
+static float reactor_fitness(const float* xs, const float* us, float tg, int S) {
+  const float Q[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.01f, 0.0f, 0.0f, 0.0f, 0.0f}, r = 0.0001f;
+  float cs = 0.0f;
+  for (int k = 0; k < S; ++k) {
+    const float e[3] = {xs[3 * k + 0] - 0.0f, xs[3 * k + 1] - tg, xs[3 * k + 2] - 0.0f};
+    cs = cs + (quad_form(e, Q, 3) + (us[k] * r) * us[k]);
+  }
+  return cs;
+}
+
 /* pairwise (xor-butterfly) sum over padded chunks of 64 -- the kernel's reduction order */
 static float pairwise_sum(const float* v, int R) {
   const int nch = (R + 63) / 64;
@@ -345,12 +435,9 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
     float* fr = (float*)malloc(sizeof(float) * (size_t)R);
     for (int r = 0; r < R; ++r) {
       c.target = ro->targets ? ro->targets + (size_t)r * m->n_targets : NULL;
-      if (ro->params) {
-        c.l1 = ro->params[4 * r + 0]; c.l2 = ro->params[4 * r + 1];
-        c.m1 = ro->params[4 * r + 2]; c.m2 = ro->params[4 * r + 3];
-      } else {
-        c.l1 = c.l2 = c.m1 = c.m2 = 1.0f;
-      }
+      static const float ones[8] = {1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f};
+      const int npar = m->env == ENV_HARMONIC ? 2 : (m->env == ENV_REACTOR ? 8 : 4);
+      c.prm = ro->params ? ro->params + (size_t)r * npar : ones;
       float s0[OR_MAX_S];
       for (int i = 0; i < dim; ++i) s0[i] = 0.0f;
       for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
@@ -376,16 +463,17 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
             for (int d = 0; d < m->n_var; ++d) xs[(base + k) * m->n_var + d] = saved[(size_t)k * dim + d];
       } else {
         /* observations at the saved points (lax.scan f_obs) and the readout/policy */
-        float yk[4], data[OR_MAX_D];
-        float xk[4];
+        const int nv = m->n_var;
+        float yk[OR_MAX_D], data[OR_MAX_D];
+        float xk[OR_MAX_D];
         for (int k = 0; k < S; ++k) {
-          for (int i = 0; i < 4; ++i) xk[i] = saved[(size_t)k * dim + i];
-          acro_f_obs(&c, ro->ts[k], xk, yk); /* lax.scan(f_obs, key, (ts, xs)), dyn.py:99 */
+          for (int i = 0; i < nv; ++i) xk[i] = saved[(size_t)k * dim + i];
+          ctl_f_obs(&c, ro->ts[k], xk, yk); /* lax.scan(f_obs, key, (ts, xs)), dyn.py:99 */
           if (m->model == 1) { /* dyn.py:101: readout([y, a, 0_u, target]) */
             const int no = m->n_obs, na = m->state_size, nu = m->n_control, nt = m->n_targets;
             const int D = no + na + nu + nt;
             for (int i = 0; i < no; ++i) data[i] = yk[i];
-            for (int i = 0; i < na; ++i) data[no + i] = saved[(size_t)k * dim + 4 + i];
+            for (int i = 0; i < na; ++i) data[no + i] = saved[(size_t)k * dim + nv + i];
             for (int i = 0; i < nu; ++i) data[no + na + i] = 0.0f;
             for (int i = 0; i < nt; ++i) data[no + na + nu + i] = c.target[i];
             for (int j = 0; j < nu; ++j) uu[(size_t)k * 8 + j] = tree_eval(&c, na + j, data, D);
@@ -395,23 +483,25 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
             for (int i = 0; i < nt; ++i) data[no + i] = c.target[i];
             uu[(size_t)k * 8] = tree_eval(&c, 0, data, no + nt);
           }
-          if (xs) for (int i = 0; i < 4; ++i) xs[(base + k) * 4 + i] = xk[i];
+          if (xs) for (int i = 0; i < nv; ++i) xs[(base + k) * nv + i] = xk[i];
           if (ys) for (int i = 0; i < m->n_obs; ++i) ys[(base + k) * m->n_obs + i] = yk[i];
           if (us) for (int j = 0; j < m->n_control; ++j) us[(base + k) * m->n_control + j] = uu[(size_t)k * 8 + j];
           if (acts && m->model == 1)
             for (int i = 0; i < m->state_size; ++i)
-              acts[(base + k) * m->state_size + i] = saved[(size_t)k * dim + 4 + i];
+              acts[(base + k) * m->state_size + i] = saved[(size_t)k * dim + nv + i];
         }
-        /* acrobot fitness uses the first control only (R = [[0.01]], n_control = 1) */
+        /* the fitness functions use the first control only (n_control = 1) */
         float ucol[4096];
         float* up = (S <= 4096) ? ucol : (float*)malloc(sizeof(float) * S);
         float xcol[4 * 4096];
         float* xp = (S <= 4096) ? xcol : (float*)malloc(sizeof(float) * 4 * S);
         for (int k = 0; k < S; ++k) {
           up[k] = uu[(size_t)k * 8];
-          for (int i = 0; i < 4; ++i) xp[4 * k + i] = saved[(size_t)k * dim + i];
+          for (int i = 0; i < nv; ++i) xp[nv * k + i] = saved[(size_t)k * dim + i];
         }
-        f = acro_fitness(xp, up, ro->ts, S);
+        if (m->env == ENV_HARMONIC) f = ho_fitness(xp, up, c.prm, c.target[0], S);
+        else if (m->env == ENV_REACTOR) f = reactor_fitness(xp, up, c.target[0], S);
+        else f = acro_fitness(xp, up, ro->ts, S);
         if (up != ucol) free(up);
         if (xp != xcol) free(xp);
       }
@@ -448,13 +538,37 @@ void oracle_wrap(const float* x, float* o, long n) {
 void oracle_acro_drift(const float* params4, const float* state4, float u, float* out4) {
   OrCtx c;
   memset(&c, 0, sizeof(c));
-  c.l1 = params4[0]; c.l2 = params4[1]; c.m1 = params4[2]; c.m2 = params4[3];
+  c.prm = params4;
   acro_drift(&c, state4, u, out4);
 }
-void oracle_acro_f_obs(const float* x4, float* y4) {
+void oracle_expf(const float* x, float* o, long n) {
+  for (long i = 0; i < n; ++i) o[i] = mtgp_expf(x[i]);
+}
+void oracle_env_drift(int env, const float* params, const float* state, float u, float* out) {
+  OrModel m;
+  memset(&m, 0, sizeof(m));
+  m.env = env;
   OrCtx c;
   memset(&c, 0, sizeof(c));
-  acro_f_obs(&c, 0.0f, x4, y4);
+  c.m = &m;
+  c.prm = params;
+  env_drift(&c, state, u, out);
+}
+float oracle_env_fitness(int env, const float* xs, const float* us, const float* ts, const float* params, float tg,
+                         int S) {
+  if (env == ENV_HARMONIC) return ho_fitness(xs, us, params, tg, S);
+  if (env == ENV_REACTOR) return reactor_fitness(xs, us, tg, S);
+  return acro_fitness(xs, us, ts, S);
+}
+void oracle_acro_f_obs(const float* x4, float* y4) {
+  OrModel m;
+  memset(&m, 0, sizeof(m));
+  m.n_var = m.n_obs = 4;
+  m.env = ENV_ACROBOT;
+  OrCtx c;
+  memset(&c, 0, sizeof(c));
+  c.m = &m;
+  ctl_f_obs(&c, 0.0f, x4, y4);
 }
 /* PRNG spec hooks: normals of fold_in(key, bitcast(t)), normals of a key, threefry, erfinv, log1p */
 void oracle_obs_normals(const uint32_t* key, float t, int n, int impl, float* out) {

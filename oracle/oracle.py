@@ -29,7 +29,7 @@ class OrModel(ctypes.Structure):
                 ("n_obs", ctypes.c_int32), ("n_control", ctypes.c_int32), ("n_targets", ctypes.c_int32),
                 ("n_steps", ctypes.c_int32), ("save_every", ctypes.c_int32), ("n_save", ctypes.c_int32),
                 ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float),
-                ("prng_impl", ctypes.c_int32)]
+                ("prng_impl", ctypes.c_int32), ("env", ctypes.c_int32)]
 
 
 class OrRollouts(ctypes.Structure):
@@ -57,6 +57,10 @@ def lib():
         L.oracle_wrap.argtypes = [vp, vp, ctypes.c_long]
         L.oracle_acro_drift.argtypes = [vp, vp, ctypes.c_float, vp]
         L.oracle_acro_f_obs.argtypes = [vp, vp]
+        L.oracle_expf.argtypes = [vp, vp, ctypes.c_long]
+        L.oracle_env_drift.argtypes = [ctypes.c_int, vp, vp, ctypes.c_float, vp]
+        L.oracle_env_fitness.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_float, ctypes.c_int]
+        L.oracle_env_fitness.restype = ctypes.c_float
         L.oracle_acro_fitness.argtypes = [vp, vp, vp, ctypes.c_int]
         L.oracle_acro_fitness.restype = ctypes.c_float
         L.oracle_pairwise_sum.argtypes = [vp, ctypes.c_int]
@@ -109,7 +113,7 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
     Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c])."""
     pop = np.ascontiguousarray(pop, np.float32)
     P, T, N, _ = pop.shape
-    m = OrModel(**{k: model.get(k, 0) if k == "prng_impl" else model[k] for k, _ in OrModel._fields_})
+    m = OrModel(**{k: model.get(k, 0) if k in ("prng_impl", "env") else model[k] for k, _ in OrModel._fields_})
     x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
     R = x0.shape[0]
     prm = None if rollouts.get("params") is None else np.ascontiguousarray(rollouts["params"], np.float32)
@@ -133,7 +137,7 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
         if model["model"] == 3:
             bufs[0] = np.empty((P, R, S, model["n_var"]), np.float32)
         else:
-            bufs[0] = np.empty((P, R, S, 4), np.float32)
+            bufs[0] = np.empty((P, R, S, model["n_var"]), np.float32)
             bufs[1] = np.empty((P, R, S, model["n_obs"]), np.float32)
             bufs[2] = np.empty((P, R, S, model["n_control"]), np.float32)
             if model["model"] == 1:
@@ -155,6 +159,30 @@ def acro_drift(params4, state4, u):
     o = np.empty(4, np.float32)
     lib().oracle_acro_drift(_p(p), _p(x), ctypes.c_float(u), _p(o))
     return o
+
+
+def expf(x):
+    x = np.ascontiguousarray(x, np.float32)
+    o = np.empty_like(x)
+    lib().oracle_expf(_p(x), _p(o), x.size)
+    return o
+
+
+def env_drift(env: int, params, state, u):
+    p = np.ascontiguousarray(params, np.float32)
+    x = np.ascontiguousarray(state, np.float32)
+    o = np.empty(x.shape[0], np.float32)
+    lib().oracle_env_drift(env, _p(p), _p(x), ctypes.c_float(u), _p(o))
+    return o
+
+
+def env_fitness(env: int, xs, us, ts, params, target):
+    xs = np.ascontiguousarray(xs, np.float32)
+    us = np.ascontiguousarray(us, np.float32).reshape(-1)
+    ts = np.ascontiguousarray(ts, np.float32)
+    p = np.ascontiguousarray(params, np.float32)
+    return np.float32(lib().oracle_env_fitness(env, _p(xs), _p(us), _p(ts), _p(p), ctypes.c_float(target),
+                                               xs.shape[0]))
 
 
 def acro_f_obs(x4):

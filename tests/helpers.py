@@ -9,22 +9,39 @@ CONTROL_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("
 SR_OPS = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("/", None, 2, 0.1)]  # SymbolicRegression.ipynb
 
 
-def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2, obs_noise=0.0):
-    env = mt.Acrobot(0.0, obs_noise)
-    vl = [["y1", "y2", "y3", "y4"] + [f"a{i + 1}" for i in range(state_size)] + ["u"],
-          [f"a{i + 1}" for i in range(state_size)]]
+ENVS = {"acrobot": mt.Acrobot, "harmonic": mt.HarmonicOscillator, "reactor": mt.StirredTankReactor}
+
+
+def make_env(name, obs_noise):
+    return ENVS[name](0.0, obs_noise)
+
+
+def _mode(name):
+    return "Constant" if name == "acrobot" else "Different"
+
+
+def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2, obs_noise=0.0, env="acrobot",
+                  h=0.05):
+    name = env
+    env = make_env(name, obs_noise)
+    ys = [f"y{i + 1}" for i in range(env.n_obs)]
+    acts = [f"a{i + 1}" for i in range(state_size)]
+    tg = [f"tar{i + 1}" for i in range(env.n_targets)]
+    vl = [ys + acts + ["u"] + tg, acts + tg]
     lib = mt.NodeLibrary(CONTROL_OPS, vl, [state_size, 1])
-    ff = mt.DynamicEvaluator(env, state_size, 0.05, solver=mt.RK4())
-    data = mt.control_data(env, R, 0.05, None, seed=seed + 1, n_steps=n_steps)
+    ff = mt.DynamicEvaluator(env, state_size, h, solver=mt.RK4())
+    data = mt.control_data(env, R, h, None, seed=seed + 1, n_steps=n_steps, mode=_mode(name))
     pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
     return env, lib, ff, data, pop
 
 
-def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0):
-    env = mt.Acrobot(0.0, obs_noise)
-    lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1])
-    ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4())
-    data = mt.control_data(env, R, 0.05, None, seed=seed + 1, n_steps=n_steps)
+def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0, env="acrobot", h=0.05):
+    name = env
+    env = make_env(name, obs_noise)
+    vl = [[f"y{i + 1}" for i in range(env.n_obs)] + [f"tar{i + 1}" for i in range(env.n_targets)]]
+    lib = mt.NodeLibrary(CONTROL_OPS, vl, [1])
+    ff = mt.FeedforwardEvaluator(env, h, solver=mt.RK4())
+    data = mt.control_data(env, R, h, None, seed=seed + 1, n_steps=n_steps, mode=_mode(name))
     pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
     return env, lib, ff, data, pop
 
@@ -48,7 +65,7 @@ def oracle_model(ff, d, parsimony=0.0):
                 n_obs=env.n_obs if env else 0, n_control=env.n_control if env else 0,
                 n_targets=env.n_targets if env else 0, n_steps=d["n_steps"], save_every=d["save_every"],
                 n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony,
-                prng_impl=d.get("prng_impl", 0))
+                prng_impl=d.get("prng_impl", 0), env=d.get("env", 0))
 
 
 def oracle_rollouts(d, data=None):

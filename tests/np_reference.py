@@ -133,3 +133,59 @@ def rk4(rhs, s0, h, n):
             s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
             out.append(s.copy())
     return np.array(out)
+
+
+# ---- HarmonicOscillator / StirredTankReactor (harmonic_oscillator.py:8-80, reactor.py:7-81)
+def ho_drift(x, u, omega, zeta):
+    A = np.array([[0.0, 1.0], [-omega, -zeta]])
+    b = np.array([[0.0], [1.0]])
+    return A @ x + b @ np.atleast_1d(u)
+
+
+def reactor_drift(x, u, Vol, Cp, dHr, UA, q, Tf, Tcf, Volc):
+    Tc, T, c = x
+    control = np.clip(u, 0, 300)
+    k = 7.2e10 * np.exp(-72750 / 8.314 / T)
+    dc = (q / Vol) * (1.0 - c) - k * c
+    dT = (q / Vol) * (Tf - T) + (-dHr / Cp) * k * c + (UA / Vol / Cp) * (Tc - T)
+    dTc = (control / Volc) * (Tcf - Tc) + (UA / Volc / Cp) * (T - Tc)
+    return np.array([dTc, dT, dc])
+
+
+def env_drift(name, x, u, params):
+    return ho_drift(x, u, *params) if name == "harmonic" else reactor_drift(x, u, *params)
+
+
+def env_fitness(name, xs, us, params, target):
+    """fitness_function over the saved points (sum of quadratic costs), float64."""
+    xs = np.asarray(xs, np.float64)
+    us = np.asarray(us, np.float64).reshape(-1)
+    if name == "harmonic":
+        omega, zeta = params
+        A = np.array([[0.0, 1.0], [-omega, -zeta]])
+        b = np.array([[0.0], [1.0]])
+        xd = np.array([target, 0.0])
+        ud = (-np.linalg.pinv(b) @ A @ xd)[0]
+        Q, R = np.array([[0.5, 0], [0, 0]]), 0.5
+    else:
+        xd = np.array([0.0, target, 0.0])
+        ud = 0.0
+        Q, R = np.diag([0.0, 0.01, 0.0]), 0.0001
+    e = xs - xd
+    return float(np.sum(np.einsum("si,ij,sj->s", e, Q, e) + (us - ud) * R * (us - ud)))
+
+
+def dyn_rhs_env(name, cand, lib, s, state_size, params, target, n_var):
+    x, a = s[:n_var], s[n_var:]
+    y = np.array(x, np.float64)  # C = I, no noise, no wrap
+    tg = np.atleast_1d(target).astype(np.float64)
+    u = eval_tree(cand[state_size], lib, np.concatenate([np.zeros(n_var), a, np.zeros(1), tg]))
+    dx = env_drift(name, x, u, params)
+    d = np.concatenate([y, a, [u], tg])
+    da = [eval_tree(cand[i], lib, d) for i in range(state_size)]
+    return np.concatenate([dx, da])
+
+
+def ff_rhs_env(name, cand, lib, s, params, target):
+    u = eval_tree(cand[0], lib, np.concatenate([np.array(s, np.float64), np.atleast_1d(target)]))
+    return env_drift(name, s, u, params)

@@ -252,3 +252,50 @@ def test_obs_noise_dense_w_bitexact():
     torch.cuda.synchronize()
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
     _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
+
+
+# ---------------------------------------------------------------- other environments
+_H = {"harmonic": 0.05, "reactor": 0.002}  # reactor: a mix of finite and NaN (terminated) rollouts
+
+@pytest.mark.parametrize("env", ["harmonic", "reactor"])
+@pytest.mark.parametrize("state_size", [1, 3])
+def test_dynamic_other_envs_bitexact(env, state_size):
+    """HarmonicOscillator / StirredTankReactor with the dynamic evaluator: trajectories,
+    per-rollout quadratic costs and fitness bit-exact vs the oracle ('Different' parameters)."""
+    _, lib, ff, data, pop = dynamic_setup(P=40, R=16, n_steps=80, env=env, state_size=state_size, seed=3,
+                                          h=_H[env])
+    res, ref, d = _run(ff, lib, data, pop, parsimony=0.5)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us", "acts"])
+
+
+@pytest.mark.parametrize("env", ["harmonic", "reactor"])
+def test_static_other_envs_bitexact(env):
+    _, lib, ff, data, pop = static_setup(P=40, R=16, n_steps=80, env=env, seed=4, h=_H[env])
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us"])
+
+
+@pytest.mark.parametrize("env", ["harmonic", "reactor"])
+@pytest.mark.parametrize("kind", ["dynamic", "static"])
+def test_other_envs_obs_noise_bitexact(env, kind):
+    """Observation noise with W = obs_noise*I (oscillator) and obs_noise*I*[15, 15, 0.1] (reactor)."""
+    setup = dynamic_setup if kind == "dynamic" else static_setup
+    _, lib, ff, data, pop = setup(P=32, R=16, n_steps=50, env=env, obs_noise=0.1, seed=5, h=_H[env])
+    res, ref, d = _run(ff, lib, data, pop)
+    names = ["xs", "ys", "us", "acts"] if kind == "dynamic" else ["xs", "ys", "us"]
+    _check(res, ref, pop.shape[0], 16, names)
+
+
+@pytest.mark.parametrize("env", ["harmonic", "reactor"])
+def test_other_envs_fitness_only_and_interpreter(env):
+    """Fitness-only mode (early exit once every lane has terminated) and the interpreter path
+    agree bit-for-bit with the JIT trajectory run; terminated rollouts give NaN costs -> max_fitness."""
+    _, lib, ff, data, pop = dynamic_setup(P=48, R=16, n_steps=100, env=env, seed=6, h=0.2)
+    a = _run_engine(ff, lib, data, pop, True)
+    b = _run_engine(ff, lib, data, pop, False)
+    for k in a:
+        assert bits_equal(a[k], b[k]), mismatch_report(a[k], b[k], k)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    c = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=False, rollout_fitness=True)
+    assert bits_equal(c["rollout_fitness"].cpu().numpy(), a["rollout_fitness"])
+    assert bits_equal(c["fitness"].cpu().numpy(), a["fitness"])
