@@ -26,6 +26,20 @@
 #include "mtgp_flatten.h"
 #include "mtgp_jit.h"
 
+// Translation units.  The library is compiled from this file several times in parallel
+// (__graft_entry__.build_hip): MTGP_TU=0 holds the C ABI, the Acrobot / SR / JIT / flatten /
+// schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor
+// control kernels behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
+#ifndef MTGP_TU
+#define MTGP_TU_MAIN 1
+#define MTGP_TU_HARMONIC 1
+#define MTGP_TU_REACTOR 1
+#else
+#define MTGP_TU_MAIN (MTGP_TU == 0)
+#define MTGP_TU_HARMONIC (MTGP_TU == 1)
+#define MTGP_TU_REACTOR (MTGP_TU == 2)
+#endif
+
 namespace {
 
 constexpr int kWave = 64;
@@ -1139,6 +1153,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   if (w == 0) finish_group(A, Ln, tot / (float)S);
 }
 
+#if MTGP_TU_MAIN
 // --------------------------------------------------------------------------------------
 // tree_evaluator plugin (gp.py:390-401): every program on M shared data vectors.
 // One wave per (individual, program, chunk of 64 data vectors); data vector in LDS.
@@ -1249,7 +1264,10 @@ __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict
   order[q] = p;
 }
 
+#endif  // MTGP_TU_MAIN
+
 hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
+#if MTGP_TU_MAIN
 // --------------------------------------------------------------------------------------
 // Program JIT build (mtgp_jit.h): one unit of code per (wave, role).  Pass 1 sizes every
 // unit, one block scans the sizes into byte offsets, pass 2 writes the code (vector stores)
@@ -1393,6 +1411,8 @@ hsa_status_t jit_find_pool(hsa_amd_memory_pool_t p, void* data) {
   return HSA_STATUS_SUCCESS;
 }
 
+#endif  // MTGP_TU_MAIN
+
 bool g_timing = false;
 bool g_have_timing = false;
 
@@ -1456,6 +1476,32 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
   }
 }
 
+
+// entries of the split-off environment TUs (hidden: not part of the C ABI)
+#define MTGP_TU_ENTRY_ARGS                                                                              \
+  const void* A, const MtgpModel* model, const MtgpRollouts* ro, bool jit, bool noise, bool traj,       \
+      unsigned grid, unsigned block, hipStream_t s
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS);
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
+#if MTGP_TU_HARMONIC
+int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS) {
+  return launch_ctl<EnvHarmonic>(*(const KArgs*)A, model, ro, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+#if MTGP_TU_REACTOR
+int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS) {
+  return launch_ctl<EnvReactor>(*(const KArgs*)A, model, ro, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+
+#if MTGP_TU_MAIN
+// a split-off TU's launch, timed with this TU's events (mtgp_last_kernel_ms)
+template <class F>
+int launch_tu(F&& entry, hipStream_t s) {
+  int rc = MTGP_OK;
+  const int lr = launch_timed([&] { rc = entry(); }, s);
+  return rc != MTGP_OK ? rc : lr;
+}
 
 extern "C" {
 
@@ -1696,9 +1742,9 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     switch (model->env) {
       case MTGP_ENV_ACROBOT: return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
       case MTGP_ENV_HARMONIC_OSCILLATOR:
-        return launch_ctl<EnvHarmonic>(A, model, rollouts, jit, noise, traj, grid, block, s);
+        return launch_tu([&] { return mtgp_tu_launch_harmonic(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
       case MTGP_ENV_STIRRED_TANK_REACTOR:
-        return launch_ctl<EnvReactor>(A, model, rollouts, jit, noise, traj, grid, block, s);
+        return launch_tu([&] { return mtgp_tu_launch_reactor(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
       default: return MTGP_ERR_ARG;
     }
   } else if (model->model == MTGP_MODEL_SR) {
@@ -1735,3 +1781,4 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
 }
 
 }  // extern "C"
+#endif  // MTGP_TU_MAIN
