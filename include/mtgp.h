@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 7
+#define MTGP_ABI_VERSION 8
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -137,7 +137,18 @@ typedef struct {
                              /* 0 threefry original (JAX <= 0.4.x default),        */
                              /* 1 threefry partitionable (JAX >= 0.5 default)      */
   int32_t env;               /* control models: MTGP_ENV_* (0 = Acrobot)            */
+  /* Solver (ABI v8).  MTGP_SOLVER_RK4: fixed step h, n_steps / save_every as above (BASELINE).
+   * MTGP_SOLVER_DOPRI5: diffrax.Dopri5 + PIDController(rtol, atol, dtmin, dtmax) from dt0 = h
+   * with SaveAt(ts) and at most max_steps step attempts (include/mtgp_dopri5.h, the notebooks'
+   * setting, e.g. SymbolicRegression.ipynb:136); n_steps / save_every are ignored.  Implemented
+   * for MTGP_MODEL_SR with n_var <= 4; other models return MTGP_ERR_ARG. */
+  int32_t solver;
+  int32_t max_steps; /* Dopri5: accepted + rejected steps before the solve gives up      */
+  float rtol, atol;  /* PIDController tolerances                                         */
+  float dtmin;       /* <= 0: None; else force_dtmin: steps at dtmin are always accepted */
+  float dtmax;       /* <= 0: None                                                       */
 } MtgpModel;
+enum { MTGP_SOLVER_RK4 = 0, MTGP_SOLVER_DOPRI5 = 1 };
 
 typedef struct {
   const float* x0;      /* [R, n_var]                                       */

@@ -1,0 +1,123 @@
+/*
+ * mtgp_dopri5.h -- fp32 arithmetic spec of the adaptive Dopri5 + PID solve.
+ *
+ * The notebooks run every evaluator with
+ *     solver=diffrax.Dopri5(), stepsize_controller=diffrax.PIDController(rtol, atol, dtmin=0.001)
+ *     (SymbolicRegression.ipynb:136, DynamicPolicy.ipynb:105, StaticPolicy.ipynb:102)
+ * through diffeqsolve(..., saveat=SaveAt(ts), event=Event(cond_fn_nan), throw=False)
+ *     (SR_evaluator.py:76-79, dynamic_evaluate.py:93-96, feedforward_evaluate.py:90-93).
+ * diffrax is a third-party dependency absent from this image and unpinned by the reference (no
+ * lock file; diffrax.Event implies >= 0.6): this header restates its published algorithm, and
+ * like mtgp_f32math.h it is the shared arithmetic spec that the GPU kernel (k_sr_dopri5) and the
+ * CPU oracle (oracle/mtgp_oracle.c solve_dopri5) both follow, so that they agree bit for bit.
+ * The stepping loop itself is written independently on each side.
+ *
+ * Per rollout (state y, time t, step h, FSAL derivative f0 = f(t, y)):
+ *   stages  f_i = f(t + c_i h, y + h * sum_{j<i, a_ij != 0} a_ij f_j), i = 1..6 (ascending-j fma
+ *           chain, first term a_i0 * f0); y1 = stage-6 input (Dopri5 is FSAL: b = a_6j);
+ *   error   err = h * sum_j e_j f_j (e = b - b_hat, same chain form);
+ *   norm    m = mean_i (err_i / (atol + rtol * max(|y_i|, |y1_i|)))^2  (rms_norm squared,
+ *           summed in index order; "scaled error < 1" is tested as m < 1);
+ *   accept  keep = m < 1 || at_dtmin  (force_dtmin=True);
+ *   factor  PIDController defaults pcoeff 0, icoeff 1, dcoeff 0, safety 0.9, factormin 0.2,
+ *           factormax 10, error_order = Dopri5.order = 5:
+ *             factor = clip(0.9 * m^(-1/10), keep ? 1 : 0.2, 10); m == 0 -> 10; m inf/NaN -> the
+ *             lower clip (diffrax: inv_scaled_error 0; a NaN error is treated like inf here)
+ *   next    dt = h * factor; dt = min(dt, dtmax); at_dtmin = dt <= dtmin; dt = max(dt, dtmin)
+ *           t <- keep ? t + h : t;  tnext = t + dt, and if tnext > t_end - 1e-6:
+ *           tnext = keep ? t_end : t + 0.5 (t_end - t)        (diffrax _clip_to_end, f32 tol)
+ *   saves   SaveAt(ts): ts[0] -> y0; each accepted step [t, t + h] saves every pending ts[k] with
+ *           ts[k] <= t + h through the Dopri5 dense output: y_mid = y + h sum_j cmid_j f_j,
+ *           k0 = h f0, k1 = h f6, the quartic through (y, y1, y_mid, k0, k1)
+ *           (diffrax FourthOrderPolynomialInterpolation) at theta = (ts[k] - t) / h;
+ *   stop    after an accepted step whose y1 makes the event condition negative (saves of that
+ *           step are written first); after max_steps attempts (accepted + rejected); at t_end.
+ *           Unsaved points are +inf (throw=False).
+ */
+#ifndef MTGP_DOPRI5_H
+#define MTGP_DOPRI5_H
+#include "mtgp_f32math.h"
+#include "mtgp_prng.h" /* mtgp_logf_pos: the fdlibm log spec shared with the PRNG */
+
+/* Dormand-Prince 5(4) tableau, each entry the f32 rounding of the exact rational */
+#define MTGP_DP_F(num, den) ((float)((double)(num) / (double)(den)))
+#define MTGP_DP_END_TOL 1e-6f
+#define MTGP_DP_SAFETY 0.9f
+#define MTGP_DP_FACTORMIN 0.2f
+#define MTGP_DP_FACTORMAX 10.0f
+
+/* c_i */
+#define MTGP_DP_C1 MTGP_DP_F(1, 5)
+#define MTGP_DP_C2 MTGP_DP_F(3, 10)
+#define MTGP_DP_C3 MTGP_DP_F(4, 5)
+#define MTGP_DP_C4 MTGP_DP_F(8, 9)
+
+/* a_ij rows 1..6 (row 6 = b); zero entries are skipped by the chain */
+#define MTGP_DP_TABLE_A                                                                          \
+  {                                                                                              \
+    {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f},                                                        \
+    {MTGP_DP_F(1, 5), 0.0f, 0.0f, 0.0f, 0.0f, 0.0f},                                             \
+    {MTGP_DP_F(3, 40), MTGP_DP_F(9, 40), 0.0f, 0.0f, 0.0f, 0.0f},                                \
+    {MTGP_DP_F(44, 45), MTGP_DP_F(-56, 15), MTGP_DP_F(32, 9), 0.0f, 0.0f, 0.0f},                 \
+    {MTGP_DP_F(19372, 6561), MTGP_DP_F(-25360, 2187), MTGP_DP_F(64448, 6561),                    \
+     MTGP_DP_F(-212, 729), 0.0f, 0.0f},                                                          \
+    {MTGP_DP_F(9017, 3168), MTGP_DP_F(-355, 33), MTGP_DP_F(46732, 5247), MTGP_DP_F(49, 176),     \
+     MTGP_DP_F(-5103, 18656), 0.0f},                                                             \
+    {MTGP_DP_F(35, 384), 0.0f, MTGP_DP_F(500, 1113), MTGP_DP_F(125, 192),                        \
+     MTGP_DP_F(-2187, 6784), MTGP_DP_F(11, 84)},                                                 \
+  }
+/* error weights e = b - b_hat over f0..f6 */
+#define MTGP_DP_TABLE_E                                                                          \
+  {MTGP_DP_F(71, 57600), 0.0f, MTGP_DP_F(-71, 16695), MTGP_DP_F(71, 1920),                       \
+   MTGP_DP_F(-17253, 339200), MTGP_DP_F(22, 525), MTGP_DP_F(-1, 40)}
+/* dense-output midpoint weights (diffrax _Dopri5Interpolation.c_mid = Shampine's) */
+#define MTGP_DP_TABLE_CMID                                                                       \
+  {MTGP_DP_F(6025192743.0, 2.0 * 30085553152.0), 0.0f,                                           \
+   MTGP_DP_F(51252292925.0, 2.0 * 65400821598.0), MTGP_DP_F(-2691868925.0, 2.0 * 45128329728.0), \
+   MTGP_DP_F(187940372067.0, 2.0 * 1594534317056.0), MTGP_DP_F(-1776094331.0, 2.0 * 19743644256.0), \
+   MTGP_DP_F(11237099.0, 2.0 * 235043384.0)}
+
+/* stage time offset c_i (i = 0..6) */
+MTGP_INLINE MTGP_HD float mtgp_dp_c(int i) {
+  return i == 0 ? 0.0f : i == 1 ? MTGP_DP_C1 : i == 2 ? MTGP_DP_C2 : i == 3 ? MTGP_DP_C3 : i == 4 ? MTGP_DP_C4 : 1.0f;
+}
+
+/* one term of a weighted chain: acc + w * f (fma), the first term (first != 0) w * f, w == 0 skipped */
+MTGP_INLINE MTGP_HD float mtgp_dp_term(float acc, float w, float f, int first) {
+  return first ? w * f : (w != 0.0f ? MTGP_FMAF(w, f, acc) : acc);
+}
+
+/* PID step factor from m = mean squared scaled error (see the header comment) */
+MTGP_INLINE MTGP_HD float mtgp_dp_factor(float m, int keep) {
+  const float lo = keep ? 1.0f : MTGP_DP_FACTORMIN;
+  if (m == 0.0f) return MTGP_DP_FACTORMAX;
+  if (!mtgp_isfinite(m)) return lo;
+  float f = MTGP_DP_SAFETY * mtgp_expf(-0.1f * mtgp_logf_pos(m));
+  f = f < lo ? lo : f;
+  return f > MTGP_DP_FACTORMAX ? MTGP_DP_FACTORMAX : f;
+}
+
+/* scaled error of one component: err / (atol + rtol * max(|y0|, |y1|)) */
+MTGP_INLINE MTGP_HD float mtgp_dp_scaled(float err, float y0, float y1, float rtol, float atol) {
+  const float a0 = MTGP_FABSF(y0), a1 = MTGP_FABSF(y1);
+  const float ym = (mtgp_isnan(a0) || mtgp_isnan(a1)) ? mtgp_qnan() : (a0 > a1 ? a0 : a1); /* jnp.maximum */
+  return err / MTGP_FMAF(rtol, ym, atol);
+}
+
+/* the next attempt's end time (diffrax _clip_to_end) */
+MTGP_INLINE MTGP_HD float mtgp_dp_clip_end(float t, float dt, float t_end, int keep) {
+  const float tn = t + dt;
+  if (tn > t_end - MTGP_DP_END_TOL) return keep ? t_end : MTGP_FMAF(0.5f, t_end - t, t);
+  return tn;
+}
+
+/* dense output of one component at theta in [0, 1] of an accepted step:
+ * y0, y1 (= y0 + ...), ymid = y0 + h * sum cmid_j f_j, k0 = h f0, k1 = h f6 */
+MTGP_INLINE MTGP_HD float mtgp_dp_interp(float y0, float y1, float ymid, float k0, float k1, float th) {
+  const float a = (2.0f * (k1 - k0) - 8.0f * (y1 + y0)) + 16.0f * ymid;
+  const float b = (((5.0f * k0 - 3.0f * k1) + 18.0f * y0) + 14.0f * y1) - 32.0f * ymid;
+  const float c = (((k1 - 4.0f * k0) - 11.0f * y0) - 5.0f * y1) + 16.0f * ymid;
+  return MTGP_FMAF(MTGP_FMAF(MTGP_FMAF(MTGP_FMAF(a, th, b), th, c), th, k0), th, y0);
+}
+
+#endif /* MTGP_DOPRI5_H */

@@ -23,6 +23,7 @@
 #include "mtgp.h"
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
+#include "mtgp_dopri5.h"
 #include "mtgp_flatten.h"
 #include "mtgp_jit.h"
 
@@ -1007,6 +1008,150 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 }
 
 // --------------------------------------------------------------------------------------
+// Symbolic regression with adaptive Dopri5 + PIDController, SaveAt(ts) by dense output and the
+// NaN event (SR_evaluator.py:57-94 with the notebook's solver, SymbolicRegression.ipynb:136):
+// every rule is the fp32 spec of include/mtgp_dopri5.h.  Each lane (individual, rollout) has its
+// own t, step and accept/reject history; the wave iterates while any lane is still integrating
+// and runs the six new stage RHS evaluations (Dopri5 is FSAL) for all lanes together, since the
+// programs are shared per group.  Lanes that are done keep computing but never commit.
+__constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
+
+template <int NV, bool TRAJ, bool JIT>
+__global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
+  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
+  Lane Ln;
+  if (!lane_setup(A, Ln)) return;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* dcol = &lds[Ln.wave][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  DataVec<JIT> D(dcol, st);
+  if (JIT) asm volatile("s_icache_inv");
+  const int S = A.m.n_save, max_steps = A.m.max_steps;
+  const float rtol = A.m.rtol, atol = A.m.atol, dtmin = A.m.dtmin, dtmax = A.m.dtmax;
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  const float* __restrict__ ts = A.ro.ts;
+  const float t_end = ts[S - 1];
+  constexpr float E[7] = MTGP_DP_TABLE_E;
+  constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+  float tot = 0.0f;
+  // one save point: MSE term (components in index order, sr.py:24) and the trajectory row
+  auto save = [&](int k, const float* v) {
+    float sq = 0.0f;
+#pragma unroll
+    for (int d = 0; d < NV; ++d) {
+      const float e = v[d] - A.ro.ys_true[((size_t)k * NV + d) * R + rr];
+      sq = (d == 0) ? e * e : sq + e * e;
+    }
+    tot = tot + sq;
+    if (TRAJ && active && A.out.xs) {
+#pragma unroll
+      for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d]);
+    }
+  };
+  auto bad = [&](const float* v) {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) b = b || !mtgp_isfinite(v[i]);
+    return b;
+  };
+  float y[NV], y1[NV], kx[NV], f[7][NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
+  save(0, y);
+  int k = 1, steps = 0;
+  bool at_dtmin = false, prev_ok = !bad(y);
+  float t = ts[0];
+  float tnext = t + A.m.h;
+  tnext = tnext > t_end ? t_end : tnext;
+  // FSAL seed f0 = f(t0, y0)
+#pragma unroll
+  for (int i = 0; i < NV; ++i) D.put(i, y[i]);
+  run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
+#pragma unroll
+  for (int i = 0; i < NV; ++i) f[0][i] = kx[i];
+  bool live = active && t < t_end && steps < max_steps;
+  while (__any(live)) {
+    const float h = tnext - t;
+#pragma unroll 1
+    for (int s = 1; s <= 6; ++s) {  // stage s input y + h sum_{j<s} a_sj f_j (wave-uniform s)
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
+        const float yi = MTGP_FMAF(h, acc, y[i]);
+        y1[i] = yi;  // the stage-6 input is the step's solution
+        D.put(i, yi);
+      }
+      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
+#pragma unroll
+      for (int j = 1; j < 7; ++j)
+#pragma unroll
+        for (int i = 0; i < NV; ++i) f[j][i] = (j == s) ? kx[i] : f[j][i];
+    }
+    if (live) {
+      float msum = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
+        const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], rtol, atol);
+        msum = (i == 0) ? sc * sc : msum + sc * sc;
+      }
+      const float ms = msum / (float)NV;
+      const bool keep = (ms < 1.0f) || at_dtmin;
+      float dt = h * mtgp_dp_factor(ms, keep);
+      if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
+      if (dtmin > 0.0f) {
+        at_dtmin = dt <= dtmin;
+        dt = dt < dtmin ? dtmin : dt;
+      }
+      ++steps;
+      bool stop = false;
+      if (keep) {
+        while (k < S && ts[k] <= tnext) {  // SaveAt(ts) through the dense output
+          const float th = (ts[k] - t) / h;
+          float v[NV];
+#pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            float acc = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, CM[j], f[j][i], j == 0);
+            const float ymid = MTGP_FMAF(h, acc, y[i]);
+            v[i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
+          }
+          save(k, v);
+          ++k;
+        }
+        t = tnext;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          y[i] = y1[i];
+          f[0][i] = f[6][i];  // FSAL
+        }
+        const bool ok = !bad(y);
+        stop = prev_ok && !ok;  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
+        prev_ok = ok;
+      }
+      if (stop || !(t < t_end) || steps >= max_steps) live = false;
+      else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+    }
+  }
+  if (active) {  // unsaved points are +inf (throw=False)
+    float inf[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) inf[i] = kInf;
+    for (; k < S; ++k) save(k, inf);
+  }
+  finish_group(A, Ln, tot / (float)S);
+}
+
+// --------------------------------------------------------------------------------------
 // Symbolic regression with a wide state (5 <= n_var <= MTGP_MAX_DATA, BASELINE C5: the 64-dim
 // "neural-ODE" SR).  One workgroup = NW = ceil(n_var / 8) waves over the same lanes (G
 // individuals x Rp rollouts, like every kernel here); wave w owns components [8w, 8w + 8): it
@@ -1707,8 +1852,16 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
   if ((int64_t)P * rollouts->R > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
   if ((int64_t)P * n_prog * L * (int64_t)sizeof(MtgpInstr) > UINT32_MAX) return MTGP_ERR_ARG;  // 32-bit program offsets
-  if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
-  if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
+  const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
+  if (model->solver != MTGP_SOLVER_RK4 && !dopri5) return MTGP_ERR_ARG;
+  if (dopri5) {  // adaptive: save points come from ts, steps from the controller
+    if (model->model != MTGP_MODEL_SR || model->n_var < 1 || model->n_var > 4) return MTGP_ERR_ARG;
+    if (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f)) return MTGP_ERR_ARG;
+    if (!(model->rtol >= 0.0f) || !(model->atol >= 0.0f)) return MTGP_ERR_ARG;
+  } else {
+    if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
+    if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
+  }
   if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;
   if (P == 0) return MTGP_OK;
   KArgs A;
@@ -1762,7 +1915,13 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
 #define MTGP_SR(NV)                                                                                       \
   case NV:                                                                                                \
     return launch_timed([&] {                                                                             \
-      if (jit) {                                                                                          \
+      if (dopri5) {                                                                                       \
+        if (jit) {                                                                                        \
+          if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, true>), grid, block, 0, s, A);              \
+          else hipLaunchKernelGGL((k_sr_dopri5<NV, false, true>), grid, block, 0, s, A);                  \
+        } else if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, false>), grid, block, 0, s, A);        \
+        else hipLaunchKernelGGL((k_sr_dopri5<NV, false, false>), grid, block, 0, s, A);                   \
+      } else if (jit) {                                                                                   \
         if (traj) hipLaunchKernelGGL((k_sr<NV, true, true>), grid, block, 0, s, A);                       \
         else hipLaunchKernelGGL((k_sr<NV, false, true>), grid, block, 0, s, A);                           \
       } else if (traj) hipLaunchKernelGGL((k_sr<NV, true, false>), grid, block, 0, s, A);                 \

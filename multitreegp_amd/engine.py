@@ -288,6 +288,8 @@ class DeviceEngine:
         m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
         m.prng_impl = d.get("prng_impl", 0)
         m.env = d.get("env", nat.ENV_ACROBOT)
+        m.solver, m.max_steps = d.get("solver", nat.SOLVER_RK4), d.get("max_steps", 0)
+        m.rtol, m.atol, m.dtmin, m.dtmax = d.get("rtol", 0.0), d.get("atol", 0.0), d.get("dtmin", 0.0), d.get("dtmax", 0.0)
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R

@@ -7,9 +7,10 @@ Each class keeps the reference constructor signature and exposes the same two ca
 The population path (``GeneticProgramming.evaluate_population``) batches all candidates into
 one launch; these per-candidate calls exist for API parity and trajectory inspection.
 
-Solver: BASELINE.json prescribes an explicit fixed-step RK4.  ``solver`` must be
-``RK4()`` (or the string "rk4") and ``stepsize_controller`` ``ConstantStepSize()``; adaptive
-Dopri5 + PID (the notebooks' choice) is SURVEY.md §8f row 2 and raises NotImplementedError.
+Solver: BASELINE.json prescribes an explicit fixed-step RK4 (``RK4()`` or "rk4" with
+``ConstantStepSize()``).  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)``
+(spec include/mtgp_dopri5.h) runs on the GPU for ``SREvaluator`` with
+n_var <= 4; the control evaluators raise NotImplementedError for it.
 """
 from __future__ import annotations
 
@@ -36,16 +37,60 @@ class ConstantStepSize:
         return "ConstantStepSize()"
 
 
-def _check_solver(solver, controller):
+class Dopri5:
+    """diffrax.Dopri5: Dormand-Prince 5(4), FSAL, with the Shampine dense output."""
+    name = "Dopri5"
+
+    def __repr__(self):
+        return "Dopri5()"
+
+
+class PIDController:
+    """diffrax.PIDController with its defaults (pcoeff 0, icoeff 1, dcoeff 0: an integral
+    controller; safety 0.9, factormin 0.2, factormax 10, force_dtmin True, rms norm)."""
+    name = "PIDController"
+
+    def __init__(self, rtol: float, atol: float, pcoeff: float = 0.0, icoeff: float = 1.0, dcoeff: float = 0.0,
+                 dtmin: float = None, dtmax: float = None, force_dtmin: bool = True, factormin: float = 0.2,
+                 factormax: float = 10.0, safety: float = 0.9):
+        if (pcoeff, icoeff, dcoeff) != (0.0, 1.0, 0.0) or (factormin, factormax, safety) != (0.2, 10.0, 0.9):
+            raise NotImplementedError("only the default PIDController coefficients are implemented on the GPU")
+        if not force_dtmin:
+            raise NotImplementedError("force_dtmin=False (error on dtmin) is not implemented")
+        if rtol < 0 or atol < 0:
+            raise ValueError("rtol and atol must be >= 0")
+        self.rtol, self.atol = float(rtol), float(atol)
+        self.dtmin = None if dtmin is None else float(dtmin)
+        self.dtmax = None if dtmax is None else float(dtmax)
+
+    def __repr__(self):
+        return f"PIDController(rtol={self.rtol}, atol={self.atol}, dtmin={self.dtmin}, dtmax={self.dtmax})"
+
+
+def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
+    """-> "rk4" or "dopri5" (the latter needs a PIDController and an evaluator that supports it)."""
     sname = solver.lower() if isinstance(solver, str) else getattr(solver, "name", type(solver).__name__)
-    if str(sname).lower() != "rk4":
-        raise NotImplementedError(
-            f"solver {solver!r}: only fixed-step RK4 is implemented on the MI355X path "
-            "(adaptive Dopri5/PID is SURVEY.md §8f row 2)")
-    if controller is not None:
-        cname = getattr(controller, "name", type(controller).__name__)
-        if cname != "ConstantStepSize":
-            raise NotImplementedError(f"stepsize_controller {controller!r}: only ConstantStepSize is implemented")
+    sname = str(sname).lower()
+    cname = None if controller is None else getattr(controller, "name", type(controller).__name__)
+    if sname == "dopri5":
+        if not adaptive_ok:
+            raise NotImplementedError(f"solver {solver!r}: adaptive Dopri5 is implemented for SREvaluator only "
+                                      "(control evaluators: fixed-step RK4)")
+        if cname != "PIDController":
+            raise NotImplementedError("Dopri5 needs a PIDController (fixed-step Dopri5 is not implemented)")
+        return "dopri5"
+    if sname != "rk4":
+        raise NotImplementedError(f"solver {solver!r}: implemented solvers are RK4 (fixed step) and Dopri5 (PID)")
+    if cname is not None and cname != "ConstantStepSize":
+        raise NotImplementedError(f"stepsize_controller {controller!r}: RK4 runs with ConstantStepSize only")
+    return "rk4"
+
+
+def _solver_fields(kind: str, controller, max_steps: int) -> dict:
+    if kind != "dopri5":
+        return dict(solver=nat.SOLVER_RK4, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0)
+    return dict(solver=nat.SOLVER_DOPRI5, max_steps=int(max_steps), rtol=controller.rtol, atol=controller.atol,
+                dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0)
 
 
 def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool = True) -> Tuple[int, int, int]:
@@ -252,7 +297,8 @@ class SREvaluator(_CandidateAPI):
     max_fitness = 1e5
 
     def __init__(self, solver=None, dt0: float = 0.01, max_steps: int = 16 ** 4, stepsize_controller=None):
-        _check_solver(solver if solver is not None else RK4(), stepsize_controller)
+        self.solver_kind = _check_solver(solver if solver is not None else RK4(), stepsize_controller,
+                                         adaptive_ok=True)
         self.dt0 = float(dt0)
         self.solver = solver if solver is not None else RK4()
         self.max_steps = max_steps
@@ -268,13 +314,23 @@ class SREvaluator(_CandidateAPI):
         ys = _f32(ys)
         if ys.shape[0] != R or ys.shape[2] != nv:
             raise ValueError("ys must be [R, S, n_var]")
-        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+        if self.solver_kind == "dopri5":  # save points straight from ts, steps from the controller
+            ts32 = _f32(ts)
+            S = int(ts32.shape[0])
+            if S < 2 or np.any(np.diff(ts32) < 0):
+                raise ValueError("ts needs at least two non-decreasing save points")
+            if nv > 4:
+                raise NotImplementedError("Dopri5 SR is implemented for n_var <= 4 (wide-state SR: RK4)")
+            n_steps, save_every = 0, 1
+        else:
+            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
         if ys.shape[1] != S:
             raise ValueError("ys must have len(ts) save points")
         ys_tm = np.ascontiguousarray(np.transpose(ys, (1, 2, 0)))  # [S, n_var, R] time-major
         self._n_var = nv
         return dict(x0=x0, params=None, targets=None, ts=_f32(ts), ys_true=ys_tm, R=R,
-                    n_steps=n_steps, save_every=save_every, n_save=S, n_var=nv)
+                    n_steps=n_steps, save_every=save_every, n_save=S, n_var=nv,
+                    **_solver_fields(self.solver_kind, self.stepsize_controller, self.max_steps))
 
     def n_trees(self) -> int:
         return self._n_var
@@ -289,5 +345,5 @@ class SREvaluator(_CandidateAPI):
         return specs, roles
 
 
-__all__ = ["RK4", "ConstantStepSize", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
+__all__ = ["RK4", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
            "rk4_schedule"]

@@ -27,6 +27,7 @@
 #include <string.h>
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
+#include "mtgp_dopri5.h"
 
 #define OR_MAX_N 256
 #define OR_MAX_D 64
@@ -101,6 +102,9 @@ typedef struct {
   float h, max_fitness, parsimony;
   int32_t prng_impl; /* mtgp_prng.h: 0 threefry original layout, 1 partitionable */
   int32_t env;       /* control models: 0 Acrobot, 1 HarmonicOscillator, 2 StirredTankReactor */
+  int32_t solver;    /* 0 fixed-step RK4 (BASELINE.json), 1 Dopri5 + PIDController (notebooks) */
+  int32_t max_steps; /* Dopri5: step attempts, accepted + rejected (diffeqsolve max_steps) */
+  float rtol, atol, dtmin, dtmax; /* PIDController; dtmin / dtmax <= 0: None */
 } OrModel;
 
 enum { ENV_ACROBOT = 0, ENV_HARMONIC = 1, ENV_REACTOR = 2 };
@@ -324,6 +328,81 @@ static void solve(const OrCtx* c, float t0, const float* s0, float* saved) {
     for (int i = 0; i < n; ++i) saved[(size_t)k * n + i] = mtgp_u2f(0x7f800000u);
 }
 
+/* diffeqsolve(Dopri5(), t0=ts[0], t1=ts[-1], dt0=h, SaveAt(ts), PIDController(rtol, atol, dtmin,
+ * dtmax), Event(cond_fn), max_steps, throw=False) -- diffrax restated in the fp32 spec of
+ * include/mtgp_dopri5.h (see its header comment for every rule used below). */
+static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float* saved) {
+  static const float A[7][6] = MTGP_DP_TABLE_A;
+  static const float E[7] = MTGP_DP_TABLE_E;
+  static const float CM[7] = MTGP_DP_TABLE_CMID;
+  const OrModel* m = c->m;
+  const int n = state_dim(m), S = m->n_save;
+  const float t_end = ts[S - 1];
+  float y[OR_MAX_S], f[7][OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  for (int i = 0; i < n; ++i) y[i] = s0[i];
+  for (int i = 0; i < n; ++i) saved[i] = y[i];
+  int k = 1, steps = 0, at_dtmin = 0;
+  float t = ts[0];
+  float tnext = t + m->h;
+  if (tnext > t_end) tnext = t_end;
+  float prev = cond_fn(m, y);
+  rhs(c, t, y, f[0]);
+  while (t < t_end && steps < m->max_steps) {
+    const float h = tnext - t;
+    for (int st = 1; st <= 6; ++st) {
+      for (int i = 0; i < n; ++i) {
+        float acc = 0.0f;
+        for (int j = 0; j < st; ++j) acc = mtgp_dp_term(acc, A[st][j], f[j][i], j == 0);
+        yi[i] = MTGP_FMAF(h, acc, y[i]);
+        if (st == 6) y1[i] = yi[i];
+      }
+      rhs(c, t + mtgp_dp_c(st) * h, yi, f[st]);
+    }
+    float msum = 0.0f;
+    for (int i = 0; i < n; ++i) {
+      float acc = 0.0f;
+      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
+      const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], m->rtol, m->atol);
+      msum = (i == 0) ? sc * sc : msum + sc * sc;
+    }
+    const float ms = msum / (float)n;
+    const int keep = (ms < 1.0f) || at_dtmin;
+    float dt = h * mtgp_dp_factor(ms, keep);
+    if (m->dtmax > 0.0f && dt > m->dtmax) dt = m->dtmax;
+    if (m->dtmin > 0.0f) {
+      at_dtmin = dt <= m->dtmin;
+      if (dt < m->dtmin) dt = m->dtmin;
+    }
+    ++steps;
+    int done = 0;
+    if (keep) {
+      const float t1 = tnext;
+      while (k < S && ts[k] <= t1) { /* SaveAt(ts) by the dense output */
+        const float th = (ts[k] - t) / h;
+        for (int i = 0; i < n; ++i) {
+          float acc = 0.0f;
+          for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, CM[j], f[j][i], j == 0);
+          const float ymid = MTGP_FMAF(h, acc, y[i]);
+          saved[(size_t)k * n + i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
+        }
+        ++k;
+      }
+      t = t1;
+      for (int i = 0; i < n; ++i) {
+        y[i] = y1[i];
+        f[0][i] = f[6][i]; /* FSAL */
+      }
+      const float cur = cond_fn(m, y);
+      if (prev > 0.0f && cur < 0.0f) done = 1;
+      prev = cur;
+    }
+    if (done) break;
+    tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+  }
+  for (; k < S; ++k)
+    for (int i = 0; i < n; ++i) saved[(size_t)k * n + i] = mtgp_u2f(0x7f800000u);
+}
+
 /* Acrobot.fitness_function (acrobot.py:77-84) on full arrays. */
 static float acro_fitness(const float* xs, const float* us, const float* ts, int S) {
   int fs = 0, found = 0;
@@ -443,7 +522,8 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
       for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
       c.key = ro->obs_keys ? ro->obs_keys + 2 * (size_t)r : NULL;
       c.W = ro->obs_w;
-      solve(&c, ro->ts[0], s0, saved);
+      if (m->solver == 1) solve_dopri5(&c, ro->ts, s0, saved);
+      else solve(&c, ro->ts[0], s0, saved);
       float f;
       const size_t base = ((size_t)p * R + r) * S;
       if (m->model == 3) {

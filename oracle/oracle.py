@@ -17,7 +17,8 @@ LIB = os.path.join(HERE, "build", "libmtgp_oracle.so")
 
 def build(force: bool = False) -> str:
     src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h"),
-           os.path.join(HERE, "..", "include", "mtgp_prng.h")]
+           os.path.join(HERE, "..", "include", "mtgp_prng.h"),
+           os.path.join(HERE, "..", "include", "mtgp_dopri5.h")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
         subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
                        stdout=subprocess.DEVNULL)
@@ -29,7 +30,11 @@ class OrModel(ctypes.Structure):
                 ("n_obs", ctypes.c_int32), ("n_control", ctypes.c_int32), ("n_targets", ctypes.c_int32),
                 ("n_steps", ctypes.c_int32), ("save_every", ctypes.c_int32), ("n_save", ctypes.c_int32),
                 ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float),
-                ("prng_impl", ctypes.c_int32), ("env", ctypes.c_int32)]
+                ("prng_impl", ctypes.c_int32), ("env", ctypes.c_int32),
+                ("solver", ctypes.c_int32), ("max_steps", ctypes.c_int32), ("rtol", ctypes.c_float),
+                ("atol", ctypes.c_float), ("dtmin", ctypes.c_float), ("dtmax", ctypes.c_float)]
+
+_MODEL_DEFAULTS = dict(prng_impl=0, env=0, solver=0, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0)
 
 
 class OrRollouts(ctypes.Structure):
@@ -113,7 +118,8 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
     Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c])."""
     pop = np.ascontiguousarray(pop, np.float32)
     P, T, N, _ = pop.shape
-    m = OrModel(**{k: model.get(k, 0) if k in ("prng_impl", "env") else model[k] for k, _ in OrModel._fields_})
+    m = OrModel(**{k: model.get(k, _MODEL_DEFAULTS[k]) if k in _MODEL_DEFAULTS else model[k]
+                   for k, _ in OrModel._fields_})
     x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
     R = x0.shape[0]
     prm = None if rollouts.get("params") is None else np.ascontiguousarray(rollouts["params"], np.float32)

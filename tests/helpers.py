@@ -46,10 +46,16 @@ def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0, en
     return env, lib, ff, data, pop
 
 
-def sr_setup(P=24, R=8, n_save=21, save_every=4, h=0.05, depth=5, N=30, seed=0, n_var=2):
+def sr_setup(P=24, R=8, n_save=21, save_every=4, h=0.05, depth=5, N=30, seed=0, n_var=2, solver=None):
+    """solver: None (fixed-step RK4) or (rtol, atol, dtmin, max_steps) for Dopri5 + PIDController."""
     env = mt.VanDerPolOscillator(0, 0) if n_var == 2 else mt.LinearSystem(n_var)
     lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(n_var)]], [n_var])
-    ff = mt.SREvaluator(solver=mt.RK4(), dt0=h)
+    if solver is None:
+        ff = mt.SREvaluator(solver=mt.RK4(), dt0=h)
+    else:
+        rtol, atol, dtmin, max_steps = solver
+        ff = mt.SREvaluator(solver=mt.Dopri5(), dt0=h, max_steps=max_steps,
+                            stepsize_controller=mt.PIDController(rtol=rtol, atol=atol, dtmin=dtmin))
     rng = np.random.default_rng(seed + 1)
     x0 = env.sample_init_states(R, rng)
     ts = (np.arange(n_save, dtype=np.float32) * np.float32(h * save_every)).astype(np.float32)
@@ -65,7 +71,9 @@ def oracle_model(ff, d, parsimony=0.0):
                 n_obs=env.n_obs if env else 0, n_control=env.n_control if env else 0,
                 n_targets=env.n_targets if env else 0, n_steps=d["n_steps"], save_every=d["save_every"],
                 n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony,
-                prng_impl=d.get("prng_impl", 0), env=d.get("env", 0))
+                prng_impl=d.get("prng_impl", 0), env=d.get("env", 0), solver=d.get("solver", 0),
+                max_steps=d.get("max_steps", 0), rtol=d.get("rtol", 0.0), atol=d.get("atol", 0.0),
+                dtmin=d.get("dtmin", 0.0), dtmax=d.get("dtmax", 0.0))
 
 
 def oracle_rollouts(d, data=None):

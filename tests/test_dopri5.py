@@ -1,0 +1,186 @@
+"""Adaptive Dopri5 + PIDController (spec include/mtgp_dopri5.h).
+
+diffrax is not importable here and the reference holds no solver fixtures, so the restatement is
+pinned by known answers (the harmonic oscillator's closed form), by scipy's independent
+Dormand-Prince RK45 (same tableau and error estimate, its own controller and interpolant) and by
+the controller's documented edge behaviour; the GPU kernel must then match the oracle bit for bit
+(parity vs diffrax itself: unpinned)."""
+import numpy as np
+import pytest
+
+import multitreegp_amd as mt
+from multitreegp_amd.evaluators import _check_solver
+from oracle import oracle as orc
+
+from helpers import SR_OPS, oracle_model, oracle_rollouts, sr_setup
+
+
+def _oscillator(N=4):
+    """trees [x1, 0 - x0]: dx0 = x1, dx1 = -x0 (tests/test_oracle.py's RK4 known answer)."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    cand = np.zeros((1, 2, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 1] = [lib.string_to_node["x1"], -1, -1, 0]
+    cand[0, 1, N - 3] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 1, N - 2] = [1, -1, -1, 0.0]
+    cand[0, 1, N - 1] = [lib.string_to_node["-"], N - 2, N - 3, 0]
+    return lib, cand
+
+
+def _model(S, rtol, atol, dtmin=0.0, max_steps=1000, h=0.01, dtmax=0.0):
+    return dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                n_save=S, h=h, max_fitness=1e5, parsimony=0.0, solver=1, max_steps=max_steps, rtol=rtol,
+                atol=atol, dtmin=dtmin, dtmax=dtmax)
+
+
+X0 = np.array([[1.0, 0.0], [0.3, -0.7], [-2.0, 1.5]], np.float32)
+TS = (np.arange(101) * np.float32(0.2)).astype(np.float32)  # SymbolicRegression.ipynb:51 save grid
+
+
+def _exact(x0, t):
+    t = t.astype(np.float64)
+    return np.stack([x0[:, :1] * np.cos(t) + x0[:, 1:] * np.sin(t),
+                     -x0[:, :1] * np.sin(t) + x0[:, 1:] * np.cos(t)], -1)
+
+
+@pytest.mark.parametrize("tol,atol_err", [(1e-6, 2e-5), (1e-4, 4e-3)])
+def test_dopri5_oscillator_known_answer(tol, atol_err):
+    lib, cand = _oscillator()
+    out = orc.evaluate(_model(len(TS), tol, tol, dtmin=0.001), cand, lib,
+                       dict(x0=X0, ts=TS, ys_true=np.zeros((3, len(TS), 2), np.float32)), trajectories=True)
+    xs = out["xs"][0]
+    assert np.all(xs[:, 0] == X0)  # SaveAt ts[0] = y0 exactly
+    np.testing.assert_allclose(xs, _exact(X0, TS), atol=atol_err)
+
+
+def test_dopri5_vs_scipy_rk45():
+    """scipy's RK45 is the same Dormand-Prince pair with an integral controller of the same
+    exponent (-1/5), safety and clip range; step sequences and interpolants differ in detail, so
+    the saved trajectories agree to the tolerance scale, not bit for bit."""
+    from scipy.integrate import solve_ivp
+    lib, cand = _oscillator()
+    tol = 1e-6
+    out = orc.evaluate(_model(len(TS), tol, tol, dtmin=0.001), cand, lib,
+                       dict(x0=X0, ts=TS, ys_true=np.zeros((3, len(TS), 2), np.float32)), trajectories=True)
+    for r in range(3):
+        sol = solve_ivp(lambda t, x: [x[1], -x[0]], (0.0, float(TS[-1])), X0[r].astype(np.float64), method="RK45",
+                        t_eval=TS.astype(np.float64), rtol=tol, atol=tol, first_step=0.01)
+        np.testing.assert_allclose(out["xs"][0, r], sol.y.T, atol=5e-5)
+
+
+def test_dopri5_max_steps_leaves_inf_and_max_fitness():
+    lib, cand = _oscillator()
+    out = orc.evaluate(_model(len(TS), 1e-9, 1e-9, max_steps=20), cand, lib,
+                       dict(x0=X0, ts=TS, ys_true=np.zeros((3, len(TS), 2), np.float32)), trajectories=True)
+    xs = out["xs"][0]
+    assert np.isinf(xs[:, -1]).all()  # t_end never reached within 20 attempts
+    assert np.isfinite(xs[:, :2]).all()
+    assert np.isinf(out["rollout_fitness"][0]).all()
+    assert out["fitness"][0] == np.float32(1e5)
+
+
+def test_dopri5_force_dtmin_equals_fixed_dtmin_steps():
+    """With an unreachable tolerance every attempt is rejected down to dtmin, then force_dtmin
+    accepts: the solve is fixed-step Dopri5 at dtmin after the first shrinking attempts, so it is
+    still close to the exact solution and uses far fewer attempts than the tolerance would."""
+    lib, cand = _oscillator()
+    ts = (np.arange(11) * np.float32(0.2)).astype(np.float32)
+    out = orc.evaluate(_model(len(ts), 0.0, 1e-30, dtmin=0.01, max_steps=400), cand, lib,
+                       dict(x0=X0, ts=ts, ys_true=np.zeros((3, len(ts), 2), np.float32)), trajectories=True)
+    xs = out["xs"][0]
+    assert np.isfinite(xs).all()
+    np.testing.assert_allclose(xs, _exact(X0, ts), atol=1e-5)
+
+
+def test_dopri5_event_terminates_on_blow_up():
+    """dx = x * x blows up in finite time 1/x0: Event(cond_fn_nan) (SR_evaluator.py:93-94) stops
+    the solve after the first accepted non-finite state; later save points are +inf."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0"]], [1])
+    N = 3
+    cand = np.zeros((1, 1, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 2] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 0, N - 1] = [lib.string_to_node["*"], N - 2, N - 2, 0]
+    x0 = np.array([[1.0], [0.1]], np.float32)
+    ts = (np.arange(21) * np.float32(0.1)).astype(np.float32)
+    m = _model(len(ts), 1e-4, 1e-4, dtmin=0.001, max_steps=2000)
+    m["n_var"] = 1
+    out = orc.evaluate(m, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((2, len(ts), 1), np.float32)),
+                       trajectories=True)
+    xs = out["xs"][0, :, :, 0]
+    np.testing.assert_allclose(xs[1, :], 0.1 / (1 - 0.1 * ts), rtol=1e-3)  # no blow-up before t = 10
+    assert np.isfinite(xs[0, :10]).all()  # 1 / (1 - t), t < 1
+    np.testing.assert_allclose(xs[0, :10], 1.0 / (1.0 - ts[:10]), rtol=2e-3)
+    assert np.isinf(xs[0, -1])
+    assert out["fitness"][0] == np.float32((1e5 + out["rollout_fitness"][0, 1]) / 2)
+
+
+def test_solver_selection_api():
+    assert _check_solver(mt.RK4(), None) == "rk4"
+    assert _check_solver("rk4", mt.ConstantStepSize()) == "rk4"
+    pid = mt.PIDController(rtol=1e-6, atol=1e-6, dtmin=0.001)
+    assert _check_solver(mt.Dopri5(), pid, adaptive_ok=True) == "dopri5"
+    with pytest.raises(NotImplementedError):
+        _check_solver(mt.Dopri5(), pid)  # control evaluators: RK4 only
+    with pytest.raises(NotImplementedError):
+        _check_solver(mt.Dopri5(), None, adaptive_ok=True)
+    with pytest.raises(NotImplementedError):
+        mt.PIDController(rtol=1e-3, atol=1e-3, pcoeff=0.3)
+    with pytest.raises(NotImplementedError):
+        mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05, solver=mt.Dopri5(), stepsize_controller=pid)
+    env, lib, ff, data, pop = sr_setup(P=2, R=4, solver=(1e-6, 1e-6, 0.001, 500))
+    d = ff.prepare(data)
+    assert d["solver"] == 1 and d["max_steps"] == 500 and d["dtmin"] == np.float32(0.001)
+    assert d["n_save"] == len(data[1])
+
+
+def test_dopri5_sr_population_oracle_is_deterministic():
+    """random reference-distribution trees (blow-ups, stiff candidates, early events): the
+    population path runs and the per-lane controller gives finite or max fitness everywhere."""
+    env, lib, ff, data, pop = sr_setup(P=16, R=4, seed=3, solver=(1e-6, 1e-6, 0.001, 500))
+    d = ff.prepare(data)
+    a = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    b = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    assert np.array_equal(a["fitness"].view(np.uint32), b["fitness"].view(np.uint32))
+    assert np.all((a["fitness"] >= 0) & (a["fitness"] <= 1e5))
+
+
+# ------------------------------------------------------------------ GPU parity (k_sr_dopri5)
+def _gpu_run(ff, lib, data, pop, jit, traj=True):
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=jit)
+    res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=traj,
+                       rollout_fitness=True)
+    torch.cuda.synchronize()
+    assert DeviceEngine.jit_ok(res["_flat"]) == jit
+    return {k: v.cpu().numpy() for k, v in res.items() if isinstance(v, torch.Tensor)}, eng.prepare_data(data)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+@pytest.mark.parametrize("n_var,tol,R", [(2, 1e-6, 16), (2, 1e-4, 5), (1, 1e-5, 8), (3, 1e-6, 4), (4, 1e-5, 33)])
+def test_gpu_dopri5_sr_bitexact(jit, n_var, tol, R):
+    """Per-lane adaptive steps, rejections, forced dtmin steps, events and max_steps exits on
+    reference-distribution random trees: fitness, per-rollout fitness and the SaveAt(ts)
+    trajectories are bit-identical to the oracle."""
+    from helpers import bits_equal, mismatch_report
+    env, lib, ff, data, pop = sr_setup(P=37, R=R, n_save=26, save_every=4, h=0.01, seed=11 + n_var, n_var=n_var,
+                                       solver=(tol, tol, 0.001, 300))
+    res, d = _gpu_run(ff, lib, data, pop, jit)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, S = pop.shape[0], d["n_save"]
+    xs = res["xs"].reshape(S, n_var, P, R).transpose(2, 3, 0, 1)  # time-major -> [P, R, S, n_var]
+    assert bits_equal(xs, ref["xs"]), mismatch_report(xs, ref["xs"], "xs")
+
+
+@pytest.mark.gpu
+def test_gpu_dopri5_fitness_only_matches_trajectory_mode():
+    from helpers import bits_equal
+    env, lib, ff, data, pop = sr_setup(P=64, R=16, n_save=101, save_every=4, h=0.01, seed=5,
+                                       solver=(1e-6, 1e-6, 0.001, 500))
+    a, _ = _gpu_run(ff, lib, data, pop, True, traj=True)
+    b, _ = _gpu_run(ff, lib, data, pop, True, traj=False)
+    assert bits_equal(a["fitness"], b["fitness"]) and bits_equal(a["rollout_fitness"], b["rollout_fitness"])
