@@ -20,6 +20,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <stdint.h>
+#include <type_traits>
 #include "mtgp.h"
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
@@ -30,15 +31,18 @@
 // Translation units.  The library is compiled from this file several times in parallel
 // (__graft_entry__.build_hip): MTGP_TU=0 holds the C ABI, the Acrobot / SR / JIT / flatten /
 // schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor
-// control kernels behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
+// control kernels (RK4 and Dopri5), MTGP_TU=3 Acrobot's Dopri5 control kernels, behind one hidden
+// C++ entry each.  Without MTGP_TU it is one monolithic TU.
 #ifndef MTGP_TU
 #define MTGP_TU_MAIN 1
 #define MTGP_TU_HARMONIC 1
 #define MTGP_TU_REACTOR 1
+#define MTGP_TU_ACRO_DOPRI5 1
 #else
 #define MTGP_TU_MAIN (MTGP_TU == 0)
 #define MTGP_TU_HARMONIC (MTGP_TU == 1)
 #define MTGP_TU_REACTOR (MTGP_TU == 2)
+#define MTGP_TU_ACRO_DOPRI5 (MTGP_TU == 3)
 #endif
 
 namespace {
@@ -931,6 +935,218 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   finish_group(A, Ln, Env::fit_final(fit, S));
 }
 
+// Dormand-Prince a_ij (include/mtgp_dopri5.h), read with scalar loads by the rolled stage loops
+static __constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
+
+// --------------------------------------------------------------------------------------
+// Control evaluators with adaptive Dopri5 + PIDController (the notebooks' solver,
+// DynamicPolicy.ipynb:105, StaticPolicy.ipynb:102; spec include/mtgp_dopri5.h).  NA > 0: the
+// dynamic evaluator (state [x, a], the RHS of dyn.py:107-118); NA == 0: the static policy
+// (ff.py:104-110).  Per-lane t / step / controller state; every wave-uniform program call (the
+// six FSAL stages, then one call per round of pending save points, then the +inf fill) runs for
+// all lanes, and only the lanes concerned commit.  Save points: dense output of [x, a] at ts[k],
+// then f_obs(ts[k], x) and the save-time readout / policy (dyn.py:99-101, ff.py:96-97).
+template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dopri5(KArgs A) {
+  constexpr int NV = Env::NV;
+  constexpr bool DYN = NA > 0;
+  constexpr int NAX = DYN ? NA : 1;
+  constexpr int ND = NV + NA;  // integrated state
+  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
+  Lane Ln;
+  if (!lane_setup(A, Ln)) return;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* dcol = &lds[Ln.wave][Ln.lane];
+  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  DataVec<JIT> D(dcol, st);
+  if (JIT) asm volatile("s_icache_inv");
+  const int S = A.m.n_save, max_steps = A.m.max_steps;
+  const float rtol = A.m.rtol, atol = A.m.atol, dtmin = A.m.dtmin, dtmax = A.m.dtmax;
+  const float* __restrict__ ts = A.ro.ts;
+  const float t_end = ts[S - 1];
+  ObsNoise<NV> nzc;
+  if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
+  constexpr int uslot = DYN ? NV + NA : NV;  // static: targets follow y directly
+  Env env;
+  env.load(A.ro, rr, A.m.n_targets);
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  const int tslot = DYN ? uslot + 1 : NV;
+#pragma unroll
+  for (int t = 0; t < kDMax; ++t)
+    if (t >= tslot && t - tslot < A.m.n_targets) D.put(t, A.ro.targets[rr * A.m.n_targets + (t - tslot)]);
+  constexpr float E[7] = MTGP_DP_TABLE_E;
+  constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+
+  // RHS at time tc of state s -> ds (dyn.py:107-118 / ff.py:104-110)
+  auto rhs = [&](float tc, const float* s, float* ds) {
+    float y[NV], nzv[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+    if (NOISE) obs_noise_vec<NV>(nzc, tc, nzv);
+    ctl_obs_apply<Env>(s, nzv, y);
+    float ur[1];
+    if (DYN) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) D.put(NV + j, s[NV + j]);
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // reads [0, a, 0, tar]
+      env.drift(s, ur[0], ds);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) D.put(i, y[i]);
+      D.put(uslot, ur[0]);
+      float ka[NAX];
+      run_role<JIT, NAX>(A, Ln, ng, 1, A.m.prog_state, D, ka);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) ds[NV + j] = ka[j];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) D.put(i, y[i]);
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+      env.drift(s, ur[0], ds);
+    }
+  };
+  // one save point of lanes with `on` (wave-uniform call): observation at ts[k], readout, fitness, rows
+  typename Env::Fit fit = Env::fit_init(active);
+  auto save_round = [&](bool on, int k, const float* sk, bool fill) {
+    float y[NV];
+    ctl_obs<Env, NOISE>(nzc, on ? ts[k] : 0.0f, sk, y);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) D.put(i, y[i]);
+    float ur[1];
+    if (DYN) {
+#pragma unroll
+      for (int j = 0; j < NA; ++j) D.put(NV + j, sk[NV + j]);
+      D.put(uslot, 0.0f);
+      run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, ur);  // readout([y, a, 0, tar]) dyn.py:101
+    } else {
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // policy([y, tar]) ff.py:97
+    }
+    if (!on) return;
+    if (!fill) env.fit_update(fit, k, S, ts, ur[0], sk);
+    if (TRAJ && active) {
+      if (A.out.xs) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, sk[i]);
+      }
+      if (A.out.ys) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
+      }
+      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, ur[0]);
+      if (DYN && A.out.acts) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NAX + j) * PR, loff, sk[NV + j]);
+      }
+    }
+  };
+
+  float y[ND], y1[ND], f[7][ND];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
+#pragma unroll
+  for (int j = NV; j < ND; ++j) y[j] = 0.0f;
+  save_round(active, 0, y, false);
+  int k = 1, steps = 0;
+  bool at_dtmin = false, prev_ok = !Env::bad(y, ND);
+  float t = ts[0];
+  float tnext = t + A.m.h;
+  tnext = tnext > t_end ? t_end : tnext;
+  rhs(t, y, f[0]);
+  bool live = active && t < t_end && steps < max_steps;
+  while (__any(live)) {
+    const float h = tnext - t;
+#pragma unroll 1
+    for (int s = 1; s <= 6; ++s) {
+      float yi[ND], fs[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
+        yi[i] = MTGP_FMAF(h, acc, y[i]);
+        y1[i] = yi[i];
+      }
+      rhs(t + mtgp_dp_c(s) * h, yi, fs);
+#pragma unroll
+      for (int j = 1; j < 7; ++j)
+#pragma unroll
+        for (int i = 0; i < ND; ++i) f[j][i] = (j == s) ? fs[i] : f[j][i];
+    }
+    bool keep = false, stop = false;
+    float dt = 0.0f;
+    if (live) {
+      float msum = 0.0f;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
+        const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], rtol, atol);
+        msum = (i == 0) ? sc * sc : msum + sc * sc;
+      }
+      const float ms = msum / (float)ND;
+      keep = (ms < 1.0f) || at_dtmin;
+      dt = h * mtgp_dp_factor(ms, keep);
+      if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
+      if (dtmin > 0.0f) {
+        at_dtmin = dt <= dtmin;
+        dt = dt < dtmin ? dtmin : dt;
+      }
+      ++steps;
+    }
+    // SaveAt(ts) through the dense output of the accepted steps, one save point per round
+    bool sv = live && keep && k < S && ts[k] <= tnext;
+    while (__any(sv)) {
+      float sk[ND];
+      const float th = sv ? (ts[k] - t) / h : 0.0f;
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, CM[j], f[j][i], j == 0);
+        const float ymid = MTGP_FMAF(h, acc, y[i]);
+        sk[i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
+      }
+      save_round(sv, k, sk, false);
+      if (sv) {
+        ++k;
+        sv = k < S && ts[k] <= tnext;
+      }
+    }
+    if (live) {
+      if (keep) {
+        t = tnext;
+#pragma unroll
+        for (int i = 0; i < ND; ++i) {
+          y[i] = y1[i];
+          f[0][i] = f[6][i];  // FSAL
+        }
+        const bool ok = !Env::bad(y, ND);
+        stop = prev_ok && !ok;  // Event(cond_fn_nan), dyn.py:94
+        prev_ok = ok;
+      }
+      if (stop || !(t < t_end) || steps >= max_steps || (!TRAJ && fit.settled)) live = false;
+      else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+    }
+  }
+  // unsaved points are +inf (throw=False); their fitness terms follow Env::fit_kill
+  bool fl = active && k < S;
+  if (fl && !fit.settled) Env::fit_kill(fit);  // (settled: the fitness is already final)
+  if (TRAJ) {
+    float sk[ND];
+#pragma unroll
+    for (int i = 0; i < ND; ++i) sk[i] = kInf;
+    while (__any(fl)) {
+      save_round(fl, k, sk, true);
+      if (fl) fl = ++k < S;
+    }
+  }
+  finish_group(A, Ln, Env::fit_final(fit, S));
+}
+
 // --------------------------------------------------------------------------------------
 // Symbolic regression of an ODE (SR_evaluator.py:57-94): dx_i = tree_i(x); MSE vs ys_true.
 template <int NV, bool TRAJ, bool JIT>
@@ -1014,8 +1230,6 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 // own t, step and accept/reject history; the wave iterates while any lane is still integrating
 // and runs the six new stage RHS evaluations (Dopri5 is FSAL) for all lanes together, since the
 // programs are shared per group.  Lanes that are done keep computing but never commit.
-__constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
-
 template <int NV, bool TRAJ, bool JIT>
 __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
@@ -1600,6 +1814,23 @@ int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 
   return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
 }
 
+// adaptive Dopri5 variants (k_ctl_dopri5): static = NA 0
+template <class Env>
+int launch_ctl_dp(const KArgs& A, const MtgpModel* model, bool jit, bool noise, bool traj, dim3 grid, dim3 block,
+                  hipStream_t s) {
+  if (model->model == MTGP_MODEL_STATIC) return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 0); }, s);
+  switch (model->state_size) {
+    case 1: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 1); }, s);
+    case 2: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 2); }, s);
+    case 3: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 3); }, s);
+    default: return MTGP_ERR_ARG;
+  }
+}
+// Acrobot's Dopri5 kernels live in their own translation unit (MTGP_TU 3)
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_dopri5(const void* A, const MtgpModel* model,
+                                                                        bool jit, bool noise, bool traj,
+                                                                        unsigned grid, unsigned block, hipStream_t s);
+
 // dynamic / static evaluator on environment Env: shape checks, then the kernel variant
 template <class Env>
 int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, bool jit, bool noise, bool traj,
@@ -1610,9 +1841,19 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
   if (model->env != MTGP_ENV_ACROBOT && model->n_targets < 1) return MTGP_ERR_ARG;  // x_d needs the target
   if (model->model == MTGP_MODEL_STATIC) {
     if (NV + model->n_targets > kDMax) return MTGP_ERR_ARG;
-    return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_static, Env); }, s);
+  } else if (NV + model->state_size + 1 + model->n_targets > kDMax) {
+    return MTGP_ERR_ARG;
   }
-  if (NV + model->state_size + 1 + model->n_targets > kDMax) return MTGP_ERR_ARG;
+  if (model->solver == MTGP_SOLVER_DOPRI5) {
+    if constexpr (std::is_same<Env, EnvAcrobot>::value) {
+      int rc = MTGP_OK;
+      const int lr = launch_timed([&] { rc = mtgp_tu_launch_acrobot_dopri5(&A, model, jit, noise, traj, grid.x, block.x, s); }, s);
+      return rc != MTGP_OK ? rc : lr;
+    } else {
+      return launch_ctl_dp<Env>(A, model, jit, noise, traj, grid, block, s);
+    }
+  }
+  if (model->model == MTGP_MODEL_STATIC) return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_static, Env); }, s);
   switch (model->state_size) {
     case 1: return launch_dyn<Env, 1>(A, jit, noise, traj, grid, block, s);
     case 2: return launch_dyn<Env, 2>(A, jit, noise, traj, grid, block, s);
@@ -1628,6 +1869,12 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
       unsigned grid, unsigned block, hipStream_t s
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
+#if MTGP_TU_ACRO_DOPRI5
+int mtgp_tu_launch_acrobot_dopri5(const void* A, const MtgpModel* model, bool jit, bool noise, bool traj, unsigned grid,
+                                  unsigned block, hipStream_t s) {
+  return launch_ctl_dp<EnvAcrobot>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
 #if MTGP_TU_HARMONIC
 int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS) {
   return launch_ctl<EnvHarmonic>(*(const KArgs*)A, model, ro, jit, noise, traj, dim3(grid), dim3(block), s);
@@ -1855,7 +2102,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
   if (model->solver != MTGP_SOLVER_RK4 && !dopri5) return MTGP_ERR_ARG;
   if (dopri5) {  // adaptive: save points come from ts, steps from the controller
-    if (model->model != MTGP_MODEL_SR || model->n_var < 1 || model->n_var > 4) return MTGP_ERR_ARG;
+    if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > 4)) return MTGP_ERR_ARG;
     if (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f)) return MTGP_ERR_ARG;
     if (!(model->rtol >= 0.0f) || !(model->atol >= 0.0f)) return MTGP_ERR_ARG;
   } else {

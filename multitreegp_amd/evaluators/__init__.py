@@ -9,8 +9,8 @@ one launch; these per-candidate calls exist for API parity and trajectory inspec
 
 Solver: BASELINE.json prescribes an explicit fixed-step RK4 (``RK4()`` or "rk4" with
 ``ConstantStepSize()``).  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)``
-(spec include/mtgp_dopri5.h) runs on the GPU for ``SREvaluator`` with
-n_var <= 4; the control evaluators raise NotImplementedError for it.
+(spec include/mtgp_dopri5.h) runs on the GPU for the dynamic and static
+control evaluators (every environment) and for ``SREvaluator`` with n_var <= 4.
 """
 from __future__ import annotations
 
@@ -74,8 +74,7 @@ def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
     cname = None if controller is None else getattr(controller, "name", type(controller).__name__)
     if sname == "dopri5":
         if not adaptive_ok:
-            raise NotImplementedError(f"solver {solver!r}: adaptive Dopri5 is implemented for SREvaluator only "
-                                      "(control evaluators: fixed-step RK4)")
+            raise NotImplementedError(f"solver {solver!r}: adaptive Dopri5 is not implemented here")
         if cname != "PIDController":
             raise NotImplementedError("Dopri5 needs a PIDController (fixed-step Dopri5 is not implemented)")
         return "dopri5"
@@ -117,6 +116,22 @@ def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool 
     if n_steps > max_steps:
         raise ValueError(f"{n_steps} RK4 steps exceed max_steps={max_steps}")
     return n_steps, save_every, S
+
+
+def adaptive_schedule(ts: np.ndarray, acrobot_mask: bool = False) -> Tuple[int, int, int]:
+    """Dopri5: save points straight from ts (SaveAt(ts)), any non-decreasing grid; with
+    acrobot_mask the one-pass Acrobot fitness needs ts[k]/(ts[1]-ts[0]) in (k-1, k+1] as for RK4.
+    -> (n_steps 0, save_every 1, n_save)."""
+    ts = np.asarray(ts, dtype=np.float32)
+    S = int(ts.shape[0])
+    if S < 2 or np.any(np.diff(ts) < 0):
+        raise ValueError("ts needs at least two non-decreasing save points")
+    if acrobot_mask:
+        ratio = ts / np.float32(ts[1] - ts[0])
+        k = np.arange(S, dtype=np.float32)
+        if not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
+            raise NotImplementedError("ts with an offset start (ts[0] != 0 style masks) is not supported")
+    return 0, 1, S
 
 
 def _f32(a) -> np.ndarray:
@@ -188,7 +203,8 @@ class _ControlEvaluator(_CandidateAPI):
     max_fitness = 1e4
 
     def __init__(self, env, dt0: float, solver=None, max_steps: int = 16 ** 4, stepsize_controller=None):
-        _check_solver(solver if solver is not None else RK4(), stepsize_controller)
+        self.solver_kind = _check_solver(solver if solver is not None else RK4(), stepsize_controller,
+                                         adaptive_ok=True)
         name = type(env).__name__
         if name not in ENVIRONMENTS:
             # CartPole / Acrobot2 / ChangingHarmonicOscillator / HarmonicOscillator2 have no
@@ -231,9 +247,14 @@ class _ControlEvaluator(_CandidateAPI):
         tg = _f32(targets).reshape(R, -1)
         if tg.shape[1] != self.env.n_targets:
             raise ValueError(f"targets must be [R, {self.env.n_targets}]")
-        n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps, acrobot_mask=self.env_id == nat.ENV_ACROBOT)
+        acro = self.env_id == nat.ENV_ACROBOT
+        if self.solver_kind == "dopri5":
+            n_steps, save_every, S = adaptive_schedule(ts, acrobot_mask=acro)
+        else:
+            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps, acrobot_mask=acro)
         out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R, n_var=nv, env=self.env_id,
-                   n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code())
+                   n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code(),
+                   **_solver_fields(self.solver_kind, self.stepsize_controller, self.max_steps))
         obs_noise = float(getattr(self.env, "obs_noise", 0.0))
         if obs_noise != 0.0:
             keys = np.ascontiguousarray(np.asarray(obs_keys), dtype=np.uint32)
@@ -315,13 +336,9 @@ class SREvaluator(_CandidateAPI):
         if ys.shape[0] != R or ys.shape[2] != nv:
             raise ValueError("ys must be [R, S, n_var]")
         if self.solver_kind == "dopri5":  # save points straight from ts, steps from the controller
-            ts32 = _f32(ts)
-            S = int(ts32.shape[0])
-            if S < 2 or np.any(np.diff(ts32) < 0):
-                raise ValueError("ts needs at least two non-decreasing save points")
             if nv > 4:
                 raise NotImplementedError("Dopri5 SR is implemented for n_var <= 4 (wide-state SR: RK4)")
-            n_steps, save_every = 0, 1
+            n_steps, save_every, S = adaptive_schedule(ts)
         else:
             n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
         if ys.shape[1] != S:
@@ -346,4 +363,4 @@ class SREvaluator(_CandidateAPI):
 
 
 __all__ = ["RK4", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
-           "rk4_schedule"]
+           "rk4_schedule", "adaptive_schedule"]

@@ -20,8 +20,17 @@ def _mode(name):
     return "Constant" if name == "acrobot" else "Different"
 
 
+def _ctl_solver(solver):
+    """None: fixed-step RK4; (rtol, atol, dtmin, max_steps): Dopri5 + PIDController."""
+    if solver is None:
+        return dict(solver=mt.RK4())
+    rtol, atol, dtmin, max_steps = solver
+    return dict(solver=mt.Dopri5(), max_steps=max_steps,
+                stepsize_controller=mt.PIDController(rtol=rtol, atol=atol, dtmin=dtmin))
+
+
 def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2, obs_noise=0.0, env="acrobot",
-                  h=0.05):
+                  h=0.05, solver=None):
     name = env
     env = make_env(name, obs_noise)
     ys = [f"y{i + 1}" for i in range(env.n_obs)]
@@ -29,18 +38,18 @@ def dynamic_setup(P=24, R=8, n_steps=60, depth=6, N=40, seed=0, state_size=2, ob
     tg = [f"tar{i + 1}" for i in range(env.n_targets)]
     vl = [ys + acts + ["u"] + tg, acts + tg]
     lib = mt.NodeLibrary(CONTROL_OPS, vl, [state_size, 1])
-    ff = mt.DynamicEvaluator(env, state_size, h, solver=mt.RK4())
+    ff = mt.DynamicEvaluator(env, state_size, h, **_ctl_solver(solver))
     data = mt.control_data(env, R, h, None, seed=seed + 1, n_steps=n_steps, mode=_mode(name))
     pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
     return env, lib, ff, data, pop
 
 
-def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0, env="acrobot", h=0.05):
+def static_setup(P=24, R=8, n_steps=60, depth=5, N=30, seed=0, obs_noise=0.0, env="acrobot", h=0.05, solver=None):
     name = env
     env = make_env(name, obs_noise)
     vl = [[f"y{i + 1}" for i in range(env.n_obs)] + [f"tar{i + 1}" for i in range(env.n_targets)]]
     lib = mt.NodeLibrary(CONTROL_OPS, vl, [1])
-    ff = mt.FeedforwardEvaluator(env, h, solver=mt.RK4())
+    ff = mt.FeedforwardEvaluator(env, h, **_ctl_solver(solver))
     data = mt.control_data(env, R, h, None, seed=seed + 1, n_steps=n_steps, mode=_mode(name))
     pop = sample_population(seed, lib, P, 1, max_init_depth=depth, max_nodes=N)[0]
     return env, lib, ff, data, pop

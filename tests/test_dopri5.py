@@ -121,13 +121,13 @@ def test_solver_selection_api():
     pid = mt.PIDController(rtol=1e-6, atol=1e-6, dtmin=0.001)
     assert _check_solver(mt.Dopri5(), pid, adaptive_ok=True) == "dopri5"
     with pytest.raises(NotImplementedError):
-        _check_solver(mt.Dopri5(), pid)  # control evaluators: RK4 only
+        _check_solver(mt.Dopri5(), pid)  # callers that do not opt in
     with pytest.raises(NotImplementedError):
         _check_solver(mt.Dopri5(), None, adaptive_ok=True)
     with pytest.raises(NotImplementedError):
         mt.PIDController(rtol=1e-3, atol=1e-3, pcoeff=0.3)
     with pytest.raises(NotImplementedError):
-        mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05, solver=mt.Dopri5(), stepsize_controller=pid)
+        mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05, solver=mt.Dopri5(), stepsize_controller=mt.ConstantStepSize())
     env, lib, ff, data, pop = sr_setup(P=2, R=4, solver=(1e-6, 1e-6, 0.001, 500))
     d = ff.prepare(data)
     assert d["solver"] == 1 and d["max_steps"] == 500 and d["dtmin"] == np.float32(0.001)
@@ -184,3 +184,51 @@ def test_gpu_dopri5_fitness_only_matches_trajectory_mode():
     a, _ = _gpu_run(ff, lib, data, pop, True, traj=True)
     b, _ = _gpu_run(ff, lib, data, pop, True, traj=False)
     assert bits_equal(a["fitness"], b["fitness"]) and bits_equal(a["rollout_fitness"], b["rollout_fitness"])
+
+
+# ------------------------------------------------------------------ control evaluators
+def test_dopri5_acrobot_oracle_vs_fixed_rk4():
+    """Dynamic Acrobot policy (DynamicPolicy.ipynb:105 solver settings): at a tight tolerance the
+    adaptive trajectories agree with fine fixed-step RK4 up to the chaos of the dynamics (short
+    horizon), and the oracle is deterministic."""
+    from helpers import dynamic_setup
+    env, lib, ff, data, pop = dynamic_setup(P=6, R=4, n_steps=20, seed=2, solver=(1e-7, 1e-7, 0.0001, 4000))
+    d = ff.prepare(data)
+    dp = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    env2, lib2, ff2, data2, pop2 = dynamic_setup(P=6, R=4, n_steps=20, seed=2)
+    d2 = ff2.prepare(data2)
+    rk = orc.evaluate(oracle_model(ff2, d2), pop2, lib2, oracle_rollouts(d2), trajectories=True)
+    fin = np.isfinite(rk["xs"]).all(axis=(2, 3)) & np.isfinite(dp["xs"]).all(axis=(2, 3))
+    assert fin.sum() >= 12
+    np.testing.assert_allclose(dp["xs"][fin][:, :8], rk["xs"][fin][:, :8], atol=2e-3)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+@pytest.mark.parametrize("kind,env,obs_noise,state_size", [
+    ("dynamic", "acrobot", 0.0, 2), ("dynamic", "acrobot", 0.1, 1), ("static", "acrobot", 0.0, 0),
+    ("static", "acrobot", 0.1, 0), ("dynamic", "harmonic", 0.1, 2), ("dynamic", "reactor", 0.0, 3),
+    ("static", "harmonic", 0.0, 0), ("static", "reactor", 0.1, 0)])
+def test_gpu_dopri5_control_bitexact(jit, kind, env, obs_noise, state_size):
+    """The notebooks' Dopri5 + PIDController(1e-4, 1e-4, dtmin=0.001) on every environment, with
+    and without observation noise: fitness, per-rollout fitness and xs/ys/us/acts bit-identical to
+    the oracle (interpolated save points, save-time readout, event and +inf fill)."""
+    from helpers import bits_equal, dynamic_setup, mismatch_report, static_setup
+    solver = (1e-4, 1e-4, 0.001, 300)
+    if kind == "dynamic":
+        e, lib, ff, data, pop = dynamic_setup(P=29, R=6, n_steps=40, seed=3, state_size=state_size,
+                                              obs_noise=obs_noise, env=env, solver=solver)
+    else:
+        e, lib, ff, data, pop = static_setup(P=29, R=6, n_steps=40, seed=3, obs_noise=obs_noise, env=env,
+                                             solver=solver)
+    res, d = _gpu_run(ff, lib, data, pop, jit)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, R, S = pop.shape[0], d["R"], d["n_save"]
+    for k in ("xs", "ys", "us", "acts"):
+        if k not in ref:
+            continue
+        c = ref[k].shape[-1]
+        got = res[k].reshape(S, c, P, R).transpose(2, 3, 0, 1)
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
