@@ -40,6 +40,9 @@ def parse():
     ap.add_argument("--rollouts", type=int, default=None)
     ap.add_argument("--ode-steps", type=int, default=200)
     ap.add_argument("--no-traj", action="store_true", help="fitness-only mode (early exit allowed)")
+    ap.add_argument("--solver", default="rk4", choices=["rk4", "dopri5"],
+                    help="dopri5: the notebooks' Dopri5 + PIDController(rtol=atol=1e-4, dtmin=0.001), max_steps 1000 "
+                         "(DynamicPolicy.ipynb:105 / StaticPolicy.ipynb:102); c2/c3 only")
     ap.add_argument("--obs-noise", type=float, default=0.0,
                     help="Acrobot observation noise (the notebooks use 0.1): in-kernel threefry normals per stage")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -97,16 +100,20 @@ def setup_workload(args, rank):
     env = mt.Acrobot(0.0, getattr(args, "obs_noise", 0.0))
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
            ("cos", None, 1, 0.1)]
+    if args.solver == "dopri5":
+        solver = dict(solver=mt.Dopri5(), stepsize_controller=mt.PIDController(rtol=1e-4, atol=1e-4, dtmin=0.001))
+    else:
+        solver = dict(solver=mt.RK4())
     if args.config == "c2":
         lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4"]], [1])
-        ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4(), max_steps=1000)
+        ff = mt.FeedforwardEvaluator(env, 0.05, max_steps=1000, **solver)
         data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
         pop = _cached_population(f"c2_{args.pop}_r{rank}",
                                  lambda: sample_population(3000 + rank, lib, args.pop, 1, max_init_depth=4,
                                                            max_nodes=30)[0])
         return env, lib, ff, data, pop
     lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
-    ff = mt.DynamicEvaluator(env, 2, 0.05, solver=mt.RK4(), max_steps=1000)
+    ff = mt.DynamicEvaluator(env, 2, 0.05, max_steps=1000, **solver)
     data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
     pop = _cached_population(f"c3_{args.pop}_r{rank}",
                              lambda: sample_population(1000 + rank, lib, args.pop, 1, max_init_depth=10,
@@ -114,7 +121,7 @@ def setup_workload(args, rank):
     return env, lib, ff, data, pop
 
 
-def cpu_baseline(args, lib, ff, data, pop):
+def cpu_baseline(args, lib, ff, data, pop, steps=None):
     """Time the C oracle (OpenMP port of the reference path) on a bounded sample."""
     from oracle import oracle as orc
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -131,9 +138,14 @@ def cpu_baseline(args, lib, ff, data, pop):
         if dt > args.cpu_seconds / 4 or n >= pop.shape[0]:
             break
         n = min(pop.shape[0], int(n * max(2.0, args.cpu_seconds / 4 / max(dt, 1e-3))))
-    units = n * d["R"] * d["n_steps"]
+    if steps is not None:  # Dopri5: the oracle takes exactly the GPU's (bit-identical) steps
+        units = int(steps[:n].sum())
+        what = f"{units} Dopri5 step attempts"
+    else:
+        units = n * d["R"] * d["n_steps"]
+        what = f"{d['n_steps']} RK4 steps"
     return {"value": units / dt, "unit": "ODE-steps/s", "cores": threads, "kind": "port",
-            "sample": f"{n} individuals x {d['R']} rollouts x {d['n_steps']} RK4 steps of the "
+            "sample": f"{n} individuals x {d['R']} rollouts x {what} of the "
                       f"{args.config.upper()} workload, "
                       f"trajectories on, oracle/mtgp_oracle.c row-order interpreter, {threads} OpenMP threads, "
                       f"{dt:.2f} s"}
@@ -160,10 +172,11 @@ def main():
     eng = DeviceEngine(ff, lib, 0.0, dev)
     pop_dev = torch.from_numpy(pop).to(dev)
     traj = not args.no_traj
+    adaptive = args.solver == "dopri5"
     nat.load().mtgp_set_timing(1)
 
     def step():
-        res = eng.evaluate(pop_dev, data, trajectories=traj, check=False)
+        res = eng.evaluate(pop_dev, data, trajectories=traj, check=False, step_counts=adaptive)
         fit = mdist.gather_fitness(res["fitness"], P * ws, P) if ws > 1 else res["fitness"]
         return res, fit
 
@@ -192,7 +205,14 @@ def main():
 
     d = eng.prepare_data(data)
     R, S, n_steps = d["R"], d["n_save"], d["n_steps"]
-    units_per_step = P * R * n_steps * ws
+    steps_host = res["steps"].cpu().numpy() if adaptive else None
+    if adaptive:  # step attempts of this rank; every rank evaluates its own shard of the same size
+        t = torch.tensor([int(steps_host.sum())], dtype=torch.float64, device=dev)
+        if ws > 1:
+            dist.all_reduce(t)
+        units_per_step = float(t.item())
+    else:
+        units_per_step = P * R * n_steps * ws
     value = units_per_step / (ms_per_step / 1e3)
 
     # roofline of the dominant kernel (the fused RK4 evaluator): algorithmic bytes per launch
@@ -207,7 +227,7 @@ def main():
     achieved = alg_bytes / (kmean / 1e3) / 1e9
     traffic = None
     tj = args.traffic_json if args.config == "c3" else args.traffic_json.replace(".json", f"_{args.config}.json")
-    if os.path.exists(tj) and not args.obs_noise:
+    if os.path.exists(tj) and not args.obs_noise and args.solver == "rk4":
         try:
             t = json.load(open(tj))
             if t.get("trajectories", True) == traj:
@@ -251,8 +271,16 @@ def main():
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes},
     }
+    if adaptive:
+        out["metric"] = ("population x rollout ODE-steps/sec (adaptive Dopri5 + PIDController; a step = one step "
+                         "attempt, rejected ones included)")
+        out["config"]["workload"] = out["config"]["workload"].replace(
+            "RK4 h=0.05 x 0", "Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000")
+        out["config"]["ode_steps"] = units_per_step / (P * R * ws)  # mean attempts per rollout
+        out["config"]["solver"] = "dopri5"
+        out["roofline"]["traffic"] = None  # PMC traffic was collected for the RK4 kernel
     if rank == 0 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop)
+        out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if ws > 1:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 8
+#define MTGP_ABI_VERSION 9
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -178,6 +178,8 @@ typedef struct {
   float* ys;              /* [n_save, n_obs, P*R] or NULL (control models)    */
   float* us;              /* [n_save, n_control, P*R] or NULL                 */
   float* acts;            /* [n_save, state_size, P*R] or NULL (dynamic)      */
+  int32_t* steps;         /* [P, R] Dopri5 step attempts (accepted + rejected) or NULL (ABI v9; */
+                          /* the fixed-step RK4 kernels leave it untouched)                      */
 } MtgpOutputs;
 
 /* ------------------------------------------------------------- entry points */

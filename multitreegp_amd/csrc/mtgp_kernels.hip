@@ -1132,6 +1132,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
   }
+  if (active && A.out.steps) A.out.steps[loff] = steps;
   // unsaved points are +inf (throw=False); their fitness terms follow Env::fit_kill
   bool fl = active && k < S;
   if (fl && !fit.settled) Env::fit_kill(fit);  // (settled: the fitness is already final)
@@ -1356,6 +1357,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
       else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
   }
+  if (active && A.out.steps) A.out.steps[loff] = steps;
   if (active) {  // unsaved points are +inf (throw=False)
     float inf[NV];
 #pragma unroll

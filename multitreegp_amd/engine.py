@@ -263,7 +263,8 @@ class DeviceEngine:
 
     # ----------------------------------------------------------------- eval
     def evaluate(self, pop: torch.Tensor, data, trajectories: bool = False, rollout_fitness: bool = False,
-                 flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True) -> dict:
+                 flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True,
+                 step_counts: bool = False) -> dict:
         """Run flatten + fused RK4 kernel.  Returns device tensors:
         fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts time-major [S, c, P*R]).
         schedule: pair expensive with cheap individuals in each wave (results are identical)."""
@@ -303,6 +304,9 @@ class DeviceEngine:
         if rollout_fitness:
             res["rollout_fitness"] = torch.empty((P, R), dtype=torch.float32, device=dev)
             out.rollout_fitness = res["rollout_fitness"].data_ptr()
+        if step_counts:  # Dopri5: step attempts per (individual, rollout)
+            res["steps"] = torch.zeros((P, R), dtype=torch.int32, device=dev)
+            out.steps = res["steps"].data_ptr()
         if trajectories:
             PR = P * R
             if self.ff.model_id == nat.MODEL_SR:

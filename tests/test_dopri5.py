@@ -232,3 +232,21 @@ def test_gpu_dopri5_control_bitexact(jit, kind, env, obs_noise, state_size):
         c = ref[k].shape[-1]
         got = res[k].reshape(S, c, P, R).transpose(2, 3, 0, 1)
         assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+
+
+@pytest.mark.gpu
+def test_gpu_dopri5_step_counts():
+    """MtgpOutputs.steps: attempts per (individual, rollout), within [1, max_steps]; asking for
+    them changes no result."""
+    import torch
+    from helpers import bits_equal, dynamic_setup
+    from multitreegp_amd.engine import DeviceEngine
+    e, lib, ff, data, pop = dynamic_setup(P=40, R=8, n_steps=40, seed=5, solver=(1e-4, 1e-4, 0.001, 250))
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    pd = torch.from_numpy(pop).cuda()
+    a = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True, step_counts=True)
+    b = eng.evaluate(pd, data, trajectories=True, rollout_fitness=True)
+    torch.cuda.synchronize()
+    st = a["steps"].cpu().numpy()
+    assert st.shape == (40, 8) and st.min() >= 1 and st.max() <= 250
+    assert bits_equal(a["rollout_fitness"].cpu().numpy(), b["rollout_fitness"].cpu().numpy())
