@@ -946,8 +946,11 @@ static __constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
 // six FSAL stages, then one call per round of pending save points, then the +inf fill) runs for
 // all lanes, and only the lanes concerned commit.  Save points: dense output of [x, a] at ts[k],
 // then f_obs(ts[k], x) and the save-time readout / policy (dyn.py:99-101, ff.py:96-97).
+#ifndef MTGP_DP_WAVES
+#define MTGP_DP_WAVES 4  // waves per SIMD the Dopri5 control kernels are register-budgeted for
+#endif
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dopri5(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_DP_WAVES))) k_ctl_dopri5(KArgs A) {
   constexpr int NV = Env::NV;
   constexpr bool DYN = NA > 0;
   constexpr int NAX = DYN ? NA : 1;
@@ -981,7 +984,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   constexpr float CM[7] = MTGP_DP_TABLE_CMID;
 
   // RHS at time tc of state s -> ds (dyn.py:107-118 / ff.py:104-110)
-  auto rhs = [&](float tc, const float* s, float* ds) {
+  auto rhs = [&](float tc, const float* s, float* ds) __attribute__((always_inline)) {
     float y[NV], nzv[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
@@ -1009,7 +1012,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   };
   // one save point of lanes with `on` (wave-uniform call): observation at ts[k], readout, fitness, rows
   typename Env::Fit fit = Env::fit_init(active);
-  auto save_round = [&](bool on, int k, const float* sk, bool fill) {
+  auto save_round = [&](bool on, int k, const float* sk, bool fill) __attribute__((always_inline)) {
     float y[NV];
     ctl_obs<Env, NOISE>(nzc, on ? ts[k] : 0.0f, sk, y);
 #pragma unroll
@@ -1253,7 +1256,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
   constexpr float CM[7] = MTGP_DP_TABLE_CMID;
   float tot = 0.0f;
   // one save point: MSE term (components in index order, sr.py:24) and the trajectory row
-  auto save = [&](int k, const float* v) {
+  auto save = [&](int k, const float* v) __attribute__((always_inline)) {
     float sq = 0.0f;
 #pragma unroll
     for (int d = 0; d < NV; ++d) {
@@ -1266,7 +1269,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
       for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d]);
     }
   };
-  auto bad = [&](const float* v) {
+  auto bad = [&](const float* v) __attribute__((always_inline)) {
     bool b = false;
 #pragma unroll
     for (int i = 0; i < NV; ++i) b = b || !mtgp_isfinite(v[i]);
