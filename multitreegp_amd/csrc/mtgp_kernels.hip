@@ -947,7 +947,7 @@ static __constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
 // all lanes, and only the lanes concerned commit.  Save points: dense output of [x, a] at ts[k],
 // then f_obs(ts[k], x) and the save-time readout / policy (dyn.py:99-101, ff.py:96-97).
 #ifndef MTGP_DP_WAVES
-#define MTGP_DP_WAVES 4  // waves per SIMD the Dopri5 control kernels are register-budgeted for
+#define MTGP_DP_WAVES 2  // register budget of the Dopri5 control kernels (A/B: 2 beats 4, C3 23 vs 28 ms)
 #endif
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_DP_WAVES))) k_ctl_dopri5(KArgs A) {
