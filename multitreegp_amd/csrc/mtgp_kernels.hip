@@ -1542,18 +1542,21 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
 }
 
 // --------------------------------------------------------------------------------------
-// Flatten: one thread per (individual, program spec); per-row scratch in LDS.
+// Flatten: one thread per (individual, program spec); per-row scratch in private memory.
+#ifndef MTGP_FLATTEN_TPB
+#define MTGP_FLATTEN_TPB 32
+#endif
 template <int NMAX>
 __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, int P, int T, int N,
                                                 MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                 int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                 int32_t* nodes_out, int32_t* status_out) {
   // per-lane row table in private memory: an LDS table (28 B x NMAX x 64 lanes = 112 KB at
-  // NMAX = 64) allowed one wave per CU; private arrays let the flatten run at full occupancy
-  constexpr int TPB = 64;
+  // NMAX = 64) allowed one wave per CU; private arrays let the flatten run at full occupancy.
+  // Launched with MTGP_FLATTEN_TPB-lane blocks: the per-lane walk is latency-bound, so spreading
+  // P*n_prog lanes over twice the waves (C3: 512 -> 1024, one per SIMD) shortens the launch.
   mtgp::RowInfo info_priv[NMAX];
-  const int t_in = threadIdx.x;
-  const long gid = (long)blockIdx.x * TPB + t_in;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const long total = (long)P * n_prog;
   if (gid >= total) return;
   const int p = (int)(gid / n_prog), j = (int)(gid % n_prog);
@@ -1565,11 +1568,11 @@ __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, i
   const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
   len_out[(size_t)p * n_prog + j] = n > 0 ? n : 0;
   status_out[(size_t)p * n_prog + j] = n > 0 ? 0 : -n;
-  if (j == 0) {
-    int c = 0;
-    for (int t = 0; t < T; ++t) c += mtgp::count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
-    nodes_out[p] = c;
-  }
+  // node count (gp.py:424 parsimony): the individual's trees are shared out over its n_prog
+  // lanes (tree t -> lane t % n_prog) and summed with integer atomics into the zeroed nodes_out
+  int c = 0;
+  for (int t = j; t < T; t += n_prog) c += mtgp::count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
+  if (c != 0) atomicAdd(&nodes_out[p], c);
 }
 
 // --------------------------------------------------------------------------------------
@@ -2030,18 +2033,18 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const
   hipStream_t s = (hipStream_t)stream;
   const long total = (long)P * n_prog;
   MtgpNodeLibrary libv = *lib;
+  if (hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+  const int tpb = MTGP_FLATTEN_TPB;  // one lane per program
+  const dim3 grid((unsigned)((total + tpb - 1) / tpb)), block(tpb);
   if (N <= 64) {
-    const int tpb = 64;  // one lane per program (k_flatten TPB)
-    hipLaunchKernelGGL(k_flatten<64>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T, N,
-                       libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+    hipLaunchKernelGGL(k_flatten<64>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
+                       len_out, nodes_out, status_out);
   } else if (N <= 128) {
-    const int tpb = 64;
-    hipLaunchKernelGGL(k_flatten<128>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
-                       N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+    hipLaunchKernelGGL(k_flatten<128>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
+                       len_out, nodes_out, status_out);
   } else {
-    const int tpb = 64;
-    hipLaunchKernelGGL(k_flatten<256>, dim3((unsigned)((total + tpb - 1) / tpb)), dim3(64), 0, s, population, P, T,
-                       N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out);
+    hipLaunchKernelGGL(k_flatten<256>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
+                       len_out, nodes_out, status_out);
   }
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
