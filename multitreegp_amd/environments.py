@@ -227,3 +227,21 @@ def jax_control_data(key, env, batch_size: int, dt: float, T: float = None, n_st
         ts = (np.arange(n_steps + 1, dtype=np.float32) * np.float32(dt)).astype(np.float32)
     params = env.sample_params(batch_size, "Constant", ts, None)
     return x0, ts, targets, prng.split(nk1, batch_size), prng.split(nk2, batch_size), params
+
+
+def jax_sr_data(key, env, batch_size: int, T: float, dt: float = 0.2, ground_truth_h: float = 1e-3):
+    """SymbolicRegression.ipynb get_data restated with the JAX-compatible host PRNG:
+        x_key, noise_key = jr.split(key)
+        x0s = env.sample_init_states(batch_size, x_key)   (VanDerPol: 0 + 1 * normal(x_key, (batch, 2)))
+        noise_keys = jr.split(noise_key, batch_size)
+        ts = jnp.arange(0, T, 0.2)
+        xs = vmap(diffeqsolve(Dopri5, PIDController(1e-7, 1e-7, dtmin=0.001), dt0=0.001))(x0s)
+    The ground-truth trajectories come from a fine float64 RK4 (`ground_truth`) instead of
+    the notebook's float32 Dopri5 at tolerance 1e-7: both approximate the exact solution far
+    below the MSE scale the SR fitness resolves.  -> (x0s, ts, xs, noise_keys)."""
+    key = np.asarray(key, np.uint32)
+    x_key, noise_key = prng.split(key)
+    x0 = prng.normal(x_key, (batch_size, env.n_var))
+    ts = np.arange(0, T, dt, dtype=np.float32)
+    xs = ground_truth(env, x0, ts, h=ground_truth_h)
+    return x0, ts, xs, prng.split(noise_key, batch_size)

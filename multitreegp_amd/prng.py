@@ -115,3 +115,36 @@ def uniform(key, shape=(), minval=0.0, maxval=1.0) -> np.ndarray:
     f = ((bits >> np.uint32(9)) | np.uint32(0x3F800000)).view(np.float32) - np.float32(1.0)
     v = (f * (hi - lo) + lo).astype(np.float32)
     return np.maximum(lo, v).astype(np.float32)
+
+
+# XLA ErfInv32 (Giles 2010, single precision) coefficients, as include/mtgp_prng.h
+_ERFINV_SMALL = (2.81022636e-08, 3.43273939e-07, -3.5233877e-06, -4.39150654e-06, 0.00021858087, -0.00125372503,
+                 -0.00417768164, 0.246640727, 1.50140941)
+_ERFINV_LARGE = (-0.000200214257, 0.000100950558, 0.00134934322, -0.00367342844, 0.00573950773, -0.0076224613,
+                 0.00943887047, 1.00167406, 2.83297682)
+
+
+def _erfinv(x: np.ndarray) -> np.ndarray:
+    """float32 erfinv by Giles' polynomial in w = -log1p(-x^2) (host log1p: the C library's)."""
+    x = np.asarray(x, np.float32)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        w = -np.log1p(-(x * x)).astype(np.float32)
+        ws = (w - np.float32(2.5)).astype(np.float32)
+        wl = (np.sqrt(w) - np.float32(3.0)).astype(np.float32)
+        ps = np.full_like(x, np.float32(_ERFINV_SMALL[0]))
+        pl = np.full_like(x, np.float32(_ERFINV_LARGE[0]))
+        for cs, cl in zip(_ERFINV_SMALL[1:], _ERFINV_LARGE[1:]):
+            ps = (np.float32(cs) + ps * ws).astype(np.float32)
+            pl = (np.float32(cl) + pl * wl).astype(np.float32)
+        r = (np.where(w < np.float32(5.0), ps, pl) * x).astype(np.float32)
+    return np.where(np.abs(x) == np.float32(1.0), x * np.float32(np.inf), r).astype(np.float32)
+
+
+def normal(key, shape=()) -> np.ndarray:
+    """jax.random.normal in float32 (jax/_src/random.py _normal_real):
+    u = uniform(key, shape, minval=nextafter(-1, 0), maxval=1); sqrt(2) * erf_inv(u).
+    The device's own draws (observation noise) use include/mtgp_prng.h; this host helper
+    builds initial states (SymbolicRegression.ipynb get_data: VanDerPol x0 ~ N(0, 1))."""
+    lo = np.nextafter(np.float32(-1.0), np.float32(0.0))
+    u = uniform(key, shape, lo, np.float32(1.0))
+    return (np.float32(np.sqrt(2.0)) * _erfinv(u)).astype(np.float32)

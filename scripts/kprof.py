@@ -21,7 +21,7 @@ ap.add_argument("--lib", default=nat.LIB_PATH)
 ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
 a = ap.parse_args()
 env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=200,
-                                                                      config=a.config), 0)
+                                                                      config=a.config, solver="rk4", obs_noise=0.0), 0)
 eng = DeviceEngine(ff, lib, 0.0, "cuda:0", native=nat.load(a.lib))
 pd = torch.from_numpy(pop).cuda()
 for _ in range(a.iters):

@@ -108,3 +108,39 @@ def mismatch_report(a, b, name):
     diff = ~((a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b)))
     idx = np.argwhere(diff)
     return f"{name}: {diff.sum()} / {diff.size} differ; first {idx[:5].tolist()} gpu={a[tuple(idx[0])] if len(idx) else None} ref={b[tuple(idx[0])] if len(idx) else None}"
+
+
+def tree_from_expr(expr, lib, N=30):
+    """Reference [N, 4] tree (root at row N-1, descending rows = preorder, a_idx = k-1,
+    b_idx = k-1-|subtree(a)|, empty rows packed at the bottom; initialization.py:46-49,
+    gp.py:272-296) from a nested tuple: ("op", child[, child]), a variable name or a float
+    coefficient."""
+    rows = []
+
+    def pre(e):
+        if isinstance(e, str):
+            rows.append([lib.string_to_node[e], -1, -1, 0.0])
+            return 1
+        if isinstance(e, (float, np.floating)):
+            rows.append([1, -1, -1, float(e)])
+            return 1
+        op, *children = e
+        at = len(rows)
+        rows.append(None)
+        sizes = [pre(c) for c in children]
+        rows[at] = (op, sizes)
+        return 1 + sum(sizes)
+
+    pre(expr)
+    if len(rows) > N:
+        raise ValueError(f"{len(rows)} nodes > max_nodes {N}")
+    t = np.zeros((N, 4), np.float32)
+    t[:, 1:3] = -1
+    for i, r in enumerate(rows):
+        k = N - 1 - i
+        if isinstance(r, tuple):
+            op, sizes = r
+            t[k] = [lib.string_to_node[op], k - 1, (k - 1 - sizes[0]) if len(sizes) == 2 else -1, 0.0]
+        else:
+            t[k] = r
+    return t
