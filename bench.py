@@ -34,8 +34,8 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pop", type=int, default=None, help="individuals per GPU (default: the config's)")
     ap.add_argument("--rollouts", type=int, default=None)
     ap.add_argument("--ode-steps", type=int, default=200)
@@ -47,7 +47,8 @@ def parse():
                     help="Acrobot observation noise (the notebooks use 0.1): in-kernel threefry normals per stage")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--no-pmc", action="store_true",
+                    help="skip the live rocprofv3 PMC passes (HBM traffic, VALU issue) of the dominant kernel")
     a = ap.parse_args()
     defaults = {"c2": (1024, 16), "c3": (8192, 32), "c5": (4096, 8)}[a.config]
     a.pop = a.pop or defaults[0]
@@ -121,6 +122,50 @@ def setup_workload(args, rank):
     return env, lib, ff, data, pop
 
 
+def cpu_model() -> str:
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def pmc_passes(args, kernel_substr):
+    """Live rocprofv3 PMC of the dominant kernel on this same workload (rank 0, N = 1), one
+    counter group per pass as MI355X_MICROARCH.md's HBM/rocprofv3 section prescribes:
+      FETCH_SIZE (KiB, x2: gfx950 counts half of a wide coalesced read) | WRITE_SIZE (KiB) |
+      SQ_INSTS_VALU, SQ_WAVES, GRBM_GUI_ACTIVE (sum over 8 XCDs -> / 8 = kernel cycles).
+    Each pass is a child process (scripts/kprof.py, one evaluation) under a hard time limit;
+    any failure leaves the field null.  -> dict or None"""
+    import shutil
+    import subprocess
+    import tempfile
+    rp = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(rp):
+        return None
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from pmc_summary import collect
+    cmd_tail = ["--", sys.executable, os.path.join(ROOT, "scripts", "kprof.py"), "--iters", "1", "--config",
+                args.config, "--pop", str(args.pop), "--rollouts", str(args.rollouts), "--solver", args.solver,
+                "--obs-noise", str(args.obs_noise), "--ode-steps", str(args.ode_steps)] + \
+        (["--no-traj"] if args.no_traj else [])
+    out = {}
+    with tempfile.TemporaryDirectory(prefix="mtgp_pmc_") as d:
+        for i, counters in enumerate((["FETCH_SIZE"], ["WRITE_SIZE"], ["SQ_INSTS_VALU", "SQ_WAVES", "GRBM_GUI_ACTIVE"])):
+            sub = os.path.join(d, f"p{i}")
+            cmd = ["timeout", "-s", "KILL", "90", rp, "--pmc", *counters, "-d", sub, "-o", "p",
+                   "--output-format", "csv"] + cmd_tail
+            try:
+                subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=120)
+            except Exception:
+                return None
+            out.update(collect(sub, kernel_substr))
+    need = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")
+    return out if all(k in out for k in need) else None
+
+
 def cpu_baseline(args, lib, ff, data, pop, steps=None):
     """Time the C oracle (OpenMP port of the reference path) on a bounded sample."""
     from oracle import oracle as orc
@@ -145,10 +190,11 @@ def cpu_baseline(args, lib, ff, data, pop, steps=None):
         units = n * d["R"] * d["n_steps"]
         what = f"{d['n_steps']} RK4 steps"
     return {"value": units / dt, "unit": "ODE-steps/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"{n} individuals x {d['R']} rollouts x {what} of the "
                       f"{args.config.upper()} workload, "
-                      f"trajectories on, oracle/mtgp_oracle.c row-order interpreter, {threads} OpenMP threads, "
-                      f"{dt:.2f} s"}
+                      f"trajectories on, oracle/mtgp_oracle.c row-order interpreter, {threads} OpenMP threads "
+                      f"of {os.cpu_count()} on {cpu_model()}, {dt:.2f} s"}
 
 
 def main():
@@ -225,15 +271,19 @@ def main():
     alg_bytes = traj_bytes + prog_bytes + io_bytes
     kmean = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kmean / 1e3) / 1e9
-    traffic = None
-    tj = args.traffic_json if args.config == "c3" else args.traffic_json.replace(".json", f"_{args.config}.json")
-    if os.path.exists(tj) and not args.obs_noise and args.solver == "rk4":
-        try:
-            t = json.load(open(tj))
-            if t.get("trajectories", True) == traj:
-                traffic = t.get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    traffic = valu = None
+    pmc = None
+    if rank == 0 and ws == 1 and not args.no_pmc:
+        kname = {"c3": "k_ctl_dynamic", "c2": "k_ctl_static", "c5": "k_sr_wide"}[args.config]
+        if adaptive:
+            kname = "k_ctl_dopri5"
+        pmc = pmc_passes(args, kname)
+    if pmc is not None:
+        # HBM bytes per launch (FETCH x2 gfx950 correction, KiB -> B) and the VALU issue fraction:
+        # wave64 VALU = 2 cycles on a SIMD-32 -> at most 0.5 wave-instructions per SIMD-cycle
+        traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
+        kcycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
+        valu = pmc["SQ_INSTS_VALU"] / (1024 * 0.5 * kcycles) if kcycles > 0 else None
     workloads = {
         "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, 3 trees, max_nodes 64, depth<=10, "
               "RK4 h=0.05 x %d, S=%d" % (P, R, n_steps, S),
@@ -269,7 +319,11 @@ def main():
         "kernel_ms": kmean,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes},
+                     "alg_bytes_per_launch": alg_bytes,
+                     "valu_frac": valu,
+                     "pmc": None if pmc is None else {k: pmc[k] for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
+                                                                           "SQ_WAVES", "GRBM_GUI_ACTIVE")
+                                                      if k in pmc}},
     }
     if adaptive:
         out["metric"] = ("population x rollout ODE-steps/sec (adaptive Dopri5 + PIDController; a step = one step "
@@ -278,7 +332,6 @@ def main():
             "RK4 h=0.05 x 0", "Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000")
         out["config"]["ode_steps"] = units_per_step / (P * R * ws)  # mean attempts per rollout
         out["config"]["solver"] = "dopri5"
-        out["roofline"]["traffic"] = None  # PMC traffic was collected for the RK4 kernel
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 9
+#define MTGP_ABI_VERSION 10
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -137,18 +137,21 @@ typedef struct {
                              /* 0 threefry original (JAX <= 0.4.x default),        */
                              /* 1 threefry partitionable (JAX >= 0.5 default)      */
   int32_t env;               /* control models: MTGP_ENV_* (0 = Acrobot)            */
-  /* Solver (ABI v8).  MTGP_SOLVER_RK4: fixed step h, n_steps / save_every as above (BASELINE).
+  /* Solver.  MTGP_SOLVER_RK4: fixed step h, n_steps / save_every as above (BASELINE).
+   * MTGP_SOLVER_EULER (ABI v10): diffrax.Euler + ConstantStepSize, the reference evaluators'
+   * default (dyn.py:11, ff.py:11, sr.py:21): y1 = y0 + f(t0, y0) * h, same step grid as RK4.
    * MTGP_SOLVER_DOPRI5: diffrax.Dopri5 + PIDController(rtol, atol, dtmin, dtmax) from dt0 = h
    * with SaveAt(ts) and at most max_steps step attempts (include/mtgp_dopri5.h, the notebooks'
    * setting, e.g. SymbolicRegression.ipynb:136); n_steps / save_every are ignored.  Implemented
-   * for MTGP_MODEL_SR with n_var <= 4; other models return MTGP_ERR_ARG. */
+   * for the dynamic and static control models (every MTGP_ENV_*) and for MTGP_MODEL_SR with
+   * n_var <= 4. */
   int32_t solver;
   int32_t max_steps; /* Dopri5: accepted + rejected steps before the solve gives up      */
   float rtol, atol;  /* PIDController tolerances                                         */
   float dtmin;       /* <= 0: None; else force_dtmin: steps at dtmin are always accepted */
   float dtmax;       /* <= 0: None                                                       */
 } MtgpModel;
-enum { MTGP_SOLVER_RK4 = 0, MTGP_SOLVER_DOPRI5 = 1 };
+enum { MTGP_SOLVER_RK4 = 0, MTGP_SOLVER_DOPRI5 = 1, MTGP_SOLVER_EULER = 2 };
 
 typedef struct {
   const float* x0;      /* [R, n_var]                                       */
@@ -187,7 +190,8 @@ int mtgp_abi_version(void);
 
 /* Flatten a device population f32 [P, T, N, 4] (gp.py:412 layout) into programs
  * prog_out[P, n_prog, L], lengths len_out[P, n_prog], node counts nodes_out[P]
- * (non-empty rows, gp.py:424) and per-program status_out[P, n_prog]. */
+ * (non-empty rows, gp.py:424) and per-program status_out[P, n_prog].  nodes_out is zeroed
+ * by mtgp_flatten itself (stream-ordered memset) before the kernel accumulates into it. */
 int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N,
                  const MtgpNodeLibrary* lib, const MtgpProgramSpec* specs, int32_t n_prog,
                  int32_t L, MtgpInstr* prog_out, int32_t* len_out, int32_t* nodes_out,
@@ -274,8 +278,9 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
                       const MtgpRollouts* rollouts, const MtgpOutputs* out, const MtgpJitCode* jit,
                       void* stream);
 
-/* Wall time of the last mtgp_eval_rk4 kernel on `stream`, measured with hipEvents
- * recorded around the launch (ms); -1 if none.  Synchronises that event. */
+/* Wall time of the calling thread's last timed mtgp_eval_rk4 kernel (ms), measured with
+ * hipEvents recorded on its stream around the launch; -1 if none.  Synchronises that event.
+ * The on/off switch (mtgp_set_timing) is process-wide; events are per host thread and device. */
 float mtgp_last_kernel_ms(void);
 int mtgp_set_timing(int enabled);
 

@@ -12,7 +12,8 @@
  * what lets the parity tests compare GPU and CPU trajectories exactly even though the
  * Acrobot is chaotic (SURVEY.md §7 "Hard parts" 1).
  *
- *   mtgp_sinf / mtgp_cosf : |error| <= ~2 ulp over the whole float range
+ *   mtgp_sinf / mtgp_cosf : |error| <= ~2 ulp over the whole float range; reduction onto
+ *       the pi grid (sin: x - 2k pi/2, cos: x - (2k+1) pi/2) and one odd polynomial (spec v2)
  *       |x| < 2^-12        : sin x = x, cos x = 1
  *       |x| < 2^17         : 3-constant float Cody-Waite reduction with fma (exact first step)
  *       |x| < 2^28         : 3-constant double Cody-Waite reduction
@@ -77,23 +78,30 @@ MTGP_INLINE MTGP_HD int mtgp_isfinite(float x) { return (mtgp_f2u(x) & 0x7f80000
 MTGP_INLINE MTGP_HD int mtgp_isnan(float x) { return (mtgp_f2u(x) & 0x7fffffffu) > 0x7f800000u; }
 MTGP_INLINE MTGP_HD float mtgp_qnan(void) { return mtgp_u2f(0x7fc00000u); }
 
-/* ---- polynomial kernels on |r| <= pi/4 (+ slack), Taylor, evaluated with fma ---- */
+/* ---- sin / cos on the pi grid (spec v2) ------------------------------------------------
+ * Both functions reduce to r = x - j*pi/2 with j of a fixed parity -- j = 2k (sin) or
+ * j = 2k+1 (cos), k = rint(x/pi) or rint(x/pi - 1/2) -- so |r| <= pi/2 (+ rounding slack) and
+ * ONE odd polynomial serves both:
+ *     sin x = (-1)^k sin r,      cos x = (-1)^(k+1) sin r,
+ * i.e. the result is sin_poly(r) with the sign bit flipped by bit 0 of (k + [cos]).  The
+ * polynomial is r + r^3 (c3 + c5 s + c7 s^2 + c9 s^3), s = r^2, a relative-error fit on
+ * |r| <= 1.0021 pi/2 with f32 coefficients (approximation error 6.3e-9, ~0.1 ulp; fit script
+ * scripts/fit_sin_poly.py).  One polynomial per lane instead of two plus quadrant selects;
+ * zeros of both functions are at r = 0, so relative accuracy near them is kept. */
+#define MTGP_SIN_C3 -1.66666597127914428711e-01f
+#define MTGP_SIN_C5 8.33306834101676940918e-03f
+#define MTGP_SIN_C7 -1.98096662643365561962e-04f
+#define MTGP_SIN_C9 2.60578394772892352194e-06f
+#define MTGP_INV_PI_F 3.18309873342514038086e-01f /* f32(1/pi) */
+#define MTGP_TRIG_FAST_MAX 131072.0f              /* 2^17: float Cody-Waite range */
+
 MTGP_INLINE MTGP_HD float mtgp_sin_poly(float r) {
-  const float r2 = r * r;
-  float p = 2.75573192e-06f;               /*  1/9!  */
-  p = MTGP_FMAF(p, r2, -1.98412698e-04f);  /* -1/7!  */
-  p = MTGP_FMAF(p, r2, 8.33333377e-03f);   /*  1/5!  */
-  p = MTGP_FMAF(p, r2, -1.66666672e-01f);  /* -1/3!  */
-  return MTGP_FMAF(r * r2, p, r);
-}
-MTGP_INLINE MTGP_HD float mtgp_cos_poly(float r) {
-  const float r2 = r * r;
-  float p = -2.75573188e-07f;              /* -1/10! */
-  p = MTGP_FMAF(p, r2, 2.48015876e-05f);   /*  1/8!  */
-  p = MTGP_FMAF(p, r2, -1.38888892e-03f);  /* -1/6!  */
-  p = MTGP_FMAF(p, r2, 4.16666679e-02f);   /*  1/4!  */
-  p = MTGP_FMAF(p, r2, -5.0e-01f);         /* -1/2!  */
-  return MTGP_FMAF(r2, p, 1.0f);
+  const float s = r * r;
+  float p = MTGP_SIN_C9;
+  p = MTGP_FMAF(p, s, MTGP_SIN_C7);
+  p = MTGP_FMAF(p, s, MTGP_SIN_C5);
+  p = MTGP_FMAF(p, s, MTGP_SIN_C3);
+  return MTGP_FMAF(r * s, p, r);
 }
 
 /* 2/pi, 384 bits, most significant word first (checked against mpmath in tests). */
@@ -119,10 +127,12 @@ MTGP_INLINE MTGP_HD uint32_t mtgp_twoopi_word(int k) {
 #endif
 }
 
-/* Payne-Hanek for finite |x| >= 2^28: |x| = m * 2^e (24-bit m, e >= 5).  The 96-bit window
- * W of 2/pi bits [b+1, b+96] with b = e - 2 makes m*W*2^-94 = |x|*2/pi mod 4 with the binary
- * point at a FIXED bit (94) of the product, so no limb is indexed dynamically. */
-MTGP_INLINE MTGP_HD float mtgp_reduce_payne_hanek(float ax, int* quadrant) {
+/* Payne-Hanek for finite |x| >= 2^28 (|x| = m * 2^e, 24-bit m, e >= 5): the 96-bit window W
+ * of 2/pi bits [b+1, b+96], b = e - 2, makes m*W*2^-94 = |x|*2/pi mod 4 with the binary point
+ * at a FIXED bit (94) of the product, so no limb is indexed dynamically.  v = |x|*2/pi mod 4
+ * = vi + f (vi = 0..3, f in [0, 1) as 64 fraction bits); the nearest j of parity `odd` is vi
+ * when vi has it (r = f pi/2), else vi + 1 (r = (f - 1) pi/2).  Returns r, *j = j mod 4. */
+MTGP_INLINE MTGP_HD float mtgp_reduce_payne_hanek_pi(float ax, int odd, int* j) {
   const uint32_t u = mtgp_f2u(ax);
   const uint32_t m = (u & 0x7fffffu) | 0x800000u;
   const int e = (int)((u >> 23) & 0xffu) - 150;
@@ -136,83 +146,84 @@ MTGP_INLINE MTGP_HD float mtgp_reduce_payne_hanek(float ax, int* quadrant) {
   const uint64_t lo = (uint64_t)m * Wlo;
   const uint64_t mid = (uint64_t)m * Wmid + (lo >> 32);
   const uint64_t hi = (uint64_t)m * Whi + (mid >> 32);
-  uint32_t quad = (uint32_t)(hi >> 30) & 3u;
+  const int vi = (int)((hi >> 30) & 3u);
   const uint64_t frac = ((hi & 0x3fffffffull) << 34) | ((mid & 0xffffffffull) << 2) | ((lo & 0xffffffffull) >> 30);
-  /* round to the nearest quadrant: f in [-1/2, 1/2) */
-  if (frac & 0x8000000000000000ull) quad = (quad + 1u) & 3u;
-  const double fd = (double)(int64_t)frac * 5.42101086242752217e-20; /* 2^-64 */
-  *quadrant = (int)quad;
-  return (float)(fd * 1.57079632679489656e+00);
+  double f = (double)frac * 5.42101086242752217e-20; /* 2^-64 */
+  int jj = vi;
+  if ((vi & 1) != odd) { jj = vi + 1; f = f - 1.0; }
+  *j = jj & 3;
+  return (float)(f * 1.57079632679489656e+00);
 }
 
-/* slow reduction for finite |x| >= 2^17: returns r, quadrant in *q */
-MTGP_INLINE MTGP_HD float mtgp_reduce_slow(float x, int* q) {
+/* slow reduction for finite |x| >= 2^17 onto the pi grid of parity `odd` (0 sin, 1 cos):
+ * r, and j mod 4 in *j */
+MTGP_INLINE MTGP_HD float mtgp_reduce_pi_slow(float x, int odd, int* j) {
   const float ax = MTGP_FABSF(x);
   if (ax < 268435456.0f) { /* 2^28: double Cody-Waite, 24+24+53-bit pi/2, first steps exact */
     const double xd = (double)x;
-    const double j = MTGP_RINT(xd * 6.3661977236758138e-01);
-    double r = xd - j * 1.570796251296997e+00;
-    r = r - j * 7.549789415861596e-08;
-    r = r - j * 5.390302858158119e-15;
-    *q = ((int)(int64_t)j) & 3;
+    const double k = MTGP_RINT(xd * 3.1830988618379069e-01 - (odd ? 0.5 : 0.0)); /* 1/pi */
+    const double jd = 2.0 * k + (odd ? 1.0 : 0.0);
+    double r = xd - jd * 1.570796251296997e+00;
+    r = r - jd * 7.549789415861596e-08;
+    r = r - jd * 5.390302858158119e-15;
+    *j = ((int)(int64_t)jd) & 3;
     return (float)r;
   }
-  int qq;
-  float r = mtgp_reduce_payne_hanek(ax, &qq);
-  if (x < 0.0f) { r = -r; qq = (4 - qq) & 3; }
-  *q = qq;
+  int jj;
+  float r = mtgp_reduce_payne_hanek_pi(ax, odd, &jj);
+  if (x < 0.0f) { r = -r; jj = (4 - jj) & 3; }
+  *j = jj;
   return r;
 }
 
-/* Reduction to r (|r| <~ pi/4) and quadrant.  The float Cody-Waite fast path runs
- * unconditionally (exact first step for |x| < 2^17; it yields NaN for non-finite x); lanes
- * with finite |x| >= 2^17 are redone by the slow path behind ONE wave-uniform branch. */
-MTGP_INLINE MTGP_HD float mtgp_reduce(float x, int* q) {
+/* sin (odd = 0) or cos (odd = 1) on the pi grid, fast path: exact spec result for |x| < 2^17
+ * (f32 Cody-Waite with the 3-constant pi/2 split, exact first step) and for non-finite x (NaN);
+ * *slow = 1 for the lanes (finite |x| >= 2^17) that need mtgp_trig_pi_slow instead.  Callers
+ * evaluating several arguments test all their slow flags with ONE wave-uniform branch.
+ * |x| < 2^-12: sin x = x (keeps -0 and denormals), cos x = 1. */
+MTGP_INLINE MTGP_HD float mtgp_trig_pi_fast(float x, int odd, int* slow) {
   const float ax = MTGP_FABSF(x);
-  const float j = MTGP_RINTF(x * 6.36619747e-01f); /* f32(2/pi) */
+  const float t = x * MTGP_INV_PI_F;
+  const float k = MTGP_RINTF(odd ? t - 0.5f : t);
+  const float j = odd ? MTGP_FMAF(k, 2.0f, 1.0f) : k + k;
   float r = MTGP_FMAF(j, -1.57079637e+00f, x);
   r = MTGP_FMAF(j, 4.37113883e-08f, r);
   r = MTGP_FMAF(j, 1.71512451e-15f, r);
-  const int fast = ax < 131072.0f;
-  int qq = fast ? (((int)j) & 3) : 0;
-  const int slow = !fast && mtgp_isfinite(x);
+  const int fast = ax < MTGP_TRIG_FAST_MAX;
+#if defined(__HIP_DEVICE_COMPILE__)
+  const int ki = (int)k; /* v_cvt_i32_f32 saturates (NaN -> 0): defined for every lane */
+#else
+  const int ki = fast ? (int)k : 0;
+#endif
+  *slow = !fast && mtgp_isfinite(x);
+  /* sign: bit 0 of k + odd (= bit 1 of j + odd) */
+  const float v = mtgp_u2f(mtgp_f2u(mtgp_sin_poly(r)) ^ ((uint32_t)(ki + odd) << 31));
+  return (ax < 2.44140625e-04f) ? (odd ? 1.0f : x) : v; /* 2^-12 */
+}
+
+/* the slow lanes: finite |x| >= 2^17 (double Cody-Waite below 2^28, Payne-Hanek above) */
+MTGP_INLINE MTGP_HD float mtgp_trig_pi_slow(float x, int odd) {
+  int ji;
+  const float r = mtgp_reduce_pi_slow(x, odd, &ji);
+  return mtgp_u2f(mtgp_f2u(mtgp_sin_poly(r)) ^ ((uint32_t)(ji + odd) << 30 & 0x80000000u));
+}
+
+MTGP_INLINE MTGP_HD float mtgp_trig_pi(float x, int odd) {
+  int slow;
+  float v = mtgp_trig_pi_fast(x, odd, &slow);
   if (MTGP_ANY(slow)) {
-    if (slow) r = mtgp_reduce_slow(x, &qq);
+    if (slow) v = mtgp_trig_pi_slow(x, odd);
   }
-  *q = qq;
-  return r;
+  return v;
 }
 
-/* sin and cos of x sharing one reduction; |x| < 2^-12 -> (x, 1); non-finite -> NaN */
+MTGP_INLINE MTGP_HD float mtgp_sinf(float x) { return mtgp_trig_pi(x, 0); }
+MTGP_INLINE MTGP_HD float mtgp_cosf(float x) { return mtgp_trig_pi(x, 1); }
+
+/* sin and cos of one x (bit-identical to mtgp_sinf / mtgp_cosf) */
 MTGP_INLINE MTGP_HD void mtgp_sincosf(float x, float* s, float* c) {
-  int q;
-  const float r = mtgp_reduce(x, &q);
-  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
-  float sv = (q & 1) ? pc : ps;
-  float cv = (q & 1) ? ps : pc;
-  sv = (q & 2) ? -sv : sv;
-  cv = ((q + 1) & 2) ? -cv : cv;
-  const int tiny = MTGP_FABSF(x) < 2.44140625e-04f; /* 2^-12: keeps -0 and denormals */
-  *s = tiny ? x : sv;
-  *c = tiny ? 1.0f : cv;
-}
-
-MTGP_INLINE MTGP_HD float mtgp_sinf(float x) {
-  int q;
-  const float r = mtgp_reduce(x, &q);
-  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
-  float v = (q & 1) ? pc : ps;
-  v = (q & 2) ? -v : v;
-  return (MTGP_FABSF(x) < 2.44140625e-04f) ? x : v;
-}
-
-MTGP_INLINE MTGP_HD float mtgp_cosf(float x) {
-  int q;
-  const float r = mtgp_reduce(x, &q);
-  const float ps = mtgp_sin_poly(r), pc = mtgp_cos_poly(r);
-  float v = (q & 1) ? ps : pc;
-  v = ((q + 1) & 2) ? -v : v;
-  return (MTGP_FABSF(x) < 2.44140625e-04f) ? 1.0f : v;
+  *s = mtgp_trig_pi(x, 0);
+  *c = mtgp_trig_pi(x, 1);
 }
 
 /* large |a|: exact binary long division by power-of-two multiples of b (rare path) */

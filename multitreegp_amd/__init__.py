@@ -6,7 +6,7 @@ interprets the programs inside a fixed-step RK4 integrator (multitreegp_amd/csrc
 """
 from .node_library import NodeLibrary  # noqa: F401
 from .environments import Acrobot, HarmonicOscillator, StirredTankReactor, VanDerPolOscillator, LinearSystem, control_data, ground_truth  # noqa: F401
-from .evaluators import (RK4, ConstantStepSize, Dopri5, PIDController, DynamicEvaluator, FeedforwardEvaluator,  # noqa: F401
+from .evaluators import (RK4, Euler, ConstantStepSize, Dopri5, PIDController, DynamicEvaluator, FeedforwardEvaluator,  # noqa: F401
                          SREvaluator)
 from .genetic_programming import GeneticProgramming, TreeEvaluator  # noqa: F401
 

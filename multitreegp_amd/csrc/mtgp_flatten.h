@@ -75,9 +75,23 @@ MTGP_INLINE MTGP_HD int fn_arity(int fn) {
   return (fn >= MTGP_FN_ADD && fn <= MTGP_FN_DIV) ? 2 : ((fn == MTGP_FN_SIN || fn == MTGP_FN_COS) ? 1 : 0);
 }
 
-// Resolve row i of `tree` ([N,4] f32) into info[i]; rows < i must be resolved already.
+// Rows whose value is the constant 0.0 without any lookup: f != 1.0 and int(f) (clamped) an
+// empty / zero opcode (gp.py:135).  Such rows below the root get no RowInfo: a reference to one
+// (j < i, already "evaluated") is the constant 0.0, exactly what its RowInfo would fold to.
+// zrows: bitmask over rows (N <= MTGP_MAX_NODES = 256).
+MTGP_INLINE MTGP_HD bool zero_row(const float* tree, int i, const MtgpNodeLibrary* lib) {
+  const float fv = tree[4 * i + 0];
+  if (fv == 1.0f) return false;
+  int32_t f = f2i_sat(fv);
+  if (f < 0) f = 0;
+  if (f > lib->n_funcs - 1) f = lib->n_funcs - 1;
+  return lib->fn[f] == MTGP_FN_ZERO;
+}
+
+// Resolve row i of `tree` ([N,4] f32) into info[i]; rows < i must be resolved already (or be
+// zero rows marked in zrows).
 MTGP_INLINE MTGP_HD void resolve_row(const float* tree, int N, int i, const MtgpNodeLibrary* lib,
-                                     int n_data, uint64_t zero_mask, RowInfo* info) {
+                                     int n_data, uint64_t zero_mask, RowInfo* info, const uint64_t* zrows) {
   RowInfo& r = info[i];
   const float fv = tree[4 * i + 0];
   r.afirst = 1;
@@ -112,7 +126,8 @@ MTGP_INLINE MTGP_HD void resolve_row(const float* tree, int N, int i, const Mtgp
   for (int k = 0; k < ar; ++k) {
     const int j = norm_index(tree[4 * i + 1 + k], N);
     Ref ref;
-    if (j < i) { ref.row = (int16_t)j; ref.val = 0.0f; }
+    if (j < i && ((zrows[j >> 6] >> (j & 63)) & 1ull)) { ref.row = -1; ref.val = 0.0f; }  // evaluated zero row
+    else if (j < i) { ref.row = (int16_t)j; ref.val = 0.0f; }
     else { ref.row = -1; ref.val = tree[4 * j + 3]; }  // not evaluated yet: original column
     if (k == 0) r.a = ref; else r.b = ref;
   }
@@ -318,8 +333,13 @@ MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* o
 MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNodeLibrary* lib,
                                           int n_data, uint64_t zero_mask, MtgpInstr* out, int cap,
                                           RowInfo* info, int* stack_need) {
+  uint64_t zrows[(MTGP_MAX_NODES + 63) / 64] = {0};
   for (int i = 0; i < N; ++i) {
-    resolve_row(tree, N, i, lib, n_data, zero_mask, info);
+    if (i < N - 1 && zero_row(tree, i, lib)) {  // empty rows (most of a reference tree): no RowInfo
+      zrows[i >> 6] |= 1ull << (i & 63);
+      continue;
+    }
+    resolve_row(tree, N, i, lib, n_data, zero_mask, info, zrows);
     size_row(i, info);
   }
   const int need = info[N - 1].need;

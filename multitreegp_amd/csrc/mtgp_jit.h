@@ -42,7 +42,7 @@ constexpr uint32_t kJitSrcLiteral = 255u;
 constexpr uint32_t kVop2Add = 1u, kVop2Sub = 2u, kVop2Subrev = 3u, kVop2Mul = 5u;
 constexpr uint32_t kSetpcS30 = 0xbe801d1eu;  // s_setpc_b64 s[30:31]
 // largest translation of one program instruction (push + two moves + the sin template)
-constexpr int kJitMaxWordsPerInstr = 1 + 4 + MTGP_JIT_SIN_WORDS;
+constexpr int kJitMaxWordsPerInstr = 1 + 4 + (MTGP_JIT_COS_WORDS > MTGP_JIT_SIN_WORDS ? MTGP_JIT_COS_WORDS : MTGP_JIT_SIN_WORDS);
 
 // The sin/cos templates are shared subroutines at the start of the code buffer (one copy,
 // hot in the instruction cache); generated code calls them with a PC-relative address.

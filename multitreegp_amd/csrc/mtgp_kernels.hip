@@ -20,6 +20,8 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <stdint.h>
+#include <atomic>
+#include <mutex>
 #include <type_traits>
 #include "mtgp.h"
 #include "mtgp_f32math.h"
@@ -30,19 +32,23 @@
 
 // Translation units.  The library is compiled from this file several times in parallel
 // (__graft_entry__.build_hip): MTGP_TU=0 holds the C ABI, the Acrobot / SR / JIT / flatten /
-// schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor
-// control kernels (RK4 and Dopri5), MTGP_TU=3 Acrobot's Dopri5 control kernels, behind one hidden
-// C++ entry each.  Without MTGP_TU it is one monolithic TU.
+// schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor RK4
+// control kernels, MTGP_TU=3 / 4 / 5 the Dopri5 control kernels of Acrobot / HarmonicOscillator /
+// StirredTankReactor, behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
 #ifndef MTGP_TU
 #define MTGP_TU_MAIN 1
 #define MTGP_TU_HARMONIC 1
 #define MTGP_TU_REACTOR 1
 #define MTGP_TU_ACRO_DOPRI5 1
+#define MTGP_TU_HARMONIC_DOPRI5 1
+#define MTGP_TU_REACTOR_DOPRI5 1
 #else
 #define MTGP_TU_MAIN (MTGP_TU == 0)
 #define MTGP_TU_HARMONIC (MTGP_TU == 1)
 #define MTGP_TU_REACTOR (MTGP_TU == 2)
 #define MTGP_TU_ACRO_DOPRI5 (MTGP_TU == 3)
+#define MTGP_TU_HARMONIC_DOPRI5 (MTGP_TU == 4)
+#define MTGP_TU_REACTOR_DOPRI5 (MTGP_TU == 5)
 #endif
 
 namespace {
@@ -130,14 +136,25 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
                                            float dx[4]) {
   const float control = mtgp_clip1(u_raw);
   const float th1 = x[0], th2 = x[1], thd1 = x[2], thd2 = x[3];
-  float s2, c2;
-  mtgp_sincosf(th2, &s2, &c2);  // == (mtgp_sinf(th2), mtgp_cosf(th2)) bit-for-bit
-  const float s1 = mtgp_sinf(th1);
+  // the five trig values of the drift (mtgp_sinf / mtgp_cosf bit for bit), with ONE wave-uniform
+  // test for lanes that need the slow reduction (|arg| >= 2^17)
+  const float ea = (th1 + th2) - MTGP_HALF_PI_F, eb = th1 - MTGP_HALF_PI_F;
+  int f0, f1, f2, f3, f4;
+  float s2 = mtgp_trig_pi_fast(th2, 0, &f0), c2 = mtgp_trig_pi_fast(th2, 1, &f1);
+  float s1 = mtgp_trig_pi_fast(th1, 0, &f2);
+  float ca = mtgp_trig_pi_fast(ea, 1, &f3), cb = mtgp_trig_pi_fast(eb, 1, &f4);
+  if (__builtin_expect(__any(f0 | f1 | f2 | f3 | f4), 0)) {
+    s2 = mtgp_sinf(th2);
+    c2 = mtgp_cosf(th2);
+    s1 = mtgp_sinf(th1);
+    ca = mtgp_cosf(ea);
+    cb = mtgp_cosf(eb);
+  }
   const float d1 = ((k.d1a + k.m2 * (k.l1sq_lc2sq + k.two_l1lc2 * c2)) + 1.0f) + 1.0f;
   const float d2 = k.m2 * (k.lc2sq + k.l1lc2 * c2) + 1.0f;
-  const float phi2 = k.m2lc2g * mtgp_cosf((th1 + th2) - MTGP_HALF_PI_F);
+  const float phi2 = k.m2lc2g * ca;
   const float phi1 = (((k.A0 * (thd2 * thd2)) * s2 - ((k.B0 * thd1) * thd2) * s1) +
-                      k.C0 * mtgp_cosf(th1 - MTGP_HALF_PI_F)) + phi2;
+                      k.C0 * cb) + phi2;
   const float num = ((control + (d2 / d1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
   const float den = k.den0 - (d2 * d2) / d1;
   const float a2 = num / den;
@@ -259,7 +276,14 @@ struct AcroFit {
 __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool incl, float u,
                                                 float x0, float x1) {
   if (f.settled) return;
-  const bool reached = ((-mtgp_cosf(x0)) - mtgp_cosf(x0 + x1)) > 1.5f;
+  int fa, fb;
+  const float x01 = x0 + x1;
+  float ca = mtgp_trig_pi_fast(x0, 1, &fa), cb = mtgp_trig_pi_fast(x01, 1, &fb);
+  if (__builtin_expect(__any(fa | fb), 0)) {
+    ca = mtgp_cosf(x0);
+    cb = mtgp_cosf(x01);
+  }
+  const bool reached = ((-ca) - cb) > 1.5f;
   const float cost = (u * 0.01f) * u;
   if (k == 0) {
     f.c0incl = incl ? cost : 0.0f;
@@ -548,6 +572,15 @@ __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], 
   return acc;
 }
 
+#ifndef MTGP_V_NOPROG
+#define MTGP_V_NOPROG 0
+#endif
+#ifndef MTGP_V_NOFALLBACK
+#define MTGP_V_NOFALLBACK 0  // diagnostic only: ignore the JIT's slow-lane report (A/B), never shipped
+#endif
+#ifndef MTGP_V_UNROLL
+#define MTGP_V_UNROLL 0
+#endif
 #ifndef MTGP_V_TIMING
 #define MTGP_V_TIMING 0  // diagnostic only: per-wave start/end clock + HW_ID (residency study), never shipped
 #endif
@@ -603,8 +636,13 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
       for (int q = 0; q < M; ++q) {
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first + q);
         uint64_t fl = 0;
+#if MTGP_V_NOPROG  // diagnostic only: the environment without any program call (A/B), never shipped
+        (void)off;
+        float v = 0.0f;
+#else
         float v = jit_call(A.jit_base + off, D.v, fl);
-        if (__builtin_expect(fl != 0, 0)) {  // lanes that need the Payne-Hanek sin/cos: re-run only
+#endif
+        if (!MTGP_V_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: re-run only
           bool spilled = false;               // this program, only for the groups concerned
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(L.g == gi && L.active))) continue;
@@ -728,12 +766,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     prev_ok = !Env::bad(s0, NV + NA);
   }
 
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
+  const int n_stages = euler ? 1 : 4;
   for (int step = 0;; ++step) {
     const bool last = step == n_steps;
     const bool is_save = (step % save_every) == 0;
     bool stop = last;
+#if MTGP_V_UNROLL
+#pragma unroll
+#else
 #pragma unroll 1
-    for (int stage = 0; stage < 4; ++stage) {
+#endif
+    for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
 #pragma unroll
       for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
@@ -814,9 +858,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     if (!dead) {
       float sn[NV + NA];
 #pragma unroll
-      for (int i = 0; i < NV; ++i) { x[i] = MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+      for (int i = 0; i < NV; ++i) { x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
 #pragma unroll
-      for (int j = 0; j < NA; ++j) { a[j] = MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
+      for (int j = 0; j < NA; ++j) { a[j] = euler ? a[j] + aa[j] * h : MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
       const bool ok = !Env::bad(sn, NV + NA);
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
@@ -865,12 +909,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   bool dead = !active, pending = false;
   bool prev_ok = !Env::bad(x, NV);
 
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
+  const int n_stages = euler ? 1 : 4;
   for (int step = 0;; ++step) {
     const bool last = step == n_steps;
     const bool is_save = (step % save_every) == 0;
     bool stop = last;
 #pragma unroll 1
-    for (int stage = 0; stage < 4; ++stage) {
+    for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
 #pragma unroll
       for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
@@ -926,7 +972,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     if (stop) break;
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
+      for (int i = 0; i < NV; ++i) x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
       const bool ok = !Env::bad(x, NV);
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
@@ -1181,6 +1227,8 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   };
   bool dead = !active, pending = false, prev_ok = !bad(x);
   float tot = 0.0f;
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
+  const int n_stages = euler ? 1 : 4;
   for (int step = 0;; ++step) {
     if ((step % save_every) == 0) {
       const int k = step / save_every;
@@ -1208,7 +1256,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       break;
     }
 #pragma unroll 1
-    for (int stage = 0; stage < 4; ++stage) {
+    for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], h, h2));
       run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
@@ -1217,7 +1265,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
     }
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = MTGP_FMAF(h6, ax[i], x[i]);
+      for (int i = 0; i < NV; ++i) x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
       const bool ok = !bad(x);
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
@@ -1446,6 +1494,8 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   bool dead = !active, pending = false;
   bool prev_ok = !any_bad();  // (its barrier also publishes cur)
   float tot = 0.0f;
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
+  const int n_stages = euler ? 1 : 4;
   for (int step = 0;; ++step) {
     if ((step % save_every) == 0) {
       const int k = step / save_every;
@@ -1480,7 +1530,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       break;
     }
 #pragma unroll 1
-    for (int stage = 0; stage < 4; ++stage) {
+    for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; k parks in nxt
       for (int t = 0; t < kWideComp; ++t) {
         const int c = c0 + t;
@@ -1503,7 +1553,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
     }
     if (!dead) {
 #pragma unroll
-      for (int t = 0; t < kWideComp; ++t) x[t] = MTGP_FMAF(h6, ax[t], x[t]);
+      for (int t = 0; t < kWideComp; ++t) x[t] = euler ? x[t] + ax[t] * h : MTGP_FMAF(h6, ax[t], x[t]);
     }
 #pragma unroll
     for (int t = 0; t < kWideComp; ++t)
@@ -1546,6 +1596,7 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
 #ifndef MTGP_FLATTEN_TPB
 #define MTGP_FLATTEN_TPB 32
 #endif
+static_assert(MTGP_FLATTEN_TPB > 0 && MTGP_FLATTEN_TPB <= 64, "k_flatten is built for blocks of at most 64 lanes");
 template <int NMAX>
 __global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, int P, int T, int N,
                                                 MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
@@ -1633,7 +1684,6 @@ __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict
 
 #endif  // MTGP_TU_MAIN
 
-hipEvent_t g_ev0 = nullptr, g_ev1 = nullptr;
 #if MTGP_TU_MAIN
 // --------------------------------------------------------------------------------------
 // Program JIT build (mtgp_jit.h): one unit of code per (wave, role).  Pass 1 sizes every
@@ -1780,18 +1830,37 @@ hsa_status_t jit_find_pool(hsa_amd_memory_pool_t p, void* data) {
 
 #endif  // MTGP_TU_MAIN
 
-bool g_timing = false;
-bool g_have_timing = false;
+// Kernel timing (mtgp_set_timing / mtgp_last_kernel_ms): the switch is process-wide, the event
+// pair and the "last launch" record are per host thread and re-created when the thread moves to
+// another device, so concurrent callers on different threads / streams / devices never share
+// events.
+std::atomic<bool> g_timing{false};
+struct TimingState {
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  int device = -1;
+  bool have = false;
+};
+thread_local TimingState t_timing;
 
 template <class F>
 int launch_timed(F&& launch, hipStream_t s) {
-  if (g_timing) {
-    if (!g_ev0) { (void)hipEventCreate(&g_ev0); (void)hipEventCreate(&g_ev1); }
-    (void)hipEventRecord(g_ev0, s);
+  const bool timing = g_timing.load(std::memory_order_relaxed);
+  TimingState& ts = t_timing;
+  if (timing) {
+    int dev = -1;
+    (void)hipGetDevice(&dev);
+    if (!ts.ev0 || ts.device != dev) {
+      if (ts.ev0) { (void)hipEventDestroy(ts.ev0); (void)hipEventDestroy(ts.ev1); }
+      (void)hipEventCreate(&ts.ev0);
+      (void)hipEventCreate(&ts.ev1);
+      ts.device = dev;
+      ts.have = false;
+    }
+    (void)hipEventRecord(ts.ev0, s);
   }
   launch();
   if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
-  if (g_timing) { (void)hipEventRecord(g_ev1, s); g_have_timing = true; }
+  if (timing) { (void)hipEventRecord(ts.ev1, s); ts.have = true; }
   return MTGP_OK;
 }
 
@@ -1834,10 +1903,18 @@ int launch_ctl_dp(const KArgs& A, const MtgpModel* model, bool jit, bool noise, 
     default: return MTGP_ERR_ARG;
   }
 }
-// Acrobot's Dopri5 kernels live in their own translation unit (MTGP_TU 3)
-__attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_dopri5(const void* A, const MtgpModel* model,
-                                                                        bool jit, bool noise, bool traj,
-                                                                        unsigned grid, unsigned block, hipStream_t s);
+// every environment's Dopri5 kernels live in their own translation unit (MTGP_TU 3, 4, 5)
+#define MTGP_TU_DP_ARGS \
+  const void* A, const MtgpModel* model, bool jit, bool noise, bool traj, unsigned grid, unsigned block, hipStream_t s
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_dopri5(MTGP_TU_DP_ARGS);
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic_dopri5(MTGP_TU_DP_ARGS);
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor_dopri5(MTGP_TU_DP_ARGS);
+template <class Env>
+int launch_dp_entry(MTGP_TU_DP_ARGS) {
+  if constexpr (std::is_same<Env, EnvAcrobot>::value) return mtgp_tu_launch_acrobot_dopri5(A, model, jit, noise, traj, grid, block, s);
+  else if constexpr (std::is_same<Env, EnvHarmonic>::value) return mtgp_tu_launch_harmonic_dopri5(A, model, jit, noise, traj, grid, block, s);
+  else return mtgp_tu_launch_reactor_dopri5(A, model, jit, noise, traj, grid, block, s);
+}
 
 // dynamic / static evaluator on environment Env: shape checks, then the kernel variant
 template <class Env>
@@ -1853,13 +1930,9 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
     return MTGP_ERR_ARG;
   }
   if (model->solver == MTGP_SOLVER_DOPRI5) {
-    if constexpr (std::is_same<Env, EnvAcrobot>::value) {
-      int rc = MTGP_OK;
-      const int lr = launch_timed([&] { rc = mtgp_tu_launch_acrobot_dopri5(&A, model, jit, noise, traj, grid.x, block.x, s); }, s);
-      return rc != MTGP_OK ? rc : lr;
-    } else {
-      return launch_ctl_dp<Env>(A, model, jit, noise, traj, grid, block, s);
-    }
+    int rc = MTGP_OK;
+    const int lr = launch_timed([&] { rc = launch_dp_entry<Env>(&A, model, jit, noise, traj, grid.x, block.x, s); }, s);
+    return rc != MTGP_OK ? rc : lr;
   }
   if (model->model == MTGP_MODEL_STATIC) return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_static, Env); }, s);
   switch (model->state_size) {
@@ -1878,9 +1951,18 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
 #if MTGP_TU_ACRO_DOPRI5
-int mtgp_tu_launch_acrobot_dopri5(const void* A, const MtgpModel* model, bool jit, bool noise, bool traj, unsigned grid,
-                                  unsigned block, hipStream_t s) {
+int mtgp_tu_launch_acrobot_dopri5(MTGP_TU_DP_ARGS) {
   return launch_ctl_dp<EnvAcrobot>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+#if MTGP_TU_HARMONIC_DOPRI5
+int mtgp_tu_launch_harmonic_dopri5(MTGP_TU_DP_ARGS) {
+  return launch_ctl_dp<EnvHarmonic>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+#if MTGP_TU_REACTOR_DOPRI5
+int mtgp_tu_launch_reactor_dopri5(MTGP_TU_DP_ARGS) {
+  return launch_ctl_dp<EnvReactor>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
 }
 #endif
 #if MTGP_TU_HARMONIC
@@ -1916,11 +1998,10 @@ int mtgp_debug_probe(uint64_t* host, size_t n) {  // diagnostic variant only
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code) {
   if (!code || bytes == 0) return MTGP_ERR_ARG;
   *code = nullptr;
-  static bool hsa_ready = false;
-  if (!hsa_ready) {
-    if (hsa_init() != HSA_STATUS_SUCCESS) return MTGP_ERR_LAUNCH;
-    hsa_ready = true;
-  }
+  static std::once_flag hsa_once;  // thread-safe one-time HSA runtime init (HIP already holds a reference)
+  static hsa_status_t hsa_rc = HSA_STATUS_ERROR;
+  std::call_once(hsa_once, [] { hsa_rc = hsa_init(); });
+  if (hsa_rc != HSA_STATUS_SUCCESS) return MTGP_ERR_LAUNCH;
   int bus = 0, dev = 0, dom = 0;
   if (hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, device) != hipSuccess ||
       hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, device) != hipSuccess ||
@@ -2016,10 +2097,11 @@ int mtgp_set_timing(int enabled) {
 }
 
 float mtgp_last_kernel_ms(void) {
-  if (!g_have_timing) return -1.0f;
+  const TimingState& ts = t_timing;  // this thread's last timed launch
+  if (!ts.have) return -1.0f;
   float ms = -1.0f;
-  (void)hipEventSynchronize(g_ev1);
-  (void)hipEventElapsedTime(&ms, g_ev0, g_ev1);
+  (void)hipEventSynchronize(ts.ev1);
+  (void)hipEventElapsedTime(&ms, ts.ev0, ts.ev1);
   return ms;
 }
 
@@ -2108,7 +2190,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   if ((int64_t)P * rollouts->R > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
   if ((int64_t)P * n_prog * L * (int64_t)sizeof(MtgpInstr) > UINT32_MAX) return MTGP_ERR_ARG;  // 32-bit program offsets
   const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
-  if (model->solver != MTGP_SOLVER_RK4 && !dopri5) return MTGP_ERR_ARG;
+  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;
   if (dopri5) {  // adaptive: save points come from ts, steps from the controller
     if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > 4)) return MTGP_ERR_ARG;
     if (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f)) return MTGP_ERR_ARG;

@@ -8,10 +8,21 @@ for the host-side argmin / evolution.  There is no other collective on the data 
 """
 from __future__ import annotations
 
+import os
 from typing import Callable, Tuple
 
 import torch
 import torch.distributed as dist
+
+
+def local_device() -> torch.device:
+    """This process's GPU: cuda:LOCAL_RANK under torchrun (one process per GPU), else the current
+    device.  The engines bind to it, so ranks never share GPU 0 by accident."""
+    lr = os.environ.get("LOCAL_RANK")
+    if lr is not None:
+        n = torch.cuda.device_count()
+        return torch.device("cuda", int(lr) % max(n, 1))
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def world() -> Tuple[int, int]:
@@ -33,15 +44,16 @@ def gather_fitness(local: torch.Tensor, P: int, per: int, group=None) -> torch.T
     rank, ws = world()
     if ws == 1:
         return local[:P]
+    if dist.get_backend(group) == "gloo":  # CPU path: gloo takes host tensors, no all_gather_into_tensor
+        buf = torch.full((per,), float("inf"), dtype=local.dtype)
+        buf[: local.numel()] = local.cpu()
+        parts = [torch.empty_like(buf) for _ in range(ws)]
+        dist.all_gather(parts, buf, group=group)
+        return torch.cat(parts)[:P]
     buf = torch.full((per,), float("inf"), dtype=local.dtype, device=local.device)
     buf[: local.numel()] = local
     out = torch.empty((per * ws,), dtype=local.dtype, device=local.device)
-    if dist.get_backend(group) == "gloo":  # CPU test path: gloo has no all_gather_into_tensor
-        parts = list(out.chunk(ws))
-        dist.all_gather(parts, buf, group=group)
-        out = torch.cat(parts)
-    else:
-        dist.all_gather_into_tensor(out, buf, group=group)
+    dist.all_gather_into_tensor(out, buf, group=group)  # RCCL over xGMI
     return out[:P]
 
 

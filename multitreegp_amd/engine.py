@@ -22,7 +22,11 @@ from .node_library import NodeLibrary
 def _require_gpu(device) -> torch.device:
     if not torch.cuda.is_available():
         raise RuntimeError("multitreegp_amd needs a ROCm GPU (MI355X); no CPU fallback exists")
-    d = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if device is None:
+        from .distributed import local_device
+        d = local_device()  # cuda:LOCAL_RANK under torchrun
+    else:
+        d = torch.device(device)
     if d.type != "cuda":
         raise ValueError(f"device {d} is not a GPU device")
     return d
@@ -42,7 +46,7 @@ class Flattened:
     n_prog: int
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
     jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity) of the JIT
-    jit_key: Optional[tuple] = None       # (R, roles, order) the JIT units were built for
+    jit_key: Optional[tuple] = None       # (R, order, engine id, arena slot, arena generation) of that code
 
 
 class DeviceEngine:
@@ -64,6 +68,7 @@ class DeviceEngine:
         self.use_jit = (os.environ.get("MTGP_JIT", "1") != "0") if jit is None else bool(jit)
         self._arenas = [None, None]  # (pointer, bytes): a ring of two executable code buffers
         self._arena_i = 0
+        self._arena_gen = [0, 0]     # bumped whenever a slot is (re)written: stale Flattened code is rebuilt
         self._jit_last = None        # (pinned host info, event) of the previous build: capacity hint
         self._jit_bytes_per_unit = None  # learnt from earlier plans (None: estimate from G)
 
@@ -83,6 +88,7 @@ class DeviceEngine:
         """Next buffer of the executable ring, grown when needed.  Alternating buffers keeps the code
         of the previous population untouched while a new one is written (stream-ordered)."""
         self._arena_i ^= 1
+        self._arena_gen[self._arena_i] += 1
         a = self._arenas[self._arena_i]
         if a is None or a[1] < nbytes:
             if a is not None:
@@ -103,10 +109,12 @@ class DeviceEngine:
         without a host round trip: the buffer is sized from the code size per program seen in
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
-        key = (R, None if order is None else order.data_ptr())
-        if fl.jit_key == key:
-            return fl.jit
-        fl.jit_key, fl.jit = key, None
+        key = (R, None if order is None else order.data_ptr(), id(self))
+        if fl.jit_key is not None and fl.jit_key[:3] == key:
+            slot, gen = fl.jit_key[3:]
+            if slot is None or self._arena_gen[slot] == gen:  # code still in place (or none was built)
+                return fl.jit
+        fl.jit_key, fl.jit = key + (None, None), None
         if not self.use_jit or self.ff.n_data() > 8 or (m.model == nat.MODEL_SR and m.n_var > 4):
             return None
         P = fl.prog.shape[0]
@@ -139,6 +147,7 @@ class DeviceEngine:
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
         fl.jit = (ptr, offs, info, size)
+        fl.jit_key = key + (self._arena_i, self._arena_gen[self._arena_i])
         return fl.jit
 
     @staticmethod
@@ -150,10 +159,27 @@ class DeviceEngine:
         return err == 0 and 0 < total <= fl.jit[3]
 
     # ------------------------------------------------------------------ data
+    @staticmethod
+    def data_fingerprint(data) -> tuple:
+        """Content key of a reference data tuple: shape, dtype and a 128-bit hash of every array
+        (nested tuples such as `params` included).  Arrays are small (rollout data), so hashing
+        each call costs microseconds and a reused or mutated buffer can never hit a stale entry."""
+        import hashlib
+
+        def fp(x):
+            if isinstance(x, (tuple, list)):
+                return ("seq", tuple(fp(y) for y in x))
+            if x is None:
+                return None
+            a = np.ascontiguousarray(np.asarray(x))
+            return (a.shape, a.dtype.str, hashlib.blake2b(a.tobytes(), digest_size=16).digest())
+
+        return fp(data)
+
     def prepare_data(self, data) -> dict:
-        """Upload the reference data tuple once (cached on the identity of its arrays)."""
+        """Upload the reference data tuple once (cached on its content, see data_fingerprint)."""
         from . import prng
-        key = (tuple(id(x) for x in data) if isinstance(data, (tuple, list)) else id(data), prng.prng_impl_code())
+        key = (self.data_fingerprint(data), prng.prng_impl_code())
         if self._data is not None and key == self._data_key:
             return self._data
         host = self.ff.prepare(data)

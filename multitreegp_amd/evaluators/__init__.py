@@ -8,9 +8,10 @@ The population path (``GeneticProgramming.evaluate_population``) batches all can
 one launch; these per-candidate calls exist for API parity and trajectory inspection.
 
 Solver: BASELINE.json prescribes an explicit fixed-step RK4 (``RK4()`` or "rk4" with
-``ConstantStepSize()``).  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)``
-(spec include/mtgp_dopri5.h) runs on the GPU for the dynamic and static
-control evaluators (every environment) and for ``SREvaluator`` with n_var <= 4.
+``ConstantStepSize()``); omitting ``solver`` gives the reference's default ``Euler()`` (fixed
+step).  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)`` (SURVEY.md
+§8f row 2, spec include/mtgp_dopri5.h) runs on the GPU for the dynamic and static control
+evaluators (every environment) and for ``SREvaluator``.
 """
 from __future__ import annotations
 
@@ -28,6 +29,16 @@ class RK4:
 
     def __repr__(self):
         return "RK4()"
+
+
+class Euler:
+    """Explicit Euler, fixed step dt0 (diffrax.Euler + ConstantStepSize): the reference
+    evaluators' default solver (dynamic_evaluate.py:11, feedforward_evaluate.py:11,
+    SR_evaluator.py:21); y1 = y0 + f(t0, y0) * dt0, product and sum rounded separately."""
+    name = "Euler"
+
+    def __repr__(self):
+        return "Euler()"
 
 
 class ConstantStepSize:
@@ -68,7 +79,8 @@ class PIDController:
 
 
 def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
-    """-> "rk4" or "dopri5" (the latter needs a PIDController and an evaluator that supports it)."""
+    """-> "rk4", "euler" or "dopri5" (the latter needs a PIDController and an evaluator that
+    supports it)."""
     sname = solver.lower() if isinstance(solver, str) else getattr(solver, "name", type(solver).__name__)
     sname = str(sname).lower()
     cname = None if controller is None else getattr(controller, "name", type(controller).__name__)
@@ -78,16 +90,18 @@ def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
         if cname != "PIDController":
             raise NotImplementedError("Dopri5 needs a PIDController (fixed-step Dopri5 is not implemented)")
         return "dopri5"
-    if sname != "rk4":
-        raise NotImplementedError(f"solver {solver!r}: implemented solvers are RK4 (fixed step) and Dopri5 (PID)")
+    if sname not in ("rk4", "euler"):
+        raise NotImplementedError(f"solver {solver!r}: implemented solvers are Euler and RK4 (fixed step) and "
+                                  "Dopri5 (PID)")
     if cname is not None and cname != "ConstantStepSize":
-        raise NotImplementedError(f"stepsize_controller {controller!r}: RK4 runs with ConstantStepSize only")
-    return "rk4"
+        raise NotImplementedError(f"stepsize_controller {controller!r}: {sname} runs with ConstantStepSize only")
+    return sname
 
 
 def _solver_fields(kind: str, controller, max_steps: int) -> dict:
     if kind != "dopri5":
-        return dict(solver=nat.SOLVER_RK4, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0)
+        return dict(solver=nat.SOLVER_EULER if kind == "euler" else nat.SOLVER_RK4, max_steps=0, rtol=0.0, atol=0.0,
+                    dtmin=0.0, dtmax=0.0)
     return dict(solver=nat.SOLVER_DOPRI5, max_steps=int(max_steps), rtol=controller.rtol, atol=controller.atol,
                 dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0)
 
@@ -203,8 +217,8 @@ class _ControlEvaluator(_CandidateAPI):
     max_fitness = 1e4
 
     def __init__(self, env, dt0: float, solver=None, max_steps: int = 16 ** 4, stepsize_controller=None):
-        self.solver_kind = _check_solver(solver if solver is not None else RK4(), stepsize_controller,
-                                         adaptive_ok=True)
+        solver = solver if solver is not None else Euler()  # the reference default (dyn.py:11, ff.py:11)
+        self.solver_kind = _check_solver(solver, stepsize_controller, adaptive_ok=True)
         name = type(env).__name__
         if name not in ENVIRONMENTS:
             # CartPole / Acrobot2 / ChangingHarmonicOscillator / HarmonicOscillator2 have no
@@ -220,7 +234,7 @@ class _ControlEvaluator(_CandidateAPI):
         self.control_size = env.n_control
         self.latent_size = env.n_var * env.n_dim
         self.dt0 = float(dt0)
-        self.solver = solver if solver is not None else RK4()
+        self.solver = solver
         self.max_steps = max_steps
         self.stepsize_controller = stepsize_controller
 
@@ -318,10 +332,10 @@ class SREvaluator(_CandidateAPI):
     max_fitness = 1e5
 
     def __init__(self, solver=None, dt0: float = 0.01, max_steps: int = 16 ** 4, stepsize_controller=None):
-        self.solver_kind = _check_solver(solver if solver is not None else RK4(), stepsize_controller,
-                                         adaptive_ok=True)
+        solver = solver if solver is not None else Euler()  # the reference default (sr.py:21)
+        self.solver_kind = _check_solver(solver, stepsize_controller, adaptive_ok=True)
         self.dt0 = float(dt0)
-        self.solver = solver if solver is not None else RK4()
+        self.solver = solver
         self.max_steps = max_steps
         self.stepsize_controller = stepsize_controller
         self.state_size = 0
@@ -362,5 +376,5 @@ class SREvaluator(_CandidateAPI):
         return specs, roles
 
 
-__all__ = ["RK4", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
+__all__ = ["RK4", "Euler", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
            "rk4_schedule", "adaptive_schedule"]

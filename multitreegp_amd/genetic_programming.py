@@ -3,8 +3,9 @@
 Keeps the constructor signature, validation and bookkeeping of
 MultiTreeGP/genetic_programming.py:GeneticProgramming (gp.py:61-270, 403-433, 527-537) and
 replaces ``evaluate_population``'s ``jit(shard_map(vmap(fitness_function)))`` with the flatten
-+ fused RK4 HIP kernels.  Evolution (``evolve``: genetic_operators/) stays with the reference's
-host code; a maintainer swaps only this method.
++ fused RK4 / Dopri5 HIP kernels.  ``evolve`` runs the host restatement of genetic_operators/
+(multitreegp_amd.genetic_operators), so whole generations run on the GPU box; a maintainer who
+keeps the reference's JAX evolution swaps only ``evaluate_population``.
 """
 from __future__ import annotations
 
@@ -15,8 +16,17 @@ import torch
 
 from . import distributed as mdist
 from .engine import DeviceEngine
+from .genetic_operators import Operators, evolve_populations
 from .node_library import NodeLibrary
 from .sampling import sample_population
+
+
+def _seed_of(key) -> int:
+    """numpy seed from a JAX-style key (uint32 words) or an int."""
+    if isinstance(key, (int, np.integer)):
+        return int(key)
+    words = np.asarray(key, np.uint64).reshape(-1)
+    return int(sum(int(w) << (32 * i) for i, w in enumerate(words[::-1])))
 
 
 class TreeEvaluator:
@@ -30,6 +40,7 @@ class TreeEvaluator:
         self.max_nodes = max_nodes
         self.device = device
         self._engines = {}
+        self._tree_only = {}
 
     def engine(self, fitness_function, size_parsinomy: float = 0.0) -> DeviceEngine:
         key = (id(fitness_function), float(size_parsinomy))
@@ -41,7 +52,10 @@ class TreeEvaluator:
         from .evaluators import _TreeOnly
         cand = np.asarray(candidate, dtype=np.float32)
         d = np.asarray(data, dtype=np.float32).reshape(1, -1)
-        ff = _TreeOnly(cand.shape[0], d.shape[1])
+        shape = (cand.shape[0], d.shape[1])
+        ff = self._tree_only.get(shape)
+        if ff is None:  # one pseudo fitness config (hence one engine) per (trees, data) shape
+            ff = self._tree_only[shape] = _TreeOnly(*shape)
         eng = self.engine(ff)
         pop = torch.from_numpy(cand[None]).to(eng.device)
         eng.prepare_data(None)
@@ -83,8 +97,19 @@ class GeneticProgramming:
         self.size_parsinomy = size_parsinomy
         self.coefficient_sd = coefficient_sd
         assert migration_period > 1, "The migration period should be larger than 1"
+        self.migration_period = migration_period
         assert migration_percentage * population_size % 1 == 0, "The migration size should be an integer"
+        self.migration_size = int(migration_percentage * population_size)
         assert tournament_size > 1, "The number of gradient steps should be larger than 1"
+        self.tournament_size = tournament_size
+        # per-population schedules, linearly spaced over the populations (gp.py:113-121)
+        self.selection_pressures = np.linspace(*selection_pressure_factors, num_populations)
+        self.tournament_probabilities = np.array([sp * (1 - sp) ** np.arange(tournament_size)
+                                                  for sp in self.selection_pressures])
+        self.reproduction_type_probabilities = np.vstack([np.linspace(*crossover_probability_factors, num_populations),
+                                                          np.linspace(*mutation_probability_factors, num_populations),
+                                                          np.linspace(*sample_probability_factors, num_populations)]).T
+        self.reproduction_probabilities = np.linspace(*reproduction_probability_factors, num_populations)
         self.elite_size = int(elite_percentage * population_size)
         assert self.elite_size % 2 == 0, "The elite size should be a multiple of two"
         if coefficient_optimisation:
@@ -100,6 +125,7 @@ class GeneticProgramming:
             print(f"Input data should be formatted as: {self.library.input_format}.")
         self.vmap_foriloop = TreeEvaluator(self.library, max_nodes, device)
         self.device = device
+        self.operators = Operators(self.library, max_nodes, max_init_depth, coefficient_sd)
 
     # ----------------------------------------------------------------- hot path
     def _engine(self) -> DeviceEngine:
@@ -111,15 +137,7 @@ class GeneticProgramming:
         pops = np.asarray(populations, dtype=np.float32)
         P = self.num_populations * self.population_size
         flat = pops.reshape(P, *pops.shape[2:])
-        eng = self._engine()
-
-        def shard(lo: int, hi: int) -> torch.Tensor:
-            if hi <= lo:
-                return torch.empty((0,), dtype=torch.float32, device=eng.device)
-            pop_dev = torch.from_numpy(np.ascontiguousarray(flat[lo:hi])).to(eng.device, non_blocking=True)
-            return eng.evaluate(pop_dev, data)["fitness"]
-
-        fitness = mdist.sharded_fitness(shard, P).cpu().numpy()
+        fitness = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data), P).cpu().numpy()
         g = self.current_generation
         best = int(np.argmin(fitness))
         if g < self.num_generations:
@@ -128,17 +146,43 @@ class GeneticProgramming:
         return fitness.reshape(self.num_populations, self.population_size), \
             flat.reshape(self.num_populations, self.population_size, *flat.shape[1:])
 
+    def _evaluate_shard(self, flat: np.ndarray, lo: int, hi: int, data) -> torch.Tensor:
+        """Fitness of individuals [lo, hi) of the flattened population on this rank's GPU (one
+        flatten + one fused kernel launch; shard_eval, gp.py:259-262)."""
+        eng = self._engine()
+        if hi <= lo:
+            return torch.empty((0,), dtype=torch.float32, device=eng.device)
+        pop_dev = torch.from_numpy(np.ascontiguousarray(flat[lo:hi])).to(eng.device, non_blocking=True)
+        return eng.evaluate(pop_dev, data)["fitness"]
+
     # --------------------------------------------------------------- host side
     def initialize_population(self, key) -> np.ndarray:
         """gp.py:298-308 with the numpy sampler (multitreegp_amd.sampling)."""
-        seed = int(np.asarray(key).reshape(-1)[-1]) if not isinstance(key, int) else key
-        return sample_population(seed, self.library, self.population_size, self.num_populations,
+        return sample_population(_seed_of(key), self.library, self.population_size, self.num_populations,
                                  self.max_init_depth, self.max_nodes, self.coefficient_sd)
 
     def evolve(self, populations, fitness, key):
-        raise NotImplementedError(
-            "evolution (genetic_operators/) stays with the reference's host implementation; "
-            "this package replaces evaluate_population only (see INTEGRATION.md)")
+        """gp.py:475-497: optional ring migration, then per population elitism + tournament
+        selection + crossover / mutation / resampling (multitreegp_amd.genetic_operators, the
+        numpy restatement of genetic_operators/).  `key` seeds numpy's PCG64 (a JAX key's words
+        or an int)."""
+        rng = np.random.default_rng(_seed_of(key))
+        out = evolve_populations(self.operators, np.asarray(populations, np.float32), np.asarray(fitness), rng,
+                                 self.current_generation, self.migration_period, self.migration_size,
+                                 self.reproduction_type_probabilities, self.reproduction_probabilities,
+                                 self.tournament_probabilities, self.tournament_size, self.elite_size)
+        self.current_generation += 1
+        return out
+
+    def mutate_pair(self, parent1, parent2, keys, reproduction_probability: float):
+        """gp.py:499-511"""
+        return self.operators.mutate_pair(parent1, parent2, np.random.default_rng(_seed_of(keys)),
+                                          reproduction_probability)
+
+    def sample_pair(self, parent1, parent2, keys, reproduction_probability: float):
+        """gp.py:513-525"""
+        return self.operators.sample_pair(parent1, parent2, np.random.default_rng(_seed_of(keys)),
+                                          reproduction_probability)
 
     def get_statistics(self, generation: Optional[int] = None):
         if generation is not None:

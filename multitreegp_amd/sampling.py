@@ -50,14 +50,21 @@ def _prune(tree: np.ndarray, max_nodes: int) -> np.ndarray:
 
 
 def sample_tree(rng: np.random.Generator, lib: NodeLibrary, var_mask: np.ndarray, max_init_depth: int,
-                max_nodes: int, coefficient_sd: float = 1.0, map_b_to_d: np.ndarray = None) -> np.ndarray:
+                max_nodes: int, coefficient_sd: float = 1.0, map_b_to_d: np.ndarray = None,
+                depth_limit: int = None) -> np.ndarray:
     """sample_tree (initialization.py:100-124) for one tree with allowed-variable mask.
 
+    `max_init_depth` sizes the breadth-first table (2**max_init_depth - 1 rows, map_b_to_d);
+    `depth_limit` (default max_init_depth) is the depth argument of the reference's
+    sample_tree(key, depth, variable_array): operators only above depth_limit - 1 (the
+    mutations sample depth-2 and depth-1 subtrees this way, mutation.py:149, 226, 273).
     The breadth-first sampling visits only the rows it fills, so they are kept sparsely
     (row -> [f, a, b, value]) and pruned directly (prune_tree, initialization.py:56-98):
     non-empty rows, highest first, packed at the end of max_nodes rows."""
     if map_b_to_d is None:
         map_b_to_d = create_map_b_to_d(max_init_depth)
+    if depth_limit is None:
+        depth_limit = max_init_depth
     tree_size = 2 ** max_init_depth - 1
     slots = lib.slots
     op_p = lib.operator_probabilities.astype(np.float64)
@@ -89,7 +96,7 @@ def sample_tree(rng: np.random.Generator, lib: NodeLibrary, var_mask: np.ndarray
             leaf = 1
         else:
             leaf = int(lib.variable_indices[min(int(np.searchsorted(var_cdf, u_var[j], side="right")), nv - 1)])
-        if (open_slots < max_nodes - i - 1) and (depth + 1 < max_init_depth) and u_node[j] < 0.7 ** depth:
+        if (open_slots < max_nodes - i - 1) and (depth + 1 < depth_limit) and u_node[j] < 0.7 ** depth:
             index = int(lib.operator_indices[min(int(np.searchsorted(op_cdf, u_op[j], side="right")), no - 1)])
         else:
             index = leaf

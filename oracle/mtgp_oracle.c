@@ -102,7 +102,7 @@ typedef struct {
   float h, max_fitness, parsimony;
   int32_t prng_impl; /* mtgp_prng.h: 0 threefry original layout, 1 partitionable */
   int32_t env;       /* control models: 0 Acrobot, 1 HarmonicOscillator, 2 StirredTankReactor */
-  int32_t solver;    /* 0 fixed-step RK4 (BASELINE.json), 1 Dopri5 + PIDController (notebooks) */
+  int32_t solver;    /* 0 fixed-step RK4 (BASELINE.json), 1 Dopri5 + PIDController (notebooks), 2 Euler */
   int32_t max_steps; /* Dopri5: step attempts, accepted + rejected (diffeqsolve max_steps) */
   float rtol, atol, dtmin, dtmax; /* PIDController; dtmin / dtmax <= 0: None */
 } OrModel;
@@ -305,6 +305,16 @@ static void rk4_step(const OrCtx* c, float t, float* s) {
   for (int i = 0; i < n; ++i) { acc[i] = acc[i] + k[i]; s[i] = MTGP_FMAF(h6, acc[i], s[i]); }
 }
 
+/* diffrax.Euler (the reference evaluators' default solver, dyn.py:11, ff.py:11, sr.py:21):
+ * y1 = y0 + f(t0, y0) * dt, the product and the sum rounded separately (ODETerm.vf_prod, then
+ * the add), at the fixed-grid step time like rk4_step. */
+static void euler_step(const OrCtx* c, float t, float* s) {
+  const int n = state_dim(c->m);
+  float k[OR_MAX_S];
+  rhs(c, t, s, k);
+  for (int i = 0; i < n; ++i) s[i] = s[i] + k[i] * c->m->h;
+}
+
 /* Solve one rollout: saved[n_save][dim]; unsaved points after termination = +inf. */
 static void solve(const OrCtx* c, float t0, const float* s0, float* saved) {
   const OrModel* m = c->m;
@@ -315,7 +325,8 @@ static void solve(const OrCtx* c, float t0, const float* s0, float* saved) {
   float prev = cond_fn(m, s);
   int k_saved = 0, done = 0;
   for (int step = 1; step <= m->n_steps && !done; ++step) {
-    rk4_step(c, t0 + (float)(step - 1) * m->h, s);
+    if (m->solver == 2) euler_step(c, t0 + (float)(step - 1) * m->h, s);
+    else rk4_step(c, t0 + (float)(step - 1) * m->h, s);
     if (step % m->save_every == 0) {
       ++k_saved;
       for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];

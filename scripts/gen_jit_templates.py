@@ -10,14 +10,13 @@ v17-v24 template temporaries, s[30:31] return address, s[32:33] fallback lane ma
 (OR-accumulated), s[34:39] template temporaries, vcc clobbered, exec never written.
 
   SIN / COS  : subroutines (one shared copy at the start of the code buffer, called with
-               s_swappc_b64 s[40:41], returning with s_setpc_b64 s[40:41]): x in v17 -> v8.  include/mtgp_f32math.h mtgp_sinf/mtgp_cosf op for op: float
-               Cody-Waite for |x| < 2^17; for finite |x| >= 2^28 the spec's Payne-Hanek
-               reduction (96-bit window of 2/pi selected per lane, three 32x32->64 products,
-               int64 -> double, times pi/2), for 2^17 <= |x| < 2^28 the spec's double
-               Cody-Waite -- each behind an exec-masked block that is branched over when no
-               lane needs it; both Taylor polynomials, quadrant selects, |x| < 2^-12 override.
-               No lane needs the interpreter any more (s[32:33] is never set; the evaluator's
-               fallback stays for safety).  exec is saved in s[36:37] around each block.
+               s_swappc_b64 s[40:41], returning with s_setpc_b64 s[40:41]): x in v17 -> v8.
+               include/mtgp_f32math.h mtgp_trig_pi (spec v2: reduction onto the pi grid, one
+               odd polynomial, sign from bit 0 of k + odd) op for op: the float Cody-Waite hot
+               path (|x| < 2^17) straight-line; finite |x| >= 2^17 lanes take a branch (not
+               taken in the common case) to out-of-line exec-masked blocks -- the spec's double
+               Cody-Waite below 2^28, its Payne-Hanek reduction beyond -- and come back.  exec
+               is restored; s[32:33] is never set (the evaluator's fallback stays for safety).
   DIV        : v17 / v18 -> v8, the compiler's own IEEE-exact sequence for gfx950
                (v_div_scale / v_rcp / fma refinement / v_div_fmas / v_div_fixup).
 Hazards: VALU-written SGPR/VCC read by a VALU mask operand gets `s_nop 1` in between; the
@@ -33,21 +32,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "multitreegp_amd", "csrc", "mtgp_jit_blobs.h")
 LLVM_MC = os.environ.get("LLVM_MC", "/opt/rocm/lib/llvm/bin/llvm-mc")
 
-REDUCE = """
-v_mul_f32 v18, 0x3f22f983, v17
-v_rndne_f32 v18, v18
-v_fmamk_f32 v19, v18, 0xbfc90fdb, v17
-v_fmamk_f32 v19, v18, 0x333bbd2e, v19
-v_fmamk_f32 v19, v18, 0x26f72ced, v19
-v_cvt_i32_f32 v18, v18
-v_and_b32 v24, 0x7fffffff, v17
-s_mov_b32 s38, 0x4d800000
-s_mov_b32 s39, 0x7f800000
-v_cmp_le_f32_e64 s[34:35], s38, v24
-v_cmp_gt_f32_e64 s[36:37], s39, v24
-s_and_b64 s[34:35], s[34:35], s[36:37]
-s_and_saveexec_b64 s[36:37], s[34:35]
-s_cbranch_execz .Lnoph
+# Payne-Hanek window selection and 96-bit product for finite |x| >= 2^28 (|x| in v24): leaves
+# hi_lo32 in v18, mid_lo32 in v22, lo_lo32 in v20 (include/mtgp_f32math.h
+# mtgp_reduce_payne_hanek_pi: b = e - 2, k = b >> 5, s = b & 31, W = 2/pi bits [b+1, b+96])
+_PH_PRODUCT = """
 v_lshrrev_b32 v18, 23, v24
 v_add_u32 v18, 0xffffff68, v18
 v_lshrrev_b32 v19, 5, v18
@@ -106,7 +94,91 @@ v_mov_b32 v21, v19
 v_mov_b32 v18, v23
 v_mov_b32 v19, 0
 v_mad_u64_u32 v[18:19], s[34:35], v8, v21, v[18:19]
-v_lshrrev_b32 v21, 30, v18
+"""
+
+
+def _trig(odd):
+    """sin (odd = 0) / cos (odd = 1) of include/mtgp_f32math.h mtgp_trig_pi (spec v2) op for op.
+    Hot path (|x| < 2^17): t = x * f32(1/pi); k = rint(t [- 0.5]); j = 2k [+ 1]; r = x - j pi/2
+    by the 3-constant fma Cody-Waite; sin_poly(r), sign bit = bit 0 of (k + odd); |x| < 2^-12
+    override (mask kept in s[44:45]).  Finite |x| >= 2^17 lanes branch (not taken in the common
+    case) to out-of-line blocks after the return: the spec's double Cody-Waite for |x| < 2^28
+    and its Payne-Hanek reduction beyond, each under its own exec mask, then back to the
+    polynomial.  v23 carries the sign source (k + odd, or (j + odd) >> 1 on the Payne-Hanek
+    path); NaN / +-inf give NaN on the hot path.  s[32:33] is never set."""
+    t = """
+v_and_b32 v24, 0x7fffffff, v17
+s_mov_b32 s38, 0x39800000
+v_cmp_gt_f32_e64 s[44:45], s38, v24
+v_mul_f32 v18, 0x3ea2f983, v17
+"""
+    if odd:
+        t += """v_add_f32 v18, -0.5, v18
+v_rndne_f32 v18, v18
+v_cvt_i32_f32 v23, v18
+v_fma_f32 v18, v18, 2.0, 1.0
+v_add_u32 v23, 1, v23
+"""
+    else:
+        t += """v_rndne_f32 v18, v18
+v_cvt_i32_f32 v23, v18
+v_add_f32 v18, v18, v18
+"""
+    t += """v_fmamk_f32 v19, v18, 0xbfc90fdb, v17
+v_fmamk_f32 v19, v18, 0x333bbd2e, v19
+v_fmamk_f32 v19, v18, 0x26f72ced, v19
+v_subrev_u32 v20, 0x48000000, v24
+v_cmp_gt_u32_e32 vcc, 0x37800000, v20
+s_and_b64 vcc, exec, vcc
+s_cbranch_vccnz .Lslow
+.Lpoly:
+v_lshlrev_b32 v23, 31, v23
+v_mul_f32 v20, v19, v19
+v_mov_b32 v21, {C9}
+v_fmaak_f32 v21, v21, v20, {C7}
+v_fmaak_f32 v21, v21, v20, {C5}
+v_fmaak_f32 v21, v21, v20, {C3}
+v_mul_f32 v22, v19, v20
+v_fma_f32 v21, v22, v21, v19
+v_xor_b32 v21, v21, v23
+"""
+    t += ("v_cndmask_b32_e64 v8, v21, 1.0, s[44:45]\n" if odd else "v_cndmask_b32_e64 v8, v21, v17, s[44:45]\n")
+    t += "s_setpc_b64 s[40:41]\n"
+    # ---- out of line: finite |x| >= 2^17 (vcc = those lanes)
+    t += """.Lslow:
+s_mov_b64 s[34:35], vcc
+v_cmp_gt_u32_e32 vcc, 0x5800000, v20
+s_and_b64 vcc, vcc, s[34:35]
+s_and_saveexec_b64 s[36:37], vcc
+s_cbranch_execz .Lph
+v_cvt_f64_f32 v[20:21], v17
+s_mov_b32 s38, 0x6dc9c883
+s_mov_b32 s39, 0x3fd45f30
+v_mul_f64 v[18:19], v[20:21], s[38:39]
+""" + ("v_add_f64 v[18:19], v[18:19], -0.5\n" if odd else "") + """v_rndne_f64 v[18:19], v[18:19]
+v_cvt_i32_f64 v8, v[18:19]
+""" + ("v_fma_f64 v[18:19], v[18:19], 2.0, 1.0\nv_add_u32 v8, 1, v8\n" if odd else
+       "v_add_f64 v[18:19], v[18:19], v[18:19]\n") + """s_mov_b32 s38, 0x40000000
+s_mov_b32 s39, 0x3ff921fb
+v_mul_f64 v[22:23], v[18:19], s[38:39]
+v_add_f64 v[20:21], v[20:21], -v[22:23]
+s_mov_b32 s38, 0
+s_mov_b32 s39, 0x3e74442d
+v_mul_f64 v[22:23], v[18:19], s[38:39]
+v_add_f64 v[20:21], v[20:21], -v[22:23]
+s_mov_b32 s38, 0x98cc5170
+s_mov_b32 s39, 0x3cf84698
+v_mul_f64 v[22:23], v[18:19], s[38:39]
+v_add_f64 v[20:21], v[20:21], -v[22:23]
+v_cvt_f32_f64 v19, v[20:21]
+v_mov_b32 v23, v8
+.Lph:
+s_mov_b64 exec, s[36:37]
+v_subrev_u32 v20, 0x4d800000, v24
+v_cmp_gt_u32_e32 vcc, 0x32000000, v20
+s_and_saveexec_b64 s[36:37], vcc
+s_cbranch_execz .Ldone
+""" + _PH_PRODUCT + """v_lshrrev_b32 v21, 30, v18
 v_and_b32 v23, 0x3fffffff, v18
 v_lshlrev_b32 v23, 2, v23
 v_lshrrev_b32 v8, 30, v22
@@ -114,15 +186,20 @@ v_or_b32 v23, v23, v8
 v_lshrrev_b32 v20, 30, v20
 v_lshlrev_b32 v22, 2, v22
 v_or_b32 v22, v22, v20
-v_lshrrev_b32 v8, 31, v23
-v_add_u32 v21, v21, v8
-v_cvt_f64_i32 v[18:19], v23
+v_cvt_f64_u32 v[18:19], v23
 v_ldexp_f64 v[18:19], v[18:19], 32
 v_cvt_f64_u32 v[22:23], v22
 v_add_f64 v[18:19], v[18:19], v[22:23]
 s_mov_b32 s38, 0
 s_mov_b32 s39, 0x3bf00000
 v_mul_f64 v[18:19], v[18:19], s[38:39]
+v_and_b32 v20, 1, v21
+""" + ("v_xor_b32 v20, 1, v20\n" if odd else "") + """v_add_u32 v21, v21, v20
+v_cmp_ne_u32_e32 vcc, 0, v20
+v_add_f64 v[22:23], v[18:19], -1.0
+s_nop 1
+v_cndmask_b32_e32 v18, v18, v22, vcc
+v_cndmask_b32_e32 v19, v19, v23, vcc
 s_mov_b32 s38, 0x54442d18
 s_mov_b32 s39, 0x3ff921fb
 v_mul_f64 v[18:19], v[18:19], s[38:39]
@@ -132,78 +209,29 @@ v_xor_b32 v20, 0x80000000, v19
 v_sub_u32 v22, 4, v21
 s_nop 1
 v_cndmask_b32_e32 v19, v19, v20, vcc
-v_cndmask_b32_e32 v18, v21, v22, vcc
-.Lnoph:
+v_cndmask_b32_e32 v21, v21, v22, vcc
+""" + ("v_add_u32 v21, 1, v21\n" if odd else "") + """v_lshrrev_b32 v23, 1, v21
+.Ldone:
 s_mov_b64 exec, s[36:37]
-s_mov_b32 s38, 0x4d800000
-s_mov_b32 s39, 0x48000000
-v_cmp_le_f32_e64 s[34:35], s39, v24
-v_cmp_gt_f32_e64 s[36:37], s38, v24
-s_and_b64 s[34:35], s[34:35], s[36:37]
-s_and_saveexec_b64 s[36:37], s[34:35]
-s_cbranch_execz .Lfast
-v_cvt_f64_f32 v[20:21], v17
-s_mov_b32 s38, 0x6dc9c883
-s_mov_b32 s39, 0x3fe45f30
-v_mul_f64 v[22:23], v[20:21], s[38:39]
-v_rndne_f64 v[22:23], v[22:23]
-s_mov_b32 s38, 0x40000000
-s_mov_b32 s39, 0x3ff921fb
-v_mul_f64 v[18:19], v[22:23], s[38:39]
-v_add_f64 v[20:21], v[20:21], -v[18:19]
-s_mov_b32 s38, 0
-s_mov_b32 s39, 0x3e74442d
-v_mul_f64 v[18:19], v[22:23], s[38:39]
-v_add_f64 v[20:21], v[20:21], -v[18:19]
-s_mov_b32 s38, 0x98cc5170
-s_mov_b32 s39, 0x3cf84698
-v_mul_f64 v[18:19], v[22:23], s[38:39]
-v_add_f64 v[20:21], v[20:21], -v[18:19]
-v_cvt_i32_f64 v18, v[22:23]
-v_cvt_f32_f64 v19, v[20:21]
-.Lfast:
-s_mov_b64 exec, s[36:37]
-v_mul_f32 v20, v19, v19
-v_mov_b32 v21, 0x3638ef1d
-v_fmaak_f32 v21, v21, v20, 0xb9500d01
-v_fmaak_f32 v21, v21, v20, 0x3c088889
-v_fmaak_f32 v21, v21, v20, 0xbe2aaaab
-v_mul_f32 v22, v19, v20
-v_fma_f32 v21, v22, v21, v19
-v_mov_b32 v22, 0xb493f27e
-v_fmaak_f32 v22, v22, v20, 0x37d00d01
-v_fmaak_f32 v22, v22, v20, 0xbab60b61
-v_fmaak_f32 v22, v22, v20, 0x3d2aaaab
-v_fmaak_f32 v22, v22, v20, 0xbf000000
-v_fma_f32 v22, v20, v22, 1.0
-v_and_b32 v23, 1, v18
-v_cmp_ne_u32_e32 vcc, 0, v23
-s_nop 1
+s_branch .Lpoly
 """
+    return t.format(**_sin_coefficients())
+
+
+def _sin_coefficients():
+    """the polynomial's f32 coefficients, read from the spec header (one source of truth)"""
+    import struct
+    text = open(os.path.join(ROOT, "include", "mtgp_f32math.h")).read()
+    out = {}
+    for name in ("C3", "C5", "C7", "C9"):
+        m = re.search(r"#define MTGP_SIN_%s ([-+0-9.eE]+)f" % name, text)
+        out[name] = "0x%08x" % struct.unpack("<I", struct.pack("<f", float(m.group(1))))[0]
+    return out
+
 
 TEMPLATES = {
-    # v21 = sin poly(r), v22 = cos poly(r), v18 = quadrant, v24 = |x|; v8 is scratch until the end
-    "SIN": REDUCE + """
-v_cndmask_b32_e32 v23, v21, v22, vcc
-v_and_b32 v18, 2, v18
-v_lshlrev_b32 v18, 30, v18
-v_xor_b32 v23, v23, v18
-v_cmp_gt_f32_e32 vcc, 0x39800000, v24
-s_nop 1
-v_cndmask_b32_e32 v8, v23, v17, vcc
-s_setpc_b64 s[40:41]
-""",
-    "COS": REDUCE + """
-v_cndmask_b32_e32 v23, v22, v21, vcc
-v_add_u32 v18, 1, v18
-v_and_b32 v18, 2, v18
-v_lshlrev_b32 v18, 30, v18
-v_xor_b32 v23, v23, v18
-v_cmp_ngt_f32_e32 vcc, 0x39800000, v24
-s_nop 1
-v_cndmask_b32_e32 v8, 1.0, v23, vcc
-s_setpc_b64 s[40:41]
-""",
+    "SIN": _trig(0),
+    "COS": _trig(1),
     "DIV": """
 v_div_scale_f32 v19, s[34:35], v18, v18, v17
 v_rcp_f32 v20, v19
@@ -254,8 +282,9 @@ def generate():
         out += [f"//   {ln}" for ln in lines]
         body = ", ".join(f"0x{w:08x}u" for w in words)
         out.append(f"#define MTGP_JIT_{name}_WORDS {len(words)}")
-        # words inside the exec-masked blocks (skipped by s_cbranch_execz when no lane needs them)
-        skip = sum(x & 0xFFFF for x in words if (x >> 16) == 0xBF88)
+        # out-of-line words after the return (only run when some lane needs a slow reduction)
+        ret = words.index(0xBE801D28) if 0xBE801D28 in words else len(words) - 1  # s_setpc_b64 s[40:41]
+        skip = len(words) - ret - 1
         out.append(f"#define MTGP_JIT_{name}_SKIPPABLE_WORDS {skip}")
         out.append(f"static const uint32_t mtgp_jit_{name.lower()}_blob[{len(words)}] = {{{body}}};")
         out.append("")

@@ -19,9 +19,13 @@ ap.add_argument("--rollouts", type=int, default=32)
 ap.add_argument("--no-traj", action="store_true")
 ap.add_argument("--lib", default=nat.LIB_PATH)
 ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
+ap.add_argument("--solver", default="rk4", choices=["rk4", "dopri5"])
+ap.add_argument("--obs-noise", type=float, default=0.0)
+ap.add_argument("--ode-steps", type=int, default=200)
 a = ap.parse_args()
-env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=200,
-                                                                      config=a.config, solver="rk4", obs_noise=0.0), 0)
+env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps,
+                                                                      config=a.config, solver=a.solver,
+                                                                      obs_noise=a.obs_noise), 0)
 eng = DeviceEngine(ff, lib, 0.0, "cuda:0", native=nat.load(a.lib))
 pd = torch.from_numpy(pop).cuda()
 for _ in range(a.iters):

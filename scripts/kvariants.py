@@ -29,7 +29,8 @@ def main():
     ap.add_argument("--order", default="orig", help="orig | pair (long with short) | sorted (host reorder)")
     ap.add_argument("--no-schedule", action="store_true", help="disable the device schedule (mtgp_schedule)")
     a = ap.parse_args()
-    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config="c3")
+    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config="c3", solver="rk4",
+                               obs_noise=0.0)
     env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
     dev = torch.device("cuda", 0)
     engines = {}

@@ -81,3 +81,67 @@ def test_shard_bounds_cover():
                 seen.extend(range(lo, hi))
                 assert hi - lo <= per
             assert seen == list(range(P))
+
+
+def _gp_worker(rank, ws, port, q):
+    """GeneticProgramming.evaluate_population on world_size 2 with the shard evaluator injected
+    (CPU oracle): sharding, the gloo all-gather, reshape and best-so-far bookkeeping."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        q.put((rank, _gp_run()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _gp_run():
+    """Two generations of evaluate_population (num_populations 3 x population_size 6, P = 18:
+    not divisible by 4) with an oracle shard evaluator -> fitness, best_fitnesses, best_solutions."""
+    from helpers import CONTROL_OPS, oracle_model, oracle_rollouts, static_setup
+    from oracle import oracle as orc
+    import multitreegp_amd as mt
+    env, lib, ff, data, pop = static_setup(P=36, R=4, n_steps=20, seed=8)
+    gp = mt.GeneticProgramming(2, 6, ff, CONTROL_OPS, [["y1", "y2", "y3", "y4"]], [1], num_populations=3,
+                               size_parsinomy=0.5, migration_percentage=0.5, elite_percentage=0.0, verbose=False)
+    d = ff.prepare(data)
+    model, ro = oracle_model(ff, d, parsimony=0.5), oracle_rollouts(d)
+    calls = []
+
+    def shard(flat, lo, hi, data_):
+        calls.append((lo, hi))
+        if hi <= lo:
+            return torch.empty(0)
+        return torch.from_numpy(orc.evaluate(model, flat[lo:hi], lib, ro)["fitness"])
+
+    gp._evaluate_shard = shard
+    out = []
+    for g in range(2):
+        populations = pop[18 * g:18 * (g + 1)].reshape(3, 6, *pop.shape[1:])
+        fit, back = gp.evaluate_population(populations, data)
+        assert fit.shape == (3, 6) and back.shape == populations.shape
+        gp.current_generation += 1
+        out.append(fit.tobytes())
+    return out, gp.best_fitnesses.tobytes(), gp.best_solutions.tobytes(), calls
+
+
+@pytest.mark.parametrize("ws", [2])
+def test_genetic_programming_evaluate_population_sharded(ws):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gp_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=180) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_fit, want_bf, want_bs, calls = _gp_run()  # unsharded (world size 1)
+    assert calls == [(0, 18), (0, 18)]
+    for r in range(ws):
+        fits, bf, bs, rcalls = res[r]
+        assert fits == want_fit and bf == want_bf and bs == want_bs
+        assert rcalls == [(9 * r, 9 * r + 9)] * 2  # contiguous block per rank, gp.py:259 P('i')

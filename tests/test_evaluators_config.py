@@ -60,3 +60,55 @@ def test_program_specs_dynamic():
     # state equations see [y, a, u]; readout in the drift sees y = 0, u = 0; at saves u = 0
     assert specs == [(0, 7, 0), (1, 7, 0), (2, 7, 0b1001111), (2, 7, 0b1000000)]
     assert roles["prog_readout"] == 2 and roles["prog_readout_save"] == 3
+
+
+def test_data_fingerprint_follows_content():
+    """the device-data cache is keyed on content, so a mutated or re-allocated array
+    is never served stale (ids of freed temporaries can repeat)."""
+    from multitreegp_amd.engine import DeviceEngine
+    x0 = np.zeros((4, 4), np.float32)
+    params = (np.ones(4, np.float32),) * 4
+    a = DeviceEngine.data_fingerprint((x0, np.arange(3, dtype=np.float32), params))
+    b = DeviceEngine.data_fingerprint((x0.copy(), np.arange(3, dtype=np.float32), params))
+    assert a == b
+    x0[1, 2] = 1e-30
+    c = DeviceEngine.data_fingerprint((x0, np.arange(3, dtype=np.float32), params))
+    assert c != a
+    assert DeviceEngine.data_fingerprint((x0.astype(np.float64),)) != DeviceEngine.data_fingerprint((x0,))
+
+
+def test_default_solver_is_the_reference_euler():
+    """omitting `solver` gives the reference's default diffrax.Euler() (dyn.py:11,
+    ff.py:11, sr.py:21), not RK4."""
+    from multitreegp_amd import _native as nat
+    env = mt.Acrobot(0, 0)
+    for ev in (mt.DynamicEvaluator(env, 2, 0.05), mt.FeedforwardEvaluator(env, 0.05), mt.SREvaluator(dt0=0.05)):
+        assert ev.solver_kind == "euler" and type(ev.solver).__name__ == "Euler"
+    data = mt.control_data(env, 4, 0.05, None, seed=3, n_steps=10)
+    assert mt.DynamicEvaluator(env, 2, 0.05).prepare(data)["solver"] == nat.SOLVER_EULER
+    assert mt.DynamicEvaluator(env, 2, 0.05, solver=mt.RK4()).prepare(data)["solver"] == nat.SOLVER_RK4
+
+
+def test_oracle_euler_known_answer():
+    """dx/dt = -x (tree 0 - x0), Euler: x_{n+1} = x_n + (-x_n) * h in float32, saved every step."""
+    from helpers import SR_OPS, oracle_model, oracle_rollouts
+    from oracle import oracle as orc
+    lib = mt.NodeLibrary(SR_OPS, [["x0"]], [1])
+    N = 4
+    cand = np.zeros((1, 1, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 3] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 0, N - 2] = [1, -1, -1, 0.0]
+    cand[0, 0, N - 1] = [lib.string_to_node["-"], N - 2, N - 3, 0]
+    x0 = np.array([[1.0], [-0.3]], np.float32)
+    h = np.float32(0.05)
+    ts = (np.arange(21, dtype=np.float32) * h).astype(np.float32)
+    ff = mt.SREvaluator(dt0=0.05)
+    d = ff.prepare((x0, ts, np.zeros((2, 21, 1), np.float32), None))
+    out = orc.evaluate(oracle_model(ff, d), cand, lib, oracle_rollouts(d), trajectories=True)
+    want = np.empty((2, 21), np.float32)
+    x = x0[:, 0].copy()
+    for k in range(21):
+        want[:, k] = x
+        x = (x + (np.float32(0.0) - x) * h).astype(np.float32)
+    assert np.array_equal(out["xs"][0, :, :, 0].view(np.uint32), want.view(np.uint32))

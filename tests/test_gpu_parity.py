@@ -299,3 +299,54 @@ def test_other_envs_fitness_only_and_interpreter(env):
     c = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=False, rollout_fitness=True)
     assert bits_equal(c["rollout_fitness"].cpu().numpy(), a["rollout_fitness"])
     assert bits_equal(c["fitness"].cpu().numpy(), a["fitness"])
+
+
+def test_jit_code_of_a_reused_flattened_population_is_rebuilt():
+    """a Flattened keeps a pointer into the engine's two-buffer code ring.  Evaluate A,
+    B, C (C reuses A's buffer), then A again through its old Flattened: the engine sees that the
+    slot was rewritten and translates A again -- results equal the interpreter's."""
+    env, lib, ff, data, _ = dynamic_setup(P=8, R=16, n_steps=20, seed=21)
+    pops = [dynamic_setup(P=24, R=16, n_steps=20, seed=s)[4] for s in (22, 23, 24)]
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=True)
+    flats = []
+    for p in pops:
+        res = eng.evaluate(torch.from_numpy(p).cuda(), data)
+        flats.append(res["_flat"])
+    pa = torch.from_numpy(pops[0]).cuda()
+    again = eng.evaluate(pa, data, flattened=flats[0], rollout_fitness=True)
+    torch.cuda.synchronize()
+    assert DeviceEngine.jit_ok(again["_flat"])
+    ref = _run_engine(ff, lib, data, pops[0], False)
+    assert bits_equal(again["fitness"].cpu().numpy(), ref["fitness"])
+    assert bits_equal(again["rollout_fitness"].cpu().numpy(), ref["rollout_fitness"])
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "static_noise", "sr", "sr_wide"])
+@pytest.mark.parametrize("jit", [True, False])
+def test_euler_bitexact(kind, jit):
+    """diffrax.Euler (the reference default solver) in every fixed-step kernel: bit-exact with
+    the oracle's Euler (trajectories and fitness)."""
+    import multitreegp_amd as mt
+    if kind == "dynamic":
+        env, lib, ff, data, pop = dynamic_setup(P=20, R=16, n_steps=40, seed=31)
+        ff = mt.DynamicEvaluator(ff.env, 2, 0.05, solver=mt.Euler())
+        keys = ["xs", "ys", "us", "acts"]
+    elif kind == "static_noise":
+        env, lib, ff, data, pop = static_setup(P=20, R=16, n_steps=40, seed=32, obs_noise=0.1)
+        ff = mt.FeedforwardEvaluator(ff.env, 0.05, solver=mt.Euler())
+        keys = ["xs", "ys", "us"]
+    else:
+        env, lib, ff, data, pop = sr_setup(P=20, R=16, seed=33, n_var=2 if kind == "sr" else 9)
+        ff = mt.SREvaluator(solver=mt.Euler(), dt0=0.05)
+        keys = ["xs"]
+    res = _run_engine(ff, lib, data, pop, jit and kind != "sr_wide")
+    d = DeviceEngine(ff, lib, 0.0, "cuda:0").prepare_data(data)
+    assert d["solver"] == 2
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, R, S = pop.shape[0], d["R"], d["n_save"]
+    for k in keys:
+        c = ref[k].shape[-1]
+        got = res[k].reshape(S, c, P, R).transpose(2, 3, 0, 1)
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)

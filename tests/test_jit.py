@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SETPC_S40 = 0xBE801D28  # s_setpc_b64 s[40:41] (the sin/cos subroutine return)
 LLVM_MC = "/opt/rocm/lib/llvm/bin/llvm-mc"
 
 from multitreegp_amd import _native as nat  # noqa: E402
@@ -328,15 +329,113 @@ def test_wave_units_emulate_to_oracle(kind, R):
                 (np.isnan(got) and np.isnan(want)), (u, lane, got, want)
 
 
-def test_template_branch_targets_resolved():
-    """The sin/cos templates branch over their double-precision block: the assembled offset
-    must land on the exec restore (assembled from an object file, not the unresolved fixup)."""
+def test_trig_templates_hot_path_and_slow_blocks():
+    """The sin/cos templates (spec v2): a straight-line hot path up to the return whose only
+    branch is the (normally not taken) jump to the out-of-line slow blocks; those blocks mask
+    exec, restore it and branch back; no lane is ever sent to the interpreter (s[32:33])."""
     for name in ("SIN", "COS"):
         w = BLOBS[name]
-        br = [i for i, x in enumerate(w) if (x >> 16) == 0xBF88]  # s_cbranch_execz
-        assert len(br) == 2  # the Payne-Hanek block and the double Cody-Waite block
-        for b in br:
-            target = b + 1 + (w[b] & 0xFFFF)
-            assert w[target] == 0xBEFE0124, hex(w[target])  # s_mov_b64 exec, s[36:37]
-        lines = _disassemble(w + [SETPC])
-        assert any(ln.startswith("s_and_saveexec_b64 s[36:37]") for ln in lines)
+        ret = w.index(SETPC_S40)
+        hot = _disassemble(w[:ret + 1])
+        assert [ln.split()[0] for ln in hot if ln.startswith("s_cbranch")] == ["s_cbranch_vccnz"]
+        assert not any("exec" in ln and not ln.startswith("s_and_b64 vcc, exec") for ln in hot)
+        cold = _disassemble(w[ret + 1:])
+        assert any(ln.startswith("s_and_saveexec_b64") for ln in cold)
+        assert cold[-1].startswith("s_branch")
+        assert not any("s[32:33]" in ln for ln in hot + cold)
+
+
+def _emulate_trig_template(text, x):
+    """Instruction-level float32 emulation of the HOT path of a sin/cos template (up to its
+    s_setpc) on lanes x -> (v8, lanes that branch to the out-of-line slow blocks).  The slow
+    blocks (double Cody-Waite, Payne-Hanek) are checked on the GPU (scripts/micro/jit_smoke.hip,
+    test_gpu_parity slow-lane tests).  fma via float64 (exact product, one rounding)."""
+    f32 = np.float32
+    v = {17: x.astype(f32)}
+    sg = {}
+    vcc = None
+    slow = np.zeros(x.shape, bool)
+    u = lambda a: a.view(np.uint32)  # noqa: E731
+
+    def val(o):
+        if o.startswith("v"):
+            return v[int(o[1:])]
+        if o.startswith("s") and o[1:].isdigit():
+            return np.full(x.shape, np.array(sg[int(o[1:])], np.uint32).view(f32))
+        if o.startswith("0x"):
+            return np.full(x.shape, np.array(int(o, 16), np.uint32).view(f32))
+        return np.full(x.shape, f32(float(o)))
+
+    def fma(a, b, c):
+        return (a.astype(np.float64) * b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+
+    masks = {}
+    for ln in text.strip().splitlines():
+        if ln.endswith(":"):
+            continue
+        op, *rest = ln.split(None, 1)
+        a = [t.strip() for t in rest[0].split(",")] if rest else []
+        d = int(a[0][1:]) if a and a[0][:1] == "v" and a[0][1:].isdigit() else None
+        with np.errstate(all="ignore"):
+            if op == "v_and_b32":
+                v[d] = (np.uint32(int(a[1], 16)) & u(val(a[2]))).view(f32)
+            elif op == "s_mov_b32":
+                sg[int(a[0][1:])] = int(a[1], 16) if a[1].startswith("0x") else int(a[1])
+            elif op == "v_cmp_gt_f32_e64":
+                masks[a[0]] = val(a[1]) > val(a[2])
+            elif op == "v_subrev_u32":  # vdst = src1 - src0
+                v[d] = (u(val(a[2])) - u(val(a[1]))).view(f32)
+            elif op == "v_cmp_gt_u32_e32":
+                vcc = u(val(a[1])) > u(val(a[2]))
+            elif op == "s_and_b64":
+                pass  # vcc &= exec (full)
+            elif op == "s_cbranch_vccnz":
+                slow = vcc.copy()
+            elif op == "v_mul_f32":
+                v[d] = (val(a[1]) * val(a[2])).astype(f32)
+            elif op == "v_add_f32":
+                v[d] = (val(a[1]) + val(a[2])).astype(f32)
+            elif op == "v_rndne_f32":
+                v[d] = np.rint(val(a[1]))
+            elif op in ("v_fma_f32", "v_fmamk_f32", "v_fmaak_f32"):
+                v[d] = fma(val(a[1]), val(a[2]), val(a[3]))
+            elif op == "v_cvt_i32_f32":  # saturating, NaN -> 0
+                t = val(a[1]).astype(np.float64)
+                t = np.where(np.isnan(t), 0, np.clip(t, -2.0 ** 31, 2.0 ** 31 - 1))
+                v[d] = t.astype(np.int64).astype(np.int32).view(f32)
+            elif op == "v_add_u32":
+                v[d] = (val(a[2]).view(np.int32) + np.int32(int(a[1]))).astype(np.int32).view(f32)
+            elif op == "v_lshlrev_b32":
+                v[d] = (u(val(a[2])) << np.uint32(int(a[1]))).view(f32)
+            elif op == "v_xor_b32":
+                v[d] = (u(val(a[1])) ^ u(val(a[2]))).view(f32)
+            elif op == "v_mov_b32":
+                v[d] = val(a[1])
+            elif op == "v_cndmask_b32_e64":
+                v[d] = np.where(masks[a[3]], val(a[2]), val(a[1]))
+            elif op == "s_setpc_b64":
+                return v[8], slow
+            elif op != "s_nop":
+                raise AssertionError(op)
+    raise AssertionError("no s_setpc")
+
+
+def test_trig_templates_emulate_to_spec():
+    """Every hot-path lane of the sin/cos templates equals the spec (oracle) bit for bit --
+    NaN, infinities, signed zeros, denormals, tiny, the 2^17 edge and random arguments; the
+    lanes sent to the out-of-line slow blocks are exactly the finite |x| >= 2^17."""
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_jit_templates", os.path.join(ROOT, "scripts",
+                                                                                     "gen_jit_templates.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.uniform(-200, 200, 100000), rng.uniform(-2e5, 2e5, 50000),
+                        [np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-30, -1e-40, 2.44e-4, 131071.99, 131072.0,
+                         -131072.0, 1e-3, np.pi / 2, -np.pi, 3e38]]).astype(np.float32)
+    s_ref, c_ref = orc.sincos(x)
+    for name, ref in (("SIN", s_ref), ("COS", c_ref)):
+        got, flag = _emulate_trig_template(g.TEMPLATES[name], x)
+        same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
+        assert np.all(same | flag), (name, x[~(same | flag)][:5], got[~(same | flag)][:5])
+        assert np.array_equal(flag, ~(np.abs(x) < 131072.0) & np.isfinite(x)), name
