@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 10
+#define MTGP_ABI_VERSION 11
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -277,6 +277,22 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
                       int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
                       const MtgpRollouts* rollouts, const MtgpOutputs* out, const MtgpJitCode* jit,
                       void* stream);
+
+/* ------------------------------------------------- coefficient optimisation */
+/* Loss and forward-mode gradient of the SR fitness w.r.t. K parameters per individual (ABI v11),
+ * the value_and_grad of GeneticProgramming.epoch (gp.py:435-452, vmap_gradients gp.py:253).
+ * Replaces: jax.vmap(jax.value_and_grad(partial_ff)) over SR_evaluator.__call__ (sr.py:30-45).
+ * prog: mtgp_flatten output of the PARAMETERISED population: the coefficient rows being
+ *   differentiated are variable rows reading data slots n_var .. n_var + K - 1 (the host
+ *   transform, multitreegp_amd/coefficients.py), so programs read data[n_var + k] = theta[p, k].
+ * theta[P, K]: parameter values; nparam[P] (<= K): parameters in use per individual.
+ * scratch: device float [P, K, R, 2].  loss_out[P]: the evaluator's fitness without parsimony
+ *   (bit-identical to mtgp_eval_rk4's with parsimony 0); grad_out[P, K] (0 beyond nparam).
+ * model: MTGP_MODEL_SR with MTGP_SOLVER_RK4 or MTGP_SOLVER_EULER, n_var + K <= MTGP_MAX_DATA,
+ * R <= 64; anything else returns MTGP_ERR_ARG. */
+int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                 const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
+                 float* scratch, float* loss_out, float* grad_out, void* stream);
 
 /* Wall time of the calling thread's last timed mtgp_eval_rk4 kernel (ms), measured with
  * hipEvents recorded on its stream around the launch; -1 if none.  Synchronises that event.

@@ -1,0 +1,326 @@
+// mtgp_grad.hip -- forward-mode sensitivities of the SR fitness for coefficient optimisation.
+//
+// Reference: GeneticProgramming.optimise / epoch (gp.py:435-473) run
+//   loss, grads = vmap(value_and_grad(partial_ff))(candidates[..., 3:], candidates[..., :3], data)
+// i.e. reverse-mode through diffeqsolve (SR_evaluator.py:57-83, DirectAdjoint) of the evaluator's
+// clipped mean MSE (SR_evaluator.py:30-45).  Here the derivative is taken in forward mode: the
+// host (multitreegp_amd/coefficients.py) turns the coefficient rows to differentiate into
+// variable rows reading data slots n_var .. n_var + K - 1, flattens that population with the
+// ordinary flattener, and every lane of k_sr_grad integrates one (individual, parameter k,
+// rollout) triple with dual numbers (value, d/dtheta_k).  The value half performs exactly the
+// operations of k_sr (same RK4 fma form, same MSE order), so the loss equals the evaluator's
+// fitness bit for bit; the tangent half is the chain rule of those same operations.
+// k_grad_reduce then forms the per-individual loss and gradient with the evaluator's NaN/inf ->
+// max_fitness replacement, the pairwise rollout sum of finish_group and jnp.clip's derivative.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "mtgp.h"
+#include "mtgp_f32math.h"
+
+namespace {
+
+constexpr float kInf = __builtin_huge_valf();
+
+struct Dual {
+  float v, d;
+};
+
+// d(x op y) with the value computed exactly as the interpreter's handler does
+__device__ __forceinline__ Dual d_add(Dual a, Dual b) { return {a.v + b.v, a.d + b.d}; }
+__device__ __forceinline__ Dual d_sub(Dual a, Dual b) { return {a.v - b.v, a.d - b.d}; }
+__device__ __forceinline__ Dual d_mul(Dual a, Dual b) { return {a.v * b.v, a.d * b.v + a.v * b.d}; }
+__device__ __forceinline__ Dual d_div(Dual a, Dual b) {
+  const float q = a.v / b.v;
+  return {q, (a.d - q * b.d) / b.v};
+}
+__device__ __forceinline__ Dual d_sin(Dual a) { return {mtgp_sinf(a.v), mtgp_cosf(a.v) * a.d}; }
+__device__ __forceinline__ Dual d_cos(Dual a) { return {mtgp_cosf(a.v), -mtgp_sinf(a.v) * a.d}; }
+
+// family member: 0 ADD, 1 SUB (acc - o), 2 RSUB (o - acc), 3 MUL, 4 DIV (acc / o), 5 RDIV (o / acc)
+__device__ __forceinline__ Dual d_fam(int f, Dual acc, Dual o) {
+  switch (f) {
+    case 0: return d_add(acc, o);
+    case 1: return d_sub(acc, o);
+    case 2: return d_sub(o, acc);
+    case 3: return d_mul(acc, o);
+    case 4: return d_div(acc, o);
+    default: return d_div(o, acc);
+  }
+}
+
+struct GradArgs {
+  MtgpModel m;
+  const MtgpInstr* prog;
+  int n_prog, L, P, K;
+  const float* theta;     // [P, K]
+  const int32_t* nparam;  // [P]
+  MtgpRollouts ro;
+  float* part;            // [P, K, R, 2] per-rollout (F, dF/dtheta_k)
+  float* loss;            // [P]
+  float* grad;            // [P, K]
+};
+
+// Data slot s (byte offset s * MTGP_SLOT_BYTES in the program words): the stage state for
+// s < nv, parameter theta[s - nv] otherwise (tangent 1 for the lane's own parameter).
+template <int NV>
+__device__ __forceinline__ Dual slot_val(uint32_t off, const float* sv, const float* sd, int nv, const float* th,
+                                         int kk) {
+  const int s = (int)(off / MTGP_SLOT_BYTES);
+  if (s < nv) {
+    if constexpr (NV <= 4) {  // keep the small state in registers: select, not a dynamic index
+      float v = 0.0f, d = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        v = (i == s) ? sv[i] : v;
+        d = (i == s) ? sd[i] : d;
+      }
+      return {v, d};
+    } else {
+      return {sv[s], sd[s]};
+    }
+  }
+  return {th[s - nv], (s - nv == kk) ? 1.0f : 0.0f};
+}
+
+// One program (mtgp.h format, every opcode incl. the fused forms) in dual numbers.
+template <int NV>
+__device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd, int nv, const float* th, int kk) {
+  Dual acc = {0.0f, 0.0f};
+  Dual stk[MTGP_STACK_MAX];
+  int sp = 0;
+  for (int pc = 0;; ++pc) {
+    const uint32_t w = code[pc].op, op = w >> MTGP_OP_SHIFT, ax = w & 0xffffffu;
+    const float imm = code[pc].imm;
+    const uint32_t ib = __float_as_uint(imm);
+    const Dual C = {imm, 0.0f};
+    auto V = [&](uint32_t off) { return slot_val<NV>(off, sv, sd, nv, th, kk); };
+    auto push = [&]() { stk[sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1] = acc; ++sp; };
+    auto pop = [&]() { --sp; return stk[sp < 0 ? 0 : (sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1)]; };
+    switch (op) {
+      case MTGP_OP_END: return acc;
+      case MTGP_OP_LDC: acc = C; break;
+      case MTGP_OP_LDCP: push(); acc = C; break;
+      case MTGP_OP_LDV: acc = V(ib); break;
+      case MTGP_OP_LDVP: push(); acc = V(ib); break;
+      case MTGP_OP_ADDC: acc = d_fam(0, acc, C); break;
+      case MTGP_OP_SUBC: acc = d_fam(1, acc, C); break;
+      case MTGP_OP_RSUBC: acc = d_fam(2, acc, C); break;
+      case MTGP_OP_MULC: acc = d_fam(3, acc, C); break;
+      case MTGP_OP_DIVC: acc = d_fam(4, acc, C); break;
+      case MTGP_OP_RDIVC: acc = d_fam(5, acc, C); break;
+      case MTGP_OP_ADDV: acc = d_fam(0, acc, V(ib)); break;
+      case MTGP_OP_SUBV: acc = d_fam(1, acc, V(ib)); break;
+      case MTGP_OP_RSUBV: acc = d_fam(2, acc, V(ib)); break;
+      case MTGP_OP_MULV: acc = d_fam(3, acc, V(ib)); break;
+      case MTGP_OP_DIVV: acc = d_fam(4, acc, V(ib)); break;
+      case MTGP_OP_RDIVV: acc = d_fam(5, acc, V(ib)); break;
+      case MTGP_OP_ADDS: { const Dual s = pop(); acc = d_add(acc, s); break; }
+      case MTGP_OP_SUBS: { const Dual s = pop(); acc = d_sub(acc, s); break; }
+      case MTGP_OP_RSUBS: { const Dual s = pop(); acc = d_sub(s, acc); break; }
+      case MTGP_OP_MULS: { const Dual s = pop(); acc = d_mul(acc, s); break; }
+      case MTGP_OP_DIVS: { const Dual s = pop(); acc = d_div(acc, s); break; }
+      case MTGP_OP_RDIVS: { const Dual s = pop(); acc = d_div(s, acc); break; }
+      case MTGP_OP_SIN: acc = d_sin(acc); break;
+      case MTGP_OP_COS: acc = d_cos(acc); break;
+      case MTGP_OP_SINV: acc = d_sin(V(ib)); break;
+      case MTGP_OP_COSV: acc = d_cos(V(ib)); break;
+      case MTGP_OP_SINVP: push(); acc = d_sin(V(ib)); break;
+      case MTGP_OP_COSVP: push(); acc = d_cos(V(ib)); break;
+      // VC_f: acc = f(v[aux], imm); VCP: push first
+      case MTGP_OP_VC_ADD: acc = d_fam(0, V(ax), C); break;
+      case MTGP_OP_VC_SUB: acc = d_fam(1, V(ax), C); break;
+      case MTGP_OP_VC_RSUB: acc = d_fam(2, V(ax), C); break;
+      case MTGP_OP_VC_MUL: acc = d_fam(3, V(ax), C); break;
+      case MTGP_OP_VC_DIV: acc = d_fam(4, V(ax), C); break;
+      case MTGP_OP_VC_RDIV: acc = d_fam(5, V(ax), C); break;
+      case MTGP_OP_VCP_ADD: push(); acc = d_fam(0, V(ax), C); break;
+      case MTGP_OP_VCP_SUB: push(); acc = d_fam(1, V(ax), C); break;
+      case MTGP_OP_VCP_RSUB: push(); acc = d_fam(2, V(ax), C); break;
+      case MTGP_OP_VCP_MUL: push(); acc = d_fam(3, V(ax), C); break;
+      case MTGP_OP_VCP_DIV: push(); acc = d_fam(4, V(ax), C); break;
+      case MTGP_OP_VCP_RDIV: push(); acc = d_fam(5, V(ax), C); break;
+      // VV_f: acc = f(v[imm], v[aux]); VVP: push first
+      case MTGP_OP_VV_ADD: acc = d_add(V(ib), V(ax)); break;
+      case MTGP_OP_VV_SUB: acc = d_sub(V(ib), V(ax)); break;
+      case MTGP_OP_VV_MUL: acc = d_mul(V(ib), V(ax)); break;
+      case MTGP_OP_VV_DIV: acc = d_div(V(ib), V(ax)); break;
+      case MTGP_OP_VVP_ADD: push(); acc = d_add(V(ib), V(ax)); break;
+      case MTGP_OP_VVP_SUB: push(); acc = d_sub(V(ib), V(ax)); break;
+      case MTGP_OP_VVP_MUL: push(); acc = d_mul(V(ib), V(ax)); break;
+      case MTGP_OP_VVP_DIV: push(); acc = d_div(V(ib), V(ax)); break;
+      default: return acc;  // unknown word: the flattener never emits one
+    }
+  }
+}
+
+// One (individual p, parameter k, rollout r) per lane; k_sr's integration in dual numbers.
+template <int NV>
+__global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int R = A.ro.R;
+  if (gid >= (long)A.P * A.K * R) return;
+  const int r = (int)(gid % R);
+  const long pk = gid / R;
+  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
+  float* out = A.part + (size_t)gid * 2;
+  const int np = A.nparam[p];
+  if (k > 0 && k >= np) {  // unused parameter slot of this individual
+    out[0] = 0.0f;
+    out[1] = 0.0f;
+    return;
+  }
+  const int kk = k < np ? k : -1;
+  const int nv = A.m.n_var;
+  const float* th = A.theta + (size_t)p * A.K;
+  const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;
+  const int n_stages = euler ? 1 : 4;
+  float x[NV], dx[NV], kx[NV], dkx[NV], ax[NV], dax[NV], sv[NV], sd[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    x[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
+    dx[i] = kx[i] = dkx[i] = ax[i] = dax[i] = 0.0f;
+  }
+  auto bad = [&]() {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(x[i]));
+    return b;
+  };
+  bool pending = false, prev_ok = !bad();
+  float tot = 0.0f, dtot = 0.0f;
+  for (int step = 0;; ++step) {
+    if ((step % save_every) == 0) {  // MSE term of this save point (SR_evaluator.py:24)
+      const int ks = step / save_every;
+      float sq = 0.0f, dsq = 0.0f;
+#pragma unroll
+      for (int d = 0; d < NV; ++d) {
+        if (d >= nv) continue;
+        const float e = x[d] - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
+        const float de = dx[d] * (2.0f * e);  // jnp.square's JVP: g * (2 x)
+        sq = (d == 0) ? e * e : sq + e * e;
+        dsq = (d == 0) ? de : dsq + de;
+      }
+      tot = tot + sq;
+      dtot = dtot + dsq;
+    }
+    if (pending) {  // the event fired: every later save point is +inf -> non-finite fitness
+      tot = mtgp_isfinite(tot) ? kInf : tot;
+      break;
+    }
+    if (step == n_steps) break;
+#pragma unroll 1
+    for (int stage = 0; stage < n_stages; ++stage) {
+      const float hh = stage == 3 ? h : h2;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        sv[i] = stage == 0 ? x[i] : MTGP_FMAF(hh, kx[i], x[i]);
+        sd[i] = stage == 0 ? dx[i] : MTGP_FMAF(hh, dkx[i], dx[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        if (i >= nv) continue;
+        const Dual o = run_dual<NV>(progs + (size_t)i * A.L, sv, sd, nv, th, kk);
+        kx[i] = o.v;
+        dkx[i] = o.d;
+      }
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        ax[i] = stage == 0 ? kx[i] : (stage == 3 ? ax[i] + kx[i] : MTGP_FMAF(2.0f, kx[i], ax[i]));
+        dax[i] = stage == 0 ? dkx[i] : (stage == 3 ? dax[i] + dkx[i] : MTGP_FMAF(2.0f, dkx[i], dax[i]));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
+      dx[i] = euler ? dx[i] + dax[i] * h : MTGP_FMAF(h6, dax[i], dx[i]);
+    }
+    const bool ok = !bad();
+    if (prev_ok && !ok) pending = true;
+    prev_ok = ok;
+  }
+  out[0] = tot / (float)S;
+  out[1] = dtot / (float)S;
+}
+
+// One (individual, parameter) per thread: NaN/inf -> max_fitness (derivative 0), pairwise sum
+// over rollouts in finish_group's order, mean, jnp.clip(., 0, max_fitness) with JAX's derivative
+// of max/min (1 inside, 1/2 on a tie, 0 outside).
+__global__ void __launch_bounds__(256) k_grad_reduce(GradArgs A) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)A.P * A.K) return;
+  const int p = (int)(gid / A.K), k = (int)(gid % A.K);
+  const int R = A.ro.R;
+  int Rp = 1;
+  while (Rp < R) Rp <<= 1;
+  const float mx = A.m.max_fitness;
+  float v[64], dv[64];
+  for (int r = 0; r < Rp; ++r) {
+    float f = 0.0f, df = 0.0f;
+    if (r < R) {
+      const float* q = A.part + (((size_t)p * A.K + k) * R + r) * 2;
+      f = q[0];
+      df = q[1];
+      if (!mtgp_isfinite(f)) { f = mx; df = 0.0f; }
+    }
+    v[r] = f;
+    dv[r] = df;
+  }
+  for (int n = Rp; n > 1; n >>= 1)
+    for (int i = 0; i < n / 2; ++i) {
+      v[i] = v[2 * i] + v[2 * i + 1];
+      dv[i] = dv[2 * i] + dv[2 * i + 1];
+    }
+  const float mean = v[0] / (float)R;
+  float dmean = dv[0] / (float)R;
+  float c = mean;
+  if (mean < 0.0f) { c = 0.0f; dmean = 0.0f; }
+  else if (mean == 0.0f) dmean = 0.5f * dmean;
+  if (c > mx) { c = mx; dmean = 0.0f; }
+  else if (c == mx) dmean = 0.5f * dmean;
+  if (k == 0) A.loss[p] = c;
+  A.grad[gid] = k < A.nparam[p] ? dmean : 0.0f;
+}
+
+}  // namespace
+
+extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                            const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
+                            float* scratch, float* loss_out, float* grad_out, void* stream) {
+  if (!model || !prog || !ro || !nparam || !scratch || !loss_out || !grad_out || P < 0 || K < 1 || L <= 0 ||
+      n_prog <= 0 || (K > 0 && !theta))
+    return MTGP_ERR_ARG;
+  if (model->model != MTGP_MODEL_SR || model->n_var < 1 || model->n_var > MTGP_MAX_DATA ||
+      model->n_var + K > MTGP_MAX_DATA || ro->R < 1 || ro->R > 64 || !ro->x0 || !ro->ys_true ||
+      model->save_every < 1 || model->n_save < 1 || model->prog_state < 0 || model->prog_state + model->n_var > n_prog)
+    return MTGP_ERR_ARG;
+  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER) return MTGP_ERR_ARG;
+  if (P == 0) return MTGP_OK;
+  GradArgs A;
+  A.m = *model;
+  A.prog = prog;
+  A.n_prog = n_prog;
+  A.L = L;
+  A.P = P;
+  A.K = K;
+  A.theta = theta;
+  A.nparam = nparam;
+  A.ro = *ro;
+  A.part = scratch;
+  A.loss = loss_out;
+  A.grad = grad_out;
+  hipStream_t s = (hipStream_t)stream;
+  const long lanes = (long)P * K * ro->R;
+  const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
+  const int nv = model->n_var;
+  if (nv <= 2) hipLaunchKernelGGL(k_sr_grad<2>, grid, block, 0, s, A);
+  else if (nv <= 4) hipLaunchKernelGGL(k_sr_grad<4>, grid, block, 0, s, A);
+  else if (nv <= 16) hipLaunchKernelGGL(k_sr_grad<16>, grid, block, 0, s, A);
+  else hipLaunchKernelGGL(k_sr_grad<64>, grid, block, 0, s, A);
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(((long)P * K + 255) / 256)), dim3(256), 0, s, A);
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  return MTGP_OK;
+}

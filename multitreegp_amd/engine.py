@@ -288,6 +288,38 @@ class DeviceEngine:
         return fl.order
 
     # ----------------------------------------------------------------- eval
+    def model_struct(self, d: dict) -> "nat.MtgpModel":
+        """MtgpModel of this evaluator config for prepared data `d` (prepare_data)."""
+        _, roles = self._specs()
+        m = nat.MtgpModel()
+        m.model = self.ff.model_id
+        m.n_var = d.get("n_var", 4)
+        m.state_size = getattr(self.ff, "state_size", 0)
+        env = getattr(self.ff, "env", None)
+        m.n_obs = env.n_obs if env is not None else 0
+        m.n_control = env.n_control if env is not None else 0
+        m.n_targets = env.n_targets if env is not None else 0
+        m.n_steps, m.save_every, m.n_save = d["n_steps"], d["save_every"], d["n_save"]
+        m.h = self.ff.dt0
+        m.max_fitness = self.ff.max_fitness
+        m.parsimony = self.parsimony
+        m.prog_state, m.prog_readout = roles["prog_state"], roles["prog_readout"]
+        m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
+        m.prng_impl = d.get("prng_impl", 0)
+        m.env = d.get("env", nat.ENV_ACROBOT)
+        m.solver, m.max_steps = d.get("solver", nat.SOLVER_RK4), d.get("max_steps", 0)
+        m.rtol, m.atol, m.dtmin, m.dtmax = d.get("rtol", 0.0), d.get("atol", 0.0), d.get("dtmin", 0.0), d.get("dtmax", 0.0)
+        return m
+
+    @staticmethod
+    def rollouts_struct(d: dict) -> "nat.MtgpRollouts":
+        """MtgpRollouts over the device copies of prepared data `d` (no schedule)."""
+        ro = nat.MtgpRollouts()
+        ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
+        ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), d["R"]
+        ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
+        return ro
+
     def evaluate(self, pop: torch.Tensor, data, trajectories: bool = False, rollout_fitness: bool = False,
                  flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True,
                  step_counts: bool = False) -> dict:
@@ -298,31 +330,10 @@ class DeviceEngine:
         fl = flattened if flattened is not None else self.flatten(pop)
         P = pop.shape[0]
         R, S = d["R"], d["n_save"]
-        _, roles = self._specs()
-        m = nat.MtgpModel()
-        m.model = self.ff.model_id
-        m.n_var = d.get("n_var", 4)
-        m.state_size = getattr(self.ff, "state_size", 0)
-        env = getattr(self.ff, "env", None)
-        m.n_obs = env.n_obs if env is not None else 0
-        m.n_control = env.n_control if env is not None else 0
-        m.n_targets = env.n_targets if env is not None else 0
-        m.n_steps, m.save_every, m.n_save = d["n_steps"], d["save_every"], S
-        m.h = self.ff.dt0
-        m.max_fitness = self.ff.max_fitness
-        m.parsimony = self.parsimony
-        m.prog_state, m.prog_readout = roles["prog_state"], roles["prog_readout"]
-        m.prog_readout_save, m.readout_save_same = roles["prog_readout_save"], roles["readout_save_same"]
-        m.prng_impl = d.get("prng_impl", 0)
-        m.env = d.get("env", nat.ENV_ACROBOT)
-        m.solver, m.max_steps = d.get("solver", nat.SOLVER_RK4), d.get("max_steps", 0)
-        m.rtol, m.atol, m.dtmin, m.dtmax = d.get("rtol", 0.0), d.get("atol", 0.0), d.get("dtmin", 0.0), d.get("dtmax", 0.0)
-        ro = nat.MtgpRollouts()
-        ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
-        ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), R
+        m = self.model_struct(d)
+        ro = self.rollouts_struct(d)
         ro_order = self.schedule(fl, R) if schedule and P > 1 else None
         ro.order = _ptr(ro_order)
-        ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
         dev = self.device
         res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
         out = nat.MtgpOutputs()

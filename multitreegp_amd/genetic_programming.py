@@ -16,6 +16,7 @@ import torch
 
 from . import distributed as mdist
 from .engine import DeviceEngine
+from .coefficients import CoefficientOptimiser, adam
 from .genetic_operators import Operators, evolve_populations
 from .node_library import NodeLibrary
 from .sampling import sample_population
@@ -112,9 +113,12 @@ class GeneticProgramming:
         self.reproduction_probabilities = np.linspace(*reproduction_probability_factors, num_populations)
         self.elite_size = int(elite_percentage * population_size)
         assert self.elite_size % 2 == 0, "The elite size should be a multiple of two"
+        self.coefficient_optimisation = bool(coefficient_optimisation)
         if coefficient_optimisation:
-            raise NotImplementedError("coefficient optimisation (gp.py:418-473) is SURVEY.md §8f row 4")
-        self.coefficient_optimisation = False
+            assert gradient_steps > 0, "The number of gradient steps should be larger than 0"
+            CoefficientOptimiser.check_evaluator(fitness_function)
+        self.gradient_steps = gradient_steps
+        self.optimiser = optimiser if optimiser is not None else adam(learning_rate=0.001, b1=0.9, b2=0.999)
         self.fitness_function = fitness_function
         self.library = NodeLibrary(operator_list, variable_list, self.layer_sizes)
         self.node_to_string = self.library.node_to_string
@@ -133,12 +137,28 @@ class GeneticProgramming:
 
     def evaluate_population(self, populations, data) -> Tuple[np.ndarray, np.ndarray]:
         """Fitness of every candidate (gp.py:403-433): flatten, shard over ranks, one fused kernel
-        launch per rank, parsimony in-kernel, all-gather of fitness, best-so-far bookkeeping."""
+        launch per rank, parsimony in-kernel, all-gather of fitness, best-so-far bookkeeping.
+        With coefficient_optimisation, every 5th generation after generation 10 the 50 best
+        candidates (by fitness before parsimony) get `gradient_steps` optimiser steps on their
+        coefficients (gp.py:418-422; multitreegp_amd.coefficients), replicated on every rank."""
         pops = np.asarray(populations, dtype=np.float32)
         P = self.num_populations * self.population_size
         flat = pops.reshape(P, *pops.shape[2:])
-        fitness = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data), P).cpu().numpy()
         g = self.current_generation
+        if self.coefficient_optimisation and g > 10 and (g + 1) % 5 == 0:
+            raw = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data, 0.0), P)
+            raw = raw.cpu().numpy()
+            best_idx = np.argsort(raw, kind="stable")[:50]
+            opt = CoefficientOptimiser(self.vmap_foriloop.engine(self.fitness_function, 0.0))
+            opt_fit, opt_pop = opt.optimise(flat[best_idx], data, self.gradient_steps, self.optimiser)
+            flat = flat.copy()
+            flat[best_idx] = opt_pop
+            raw[best_idx] = opt_fit
+            # gp.py:424: + size_parsinomy * (non-empty rows), in float32 like the kernel's epilogue
+            counts = (flat[..., 0] != 0).sum(axis=tuple(range(1, flat.ndim - 1))).astype(np.float32)
+            fitness = (raw + np.float32(self.size_parsinomy) * counts).astype(np.float32)
+        else:
+            fitness = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data), P).cpu().numpy()
         best = int(np.argmin(fitness))
         if g < self.num_generations:
             self.best_solutions[g] = flat[best]
@@ -146,10 +166,10 @@ class GeneticProgramming:
         return fitness.reshape(self.num_populations, self.population_size), \
             flat.reshape(self.num_populations, self.population_size, *flat.shape[1:])
 
-    def _evaluate_shard(self, flat: np.ndarray, lo: int, hi: int, data) -> torch.Tensor:
+    def _evaluate_shard(self, flat: np.ndarray, lo: int, hi: int, data, parsimony=None) -> torch.Tensor:
         """Fitness of individuals [lo, hi) of the flattened population on this rank's GPU (one
         flatten + one fused kernel launch; shard_eval, gp.py:259-262)."""
-        eng = self._engine()
+        eng = self._engine() if parsimony is None else self.vmap_foriloop.engine(self.fitness_function, parsimony)
         if hi <= lo:
             return torch.empty((0,), dtype=torch.float32, device=eng.device)
         pop_dev = torch.from_numpy(np.ascontiguousarray(flat[lo:hi])).to(eng.device, non_blocking=True)

@@ -685,3 +685,163 @@ float oracle_acro_fitness(const float* xs, const float* us, const float* ts, int
   return acro_fitness(xs, us, ts, S);
 }
 float oracle_pairwise_sum(const float* v, int R) { return pairwise_sum(v, R); }
+
+/* ------------------------------------------------------------ coefficient optimisation
+ * GeneticProgramming.epoch's value_and_grad (gp.py:435-452, vmap_gradients gp.py:253) of the SR
+ * evaluator (sr.py:30-45) restated in forward mode: dual numbers (value, d/d theta) through the
+ * row-order interpreter, the fixed-step solve and the MSE.  theta = the value column entry
+ * tree[t][i][3] of one coefficient row; as in JAX, the entry is differentiated both where the
+ * coefficient row selects it (gp.py:372) and where an earlier row reads the original column of a
+ * later row (gp.py:366-369).  Reverse mode (JAX) and forward mode give the same derivative up to
+ * rounding; this oracle fixes the forward-mode operation order the GPU kernel must reproduce. */
+typedef struct {
+  float v, d;
+} ODual;
+
+static ODual od(float v, float d) { ODual r; r.v = v; r.d = d; return r; }
+static ODual od_add(ODual a, ODual b) { return od(a.v + b.v, a.d + b.d); }
+static ODual od_sub(ODual a, ODual b) { return od(a.v - b.v, a.d - b.d); }
+static ODual od_mul(ODual a, ODual b) { return od(a.v * b.v, a.d * b.v + a.v * b.d); }
+static ODual od_div(ODual a, ODual b) { const float q = a.v / b.v; return od(q, (a.d - q * b.d) / b.v); }
+static ODual od_sin(ODual a) { return od(mtgp_sinf(a.v), mtgp_cosf(a.v) * a.d); }
+static ODual od_cos(ODual a) { return od(mtgp_cosf(a.v), -mtgp_sinf(a.v) * a.d); }
+
+/* gp.py:356-388 in dual numbers; prow = the row of this tree holding theta (-1: none) */
+static ODual tree_eval_dual(const float* tree, int N, const OrLib* lib, const ODual* data, int n_data, int prow) {
+  ODual val[OR_MAX_N];
+  for (int i = 0; i < N; ++i) val[i] = od(tree[4 * i + 3], i == prow ? 1.0f : 0.0f);
+  for (int i = 0; i < N; ++i) {
+    const float f = tree[4 * i + 0];
+    const ODual x = val[or_index(tree[4 * i + 1], N)];
+    const ODual y = val[or_index(tree[4 * i + 2], N)];
+    ODual v;
+    if (f == 1.0f) {
+      v = od(tree[4 * i + 3], i == prow ? 1.0f : 0.0f);
+    } else {
+      int32_t k = or_f2i(f);
+      if (k < 0) k = 0;
+      if (k > lib->n_funcs - 1) k = lib->n_funcs - 1;
+      switch (lib->fn[k]) {
+        case FN_VAR: {
+          int d = k - lib->var_start;
+          if (d > n_data - 1) d = n_data - 1;
+          v = data[d];
+          break;
+        }
+        case FN_ADD: v = od_add(x, y); break;
+        case FN_SUB: v = od_sub(x, y); break;
+        case FN_MUL: v = od_mul(x, y); break;
+        case FN_DIV: v = od_div(x, y); break;
+        case FN_SIN: v = od_sin(x); break;
+        case FN_COS: v = od_cos(x); break;
+        default: v = od(0.0f, 0.0f); break;
+      }
+    }
+    val[i] = v;
+  }
+  return val[N - 1];
+}
+
+/* one rollout of one candidate: F = MSE and dF/dtheta (theta at tree pt, row pi; pt < 0: none) */
+static ODual sr_rollout_dual(const OrModel* m, const float* cand, int N, const OrLib* lib, const OrRollouts* ro, int r,
+                             int pt, int pi) {
+  const int nv = m->n_var, S = m->n_save;
+  ODual s[OR_MAX_S], k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
+  for (int i = 0; i < nv; ++i) s[i] = od(ro->x0[(size_t)r * nv + i], 0.0f);
+  const float h = m->h, h2 = h * 0.5f, h6 = h / 6.0f;
+  ODual tot = od(0.0f, 0.0f);
+  int bad_prev = 0;
+  for (int i = 0; i < nv; ++i) bad_prev |= !mtgp_isfinite(s[i].v);
+  int k_saved = 0, done = 0;
+#define OR_SR_RHS(in, out)                                                                          \
+  for (int q = 0; q < nv; ++q)                                                                      \
+    out[q] = tree_eval_dual(cand + (size_t)q * N * 4, N, lib, in, nv, q == pt ? pi : -1);
+#define OR_MSE_TERM(kk)                                                                             \
+  {                                                                                                 \
+    ODual sq = od(0.0f, 0.0f);                                                                      \
+    for (int dd = 0; dd < nv; ++dd) {                                                               \
+      const float e = s[dd].v - ro->ys_true[((size_t)r * S + (kk)) * nv + dd];                     \
+      const float de = s[dd].d * (2.0f * e);                                                        \
+      sq = dd == 0 ? od(e * e, de) : od(sq.v + e * e, sq.d + de);                                   \
+    }                                                                                               \
+    tot = od(tot.v + sq.v, tot.d + sq.d);                                                           \
+  }
+  OR_MSE_TERM(0)
+  for (int step = 1; step <= m->n_steps && !done; ++step) {
+    if (m->solver == 2) { /* Euler: y + f h */
+      OR_SR_RHS(s, k)
+      for (int i = 0; i < nv; ++i) s[i] = od(s[i].v + k[i].v * h, s[i].d + k[i].d * h);
+    } else { /* rk4_step's fma form, tangents by the same linear maps */
+      OR_SR_RHS(s, k)
+      for (int i = 0; i < nv; ++i) {
+        acc[i] = k[i];
+        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
+      }
+      OR_SR_RHS(tmp, k)
+      for (int i = 0; i < nv; ++i) {
+        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
+        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
+      }
+      OR_SR_RHS(tmp, k)
+      for (int i = 0; i < nv; ++i) {
+        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
+        tmp[i] = od(MTGP_FMAF(h, k[i].v, s[i].v), MTGP_FMAF(h, k[i].d, s[i].d));
+      }
+      OR_SR_RHS(tmp, k)
+      for (int i = 0; i < nv; ++i) {
+        acc[i] = od(acc[i].v + k[i].v, acc[i].d + k[i].d);
+        s[i] = od(MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d));
+      }
+    }
+    if (step % m->save_every == 0) {
+      ++k_saved;
+      OR_MSE_TERM(k_saved)
+    }
+    int bad = 0;
+    for (int i = 0; i < nv; ++i) bad |= !mtgp_isfinite(s[i].v);
+    if (!bad_prev && bad) done = 1; /* the NaN event (sr.py:93-94) */
+    bad_prev = bad;
+  }
+#undef OR_SR_RHS
+#undef OR_MSE_TERM
+  /* points after the event are +inf: the squared error is +inf (NaN stays NaN) */
+  if (k_saved + 1 < S && mtgp_isfinite(tot.v)) tot.v = mtgp_u2f(0x7f800000u);
+  return od(tot.v / (float)S, tot.d / (float)S);
+}
+
+/* loss[P] (the evaluator's fitness, no parsimony) and grad[P, K]: prow[P, K] = t * N + i of the
+ * k-th coefficient row (-1 = unused).  SR, fixed-step RK4 / Euler. */
+int oracle_sr_grad(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
+                   const int8_t* fn, const OrRollouts* ro, const int32_t* prow, int K, float* loss, float* grad) {
+  if (m->model != 3 || m->solver == 1 || N > OR_MAX_N || m->n_var > OR_MAX_S || ro->R > 64 || K < 1) return -1;
+  const int R = ro->R;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (long pk = 0; pk < (long)P * K; ++pk) {
+    const int p = (int)(pk / K), kq = (int)(pk % K);
+    const int row = prow[(size_t)p * K + kq];
+    if (row < 0 && kq > 0) { grad[pk] = 0.0f; continue; }
+    OrLib lib;
+    lib.n_funcs = n_funcs;
+    lib.var_start = var_start;
+    lib.fn = fn;
+    const float* cand = pop + (size_t)p * T * N * 4;
+    float v[64], dv[64];
+    for (int r = 0; r < R; ++r) {
+      ODual F = sr_rollout_dual(m, cand, N, &lib, ro, r, row < 0 ? -1 : row / N, row < 0 ? -1 : row % N);
+      if (!mtgp_isfinite(F.v)) F = od(m->max_fitness, 0.0f); /* sr.py:42-43, derivative of where */
+      v[r] = F.v;
+      dv[r] = F.d;
+    }
+    const float mean = pairwise_sum(v, R) / (float)R;
+    float dmean = pairwise_sum(dv, R) / (float)R;
+    /* jnp.clip = minimum(maximum(x, 0), max): JAX's max/min JVP is 1/2 on a tie */
+    float c = mean;
+    if (mean < 0.0f) { c = 0.0f; dmean = 0.0f; }
+    else if (mean == 0.0f) dmean = 0.5f * dmean;
+    if (c > m->max_fitness) { c = m->max_fitness; dmean = 0.0f; }
+    else if (c == m->max_fitness) dmean = 0.5f * dmean;
+    if (kq == 0) loss[p] = c;
+    grad[pk] = row < 0 ? 0.0f : dmean;
+  }
+  return 0;
+}

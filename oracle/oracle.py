@@ -75,6 +75,10 @@ def lib():
         L.oracle_threefry.argtypes = [vp, vp, vp, vp, vp, ctypes.c_long]
         L.oracle_erfinv.argtypes = [vp, vp, ctypes.c_long]
         L.oracle_log1p.argtypes = [vp, vp, ctypes.c_long]
+        L.oracle_sr_grad.argtypes = [ctypes.POINTER(OrModel), vp, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(OrRollouts), vp, ctypes.c_int,
+                                     vp, vp]
+        L.oracle_sr_grad.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -247,3 +251,30 @@ def log1p(x):
 def pairwise_sum(v):
     v = np.ascontiguousarray(v, np.float32)
     return np.float32(lib().oracle_pairwise_sum(_p(v), v.shape[0]))
+
+
+def sr_grad(model: dict, pop: np.ndarray, library, rollouts: dict):
+    """Loss [P] and d loss / d coefficient [P, K] of the SR evaluator (forward mode), one entry per
+    coefficient row (f == 1) of each candidate in row-major (tree, row) order; K = the largest
+    count (unused entries 0).  -> (loss, grad, rows: list of [(t, i)] per candidate)."""
+    pop = np.ascontiguousarray(pop, np.float32)
+    P, T, N, _ = pop.shape
+    rows = [np.argwhere(c[..., 0] == np.float32(1.0)) for c in pop]
+    K = max([len(r) for r in rows] + [1])
+    prow = np.full((P, K), -1, np.int32)
+    for p, r in enumerate(rows):
+        prow[p, : len(r)] = r[:, 0] * N + r[:, 1]
+    m = OrModel(**{k: model.get(k, _MODEL_DEFAULTS[k]) if k in _MODEL_DEFAULTS else model[k]
+                   for k, _ in OrModel._fields_})
+    x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
+    ts = np.ascontiguousarray(rollouts["ts"], np.float32)
+    yt = np.ascontiguousarray(rollouts["ys_true"], np.float32)
+    ro = OrRollouts(_p(x0).value, None, None, _p(ts).value, _p(yt).value, x0.shape[0], None, None)
+    loss = np.empty(P, np.float32)
+    grad = np.empty((P, K), np.float32)
+    fn = np.ascontiguousarray(library.fn_codes, np.int8)
+    rc = lib().oracle_sr_grad(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
+                              ctypes.byref(ro), _p(prow), K, _p(loss), _p(grad))
+    if rc != 0:
+        raise RuntimeError(f"oracle_sr_grad failed {rc}")
+    return loss, grad, rows

@@ -1,0 +1,307 @@
+"""Coefficient optimisation (gp.py:418-473).
+
+CPU: the oracle's forward-mode gradient (oracle/mtgp_oracle.c oracle_sr_grad) is pinned to the
+complex-step derivative of an independent float64 restatement (d f / d c = Im f(c + i e) / e,
+exact to rounding for the analytic + - * / sin cos RK4 chain); its loss equals the evaluator's
+fitness bit for bit; the host transform (coefficient rows -> parameter slots) keeps every tree's
+value; the Adam restatement matches optax's update rule; the optimise loop keeps the reference's
+best-epoch semantics.  GPU: mtgp_sr_grad is bit-exact with the oracle, and
+GeneticProgramming.evaluate_population with coefficient_optimisation=True reproduces a CPU run of
+the same loop (oracle gradients + the same Adam) bit for bit.
+"""
+import numpy as np
+import pytest
+
+import multitreegp_amd as mt
+from multitreegp_amd import coefficients as co
+from oracle import oracle as orc
+
+from helpers import SR_OPS, bits_equal, oracle_model, oracle_rollouts, sr_setup, tree_from_expr
+
+
+# ------------------------------------------------------- independent complex-step restatement
+def _eval_tree_c(tree, lib, data, prow, eps):
+    """gp.py:356-388 over complex values: the value-column entry of row `prow` carries i*eps."""
+    N = tree.shape[0]
+    val = tree[:, 3].astype(np.complex128)
+    if prow >= 0:
+        val[prow] += 1j * eps
+
+    def idx(v):
+        j = int(v) if np.isfinite(v) else 0
+        j = j + N if j < 0 else j
+        return min(max(j, 0), N - 1)
+
+    for i in range(N):
+        f, a, b, c = tree[i]
+        x, y = val[idx(a)], val[idx(b)]
+        if f == 1:
+            v = complex(c) + (1j * eps if i == prow else 0)
+        else:
+            k = min(max(int(f) if np.isfinite(f) else 0, 0), lib.n_funcs - 1)
+            if k < 2:
+                v = 0.0
+            elif k >= lib.var_start:
+                v = data[min(k - lib.var_start, len(data) - 1)]
+            else:
+                v = {"+": lambda: x + y, "-": lambda: x - y, "*": lambda: x * y, "/": lambda: x / y,
+                     "sin": lambda: np.sin(x), "cos": lambda: np.cos(x)}[lib.node_to_string[k]]()
+        val[i] = v
+    return val[N - 1]
+
+
+def _sr_loss_c(cand, lib, d, prow_t, prow_i, eps=1e-30, euler=False):
+    """SR_evaluator.__call__ (sr.py:30-45) over complex numbers: RK4 / Euler, MSE, NaN -> max, mean, clip."""
+    x0, ys = d["x0"].astype(np.float64), np.transpose(d["ys_true"], (2, 0, 1)).astype(np.float64)  # [R, S, nv]
+    R, nv = x0.shape
+    h, se, n = float(np.float32(d["h"])), d["save_every"], d["n_steps"]
+
+    def rhs(s):
+        return np.array([_eval_tree_c(cand[q], lib, s, prow_i if q == prow_t else -1, eps) for q in range(nv)])
+
+    fits = []
+    with np.errstate(all="ignore"):
+        for r in range(R):
+            s = x0[r].astype(np.complex128)
+            tot = np.sum((s - ys[r, 0]) ** 2)
+            for step in range(1, n + 1):
+                if euler:
+                    s = s + rhs(s) * h
+                else:
+                    k1 = rhs(s)
+                    k2 = rhs(s + 0.5 * h * k1)
+                    k3 = rhs(s + 0.5 * h * k2)
+                    k4 = rhs(s + h * k3)
+                    s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
+                if step % se == 0:
+                    tot = tot + np.sum((s - ys[r, step // se]) ** 2)
+            f = tot / (n // se + 1)
+            fits.append(f if np.isfinite(f.real) else complex(1e5))
+    m = np.mean(fits)
+    return m if 0 < m.real < 1e5 else complex(np.clip(m.real, 0, 1e5))
+
+
+def _setup(P=12, R=4, euler=False, seed=3):
+    env, lib, ff, data, pop = sr_setup(P=P, R=R, n_save=9, save_every=2, h=0.05, depth=4, N=20, seed=seed)
+    if euler:
+        ff = mt.SREvaluator(solver=mt.Euler(), dt0=0.05)
+    d = ff.prepare(data)
+    d["h"] = ff.dt0
+    return lib, ff, data, d, pop
+
+
+@pytest.mark.parametrize("euler", [False, True])
+def test_oracle_loss_is_the_fitness(euler):
+    lib, ff, data, d, pop = _setup(euler=euler)
+    loss, grad, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
+    assert bits_equal(loss, ref)
+    assert sum(len(r) for r in rows) > 10
+
+
+@pytest.mark.parametrize("euler", [False, True])
+def test_oracle_gradient_matches_complex_step(euler):
+    """float32 forward mode vs the float64 complex-step derivative of an independent restatement,
+    on every coefficient of candidates whose loss is finite and unclipped."""
+    lib, ff, data, d, pop = _setup(euler=euler)
+    loss, grad, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    rel = []
+    for p in range(pop.shape[0]):
+        if not (0 < loss[p] < 1e4):
+            continue
+        base = _sr_loss_c(pop[p], lib, d, -1, -1, euler=euler)
+        assert abs(base.real - loss[p]) <= 1e-3 * abs(loss[p]) + 1e-5
+        for k, (t, i) in enumerate(rows[p]):
+            g64 = _sr_loss_c(pop[p], lib, d, int(t), int(i), euler=euler).imag / 1e-30
+            rel.append(abs(grad[p, k] - g64) / (abs(g64) + 1e-6 * (1 + abs(loss[p]))))
+    rel = np.array(rel)
+    # float32 vs float64: ~1e-7 for well-conditioned candidates; a candidate dividing by a
+    # near-zero subexpression shares one ~1 % rounding factor over all its coefficients
+    assert rel.size >= 8 and np.median(rel) < 1e-5 and np.mean(rel < 1e-4) >= 0.75 and rel.max() < 0.02, rel
+
+
+def test_oracle_gradient_of_a_known_fit():
+    """dx0 = x1, dx1 = c*x0 around the Van der Pol data: the gradient in c agrees in sign and
+    size with a central difference of the oracle's own float32 loss."""
+    env, lib, ff, data, _ = sr_setup(P=2, R=4, n_save=11, save_every=2, h=0.05, N=20)
+    d = ff.prepare(data)
+
+    def cand(c):
+        return np.stack([tree_from_expr("x1", lib, 20), tree_from_expr(("*", c, "x0"), lib, 20)])[None]
+
+    loss, grad, _ = orc.sr_grad(oracle_model(ff, d), cand(-0.8), lib, oracle_rollouts(d))
+    e = 1e-2
+    up = orc.evaluate(oracle_model(ff, d), cand(-0.8 + e), lib, oracle_rollouts(d))["fitness"][0]
+    dn = orc.evaluate(oracle_model(ff, d), cand(-0.8 - e), lib, oracle_rollouts(d))["fitness"][0]
+    fd = (up - dn) / (2 * e)
+    assert abs(grad[0, 0] - fd) <= 0.02 * abs(fd) + 1e-4
+
+
+def test_parameterise_keeps_tree_values():
+    """The host transform (coefficient rows -> variable rows on slots n_var + k, opcode clamp,
+    variable clamp) leaves every tree's value unchanged, garbage arrays included."""
+    from multitreegp_amd.sampling import sample_population
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    rng = np.random.default_rng(0)
+    pop = sample_population(4, lib, 20, 1, max_init_depth=5, max_nodes=20)[0]
+    garbage = rng.normal(0, 4, size=(8, 2, 20, 4)).astype(np.float32)
+    garbage[..., 0] = rng.integers(-2, lib.n_funcs + 6, size=garbage.shape[:3]).astype(np.float32)
+    garbage[..., 0][rng.random(garbage.shape[:3]) < 0.2] = 1.0
+    pop = np.concatenate([pop, garbage])
+    rows = co.coefficient_rows(pop)
+    n_data = 2
+    tpop, theta, nparam, K, libs = co.parameterise(pop, rows, lib, n_data, 0, 64)
+    fn = np.frombuffer(bytes(libs.fn), np.int8)[: libs.n_funcs]
+    for b in range(pop.shape[0]):
+        x = rng.normal(size=2).astype(np.float32)
+        data = np.concatenate([x, theta[b]]).astype(np.float32)
+        for t in range(2):
+            v0 = orc.eval_tree(pop[b, t], lib.fn_codes, lib.n_funcs, lib.var_start, x)
+            v1 = orc.eval_tree(tpop[b, t], fn, libs.n_funcs, libs.var_start, data)
+            assert bits_equal(v0, v1), (b, t)
+    assert K == max(len(r) for r in rows) and list(nparam) == [len(r) for r in rows]
+
+
+def test_adam_matches_optax_rule():
+    """optax.adam update rule, float64 textbook vs the float32 restatement over 20 steps."""
+    rng = np.random.default_rng(1)
+    opt = co.adam(0.001, 0.9, 0.999)
+    x = rng.normal(size=7).astype(np.float32)
+    st = opt.init(x)
+    m = v = np.zeros(7)
+    x64 = x.astype(np.float64)
+    for t in range(1, 21):
+        g = rng.normal(size=7).astype(np.float32)
+        u, st = opt.update(g, st, x)
+        x = x + u
+        m = 0.9 * m + 0.1 * g
+        v = 0.999 * v + 0.001 * g.astype(np.float64) ** 2
+        x64 = x64 - 0.001 * (m / (1 - 0.9 ** t)) / (np.sqrt(v / (1 - 0.999 ** t)) + 1e-8)
+    np.testing.assert_allclose(x, x64, rtol=1e-5, atol=1e-6)
+    # the first step moves every coordinate by -lr * sign(g)
+    st = opt.init(np.zeros(3, np.float32))
+    u, _ = opt.update(np.array([2.0, -3.0, 0.0], np.float32), st)
+    np.testing.assert_allclose(u, [-0.001, 0.001, 0.0], rtol=1e-5)
+
+
+class _QuadraticOptimiser(co.CoefficientOptimiser):
+    """the optimise loop with an injected loss: sum over coefficients of (c - 3)^2"""
+
+    def __init__(self):
+        pass
+
+    def loss_and_grad(self, candidates, data, rows=None):
+        rows = co.coefficient_rows(candidates) if rows is None else rows
+        vals = [c[r[:, 0], r[:, 1], 3] for c, r in zip(candidates, rows)]
+        loss = np.array([np.sum((v - 3.0) ** 2) for v in vals], np.float32)
+        return loss, [(2 * (v - 3.0)).astype(np.float32) for v in vals]
+
+
+def test_optimise_loop_semantics():
+    """gp.py:454-473: epoch e evaluates the candidates BEFORE its update; the result is the
+    first minimum over the epochs and the candidate it was computed on."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    c = np.stack([tree_from_expr(("+", 1.0, "x0"), lib, 10), tree_from_expr(("*", 2.5, "x1"), lib, 10)])
+    cands = np.stack([c, c])
+    cands[1, 0, 8, 3] = 3.0  # second candidate: first coefficient already optimal
+    opt = _QuadraticOptimiser()
+    fit, out = opt.optimise(cands, None, 5, co.adam(0.5, 0.9, 0.999))
+    # candidate 0: moving towards 3 each epoch -> the best is the last evaluated epoch (4 updates)
+    assert fit[0] < np.sum((np.array([1.0, 2.5]) - 3) ** 2)
+    assert np.isclose(fit[0], np.sum((out[0][[0, 1], [8, 8], 3] - 3.0) ** 2))
+    # the structure is untouched, only coefficient values move
+    assert np.array_equal(out[:, :, :, :3], cands[:, :, :, :3])
+    # epoch-0 loss is the unmodified candidate's loss when nothing improves
+    fit2, out2 = opt.optimise(np.stack([cands[1]]), None, 1)
+    assert np.array_equal(out2[0], cands[1])
+
+
+def test_coefficient_optimisation_config_checks():
+    lib_ops, vl = SR_OPS, [["x0", "x1"]]
+    ff = mt.SREvaluator(solver=mt.RK4(), dt0=0.05)
+    with pytest.raises(AssertionError):
+        mt.GeneticProgramming(20, 20, ff, lib_ops, vl, [2], coefficient_optimisation=True, gradient_steps=0,
+                              verbose=False)
+    ffd = mt.SREvaluator(solver=mt.Dopri5(), dt0=0.05, stepsize_controller=mt.PIDController(1e-4, 1e-4))
+    with pytest.raises(NotImplementedError):
+        mt.GeneticProgramming(20, 20, ffd, lib_ops, vl, [2], coefficient_optimisation=True, verbose=False)
+
+
+# ------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("euler", [False, True])
+def test_gpu_sr_grad_bitexact(euler):
+    """mtgp_sr_grad vs oracle_sr_grad: loss and every coefficient's gradient bit for bit."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    lib, ff, data, d, pop = _setup(P=40, R=8, euler=euler, seed=5)
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    opt = co.CoefficientOptimiser(eng)
+    loss, grads = opt.loss_and_grad(pop, data)
+    rl, rg, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    assert bits_equal(loss, rl)
+    for p, g in enumerate(grads):
+        assert bits_equal(g, rg[p, : len(g)]), p
+    fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
+    assert bits_equal(loss, fit)
+
+
+@pytest.mark.gpu
+def test_gpu_sr_grad_chunks():
+    """More coefficients than one launch holds (cap forced to 3): the chunks give the same
+    gradients as the oracle."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    lib, ff, data, d, pop = _setup(P=16, R=4, seed=7)
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    opt = co.CoefficientOptimiser(eng)
+    opt.param_cap = lambda n_data: 3
+    loss, grads = opt.loss_and_grad(pop, data)
+    rl, rg, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    assert max(len(r) for r in rows) > 3
+    assert bits_equal(loss, rl)
+    for p, g in enumerate(grads):
+        assert bits_equal(g, rg[p, : len(g)]), p
+
+
+@pytest.mark.gpu
+def test_gpu_evaluate_population_optimises_coefficients():
+    """Generation 14 of a coefficient-optimising run (gp.py:418): the 50 best candidates get
+    gradient_steps Adam steps; fitness, population and best tracking equal a CPU restatement of
+    the same loop driven by the oracle's loss and gradients."""
+    lib, ff, data, d, pop = _setup(P=60, R=4, seed=9)
+    strategy = mt.GeneticProgramming(20, 60, ff, SR_OPS, [["x0", "x1"]], [2], max_nodes=20, size_parsinomy=0.01,
+                                     coefficient_optimisation=True, gradient_steps=4, verbose=False)
+    strategy.current_generation = 14
+    fit, newpop = strategy.evaluate_population(pop[None], data)
+    model, ro = oracle_model(ff, d), oracle_rollouts(d)
+    raw = orc.evaluate(model, pop, lib, ro)["fitness"]
+    idx = np.argsort(raw, kind="stable")[:50]
+    cands = pop[idx].copy()
+    rows = co.coefficient_rows(cands)
+    vals = np.concatenate([c[r[:, 0], r[:, 1], 3] for c, r in zip(cands, rows)]).astype(np.float32)
+    offs = np.concatenate([[0], np.cumsum([len(r) for r in rows])])
+    opt = co.adam()
+    st = opt.init(vals)
+    hist_c, hist_l = [], []
+    for _ in range(4):
+        loss, grad, _ = orc.sr_grad(model, cands, lib, ro)
+        hist_c.append(cands.copy())
+        hist_l.append(loss)
+        g = np.concatenate([grad[b, : len(r)] for b, r in enumerate(rows)]).astype(np.float32)
+        u, st = opt.update(g, st, vals)
+        vals = (vals + u).astype(np.float32)
+        for b, r in enumerate(rows):
+            cands[b][r[:, 0], r[:, 1], 3] = vals[offs[b]: offs[b + 1]]
+    Lh = np.stack(hist_l)
+    best = np.argmin(Lh, axis=0)
+    want_pop = pop.copy()
+    want_pop[idx] = np.stack([hist_c[e][b] for b, e in enumerate(best)])
+    want = raw.copy()
+    want[idx] = Lh.min(axis=0)
+    counts = (want_pop[..., 0] != 0).sum(axis=(1, 2)).astype(np.float32)
+    want = (want + np.float32(0.01) * counts).astype(np.float32)
+    assert bits_equal(newpop[0], want_pop)
+    assert bits_equal(fit[0], want)
+    assert strategy.best_fitnesses[14] == want.min()
+    assert np.any(Lh.min(axis=0) < Lh[0])  # the optimisation improved some candidates
