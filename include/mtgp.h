@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 11
+#define MTGP_ABI_VERSION 12
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -197,6 +197,16 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N,
                  int32_t L, MtgpInstr* prog_out, int32_t* len_out, int32_t* nodes_out,
                  int32_t* status_out, void* stream);
 
+/* mtgp_flatten plus the per-program sizing of the program JIT (ABI v12), so the JIT build needs no
+ * translation pass of its own: jit_words_out[P, n_prog] = code words of the program's
+ * fall-through translation (mtgp_jit.h jit_program; < 0: untranslatable) and jit_cost_out[P,
+ * n_prog] = the schedule weight mtgp_jit_cost would compute.  Either may be NULL.  population
+ * must be 16-byte aligned (rows are loaded as 16-byte vectors). */
+int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N,
+                    const MtgpNodeLibrary* lib, const MtgpProgramSpec* specs, int32_t n_prog,
+                    int32_t L, MtgpInstr* prog_out, int32_t* len_out, int32_t* nodes_out,
+                    int32_t* status_out, int32_t* jit_words_out, int32_t* jit_cost_out, void* stream);
+
 /* Same algorithm on the host (one tree), for tests and tooling. Returns program length
  * or a negative MTGP_ERR_* / -MTGP_ERR_PROG_TOO_LONG / -MTGP_ERR_STACK. */
 int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* lib,
@@ -263,6 +273,14 @@ int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, i
 int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                   const int32_t* order, const uint32_t* offsets, void* code, size_t code_bytes,
                   void* stream);
+/* The same plan / emit from mtgp_flatten_ex's jit_words (ABI v12): the unit layout is a gather +
+ * scan of the per-program sizes, and emit translates the G programs of a unit in parallel.
+ * Offsets, info and code are identical to mtgp_jit_plan / mtgp_jit_emit. */
+int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t R,
+                        const int32_t* order, uint32_t* offsets_out, int32_t* info_out, void* stream);
+int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog,
+                        int32_t L, int32_t R, const int32_t* order, const uint32_t* offsets, void* code,
+                        size_t code_bytes, void* stream);
 /* host translation of one program (tests/tooling): number of code words, or < 0 */
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
 /* Schedule weights for JIT code: cost_out[P*n_prog] = executed code words / 4 of each program

@@ -201,18 +201,96 @@ MTGP_INLINE MTGP_HD float bits_to_f32(uint32_t u) {
   return f;
 }
 
+// Superinstructions (peephole over an emitted program): a leaf load followed by the leaf
+// operation or unary that consumes it becomes one instruction.  Exact: the fused handler
+// performs the same single fp32 operation on the same operands; the only rewrites swap the
+// operands of + and * (commutative in IEEE arithmetic, signed zeros included) or turn
+// "c - v" / "c / v" into the reversed VC forms.
+MTGP_INLINE MTGP_HD bool fuse_pair(const MtgpInstr& a, const MtgpInstr& b, MtgpInstr* f) {
+  const uint32_t oa = a.op >> MTGP_OP_SHIFT, ob = b.op >> MTGP_OP_SHIFT;
+  uint32_t ia, ib;
+  __builtin_memcpy(&ia, &a.imm, 4);
+  __builtin_memcpy(&ib, &b.imm, 4);
+  const bool push = (oa == MTGP_OP_LDVP || oa == MTGP_OP_LDCP);
+  if (oa == MTGP_OP_LDV || oa == MTGP_OP_LDVP) {  // acc = v_a ...
+    const int kc = fam_idx(ob, FK_C);
+    if (kc >= 0) {  // ... op c
+      f->op = (fam_op(push ? FK_VCP : FK_VC, kc) << MTGP_OP_SHIFT) | ia;
+      f->imm = b.imm;
+      return true;
+    }
+    const int kv = fam_idx(ob, FK_V);
+    if (kv >= 0) {  // ... op v_b  ->  VV(left, right)
+      uint32_t l = ia, r = ib, op;
+      switch (kv) {
+        case 0: op = push ? MTGP_OP_VVP_ADD : MTGP_OP_VV_ADD; break;
+        case 1: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; break;
+        case 2: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; l = ib; r = ia; break;  // v_b - v_a
+        case 3: op = push ? MTGP_OP_VVP_MUL : MTGP_OP_VV_MUL; break;
+        case 4: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; break;
+        default: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; l = ib; r = ia; break;  // v_b / v_a
+      }
+      f->op = (op << MTGP_OP_SHIFT) | r;
+      f->imm = bits_to_f32(l);
+      return true;
+    }
+    if (ob == MTGP_OP_SIN || ob == MTGP_OP_COS) {
+      const uint32_t op = ob == MTGP_OP_SIN ? (push ? MTGP_OP_SINVP : MTGP_OP_SINV) : (push ? MTGP_OP_COSVP : MTGP_OP_COSV);
+      f->op = op << MTGP_OP_SHIFT;
+      f->imm = a.imm;
+      return true;
+    }
+    return false;
+  }
+  if (oa == MTGP_OP_LDC || oa == MTGP_OP_LDCP) {  // acc = c op v_b
+    const int kv = fam_idx(ob, FK_V);
+    if (kv < 0) return false;
+    const int map[6] = {0, 2, 1, 3, 5, 4};  // c+v = v+c, c-v = RSUB, v-c = SUB, c*v, c/v = RDIV, v/c = DIV
+    f->op = (fam_op(push ? FK_VCP : FK_VC, map[kv]) << MTGP_OP_SHIFT) | ib;
+    f->imm = a.imm;
+    return true;
+  }
+  return false;
+}
+
+// The emitter applies the superinstruction peephole while it writes: the last instruction is
+// held back until the next one shows whether the pair fuses (the same greedy left-to-right
+// pairing as a second pass over the finished program, without reading it back).  n counts the
+// unfused instructions (the length limits are defined on it), j the words written.
 struct Emitter {
   MtgpInstr* out;
   int cap;
   int n;
   int pending_push;
+  int j;
+  bool have;
+  MtgpInstr held;
   MTGP_HD void put(uint32_t op, uint32_t slot, float imm) {
     // V opcodes carry the slot as an LDS byte offset (mtgp.h program format)
     if (n < cap) {
-      out[n].op = op << MTGP_OP_SHIFT;
-      out[n].imm = is_var_op(op) ? bits_to_f32(slot * MTGP_SLOT_BYTES) : imm;
+      MtgpInstr x;
+      x.op = op << MTGP_OP_SHIFT;
+      x.imm = is_var_op(op) ? bits_to_f32(slot * MTGP_SLOT_BYTES) : imm;
+      if (have) {
+        MtgpInstr f;
+        if (fuse_pair(held, x, &f)) {
+          out[j++] = f;
+          have = false;
+        } else {
+          out[j++] = held;
+          held = x;
+        }
+      } else {
+        held = x;
+        have = true;
+      }
     }
     ++n;
+  }
+  MTGP_HD int finish() {
+    if (have) out[j++] = held;
+    have = false;
+    return j;
   }
   // load a leaf operand into acc (pushing the previous acc when a push is pending)
   MTGP_HD void load(const Ref& x, const RowInfo* info) {
@@ -251,13 +329,16 @@ struct Emitter {
 };
 
 // Emit the program computing row `root` into acc. Uses an explicit frame stack.
-MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* out, int cap) {
+// Returns the unfused instruction count; *fused = words written (valid when count <= cap).
+MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* out, int cap, int* fused) {
   Emitter em;
-  em.out = out; em.cap = cap; em.n = 0; em.pending_push = 0;
+  em.out = out; em.cap = cap; em.n = 0; em.pending_push = 0; em.j = 0; em.have = false;
+  *fused = 0;
   const RowInfo& rr = info[root];
   if (rr.isconst || rr.kind == K_VAR) {
     Ref x; x.row = (int16_t)root; x.val = 0.0f;
     em.load(x, info);
+    *fused = em.finish();
     return em.n;
   }
   int16_t fr_row[MTGP_MAX_NODES + 1];
@@ -324,12 +405,12 @@ MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* o
       }
     }
   }
+  if (em.n <= cap) *fused = em.finish();
   return em.n;
 }
 
-// Full flatten of one tree into `slots` instructions: the program (at most slots - 1) and
-// its MTGP_OP_END.  Returns the program length (>0, END excluded) or -MTGP_ERR_*; on error
-// the slot holds a bare END (an empty program), so an evaluator never runs stale words.
+// Full flatten of one tree: the fused program (unfused length at most cap) -> its length, or
+// -MTGP_ERR_*.
 MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNodeLibrary* lib,
                                           int n_data, uint64_t zero_mask, MtgpInstr* out, int cap,
                                           RowInfo* info, int* stack_need) {
@@ -346,83 +427,20 @@ MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNo
   if (stack_need) *stack_need = need;
   if (need > MTGP_STACK_MAX) return -MTGP_ERR_STACK;
   if (info[N - 1].len > cap) return -MTGP_ERR_PROG_TOO_LONG;
-  const int n = emit_program(N - 1, info, out, cap);
+  int fused = 0;
+  const int n = emit_program(N - 1, info, out, cap, &fused);
   if (n > cap) return -MTGP_ERR_PROG_TOO_LONG;
-  return n;
+  return fused;
 }
 
-// Superinstructions (peephole over an emitted program): a leaf load followed by the leaf
-// operation or unary that consumes it becomes one instruction.  Exact: the fused handler
-// performs the same single fp32 operation on the same operands; the only rewrites swap the
-// operands of + and * (commutative in IEEE arithmetic, signed zeros included) or turn
-// "c - v" / "c / v" into the reversed VC forms.
-MTGP_INLINE MTGP_HD bool fuse_pair(const MtgpInstr& a, const MtgpInstr& b, MtgpInstr* f) {
-  const uint32_t oa = a.op >> MTGP_OP_SHIFT, ob = b.op >> MTGP_OP_SHIFT;
-  uint32_t ia, ib;
-  __builtin_memcpy(&ia, &a.imm, 4);
-  __builtin_memcpy(&ib, &b.imm, 4);
-  const bool push = (oa == MTGP_OP_LDVP || oa == MTGP_OP_LDCP);
-  if (oa == MTGP_OP_LDV || oa == MTGP_OP_LDVP) {  // acc = v_a ...
-    const int kc = fam_idx(ob, FK_C);
-    if (kc >= 0) {  // ... op c
-      f->op = (fam_op(push ? FK_VCP : FK_VC, kc) << MTGP_OP_SHIFT) | ia;
-      f->imm = b.imm;
-      return true;
-    }
-    const int kv = fam_idx(ob, FK_V);
-    if (kv >= 0) {  // ... op v_b  ->  VV(left, right)
-      uint32_t l = ia, r = ib, op;
-      switch (kv) {
-        case 0: op = push ? MTGP_OP_VVP_ADD : MTGP_OP_VV_ADD; break;
-        case 1: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; break;
-        case 2: op = push ? MTGP_OP_VVP_SUB : MTGP_OP_VV_SUB; l = ib; r = ia; break;  // v_b - v_a
-        case 3: op = push ? MTGP_OP_VVP_MUL : MTGP_OP_VV_MUL; break;
-        case 4: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; break;
-        default: op = push ? MTGP_OP_VVP_DIV : MTGP_OP_VV_DIV; l = ib; r = ia; break;  // v_b / v_a
-      }
-      f->op = (op << MTGP_OP_SHIFT) | r;
-      f->imm = bits_to_f32(l);
-      return true;
-    }
-    if (ob == MTGP_OP_SIN || ob == MTGP_OP_COS) {
-      const uint32_t op = ob == MTGP_OP_SIN ? (push ? MTGP_OP_SINVP : MTGP_OP_SINV) : (push ? MTGP_OP_COSVP : MTGP_OP_COSV);
-      f->op = op << MTGP_OP_SHIFT;
-      f->imm = a.imm;
-      return true;
-    }
-    return false;
-  }
-  if (oa == MTGP_OP_LDC || oa == MTGP_OP_LDCP) {  // acc = c op v_b
-    const int kv = fam_idx(ob, FK_V);
-    if (kv < 0) return false;
-    const int map[6] = {0, 2, 1, 3, 5, 4};  // c+v = v+c, c-v = RSUB, v-c = SUB, c*v, c/v = RDIV, v/c = DIV
-    f->op = (fam_op(push ? FK_VCP : FK_VC, map[kv]) << MTGP_OP_SHIFT) | ib;
-    f->imm = a.imm;
-    return true;
-  }
-  return false;
-}
-
-MTGP_INLINE MTGP_HD int fuse_program(MtgpInstr* out, int n) {
-  int j = 0;
-  for (int i = 0; i < n;) {
-    MtgpInstr f;
-    if (i + 1 < n && fuse_pair(out[i], out[i + 1], &f)) {
-      out[j++] = f;
-      i += 2;
-    } else {
-      out[j++] = out[i++];
-    }
-  }
-  return j;
-}
-
+// Full flatten of one tree into `slots` instructions: the program (at most slots - 1) and
+// its MTGP_OP_END.  Returns the program length (>0, END excluded) or -MTGP_ERR_*; on error
+// the slot holds a bare END (an empty program), so an evaluator never runs stale words.
 MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLibrary* lib,
                                      int n_data, uint64_t zero_mask, MtgpInstr* out, int slots,
                                      RowInfo* info, int* stack_need) {
   if (slots < 1) return -MTGP_ERR_PROG_TOO_LONG;
-  int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
-  if (n > 0) n = fuse_program(out, n);
+  const int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
   const int at = n > 0 ? n : 0;
   out[at].op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
   out[at].imm = 0.0f;

@@ -292,6 +292,31 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
   return o.n;
 }
 
+// Group g of the unit whose first schedule slot is q0 (program j): the code jit_unit emits for
+// that group, written at `out` (= byte offset `base` in the buffer), plus the unit's final
+// s_setpc when `last`.  jit_unit == the concatenation of its groups.
+MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
+                                      int g, int j, bool last, uint32_t* out, uint32_t base) {
+  JitOut o{out, 0};
+  o.base = base;
+  const int q = q0 + g;
+  const int ind = order ? order[q] : q;
+  if (g > 0) o.movv(kJitKeep, kJitAcc);
+  const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false);
+  if (rc < 0) return rc;
+  if (g > 0) {
+    const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);
+    o.w(kMovS42);
+    o.w((uint32_t)mask);
+    o.w(kMovS43);
+    o.w((uint32_t)(mask >> 32));
+    o.w(kSelLo);
+    o.w(kSelHi);
+  }
+  if (last) o.w(kSetpcS30);
+  return o.n;
+}
+
 }  // namespace mtgp
 
 #endif  // MTGP_JIT_H

@@ -20,6 +20,7 @@
 #include <hsa/hsa.h>
 #include <hsa/hsa_ext_amd.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <atomic>
 #include <mutex>
 #include <type_traits>
@@ -28,6 +29,7 @@
 #include "mtgp_prng.h"
 #include "mtgp_dopri5.h"
 #include "mtgp_flatten.h"
+#include "mtgp_flatten_uniform.h"
 #include "mtgp_jit.h"
 
 // Translation units.  The library is compiled from this file several times in parallel
@@ -1592,37 +1594,260 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
 }
 
 // --------------------------------------------------------------------------------------
-// Flatten: one thread per (individual, program spec); per-row scratch in private memory.
-#ifndef MTGP_FLATTEN_TPB
-#define MTGP_FLATTEN_TPB 32
-#endif
-static_assert(MTGP_FLATTEN_TPB > 0 && MTGP_FLATTEN_TPB <= 64, "k_flatten is built for blocks of at most 64 lanes");
+// Flatten: one thread per (individual, program spec), row-uniform control flow
+// (mtgp_flatten_uniform.h): pass 1 resolves and sizes the rows in ascending order into an LDS
+// table [row][lane], pass 2 walks the rows in descending order and writes every reachable node's
+// word at its postorder position.  Rows are streamed from HBM eight at a time, the next eight in
+// flight while the current ones are resolved.  Optionally the lane also sizes its program's JIT
+// translation (jit_words: fall-through code words, < 0 if untranslatable; jit_cost: the schedule
+// weight), so the JIT build needs no translation pass of its own before the code is emitted.
+constexpr int32_t kFlatSerial = 0x7fff;  // status of a program left to k_flatten_serial
+
+// JIT sizing of one flattened program (mtgp_flatten_ex jit_words / jit_cost)
+__device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n, int32_t* jit_words_out,
+                                              int32_t* jit_cost_out, size_t pj) {
+  if (!jit_words_out && !jit_cost_out) return;
+  mtgp::JitOut o{nullptr, 0};
+  const int rc = mtgp::jit_program(o, out, L, false);
+  if (jit_words_out) jit_words_out[pj] = rc < 0 ? rc : o.n;
+  if (jit_cost_out) {  // = k_jit_cost: executed words of the callable translation / 4
+    const int c = rc < 0 ? rc : (o.n + 1 + mtgp::kJitTrigExecuted * o.trig);
+    jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
+  }
+}
+
+// The serial flatten_tree for the programs k_flatten flagged (a row reached from two parents):
+// a small grid strides over all programs, so the private row table it needs is allocated for few
+// waves only.
 template <int NMAX>
-__global__ void __launch_bounds__(64) k_flatten(const float* __restrict__ pop, int P, int T, int N,
-                                                MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
-                                                int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
-                                                int32_t* nodes_out, int32_t* status_out) {
-  // per-lane row table in private memory: an LDS table (28 B x NMAX x 64 lanes = 112 KB at
-  // NMAX = 64) allowed one wave per CU; private arrays let the flatten run at full occupancy.
-  // Launched with MTGP_FLATTEN_TPB-lane blocks: the per-lane walk is latency-bound, so spreading
-  // P*n_prog lanes over twice the waves (C3: 512 -> 1024, one per SIMD) shortens the launch.
-  mtgp::RowInfo info_priv[NMAX];
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__ pop, int P, int T, int N,
+                                                       MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
+                                                       int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
+                                                       int32_t* status_out, int32_t* jit_words_out,
+                                                       int32_t* jit_cost_out) {
   const long total = (long)P * n_prog;
-  if (gid >= total) return;
+  for (long pj = (long)blockIdx.x * blockDim.x + threadIdx.x; pj < total; pj += (long)gridDim.x * blockDim.x) {
+    if (status_out[pj] != kFlatSerial) continue;
+    const int p = (int)(pj / n_prog), j = (int)(pj % n_prog);
+    const MtgpProgramSpec sp = specs[j];
+    MtgpInstr* out = prog_out + (size_t)pj * L;
+    mtgp::RowInfo info[NMAX];
+    const int n = mtgp::flatten_tree(pop + ((size_t)p * T + sp.tree) * N * 4, N, &lib, sp.n_data, sp.zero_mask, out,
+                                     L, info, nullptr);
+    len_out[pj] = n > 0 ? n : 0;
+    status_out[pj] = n > 0 ? 0 : -n;
+    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, (size_t)pj);
+  }
+}
+
+// lanes per block: the flatten is issue-latency bound (one tree per lane, few lanes in total), so
+// several small waves per SIMD beat one full one
+#ifndef MTGP_FLAT_LANES
+#define MTGP_FLAT_LANES 16
+#endif
+
+template <int NMAX, int TPB>
+__global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, int P, int T, int N,
+                                                            MtgpNodeLibrary lib,
+                                                            const MtgpProgramSpec* __restrict__ specs, int n_prog,
+                                                            int L, MtgpInstr* prog_out, int32_t* len_out,
+                                                            int32_t* nodes_out, int32_t* status_out,
+                                                            int32_t* jit_words_out, int32_t* jit_cost_out) {
+  using namespace mtgp;
+  __shared__ uint32_t s_w[NMAX * TPB];    // packed row record (u_pack)
+  __shared__ uint32_t s_len[NMAX * TPB];  // unfused length (low 16, saturated) | fused length (high 16)
+  __shared__ float s_cv[NMAX * TPB];      // folded constant
+  __shared__ int32_t s_pos[NMAX * TPB];   // pass 2: first word of the node's code | push << 16
+  __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
+  for (int k = threadIdx.x; k < MTGP_MAX_FUNCS; k += TPB) s_fn[k] = lib.fn[k];
+  __syncthreads();
+  const long gid = (long)blockIdx.x * TPB + threadIdx.x;
+  if (gid >= (long)P * n_prog) return;
+  const int lane = threadIdx.x;
   const int p = (int)(gid / n_prog), j = (int)(gid % n_prog);
   const MtgpProgramSpec sp = specs[j];
-  const float* tree = pop + ((size_t)p * T + sp.tree) * N * 4;
-  mtgp::RowInfo* info = info_priv;
-  MtgpInstr* out = prog_out + ((size_t)p * n_prog + j) * L;
-  int need = 0;
-  const int n = mtgp::flatten_tree(tree, N, &lib, sp.n_data, sp.zero_mask, out, L, info, &need);
-  len_out[(size_t)p * n_prog + j] = n > 0 ? n : 0;
-  status_out[(size_t)p * n_prog + j] = n > 0 ? 0 : -n;
+  const float4* tr = reinterpret_cast<const float4*>(pop + ((size_t)p * T + sp.tree) * N * 4);
+  const size_t pj = (size_t)p * n_prog + j;
+  MtgpInstr* out = prog_out + pj * L;
+  const int cap = L - 1;
+  const int n_funcs = lib.n_funcs, var_start = lib.var_start, n_data = sp.n_data;
+  const uint64_t zmask = sp.zero_mask;
+#define MTGP_UAT(i) ((i) * TPB + lane)
+  // operand row jj of row i: an evaluated row (its table entry) or, for jj >= i, the original
+  // value column (gp.py:366-369)
+  auto operand = [&](int jj, int i, uint32_t& w, ULeaf& lf, int& len, int& flen, bool& leaf) {
+    if (jj < i) {
+      w = s_w[MTGP_UAT(jj)];
+      const uint32_t ln = s_len[MTGP_UAT(jj)];
+      len = (int)(ln & 0xffffu);
+      flen = (int)(ln >> 16);
+      lf.isc = u_isc(w);
+      lf.v = s_cv[MTGP_UAT(jj)];
+      lf.slot = u_slot(w);
+      leaf = u_leaf(w);
+    } else {
+      w = u_pack(K_CONST, 0, 0, 1, 1, 0);
+      lf.isc = true;
+      lf.v = tr[jj].w;
+      lf.slot = 0;
+      len = flen = 1;
+      leaf = true;
+    }
+  };
+  // ---- pass 1: resolve + size (resolve_row / size_row) in row order
+  int cnt = 0;  // non-empty rows of this tree (gp.py:424)
+  float4 nxt[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) nxt[k] = k < N ? tr[k] : make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int i0 = 0; i0 < N; i0 += 8) {
+    float4 cur[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      cur[k] = nxt[k];
+      nxt[k] = (i0 + 8 + k < N) ? tr[i0 + 8 + k] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int i = i0 + k;
+      if (i >= N) break;
+      const float4 row = cur[k];
+      cnt += row.x != 0.0f ? 1 : 0;
+      uint32_t kind = K_CONST, fnc = MTGP_FN_ZERO, slot = 0, isc = 1, afirst = 1, need = 0;
+      int len = 1, flen = 1;
+      float cv = 0.0f;
+      if (row.x == 1.0f) {  // coefficient (gp.py:372 select)
+        cv = row.w;
+      } else {
+        int32_t f = f2i_sat(row.x);
+        f = f < 0 ? 0 : (f > n_funcs - 1 ? n_funcs - 1 : f);
+        const int fn = s_fn[f];
+        if (fn == MTGP_FN_VAR) {
+          int sl = f - var_start;
+          if (sl > n_data - 1) sl = n_data - 1;
+          slot = (uint32_t)sl;
+          if (!((zmask >> sl) & 1ull)) { kind = K_VAR; isc = 0; }
+        } else if (fn_arity(fn) > 0) {
+          const int ar = fn_arity(fn);
+          fnc = (uint32_t)fn;
+          kind = ar == 1 ? K_UNARY : K_BINARY;
+          uint32_t wa, wb = 0;
+          ULeaf la, lb;
+          lb.isc = true; lb.v = 0.0f; lb.slot = 0;
+          int lena, flena, lenb = 1, flenb = 1;
+          bool leafa, leafb = true;
+          operand(norm_index(row.y, N), i, wa, la, lena, flena, leafa);
+          if (ar == 2) operand(norm_index(row.z, N), i, wb, lb, lenb, flenb, leafb);
+          if (la.isc && lb.isc) {  // constant subtree: folded with the kernel's fp32 primitives
+            cv = apply_fn(fn, la.v, ar == 1 ? 0.0f : lb.v);
+          } else {
+            isc = 0;
+            if (ar == 1) {
+              if (leafa) { len = 2; flen = 1; }
+              else { len = lena + 1; flen = flena + 1; need = u_need(wa); }
+            } else if (leafa && leafb) {
+              len = 2; flen = 1;
+            } else if (leafb) {
+              len = lena + 1; flen = flena + 1; need = u_need(wa);
+            } else if (leafa) {
+              len = lenb + 1; flen = flenb + 1; need = u_need(wb);
+            } else {
+              const uint32_t pa = u_need(wa), qb = u_need(wb);
+              len = lena + lenb + 1;
+              flen = flena + flenb + 1;
+              if (pa >= qb) { afirst = 1; need = pa > qb + 1 ? pa : qb + 1; }
+              else { afirst = 0; need = qb > pa + 1 ? qb : pa + 1; }
+            }
+          }
+        }  // else: empty node (gp.py:135) -> +0.0
+      }
+      s_w[MTGP_UAT(i)] = u_pack(kind, fnc, slot, isc, afirst, need > 31u ? 31u : need);
+      s_len[MTGP_UAT(i)] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
+      s_cv[MTGP_UAT(i)] = cv;
+    }
+  }
+  const uint32_t wr = s_w[MTGP_UAT(N - 1)], lr = s_len[MTGP_UAT(N - 1)];
+  int n;
+  if ((int)u_need(wr) > MTGP_STACK_MAX) n = -MTGP_ERR_STACK;
+  else if ((int)(lr & 0xffffu) > cap) n = -MTGP_ERR_PROG_TOO_LONG;
+  else n = (int)(lr >> 16);
+  // ---- pass 2: postorder positions top-down, one word per node
+  bool shared = false;
+  if (n > 0) {
+    if (u_leaf(wr)) {  // the whole tree is one leaf
+      ULeaf x;
+      x.isc = u_isc(wr); x.v = s_cv[MTGP_UAT(N - 1)]; x.slot = u_slot(wr);
+      out[0] = u_load(x, false);
+    } else {
+      UBits<NMAX> reach;
+      reach.clear();
+      reach.set(N - 1);
+      s_pos[MTGP_UAT(N - 1)] = 0;
+      for (int i = N - 1; i >= 0; --i) {
+        if (!reach.test(i)) continue;
+        const uint32_t w = s_w[MTGP_UAT(i)];
+        const int pp = s_pos[MTGP_UAT(i)], pos = pp & 0xffff;
+        const bool push = (pp >> 16) != 0;
+        const float4 row = tr[i];
+        const int fn = (int)u_fn(w);
+        uint32_t wa, wb;
+        ULeaf la, lb;
+        int lena, flena, lenb = 1, flenb = 1;
+        bool leafa, leafb = true;
+        const int ja = norm_index(row.y, N);
+        operand(ja, i, wa, la, lena, flena, leafa);
+        int jb = 0;
+        if (u_kind(w) == K_BINARY) {
+          jb = norm_index(row.z, N);
+          operand(jb, i, wb, lb, lenb, flenb, leafb);
+        }
+        auto visit = [&](int c, int cpos, bool cpush) {
+          shared = shared || reach.test(c);  // a sub-DAG reached twice: emitted twice by the walk
+          reach.set(c);
+          s_pos[MTGP_UAT(c)] = cpos | (cpush ? 1 << 16 : 0);
+        };
+        MtgpInstr x;
+        if (u_kind(w) == K_UNARY) {
+          const MtgpInstr un = u_instr(fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
+          if (leafa) { fuse_pair(u_load(la, push), un, &x); out[pos] = x; }
+          else { visit(ja, pos, push); out[pos + flena] = un; }
+        } else if (leafa && leafb) {
+          fuse_pair(u_load(la, push), u_op_leaf(fn, 0, lb), &x);
+          out[pos] = x;
+        } else if (leafb) {
+          visit(ja, pos, push);
+          out[pos + flena] = u_op_leaf(fn, 0, lb);
+        } else if (leafa) {
+          visit(jb, pos, push);
+          out[pos + flenb] = u_op_leaf(fn, 1, la);
+        } else {
+          const bool af = u_afirst(w) != 0;
+          const int f1 = af ? flena : flenb, f2 = af ? flenb : flena;
+          visit(af ? ja : jb, pos, push);
+          visit(af ? jb : ja, pos + f1, true);
+          out[pos + f1 + f2] = u_op_stack(fn, af ? 1 : 0);
+        }
+      }
+    }
+  }
+#undef MTGP_UAT
+  if (shared) {
+    // arbitrary arrays only: the serial walk duplicates the shared subtree -- left to
+    // k_flatten_serial, so that this kernel needs no private row table (scratch)
+    len_out[pj] = 0;
+    status_out[pj] = kFlatSerial;
+  } else {
+    MtgpInstr e;
+    e.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+    e.imm = 0.0f;
+    out[n > 0 ? n : 0] = e;
+    len_out[pj] = n > 0 ? n : 0;
+    status_out[pj] = n > 0 ? 0 : -n;
+    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, pj);
+  }
   // node count (gp.py:424 parsimony): the individual's trees are shared out over its n_prog
   // lanes (tree t -> lane t % n_prog) and summed with integer atomics into the zeroed nodes_out
   int c = 0;
-  for (int t = j; t < T; t += n_prog) c += mtgp::count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
+  for (int t = j; t < T; t += n_prog) c += (t == sp.tree) ? cnt : count_nodes(pop + ((size_t)p * T + t) * N * 4, N);
   if (c != 0) atomicAdd(&nodes_out[p], c);
 }
 
@@ -1759,6 +1984,112 @@ __global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t*
   const uint32_t b = offs[i], e = offs[i + 1];
   if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
   jit_unit_words(U, i, code + b / 4, b);
+}
+
+// Unit layout from the flatten's per-program code sizes (mtgp_flatten_ex jit_words): unit
+// (wave, j) = its G groups' programs + (G_live - 1) * 7 merge words + s_setpc (mtgp_jit.h
+// jit_unit), 64-byte aligned; a grid sizes the units, one block scans the sizes into byte
+// offsets.  Replaces the k_jit_count translation pass + k_jit_scan.
+__device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const int32_t* __restrict__ jw, int u) {
+  const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  int n = 1;  // s_setpc_b64
+  for (int g = 0; g < U.G; ++g) {
+    const int q = wave * U.G + g;
+    if (q >= U.P) break;
+    const int ind = U.order ? U.order[q] : q;
+    const int w = jw[(size_t)ind * U.n_prog + j];
+    if (w < 0) return w;
+    n += w + (g > 0 ? 7 : 0);
+  }
+  return n;
+}
+
+// pass 1, one thread per unit: its size in bytes, or 0x80000000 | -error
+__global__ void __launch_bounds__(256) k_jit_sizes(JitUnitArgs U, const int32_t* __restrict__ jw,
+                                                   uint32_t* __restrict__ offs) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U.n_units) return;
+  const int n = jit_unit_words_from(U, jw, u);
+  offs[u] = n > 0 ? ((uint32_t)n * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u) : (0x80000000u | (uint32_t)(-n));
+}
+
+// pass 2, one block: exclusive scan of the sizes in place (+ the shared templates in front),
+// offs[units] = total, info = {min error or 0, total bytes}.  Each thread owns a contiguous
+// run of units and loads it eight entries at a time (independent loads in flight).
+__global__ void __launch_bounds__(1024) k_jit_scan_sizes(uint32_t* __restrict__ offs, int total,
+                                                         int32_t* __restrict__ info) {
+  __shared__ uint64_t part[1024];
+  __shared__ int32_t err[1024];
+  const int t = threadIdx.x;
+  const int per = (total + 1023) / 1024;
+  const int b = t * per, e = b + per < total ? b + per : total;
+  uint64_t sum = 0;
+  int bad = 0;
+  for (int k0 = b; k0 < e; k0 += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (k0 + k < e) ? offs[k0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const bool isbad = (v[k] & 0x80000000u) != 0u;
+      const int code = -(int)(v[k] & 0x7fffffffu);
+      bad = (isbad && code < bad) ? code : bad;
+      sum += isbad ? 0u : v[k];
+    }
+  }
+  part[t] = sum;
+  err[t] = bad;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan (+ min of the error codes)
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    const int32_t m = t >= d ? err[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    err[t] = m < err[t] ? m : err[t];
+    __syncthreads();
+  }
+  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
+  for (int k0 = b; k0 < e; k0 += 8) {
+    uint32_t v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = (k0 + k < e) ? offs[k0 + k] : 0u;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k0 + k >= e) break;
+      const uint64_t w = (v[k] & 0x80000000u) ? 0u : v[k];
+      offs[k0 + k] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+      run += w;
+    }
+  }
+  if (t == 1023) {
+    const uint64_t tot = part[1023] + mtgp::kJitTemplateBytes;
+    offs[total] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+    info[0] = err[1023];
+    info[1] = (int32_t)(tot < 0x7fffffffull ? tot : 0x7fffffffull);
+  }
+}
+
+// Emit with one thread per (unit, group): group g's code starts after groups 0..g-1 (sizes from
+// jit_words), so the G programs of a unit are translated in parallel.
+__global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
+                                                        const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
+                                                        uint64_t code_bytes) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)U.n_units * U.G) return;
+  const int u = (int)(i / U.G), g = (int)(i - (long)u * U.G);
+  const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  const int q = wave * U.G + g;
+  if (q >= U.P) return;
+  const uint32_t b = offs[u], e = offs[u + 1];
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
+  uint32_t start = 0;  // words before group g inside the unit
+  for (int h = 0; h < g; ++h) {
+    const int ind = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
+    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (h > 0 ? 7u : 0u);
+  }
+  const bool last = (g == U.G - 1) || (q + 1 >= U.P);
+  const uint32_t at = b + start * 4u;
+  mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at);
 }
 
 // the shared sin/cos subroutines at the start of the code buffer
@@ -2044,6 +2375,36 @@ int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, i
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
+int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t R, const int32_t* order,
+                        uint32_t* offsets_out, int32_t* info_out, void* stream) {
+  JitUnitArgs U;
+  static const MtgpInstr dummy = {0u, 0.0f};
+  if (!jit_words || !offsets_out || !info_out || !jit_unit_args(&dummy, P, n_prog, 1, R, order, U)) return MTGP_ERR_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  if (U.n_units == 0) {
+    if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+    return hipMemsetAsync(offsets_out, 0, sizeof(uint32_t), s) == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  }
+  hipLaunchKernelGGL(k_jit_sizes, dim3((unsigned)((U.n_units + 255) / 256)), dim3(256), 0, s, U, jit_words,
+                     offsets_out);
+  hipLaunchKernelGGL(k_jit_scan_sizes, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t L,
+                        int32_t R, const int32_t* order, const uint32_t* offsets, void* code, size_t code_bytes,
+                        void* stream) {
+  JitUnitArgs U;
+  if (!jit_words || !offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
+  if (U.n_units == 0) return MTGP_OK;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(k_jit_templates, dim3(1), dim3(256), 0, s, (uint32_t*)code, (uint64_t)code_bytes);
+  const long threads = (long)U.n_units * U.G;
+  hipLaunchKernelGGL(k_jit_emit_groups, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, U, jit_words, offsets,
+                     (uint32_t*)code, (uint64_t)code_bytes);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
 int mtgp_jit_emit(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
                   const uint32_t* offsets, void* code, size_t code_bytes, void* stream) {
   JitUnitArgs U;
@@ -2105,30 +2466,51 @@ float mtgp_last_kernel_ms(void) {
   return ms;
 }
 
-int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
-                 const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
-                 int32_t* nodes_out, int32_t* status_out, void* stream) {
+int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
+                    const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
+                    int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out, int32_t* jit_cost_out,
+                    void* stream) {
   if (!population || !lib || !specs || !prog_out || !len_out || !nodes_out || !status_out) return MTGP_ERR_ARG;
   if (P < 0 || T <= 0 || N <= 0 || N > MTGP_MAX_NODES || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
   if (lib->n_funcs <= 0 || lib->n_funcs > MTGP_MAX_FUNCS) return MTGP_ERR_ARG;
+  if ((reinterpret_cast<uintptr_t>(population) & 15u) != 0) return MTGP_ERR_ARG;  // 16-byte row loads
   if (P == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const long total = (long)P * n_prog;
   MtgpNodeLibrary libv = *lib;
   if (hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
-  const int tpb = MTGP_FLATTEN_TPB;  // one lane per program
-  const dim3 grid((unsigned)((total + tpb - 1) / tpb)), block(tpb);
-  if (N <= 64) {
-    hipLaunchKernelGGL(k_flatten<64>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
-                       len_out, nodes_out, status_out);
-  } else if (N <= 128) {
-    hipLaunchKernelGGL(k_flatten<128>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
-                       len_out, nodes_out, status_out);
-  } else {
-    hipLaunchKernelGGL(k_flatten<256>, grid, block, 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out,
-                       len_out, nodes_out, status_out);
-  }
+  static const int lanes_env = [] {  // A/B knob (scripts/): MTGP_FLAT_LANES=8|16|32 at run time
+    const char* e = getenv("MTGP_FLAT_LANES");
+    const int v = e ? atoi(e) : MTGP_FLAT_LANES;
+    return (v == 8 || v == 16 || v == 32) ? v : MTGP_FLAT_LANES;
+  }();
+#define MTGP_FLAT_ONE(NM, TP)                                                                                 \
+  hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
+                     T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
+                     jit_cost_out)
+#define MTGP_FLAT_LAUNCH(NM)                                                                                \
+  do {                                                                                                      \
+    const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
+    if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                                    \
+    else if (tp >= 16) MTGP_FLAT_ONE(NM, 16);                                                               \
+    else MTGP_FLAT_ONE(NM, 8);                                                                              \
+    hipLaunchKernelGGL(k_flatten_serial<NM>, dim3((unsigned)(total < 64 * 64 ? (total + 63) / 64 : 64)),   \
+                       dim3(64), 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out, len_out,     \
+                       status_out, jit_words_out, jit_cost_out);                                            \
+  } while (0)
+  if (N <= 64) MTGP_FLAT_LAUNCH(64);
+  else if (N <= 128) MTGP_FLAT_LAUNCH(128);
+  else MTGP_FLAT_LAUNCH(256);
+#undef MTGP_FLAT_LAUNCH
+#undef MTGP_FLAT_ONE
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+}
+
+int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
+                 const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
+                 int32_t* nodes_out, int32_t* status_out, void* stream) {
+  return mtgp_flatten_ex(population, P, T, N, lib, specs, n_prog, L, prog_out, len_out, nodes_out, status_out,
+                         nullptr, nullptr, stream);
 }
 
 int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* lib, int32_t n_data,

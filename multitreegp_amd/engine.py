@@ -45,6 +45,8 @@ class Flattened:
     L: int
     n_prog: int
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
+    jit_words: Optional[torch.Tensor] = None  # int32 [P, n_prog] JIT code words per program (mtgp_flatten_ex)
+    jit_cost: Optional[torch.Tensor] = None   # int32 [P, n_prog] schedule weight of the JIT code
     jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity) of the JIT
     jit_key: Optional[tuple] = None       # (R, order, engine id, arena slot, arena generation) of that code
 
@@ -129,8 +131,12 @@ class DeviceEngine:
         offs = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
         info = torch.empty((3,), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
-        rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(),
-                                       info.data_ptr(), stream)
+        if fl.jit_words is not None:  # sizes from the flatten pass
+            rc = self.native.mtgp_jit_plan_words(fl.jit_words.data_ptr(), P, fl.n_prog, R, optr, offs.data_ptr(),
+                                                 info.data_ptr(), stream)
+        else:  # flattened without the sizing outputs: translate to size
+            rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(),
+                                           info.data_ptr(), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_plan failed: {rc}")
         info[2].fill_(n)
@@ -142,8 +148,12 @@ class DeviceEngine:
         G = 64 // (1 << max(R - 1, 0).bit_length())
         per_unit = self._jit_bytes_per_unit or 1024.0 * G
         ptr, size = self._arena(int(n * per_unit) + 4096)
-        rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(), ptr,
-                                       size, stream)
+        if fl.jit_words is not None:
+            rc = self.native.mtgp_jit_emit_words(fl.prog.data_ptr(), fl.jit_words.data_ptr(), P, fl.n_prog, fl.L,
+                                                 R, optr, offs.data_ptr(), ptr, size, stream)
+        else:
+            rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(), ptr,
+                                           size, stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
         fl.jit = (ptr, offs, info, size)
@@ -229,13 +239,25 @@ class DeviceEngine:
         plen = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
         nodes = torch.empty((P,), dtype=torch.int32, device=dev)
         status = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
+        jw = jc = None
+        if self._jit_usable():  # size the JIT translation in the same pass
+            jw = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
+            jc = torch.empty((P, n_prog), dtype=torch.int32, device=dev)
         stream = torch.cuda.current_stream(dev).cuda_stream
-        rc = self.native.mtgp_flatten(pop.data_ptr(), P, T, N, ctypes.byref(self._node_lib),
-                                      self._specs_dev.data_ptr(), n_prog, L, prog.data_ptr(),
-                                      plen.data_ptr(), nodes.data_ptr(), status.data_ptr(), stream)
+        pop = pop if pop.data_ptr() % 16 == 0 else pop.clone()
+        rc = self.native.mtgp_flatten_ex(pop.data_ptr(), P, T, N, ctypes.byref(self._node_lib),
+                                         self._specs_dev.data_ptr(), n_prog, L, prog.data_ptr(),
+                                         plen.data_ptr(), nodes.data_ptr(), status.data_ptr(), _ptr(jw), _ptr(jc),
+                                         stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_flatten failed: {rc}")
-        return Flattened(prog, plen, nodes, status, L, n_prog)
+        return Flattened(prog, plen, nodes, status, L, n_prog, jit_words=jw, jit_cost=jc)
+
+    def _jit_usable(self) -> bool:
+        """The program JIT serves the kernels whose data vector fits v0-v7 (mtgp_jit.h)."""
+        if not self.use_jit or self.ff.n_data() > 8:
+            return False
+        return not (self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4)
 
     @staticmethod
     def check_status(fl: Flattened):
@@ -261,6 +283,8 @@ class DeviceEngine:
         programs run as JIT code (sin/cos dominate there), the program length otherwise."""
         if not (self.use_jit and self.ff.n_data() <= 8):
             return fl.plen
+        if fl.jit_cost is not None:
+            return fl.jit_cost
         P = fl.plen.shape[0]
         cost = torch.empty_like(fl.plen)
         stream = torch.cuda.current_stream(self.device).cuda_stream

@@ -1,0 +1,123 @@
+"""The per-population build chain on the GPU: mtgp_flatten_ex (LDS-staged flatten + JIT sizing)
+and the word-based JIT plan / emit must reproduce the host flattener and the translation-based
+mtgp_jit_plan / mtgp_jit_emit exactly (programs, lengths, status, node counts, unit offsets, plan
+status and every code byte)."""
+import ctypes
+
+import numpy as np
+import pytest
+
+import multitreegp_amd as mt
+from multitreegp_amd import _native as nat
+from multitreegp_amd.sampling import sample_population
+
+from helpers import CONTROL_OPS, SR_OPS
+
+pytestmark = pytest.mark.gpu
+
+
+def _flatten_ex(pop, lib, specs, L):
+    import torch
+    P, T, N, _ = pop.shape
+    L_ = nat.load()
+    dev = torch.device("cuda", 0)
+    n_prog = len(specs)
+    arr = (nat.MtgpProgramSpec * n_prog)()
+    for i, (t, d, z) in enumerate(specs):
+        arr[i].tree, arr[i].n_data, arr[i].zero_mask = t, d, z
+    sp = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
+    pd = torch.from_numpy(np.ascontiguousarray(pop, np.float32)).to(dev)
+    prog = torch.empty((P * n_prog * L * 2 + 8,), dtype=torch.int32, device=dev)
+    out = {k: torch.empty(s, dtype=torch.int32, device=dev) for k, s in
+           (("plen", (P, n_prog)), ("nodes", (P,)), ("status", (P, n_prog)), ("jw", (P, n_prog)), ("jc", (P, n_prog)))}
+    libs = lib.native()
+    rc = L_.mtgp_flatten_ex(pd.data_ptr(), P, T, N, ctypes.byref(libs), sp.data_ptr(), n_prog, L, prog.data_ptr(),
+                            out["plen"].data_ptr(), out["nodes"].data_ptr(), out["status"].data_ptr(),
+                            out["jw"].data_ptr(), out["jc"].data_ptr(), None)
+    assert rc == nat.OK
+    torch.cuda.synchronize()
+    return prog, out
+
+
+def _population(kind, P, seed=0):
+    rng = np.random.default_rng(seed)
+    if kind == "dynamic":
+        vl = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
+        lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
+        pop = sample_population(seed, lib, P, 1, max_init_depth=10, max_nodes=64)[0]
+        specs = [(0, 7, 0), (1, 7, 0), (2, 7, 0b1001111), (2, 7, 0b1000000)]
+    else:  # 12-variable SR: slots >= 8 are untranslatable -> negative jit words
+        lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(12)]], [12])
+        pop = sample_population(seed, lib, P, 1, max_init_depth=6, max_nodes=40)[0]
+        specs = [(i, 12, 0) for i in range(12)]
+    g = rng.random(pop.shape[:1]) < 0.1  # garbage individuals: arbitrary arrays
+    junk = rng.normal(0, 8, size=pop.shape).astype(np.float32)
+    pop[g] = junk[g]
+    return lib, pop, specs
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "sr12"])
+def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind):
+    lib, pop, specs = _population(kind, 301)
+    P, T, N, _ = pop.shape
+    L = (2 * N + 8 + 3) // 4 * 4
+    prog, out = _flatten_ex(pop, lib, specs, L)
+    progs = prog[: P * len(specs) * L * 2].view(P, len(specs), L, 2).cpu().numpy()
+    plen, status, jw, jc = (out[k].cpu().numpy() for k in ("plen", "status", "jw", "jc"))
+    nodes = out["nodes"].cpu().numpy()
+    L_ = nat.load()
+    libs = lib.native()
+    host = np.zeros((L, 2), np.int32)
+    word = np.zeros(4096, np.uint32)
+    for p in range(P):
+        assert nodes[p] == int((pop[p, ..., 0] != 0).sum())
+        for j, (t, d, z) in enumerate(specs):
+            n = L_.mtgp_flatten_tree_host(pop[p, t].ctypes.data, N, ctypes.byref(libs), d, z, L, host.ctypes.data,
+                                          None)
+            assert plen[p, j] == max(n, 0) and status[p, j] == (0 if n > 0 else -n), (p, j)
+            assert np.array_equal(progs[p, j, : max(n, 0) + 1], host[: max(n, 0) + 1]), (p, j)
+            w = L_.mtgp_jit_translate_host(host.ctypes.data, L, word.ctypes.data, 4096)
+            assert jw[p, j] == (w - 1 if w > 0 else w + 100), (p, j, jw[p, j], w)
+    import torch
+    cost = torch.empty((P, len(specs)), dtype=torch.int32, device="cuda")
+    assert L_.mtgp_jit_cost(prog.data_ptr(), out["plen"].data_ptr(), P, len(specs), L, cost.data_ptr(), None) == 0
+    assert np.array_equal(cost.cpu().numpy(), jc)
+    if kind == "sr12":
+        assert (jw < 0).any() and (jw > 0).any()
+
+
+@pytest.mark.parametrize("kind", ["dynamic", "sr12"])
+@pytest.mark.parametrize("R", [1, 8, 32, 64])
+def test_word_based_jit_plan_and_emit_match_translation(kind, R):
+    import torch
+    lib, pop, specs = _population(kind, 257, seed=R)
+    P, T, N, _ = pop.shape
+    n_prog = len(specs)
+    L = (2 * N + 8 + 3) // 4 * 4
+    prog, out = _flatten_ex(pop, lib, specs, L)
+    L_ = nat.load()
+    order = torch.from_numpy(np.random.default_rng(R).permutation(P).astype(np.int32)).cuda()
+    n = L_.mtgp_jit_units(P, n_prog, R)
+    offs = [torch.empty((n + 1,), dtype=torch.int32, device="cuda") for _ in range(2)]
+    info = [torch.zeros((2,), dtype=torch.int32, device="cuda") for _ in range(2)]
+    assert L_.mtgp_jit_plan(prog.data_ptr(), P, n_prog, L, R, order.data_ptr(), offs[0].data_ptr(),
+                            info[0].data_ptr(), None) == 0
+    assert L_.mtgp_jit_plan_words(out["jw"].data_ptr(), P, n_prog, R, order.data_ptr(), offs[1].data_ptr(),
+                                  info[1].data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    assert np.array_equal(offs[0].cpu().numpy(), offs[1].cpu().numpy())
+    i0, i1 = info[0].cpu().numpy(), info[1].cpu().numpy()
+    assert (i0[0] < 0) == (i1[0] < 0) and i0[1] == i1[1]
+    if kind == "sr12":
+        assert i1[0] < 0
+        return
+    size = int(i1[1]) + 4096
+    # emit writes words only, so plain device buffers stand in for executable memory here
+    bufs = [torch.zeros((size // 4,), dtype=torch.int32, device="cuda") for _ in range(2)]
+    assert L_.mtgp_jit_emit(prog.data_ptr(), P, n_prog, L, R, order.data_ptr(), offs[0].data_ptr(),
+                            bufs[0].data_ptr(), size, None) == 0
+    assert L_.mtgp_jit_emit_words(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
+                                  offs[1].data_ptr(), bufs[1].data_ptr(), size, None) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(bufs[0], bufs[1])
+    assert int((bufs[1] != 0).sum()) > size // 16
