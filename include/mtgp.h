@@ -200,12 +200,16 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N,
 /* mtgp_flatten plus the per-program sizing of the program JIT (ABI v12), so the JIT build needs no
  * translation pass of its own: jit_words_out[P, n_prog] = code words of the program's
  * fall-through translation (mtgp_jit.h jit_program; < 0: untranslatable) and jit_cost_out[P,
- * n_prog] = the schedule weight mtgp_jit_cost would compute.  Either may be NULL.  population
+ * n_prog] = the schedule weight mtgp_jit_cost would compute.  Either may be NULL.  jit_mode:
+ * MTGP_JIT_MODE_REGS (data vector in v0-v7: control models, SR n_var <= 4) or MTGP_JIT_MODE_LDS
+ * (data vector = the LDS stage vector of the wide-state SR kernel, n_var 5..64).  population
  * must be 16-byte aligned (rows are loaded as 16-byte vectors). */
+enum { MTGP_JIT_MODE_REGS = 0, MTGP_JIT_MODE_LDS = 1 };
 int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N,
                     const MtgpNodeLibrary* lib, const MtgpProgramSpec* specs, int32_t n_prog,
                     int32_t L, MtgpInstr* prog_out, int32_t* len_out, int32_t* nodes_out,
-                    int32_t* status_out, int32_t* jit_words_out, int32_t* jit_cost_out, void* stream);
+                    int32_t* status_out, int32_t* jit_words_out, int32_t* jit_cost_out,
+                    int32_t jit_mode, void* stream);
 
 /* Same algorithm on the host (one tree), for tests and tooling. Returns program length
  * or a negative MTGP_ERR_* / -MTGP_ERR_PROG_TOO_LONG / -MTGP_ERR_STACK. */
@@ -256,7 +260,8 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  *    estimate when info is passed on to the evaluator, which then checks it on the device)
  *   mtgp_jit_emit   -> writes the code
  *   mtgp_eval_rk4_jit with MtgpJitCode{code, offsets}.
- * The acrobot evaluators and SR with n_var <= 4 use the code; other models ignore it. */
+ * Every evaluator uses the code; the wide-state SR kernel (n_var > 4) needs it built in
+ * MTGP_JIT_MODE_LDS (mtgp_flatten_ex / mtgp_jit_emit_words), the others in MTGP_JIT_MODE_REGS. */
 typedef struct {
   const void* code;         /* executable device memory from mtgp_jit_alloc           */
   const uint32_t* offsets;  /* [units + 1] from mtgp_jit_plan (same model, R, order)   */
@@ -280,9 +285,15 @@ int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int
                         const int32_t* order, uint32_t* offsets_out, int32_t* info_out, void* stream);
 int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog,
                         int32_t L, int32_t R, const int32_t* order, const uint32_t* offsets, void* code,
-                        size_t code_bytes, void* stream);
+                        size_t code_bytes, int32_t jit_mode, void* stream);
 /* host translation of one program (tests/tooling): number of code words, or < 0 */
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
+/* the same in either JIT mode (MTGP_JIT_MODE_*), for one program and for one unit */
+int mtgp_jit_unit_host_ex(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                          const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words,
+                          int32_t jit_mode);
+int mtgp_jit_translate_host_ex(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words,
+                               int32_t jit_mode);
 /* Schedule weights for JIT code: cost_out[P*n_prog] = executed code words / 4 of each program
  * (plen where a program cannot be translated); pass it to mtgp_schedule instead of plen. */
 int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t n_prog, int32_t L,

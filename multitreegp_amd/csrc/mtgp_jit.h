@@ -37,6 +37,14 @@ namespace mtgp {
 
 constexpr int kJitData = 0, kJitAcc = 8, kJitStack = 9, kJitT0 = 17, kJitT1 = 18;
 constexpr int kJitMaxData = 8;
+// LDS-data mode (the wide-state SR kernel, data vector = the LDS stage vector): v0 holds this
+// lane's LDS byte address of slot 0 (slot s at +s * MTGP_SLOT_BYTES); a program first loads the
+// first kJitPreSlots distinct slots it reads into v26.. (all loads in flight, one wait), slots
+// beyond that are loaded at their use into v42 / v43.
+enum { kJitModeRegs = 0, kJitModeLds = 1 };
+constexpr int kJitLdsAddr = 0, kJitPre = 26, kJitPreSlots = 16, kJitLoadTmp = 42;
+constexpr uint32_t kDsReadB32 = 0xd86c0000u;   // ds_read_b32 (word 0; | offset)
+constexpr uint32_t kWaitLgkm0 = 0xbf8cc07fu;   // s_waitcnt lgkmcnt(0)
 constexpr uint32_t kJitSrcLiteral = 255u;
 // VOP2 opcodes (gfx9 encoding)
 constexpr uint32_t kVop2Add = 1u, kVop2Sub = 2u, kVop2Subrev = 3u, kVop2Mul = 5u;
@@ -136,8 +144,56 @@ enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJit
 // Translate one END-terminated program (at most L instructions) into o; with `ret` the END
 // becomes s_setpc_b64 s[30:31], otherwise nothing (the code falls through).  Returns kJitOk
 // or a negative kJitErr* code.
-MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret) {
+MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs) {
   int sp = 0;
+  int pre[kJitPreSlots];
+  int npre = 0;
+  if (mode == kJitModeLds) {  // preload the first kJitPreSlots distinct data slots the program reads
+    for (int i = 0; i < L; ++i) {
+      const uint32_t w = prog[i].op, code = w >> MTGP_OP_SHIFT;
+      if (code == MTGP_OP_END) break;
+      union { float f; uint32_t u; } cv;
+      cv.f = prog[i].imm;
+      int cand[2], nc = 0;
+      switch (code) {
+        case MTGP_OP_LDV: case MTGP_OP_LDVP: case MTGP_OP_SINV: case MTGP_OP_COSV: case MTGP_OP_SINVP:
+        case MTGP_OP_COSVP: case MTGP_OP_ADDV: case MTGP_OP_SUBV: case MTGP_OP_RSUBV: case MTGP_OP_MULV:
+        case MTGP_OP_DIVV: case MTGP_OP_RDIVV:
+          cand[nc++] = (int)(cv.u / MTGP_SLOT_BYTES); break;
+        case MTGP_OP_VV_ADD: case MTGP_OP_VV_SUB: case MTGP_OP_VV_MUL: case MTGP_OP_VV_DIV: case MTGP_OP_VVP_ADD:
+        case MTGP_OP_VVP_SUB: case MTGP_OP_VVP_MUL: case MTGP_OP_VVP_DIV:
+          cand[nc++] = (int)(cv.u / MTGP_SLOT_BYTES);
+          cand[nc++] = (int)((w & 0xffffffu) / MTGP_SLOT_BYTES); break;
+        case MTGP_OP_VC_ADD: case MTGP_OP_VC_SUB: case MTGP_OP_VC_RSUB: case MTGP_OP_VC_MUL: case MTGP_OP_VC_DIV:
+        case MTGP_OP_VC_RDIV: case MTGP_OP_VCP_ADD: case MTGP_OP_VCP_SUB: case MTGP_OP_VCP_RSUB: case MTGP_OP_VCP_MUL:
+        case MTGP_OP_VCP_DIV: case MTGP_OP_VCP_RDIV:
+          cand[nc++] = (int)((w & 0xffffffu) / MTGP_SLOT_BYTES); break;
+        default: break;
+      }
+      for (int k = 0; k < nc; ++k) {
+        if (cand[k] >= MTGP_MAX_DATA) return kJitErrSlot;
+        bool have = false;
+        for (int q = 0; q < npre; ++q) have = have || pre[q] == cand[k];
+        if (!have && npre < kJitPreSlots) pre[npre++] = cand[k];
+      }
+    }
+    for (int q = 0; q < npre; ++q) {
+      o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
+      o.w((uint32_t)(kJitPre + q) << 24 | (uint32_t)kJitLdsAddr);
+    }
+    if (npre > 0) o.w(kWaitLgkm0);
+  }
+  // register holding data slot s: v0-v7 (register mode) or its preload / a load at the use
+  auto vslot = [&](int s_, int tmp) -> int {
+    if (mode != kJitModeLds) return kJitData + s_;
+    for (int q = 0; q < npre; ++q)
+      if (pre[q] == s_) return kJitPre + q;
+    o.w(kDsReadB32 | (uint32_t)(s_ * (int)MTGP_SLOT_BYTES));
+    o.w((uint32_t)tmp << 24 | (uint32_t)kJitLdsAddr);
+    o.w(kWaitLgkm0);
+    return tmp;
+  };
+  const int max_slot = mode == kJitModeLds ? MTGP_MAX_DATA : kJitMaxData;
   for (int i = 0; i < L; ++i) {
     const uint32_t w = prog[i].op;
     const uint32_t code = w >> MTGP_OP_SHIFT, ax = w & 0xffffffu;
@@ -152,7 +208,6 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
       return true;
     };
     const JitSrc acc = jit_reg(kJitAcc), c = jit_lit(ib);
-    const JitSrc vib = jit_reg(kJitData + sib), vax = jit_reg(kJitData + sax);
     // which operand kinds this opcode reads (checked below)
     bool uses_ib_slot = false, uses_ax_slot = false, ok = true;
     int fam = -1, kind = -1;  // family ADD SUB RSUB MUL DIV RDIV; kind 0 C, 1 V, 2 S
@@ -162,14 +217,14 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
         return kJitOk;
       case MTGP_OP_LDC: o.movc(kJitAcc, ib); continue;
       case MTGP_OP_LDCP: ok = push(); o.movc(kJitAcc, ib); break;
-      case MTGP_OP_LDV: uses_ib_slot = true; if (sib >= kJitMaxData) return kJitErrSlot; o.movv(kJitAcc, kJitData + sib); continue;
-      case MTGP_OP_LDVP: if (sib >= kJitMaxData) return kJitErrSlot; ok = push(); o.movv(kJitAcc, kJitData + sib); break;
+      case MTGP_OP_LDV: uses_ib_slot = true; if (sib >= max_slot) return kJitErrSlot; o.movv(kJitAcc, vslot(sib, kJitLoadTmp)); continue;
+      case MTGP_OP_LDVP: if (sib >= max_slot) return kJitErrSlot; ok = push(); o.movv(kJitAcc, vslot(sib, kJitLoadTmp)); break;
       case MTGP_OP_SIN: jit_trig(o, true, acc); continue;
       case MTGP_OP_COS: jit_trig(o, false, acc); continue;
       case MTGP_OP_SINV: case MTGP_OP_COSV: case MTGP_OP_SINVP: case MTGP_OP_COSVP:
-        if (sib >= kJitMaxData) return kJitErrSlot;
+        if (sib >= max_slot) return kJitErrSlot;
         if (code == MTGP_OP_SINVP || code == MTGP_OP_COSVP) ok = push();
-        jit_trig(o, code == MTGP_OP_SINV || code == MTGP_OP_SINVP, vib);
+        jit_trig(o, code == MTGP_OP_SINV || code == MTGP_OP_SINVP, jit_reg(vslot(sib, kJitLoadTmp)));
         break;
 #define MTGP_JIT_FAM(F, I)                                                  \
       case MTGP_OP_##F##C: fam = I; kind = 0; break;                        \
@@ -205,7 +260,7 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
     }
     if (!ok) return kJitErrStack;
     if (fam < 0) continue;  // handled above
-    if ((uses_ib_slot && sib >= kJitMaxData) || (uses_ax_slot && sax >= kJitMaxData)) return kJitErrSlot;
+    if ((uses_ib_slot && sib >= max_slot) || (uses_ax_slot && sax >= max_slot)) return kJitErrSlot;
     // family f in (ADD, SUB, RSUB, MUL, DIV, RDIV): R* forms swap the operands
     const int base_fn = fam == 0 ? MTGP_FN_ADD : fam <= 2 ? MTGP_FN_SUB : fam == 3 ? MTGP_FN_MUL : MTGP_FN_DIV;
     const bool rev = fam == 2 || fam == 5;
@@ -213,7 +268,7 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
     if (kind <= 2) {  // acc OP {c, V(ib), pop}
       x = acc;
       if (kind == 0) y = c;
-      else if (kind == 1) y = vib;
+      else if (kind == 1) y = jit_reg(vslot(sib, kJitLoadTmp));
       else {
         if (sp <= 0) return kJitErrStack;
         --sp;
@@ -221,12 +276,12 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
       }
     } else if (kind <= 4) {  // V(ax) OP c, optional push first
       if (kind == 4 && !push()) return kJitErrStack;
-      x = vax;
+      x = jit_reg(vslot(sax, kJitLoadTmp));
       y = c;
     } else {  // V(ib) OP V(ax)
       if (kind == 6 && !push()) return kJitErrStack;
-      x = vib;
-      y = vax;
+      x = jit_reg(vslot(sib, kJitLoadTmp));
+      y = jit_reg(vslot(sax, kJitLoadTmp + 1));
     }
     if (rev) { const JitSrc t = x; x = y; y = t; }
     jit_binop(o, base_fn, x, y);
@@ -235,10 +290,11 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
 }
 
 // One callable program: number of 32-bit code words (out == nullptr: count only) or < 0.
-MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out, uint32_t base = kJitTemplateBytes) {
+MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out, uint32_t base = kJitTemplateBytes,
+                                     int mode = kJitModeRegs) {
   JitOut o{out, 0};
   o.base = base;
-  const int rc = jit_program(o, prog, L, true);
+  const int rc = jit_program(o, prog, L, true, mode);
   return rc < 0 ? rc : o.n;
 }
 
@@ -268,7 +324,7 @@ constexpr uint32_t kSelHi = 0x00aa1119u;
 
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
-                                int wave, int j, uint32_t* out, uint32_t base) {
+                                int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs) {
   JitOut o{out, 0};
   o.base = base;
   for (int g = 0; g < G; ++g) {
@@ -276,7 +332,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
     if (q >= P) break;
     const int ind = order ? order[q] : q;
     if (g > 0) o.movv(kJitKeep, kJitAcc);
-    const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false);
+    const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false, mode);
     if (rc < 0) return rc;
     if (g > 0) {
       const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);  // g > 0 implies Rp < 64
@@ -296,13 +352,13 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
 // that group, written at `out` (= byte offset `base` in the buffer), plus the unit's final
 // s_setpc when `last`.  jit_unit == the concatenation of its groups.
 MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
-                                      int g, int j, bool last, uint32_t* out, uint32_t base) {
+                                      int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs) {
   JitOut o{out, 0};
   o.base = base;
   const int q = q0 + g;
   const int ind = order ? order[q] : q;
   if (g > 0) o.movv(kJitKeep, kJitAcc);
-  const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false);
+  const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false, mode);
   if (rc < 0) return rc;
   if (g > 0) {
     const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);

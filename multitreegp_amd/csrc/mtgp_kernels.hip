@@ -1447,14 +1447,41 @@ __device__ __forceinline__ bool lane_setup_wide(const KArgs& A, Lane& L) {
   L.active = (L.r < A.ro.R) && (q < A.P);
   L.rr = L.active ? L.r : 0;
   L.ptab = prog_table(A, L);
+  L.jok = true;
+  if (A.jit_info) L.jok = uni((int)(A.jit_info[0] == 0 && (uint64_t)(uint32_t)A.jit_info[1] <= A.jit_cap)) != 0;
+  L.jtab = 0;  // lane j < n_prog: JIT unit (lane set, program j)
+  if (A.jit_off && L.lane < A.n_prog) L.jtab = A.jit_off[(size_t)(L.q0 / L.G) * A.n_prog + L.lane];
   return true;
 }
 
-template <bool TRAJ>
+// Call a JIT unit in LDS-data mode (mtgp_jit.h kJitModeLds): v0 = this lane's LDS byte address of
+// stage-vector slot 0; result in v8; s[32:33] collects lanes that need the interpreter.
+__device__ __forceinline__ float jit_call_lds(uint64_t addr_, uint32_t lds_addr, uint64_t& flag) {
+  const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr_ >> 32)) << 32;
+  float acc;
+  asm volatile("s_swappc_b64 s[30:31], %[tgt]"
+               : "={v8}"(acc), "+{s[32:33]}"(flag)
+               : [tgt] "s"(addr), "{v0}"(lds_addr)
+               : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
+                 "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",
+                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "s30", "s31", "s34", "s35",
+                 "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "memory");
+  return acc;
+}
+
+// LDS byte address of a pointer into shared memory
+__device__ __forceinline__ uint32_t lds_address(const float* p) {
+  return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
+}
+
+
+template <bool TRAJ, bool JIT>
 __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   extern __shared__ float wl[];
   Lane Ln;
   if (!lane_setup_wide(A, Ln)) return;  // uniform over the workgroup
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
   const int NV = A.m.n_var;
   const int NW = (NV + kWideComp - 1) / kWideComp;
   const int w = Ln.wave, lane = Ln.lane, r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
@@ -1534,10 +1561,29 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; k parks in nxt
-      for (int t = 0; t < kWideComp; ++t) {
-        const int c = c0 + t;
-        if (c >= NV) break;
-        nxt[c * kWave] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+      if (JIT && Ln.jok) {  // one JIT unit call per component: the G groups' programs back to back
+        const uint32_t la = lds_address(cur);
+        for (int t = 0; t < kWideComp; ++t) {
+          const int c = c0 + t;
+          if (c >= NV) break;
+          const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c);
+          uint64_t fl = 0;
+          float v = jit_call_lds(A.jit_base + off, la, fl);
+          if (__builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: interpret those groups
+            for (int gi = 0; gi < ng; ++gi) {
+              if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
+              const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, cur, st);
+              v = (Ln.g == gi) ? tv : v;
+            }
+          }
+          nxt[c * kWave] = v;
+        }
+      } else {
+        for (int t = 0; t < kWideComp; ++t) {
+          const int c = c0 + t;
+          if (c >= NV) break;
+          nxt[c * kWave] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+        }
       }
 #pragma unroll
       for (int t = 0; t < kWideComp; ++t) {
@@ -1605,10 +1651,10 @@ constexpr int32_t kFlatSerial = 0x7fff;  // status of a program left to k_flatte
 
 // JIT sizing of one flattened program (mtgp_flatten_ex jit_words / jit_cost)
 __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n, int32_t* jit_words_out,
-                                              int32_t* jit_cost_out, size_t pj) {
+                                              int32_t* jit_cost_out, size_t pj, int jit_mode) {
   if (!jit_words_out && !jit_cost_out) return;
   mtgp::JitOut o{nullptr, 0};
-  const int rc = mtgp::jit_program(o, out, L, false);
+  const int rc = mtgp::jit_program(o, out, L, false, jit_mode);
   if (jit_words_out) jit_words_out[pj] = rc < 0 ? rc : o.n;
   if (jit_cost_out) {  // = k_jit_cost: executed words of the callable translation / 4
     const int c = rc < 0 ? rc : (o.n + 1 + mtgp::kJitTrigExecuted * o.trig);
@@ -1624,7 +1670,7 @@ __global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__
                                                        MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                        int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                        int32_t* status_out, int32_t* jit_words_out,
-                                                       int32_t* jit_cost_out) {
+                                                       int32_t* jit_cost_out, int jit_mode) {
   const long total = (long)P * n_prog;
   for (long pj = (long)blockIdx.x * blockDim.x + threadIdx.x; pj < total; pj += (long)gridDim.x * blockDim.x) {
     if (status_out[pj] != kFlatSerial) continue;
@@ -1636,7 +1682,7 @@ __global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__
                                      L, info, nullptr);
     len_out[pj] = n > 0 ? n : 0;
     status_out[pj] = n > 0 ? 0 : -n;
-    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, (size_t)pj);
+    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, (size_t)pj, jit_mode);
   }
 }
 
@@ -1652,7 +1698,8 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
                                                             const MtgpProgramSpec* __restrict__ specs, int n_prog,
                                                             int L, MtgpInstr* prog_out, int32_t* len_out,
                                                             int32_t* nodes_out, int32_t* status_out,
-                                                            int32_t* jit_words_out, int32_t* jit_cost_out) {
+                                                            int32_t* jit_words_out, int32_t* jit_cost_out,
+                                                            int jit_mode) {
   using namespace mtgp;
   __shared__ uint32_t s_w[NMAX * TPB];    // packed row record (u_pack)
   __shared__ uint32_t s_len[NMAX * TPB];  // unfused length (low 16, saturated) | fused length (high 16)
@@ -1842,7 +1889,7 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
     out[n > 0 ? n : 0] = e;
     len_out[pj] = n > 0 ? n : 0;
     status_out[pj] = n > 0 ? 0 : -n;
-    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, pj);
+    flat_jit_size(out, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
   }
   // node count (gp.py:424 parsimony): the individual's trees are shared out over its n_prog
   // lanes (tree t -> lane t % n_prog) and summed with integer atomics into the zeroed nodes_out
@@ -1920,6 +1967,7 @@ struct JitUnitArgs {
   const MtgpInstr* prog;
   int n_prog, L, P, G, Rp, n_units;
   const int32_t* order;
+  int mode;  // mtgp_jit.h kJitModeRegs / kJitModeLds
 };
 
 __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
@@ -2089,7 +2137,7 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
   }
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
   const uint32_t at = b + start * 4u;
-  mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at);
+  mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode);
 }
 
 // the shared sin/cos subroutines at the start of the code buffer
@@ -2111,6 +2159,7 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
   U.Rp = Rp;
   U.G = kWave / Rp;
   U.order = order;
+  U.mode = mtgp::kJitModeRegs;
   const long waves = ((long)P + U.G - 1) / U.G;
   if (waves * n_prog > INT32_MAX - 1) return false;
   U.n_units = (int)(waves * n_prog);
@@ -2393,9 +2442,11 @@ int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int
 
 int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t L,
                         int32_t R, const int32_t* order, const uint32_t* offsets, void* code, size_t code_bytes,
-                        void* stream) {
+                        int32_t jit_mode, void* stream) {
   JitUnitArgs U;
   if (!jit_words || !offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
+  if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
+  U.mode = jit_mode;
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_jit_templates, dim3(1), dim3(256), 0, s, (uint32_t*)code, (uint64_t)code_bytes);
@@ -2427,29 +2478,39 @@ int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
-int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
-                       int32_t unit, uint32_t* out, int32_t max_words) {
+int mtgp_jit_unit_host_ex(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                          int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode) {
   JitUnitArgs U;
   if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
+  if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   const int wave = unit / n_prog, j = unit - wave * n_prog;
-  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes);
+  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes, jit_mode);
   if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
   if (out) {
     if (n > max_words) return MTGP_ERR_ARG;
-    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes);
+    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode);
+  }
+  return n;
+}
+
+int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                       int32_t unit, uint32_t* out, int32_t max_words) {
+  return mtgp_jit_unit_host_ex(prog, P, n_prog, L, R, order, unit, out, max_words, mtgp::kJitModeRegs);
+}
+
+int mtgp_jit_translate_host_ex(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words, int32_t jit_mode) {
+  if (!prog || L <= 0 || (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds)) return MTGP_ERR_ARG;
+  const int n = mtgp::jit_translate(prog, L, nullptr, mtgp::kJitTemplateBytes, jit_mode);
+  if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;  /* translation errors: -101 .. -104 */
+  if (out) {
+    if (n > max_words) return MTGP_ERR_ARG;
+    mtgp::jit_translate(prog, L, out, mtgp::kJitTemplateBytes, jit_mode);
   }
   return n;
 }
 
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words) {
-  if (!prog || L <= 0) return MTGP_ERR_ARG;
-  const int n = mtgp::jit_translate(prog, L, nullptr);
-  if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;  /* translation errors: -101 .. -104 */
-  if (out) {
-    if (n > max_words) return MTGP_ERR_ARG;
-    mtgp::jit_translate(prog, L, out);
-  }
-  return n;
+  return mtgp_jit_translate_host_ex(prog, L, out, max_words, mtgp::kJitModeRegs);
 }
 
 int mtgp_set_timing(int enabled) {
@@ -2469,7 +2530,8 @@ float mtgp_last_kernel_ms(void) {
 int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
                     const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
                     int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out, int32_t* jit_cost_out,
-                    void* stream) {
+                    int32_t jit_mode, void* stream) {
+  if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   if (!population || !lib || !specs || !prog_out || !len_out || !nodes_out || !status_out) return MTGP_ERR_ARG;
   if (P < 0 || T <= 0 || N <= 0 || N > MTGP_MAX_NODES || n_prog <= 0 || L <= 0) return MTGP_ERR_ARG;
   if (lib->n_funcs <= 0 || lib->n_funcs > MTGP_MAX_FUNCS) return MTGP_ERR_ARG;
@@ -2487,7 +2549,7 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
 #define MTGP_FLAT_ONE(NM, TP)                                                                                 \
   hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
                      T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
-                     jit_cost_out)
+                     jit_cost_out, jit_mode)
 #define MTGP_FLAT_LAUNCH(NM)                                                                                \
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
@@ -2496,7 +2558,7 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
     else MTGP_FLAT_ONE(NM, 8);                                                                              \
     hipLaunchKernelGGL(k_flatten_serial<NM>, dim3((unsigned)(total < 64 * 64 ? (total + 63) / 64 : 64)),   \
                        dim3(64), 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out, len_out,     \
-                       status_out, jit_words_out, jit_cost_out);                                            \
+                       status_out, jit_words_out, jit_cost_out, jit_mode);                                  \
   } while (0)
   if (N <= 64) MTGP_FLAT_LAUNCH(64);
   else if (N <= 128) MTGP_FLAT_LAUNCH(128);
@@ -2510,7 +2572,7 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N, const
                  const MtgpProgramSpec* specs, int32_t n_prog, int32_t L, MtgpInstr* prog_out, int32_t* len_out,
                  int32_t* nodes_out, int32_t* status_out, void* stream) {
   return mtgp_flatten_ex(population, P, T, N, lib, specs, n_prog, L, prog_out, len_out, nodes_out, status_out,
-                         nullptr, nullptr, stream);
+                         nullptr, nullptr, mtgp::kJitModeRegs, stream);
 }
 
 int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* lib, int32_t n_data,
@@ -2593,12 +2655,12 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   A.P = P;
   A.ro = *rollouts;
   A.out = *out;
-  const bool jit = jitc && jitc->code && jitc->offsets && !(model->model == MTGP_MODEL_SR && model->n_var > 4);
+  const bool jit = jitc && jitc->code && jitc->offsets;
   A.jit_base = jit ? (uint64_t)(uintptr_t)jitc->code : 0;
   A.jit_off = jit ? jitc->offsets : nullptr;
   A.jit_info = jit ? jitc->info : nullptr;
   A.jit_cap = jit ? jitc->capacity : 0;
-  // (the wide-state SR kernel keeps its data vector in LDS: interpreter only)
+  // (the wide-state SR kernel keeps its data vector in LDS: its code is built in kJitModeLds)
   hipStream_t s = (hipStream_t)stream;
   int Rp = 1;
   while (Rp < rollouts->R) Rp <<= 1;
@@ -2627,8 +2689,11 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
       const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
       const dim3 wgrid((unsigned)(((long)P + G - 1) / G)), wblock(kWave * nw);
       return launch_timed([&] {
-        if (traj) hipLaunchKernelGGL((k_sr_wide<true>), wgrid, wblock, lds, s, A);
-        else hipLaunchKernelGGL((k_sr_wide<false>), wgrid, wblock, lds, s, A);
+        if (jit) {
+          if (traj) hipLaunchKernelGGL((k_sr_wide<true, true>), wgrid, wblock, lds, s, A);
+          else hipLaunchKernelGGL((k_sr_wide<false, true>), wgrid, wblock, lds, s, A);
+        } else if (traj) hipLaunchKernelGGL((k_sr_wide<true, false>), wgrid, wblock, lds, s, A);
+        else hipLaunchKernelGGL((k_sr_wide<false, false>), wgrid, wblock, lds, s, A);
       }, s);
     }
 #define MTGP_SR(NV)                                                                                       \

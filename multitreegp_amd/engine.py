@@ -117,8 +117,10 @@ class DeviceEngine:
             if slot is None or self._arena_gen[slot] == gen:  # code still in place (or none was built)
                 return fl.jit
         fl.jit_key, fl.jit = key + (None, None), None
-        if not self.use_jit or self.ff.n_data() > 8 or (m.model == nat.MODEL_SR and m.n_var > 4):
+        if not self._jit_usable():
             return None
+        if fl.jit_words is None and self._jit_mode() != nat.JIT_MODE_REGS:
+            return None  # the translation-based plan/emit only build register-data code
         P = fl.prog.shape[0]
         n = self.native.mtgp_jit_units(P, fl.n_prog, R)
         if n < 0:
@@ -150,7 +152,7 @@ class DeviceEngine:
         ptr, size = self._arena(int(n * per_unit) + 4096)
         if fl.jit_words is not None:
             rc = self.native.mtgp_jit_emit_words(fl.prog.data_ptr(), fl.jit_words.data_ptr(), P, fl.n_prog, fl.L,
-                                                 R, optr, offs.data_ptr(), ptr, size, stream)
+                                                 R, optr, offs.data_ptr(), ptr, size, self._jit_mode(), stream)
         else:
             rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(), ptr,
                                            size, stream)
@@ -248,16 +250,21 @@ class DeviceEngine:
         rc = self.native.mtgp_flatten_ex(pop.data_ptr(), P, T, N, ctypes.byref(self._node_lib),
                                          self._specs_dev.data_ptr(), n_prog, L, prog.data_ptr(),
                                          plen.data_ptr(), nodes.data_ptr(), status.data_ptr(), _ptr(jw), _ptr(jc),
-                                         stream)
+                                         self._jit_mode(), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_flatten failed: {rc}")
         return Flattened(prog, plen, nodes, status, L, n_prog, jit_words=jw, jit_cost=jc)
 
     def _jit_usable(self) -> bool:
-        """The program JIT serves the kernels whose data vector fits v0-v7 (mtgp_jit.h)."""
-        if not self.use_jit or self.ff.n_data() > 8:
+        """The program JIT serves every kernel: data vector in v0-v7 (control models, SR with
+        n_var <= 4) or in the wide SR kernel's LDS stage vector (mtgp_jit.h kJitModeLds)."""
+        if not self.use_jit:
             return False
-        return not (self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4)
+        return self.ff.n_data() <= 8 or self._jit_mode() == nat.JIT_MODE_LDS
+
+    def _jit_mode(self) -> int:
+        """LDS-data code for the wide-state SR kernel (n_var > 4), register-data code otherwise."""
+        return nat.JIT_MODE_LDS if self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4 else nat.JIT_MODE_REGS
 
     @staticmethod
     def check_status(fl: Flattened):
@@ -281,7 +288,7 @@ class DeviceEngine:
     def schedule_cost(self, fl: Flattened) -> torch.Tensor:
         """Per-program cost [P, n_prog] the schedule balances: the executed JIT code size when the
         programs run as JIT code (sin/cos dominate there), the program length otherwise."""
-        if not (self.use_jit and self.ff.n_data() <= 8):
+        if not self._jit_usable():
             return fl.plen
         if fl.jit_cost is not None:
             return fl.jit_cost

@@ -16,7 +16,7 @@ from helpers import CONTROL_OPS, SR_OPS
 pytestmark = pytest.mark.gpu
 
 
-def _flatten_ex(pop, lib, specs, L):
+def _flatten_ex(pop, lib, specs, L, mode=0):
     import torch
     P, T, N, _ = pop.shape
     L_ = nat.load()
@@ -33,7 +33,7 @@ def _flatten_ex(pop, lib, specs, L):
     libs = lib.native()
     rc = L_.mtgp_flatten_ex(pd.data_ptr(), P, T, N, ctypes.byref(libs), sp.data_ptr(), n_prog, L, prog.data_ptr(),
                             out["plen"].data_ptr(), out["nodes"].data_ptr(), out["status"].data_ptr(),
-                            out["jw"].data_ptr(), out["jc"].data_ptr(), None)
+                            out["jw"].data_ptr(), out["jc"].data_ptr(), mode, None)
     assert rc == nat.OK
     torch.cuda.synchronize()
     return prog, out
@@ -56,12 +56,12 @@ def _population(kind, P, seed=0):
     return lib, pop, specs
 
 
-@pytest.mark.parametrize("kind", ["dynamic", "sr12"])
-def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind):
+@pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("sr12", 0), ("sr12", 1)])
+def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
     lib, pop, specs = _population(kind, 301)
     P, T, N, _ = pop.shape
     L = (2 * N + 8 + 3) // 4 * 4
-    prog, out = _flatten_ex(pop, lib, specs, L)
+    prog, out = _flatten_ex(pop, lib, specs, L, mode)
     progs = prog[: P * len(specs) * L * 2].view(P, len(specs), L, 2).cpu().numpy()
     plen, status, jw, jc = (out[k].cpu().numpy() for k in ("plen", "status", "jw", "jc"))
     nodes = out["nodes"].cpu().numpy()
@@ -76,14 +76,15 @@ def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind):
                                           None)
             assert plen[p, j] == max(n, 0) and status[p, j] == (0 if n > 0 else -n), (p, j)
             assert np.array_equal(progs[p, j, : max(n, 0) + 1], host[: max(n, 0) + 1]), (p, j)
-            w = L_.mtgp_jit_translate_host(host.ctypes.data, L, word.ctypes.data, 4096)
+            w = L_.mtgp_jit_translate_host_ex(host.ctypes.data, L, word.ctypes.data, 4096, mode)
             assert jw[p, j] == (w - 1 if w > 0 else w + 100), (p, j, jw[p, j], w)
     import torch
     cost = torch.empty((P, len(specs)), dtype=torch.int32, device="cuda")
-    assert L_.mtgp_jit_cost(prog.data_ptr(), out["plen"].data_ptr(), P, len(specs), L, cost.data_ptr(), None) == 0
-    assert np.array_equal(cost.cpu().numpy(), jc)
+    if mode == 0:
+        assert L_.mtgp_jit_cost(prog.data_ptr(), out["plen"].data_ptr(), P, len(specs), L, cost.data_ptr(), None) == 0
+        assert np.array_equal(cost.cpu().numpy(), jc)
     if kind == "sr12":
-        assert (jw < 0).any() and (jw > 0).any()
+        assert ((jw < 0).any() if mode == 0 else (jw >= 0).all()) and (jw > 0).any()
 
 
 @pytest.mark.parametrize("kind", ["dynamic", "sr12"])
@@ -117,7 +118,45 @@ def test_word_based_jit_plan_and_emit_match_translation(kind, R):
     assert L_.mtgp_jit_emit(prog.data_ptr(), P, n_prog, L, R, order.data_ptr(), offs[0].data_ptr(),
                             bufs[0].data_ptr(), size, None) == 0
     assert L_.mtgp_jit_emit_words(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
-                                  offs[1].data_ptr(), bufs[1].data_ptr(), size, None) == 0
+                                  offs[1].data_ptr(), bufs[1].data_ptr(), size, 0, None) == 0
     torch.cuda.synchronize()
     assert torch.equal(bufs[0], bufs[1])
     assert int((bufs[1] != 0).sum()) > size // 16
+
+
+@pytest.mark.parametrize("R", [8, 64])
+def test_lds_mode_units_match_host_units(R):
+    """LDS-data mode (wide-state SR): the device-built units equal the host-built ones word for word."""
+    import torch
+    lib, pop, specs = _population("sr12", 129, seed=R)
+    P, T, N, _ = pop.shape
+    n_prog = len(specs)
+    L = (2 * N + 8 + 3) // 4 * 4
+    prog, out = _flatten_ex(pop, lib, specs, L, 1)
+    L_ = nat.load()
+    order_np = np.random.default_rng(R).permutation(P).astype(np.int32)
+    order = torch.from_numpy(order_np).cuda()
+    n = L_.mtgp_jit_units(P, n_prog, R)
+    offs = torch.empty((n + 1,), dtype=torch.int32, device="cuda")
+    info = torch.zeros((2,), dtype=torch.int32, device="cuda")
+    assert L_.mtgp_jit_plan_words(out["jw"].data_ptr(), P, n_prog, R, order.data_ptr(), offs.data_ptr(),
+                                  info.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    inf = info.cpu().numpy()
+    assert inf[0] == 0
+    size = int(inf[1]) + 4096
+    buf = torch.zeros((size // 4,), dtype=torch.int32, device="cuda")
+    assert L_.mtgp_jit_emit_words(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
+                                  offs.data_ptr(), buf.data_ptr(), size, 1, None) == 0
+    torch.cuda.synchronize()
+    code = buf.cpu().numpy().view(np.uint32)
+    o = offs.cpu().numpy().view(np.uint32)
+    hp = prog[: P * n_prog * L * 2].cpu().numpy()
+    host = np.zeros(1 << 16, np.uint32)
+    for u in range(0, n, max(1, n // 97)):
+        w = L_.mtgp_jit_unit_host_ex(hp.ctypes.data, P, n_prog, L, R, order_np.ctypes.data, u, host.ctypes.data,
+                                     host.size, 1)
+        assert w > 0
+        # the units are laid out after the templates exactly as the host lays them out (PC-relative
+        # calls aside, which SR has none of): equal words
+        assert np.array_equal(code[o[u] // 4: o[u] // 4 + w], host[:w]), u

@@ -130,12 +130,14 @@ def _setup(kind):
     return lib, pop, 4, [0]
 
 
-def _emulate(words, data, full=False):
+def _emulate(words, data, full=False, lds=False):
     """Run emitted code on data [n_data, M] (float32 lanes, M <= 64); returns v8 (or all VGPRs).
-    Honours the exec moves of per-wave units (VALU results only land in exec lanes)."""
+    Honours the exec moves of per-wave units (VALU results only land in exec lanes).  lds: the
+    data vector is the LDS stage vector (LDS-data mode: ds_read_b32 from v0 + slot * 256)."""
     M = data.shape[1]
-    v = np.zeros((32, M), np.float32)
-    v[: data.shape[0]] = data
+    v = np.zeros((64, M), np.float32)
+    if not lds:
+        v[: data.shape[0]] = data
     i = 0
     lit = lambda k: np.full(M, np.array(words[k], np.uint32).view(np.float32), np.float32)  # noqa: E731
     exec_ = np.ones(M, bool)
@@ -149,6 +151,14 @@ def _emulate(words, data, full=False):
         w = words[i]
         if w == SETPC:
             return v if full else v[8]
+        if (w & 0xFFFF0000) == 0xD86C0000:  # ds_read_b32 vdst, v0 offset:slot*256
+            assert lds and (words[i + 1] & 0xFF) == 0, hex(words[i + 1])
+            put(words[i + 1] >> 24, data[(w & 0xFFFF) // 256])
+            i += 2
+            continue
+        if w == 0xBF8CC07F:  # s_waitcnt lgkmcnt(0)
+            i += 1
+            continue
         if w == GETPC_S44:  # getpc; s_add_u32 s44, lit; s_addc_u32 s45; s_swappc_b64 s[40:41], s[44:45]
             assert words[i + 1] == 0x802CFF2C and words[i + 4] == 0xBEA81E2C, [hex(x) for x in words[i:i + 5]]
             rel = int(np.array(words[i + 2], np.uint32).view(np.int32))
@@ -439,3 +449,50 @@ def test_trig_templates_emulate_to_spec():
         same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
         assert np.all(same | flag), (name, x[~(same | flag)][:5], got[~(same | flag)][:5])
         assert np.array_equal(flag, ~(np.abs(x) < 131072.0) & np.isfinite(x)), name
+
+
+def _lds_setup():
+    lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(24)]], [24])
+    pop = sample_population(9, lib, 30, 1, max_init_depth=9, max_nodes=96)[0]
+    return lib, pop, 24
+
+
+def test_lds_mode_translation_disassembles_and_emulates_to_oracle():
+    """LDS-data mode (the wide-state SR kernel): every program preloads its first 16 distinct data
+    slots with ds_read_b32 from v0 + slot * 256 (one s_waitcnt), loads the rest at their use, and
+    computes the row-order oracle's value bit for bit; registers stay within v8-v43 / the ABI."""
+    import ctypes
+    lib, pop, n_data = _lds_setup()
+    nl = lib.native()
+    lib_n = nat.load()
+    rng = np.random.default_rng(4)
+    data = (rng.standard_normal((n_data, 17)) * 2.0).astype(np.float32)
+    out = np.zeros(1 << 15, np.uint32)
+    checked = beyond = 0
+    allowed = set(range(8, 44))
+    for p in range(pop.shape[0]):
+        for t in range(n_data):
+            raw = _raw_program(pop[p, t], nl, n_data, 0)
+            n = lib_n.mtgp_jit_translate_host_ex(raw.ctypes.data, raw.shape[0], out.ctypes.data, out.size, 1)
+            assert n > 0, n
+            words = [int(w) for w in out[:n]]
+            lines = _disassemble(words)
+            assert lines[-1] == "s_setpc_b64 s[30:31]"
+            for ln in lines[:-1]:
+                if ln.startswith("ds_read_b32"):
+                    dst = int(re.match(r"ds_read_b32 v(\d+), v0", ln).group(1))
+                    assert dst in allowed, ln
+                    beyond += dst >= 42
+                    continue
+                if ln.startswith("s_waitcnt"):
+                    continue
+                dst = ln.partition(" ")[2].split(",")[0].strip()
+                m = re.fullmatch(r"v(\d+)", dst)
+                assert m and int(m.group(1)) in allowed, ln
+            got = _emulate(words, data, lds=True)
+            want = np.array([orc.eval_tree(pop[p, t], lib.fn_codes, lib.n_funcs, lib.var_start, data[:, m])
+                             for m in range(data.shape[1])], np.float32)
+            same = (got.view(np.uint32) == want.view(np.uint32)) | (np.isnan(got) & np.isnan(want))
+            assert same.all(), (p, t, got[~same][:4], want[~same][:4])
+            checked += 1
+    assert checked >= 600
