@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 12
+#define MTGP_ABI_VERSION 13
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -143,8 +143,8 @@ typedef struct {
    * MTGP_SOLVER_DOPRI5: diffrax.Dopri5 + PIDController(rtol, atol, dtmin, dtmax) from dt0 = h
    * with SaveAt(ts) and at most max_steps step attempts (include/mtgp_dopri5.h, the notebooks'
    * setting, e.g. SymbolicRegression.ipynb:136); n_steps / save_every are ignored.  Implemented
-   * for the dynamic and static control models (every MTGP_ENV_*) and for MTGP_MODEL_SR with
-   * n_var <= 4. */
+   * for the dynamic and static control models (every MTGP_ENV_*) and for MTGP_MODEL_SR at every
+   * n_var (register-resident for n_var <= 4, the wide-state workgroup kernel up to 64). */
   int32_t solver;
   int32_t max_steps; /* Dopri5: accepted + rejected steps before the solve gives up      */
   float rtol, atol;  /* PIDController tolerances                                         */
@@ -262,12 +262,26 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  *   mtgp_eval_rk4_jit with MtgpJitCode{code, offsets}.
  * Every evaluator uses the code; the wide-state SR kernel (n_var > 4) needs it built in
  * MTGP_JIT_MODE_LDS (mtgp_flatten_ex / mtgp_jit_emit_words), the others in MTGP_JIT_MODE_REGS. */
+/* Role chains (ABI v13).  A role whose programs run back to back (the state_size state
+ * equations of a dynamic policy, the n_var trees of SR with n_var <= 4) can be built as ONE
+ * callable chain: bit j of `next` makes unit j fall through into unit j + 1 (laid out right
+ * behind it) instead of returning; bit j of `cond` makes that continuation optional (taken when
+ * the evaluator asks for it: the fixed-step dynamic kernel continues the state chain into the
+ * save-point readout at save points).  mtgp_jit_chain gives the chain the evaluator kernels of
+ * `model` call; code built with another non-zero chain is rejected (MTGP_ERR_ARG), code built
+ * without one ({0, 0}) is called one program at a time as before. */
+typedef struct {
+  uint32_t next;
+  uint32_t cond;
+} MtgpJitChain;
+
 typedef struct {
   const void* code;         /* executable device memory from mtgp_jit_alloc           */
   const uint32_t* offsets;  /* [units + 1] from mtgp_jit_plan (same model, R, order)   */
   const int32_t* info;      /* info[2] of mtgp_jit_plan, or NULL if the host checked it */
   uint64_t capacity;        /* bytes of `code`; the kernel interprets when info says the */
                             /* plan failed or the code did not fit (no host round trip) */
+  MtgpJitChain chain;       /* the chain the code was built with (ABI v13; {0, 0}: none) */
 } MtgpJitCode;
 
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code);
@@ -286,6 +300,19 @@ int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int
 int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog,
                         int32_t L, int32_t R, const int32_t* order, const uint32_t* offsets, void* code,
                         size_t code_bytes, int32_t jit_mode, void* stream);
+/* ABI v13: the role chain the evaluator of `model` (with n_prog programs) calls, and plan / emit /
+ * host emission of chained code.  chain NULL = {0, 0} = the unchained functions above. */
+int mtgp_jit_chain(const MtgpModel* model, int32_t n_prog, MtgpJitChain* chain_out);
+int mtgp_jit_plan_words_chain(const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t R,
+                              const int32_t* order, const MtgpJitChain* chain, uint32_t* offsets_out,
+                              int32_t* info_out, void* stream);
+int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog,
+                              int32_t L, int32_t R, const int32_t* order, const MtgpJitChain* chain,
+                              const uint32_t* offsets, void* code, size_t code_bytes, int32_t jit_mode,
+                              void* stream);
+int mtgp_jit_unit_host_chain(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                             const int32_t* order, const MtgpJitChain* chain, int32_t unit, uint32_t* out,
+                             int32_t max_words);
 /* host translation of one program (tests/tooling): number of code words, or < 0 */
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
 /* the same in either JIT mode (MTGP_JIT_MODE_*), for one program and for one unit */

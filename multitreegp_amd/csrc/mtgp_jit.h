@@ -322,9 +322,59 @@ constexpr uint32_t kMovS43 = 0xbeab00ffu;   // s_mov_b32 s43, literal
 constexpr uint32_t kSelLo = 0xd1000008u;    // v_cndmask_b32_e64 v8, v25, v8, s[42:43]
 constexpr uint32_t kSelHi = 0x00aa1119u;
 
+// ---- role chains (ABI v13, MtgpJitChain) ---------------------------------------------------
+// A role that runs several programs back to back (the state equations of a dynamic policy, the
+// n_var trees of SR) is ONE call: unit j with bit j of chain.next set ends by copying its result
+// to v(26 + k) (k = its position in the chain) and falls through into unit j + 1, which is laid
+// out right behind it (no alignment padding); the last unit of the chain copies its result too
+// and returns.  With bit j of chain.cond also set, unit j continues only when the call site set
+// s46 != 0 and returns otherwise; the unit after it (the save-point readout) then leaves its
+// result in v8 as a plain unit does.  Per chained call one fetch redirect replaces a return + a
+// call (two), and the call-site bookkeeping of the extra calls disappears.
+constexpr int kJitChainOut = 26, kJitChainMax = 4;
+constexpr uint32_t kCmpS46Zero = 0xbf06802eu;  // s_cmp_eq_u32 s46, 0
+constexpr uint32_t kBranchScc0Skip1 = 0xbf840001u;  // s_cbranch_scc0 +1 (over the s_setpc)
+
+// position of unit j in its chain (0 for the first)
+MTGP_JIT_HD inline int jit_chain_pos(uint32_t next, int j) {
+  int k = 0;
+  if (j >= 32) return 0;
+  while (j - k - 1 >= 0 && ((next >> (j - k - 1)) & 1u)) ++k;
+  return k;
+}
+
+// the end of unit j: s_setpc (plain unit), or the chain epilogue
+MTGP_JIT_HD inline void jit_unit_end(JitOut& o, uint32_t next, uint32_t cond, int j) {
+  if (j >= 32) { o.w(kSetpcS30); return; }  // chains cover the first 32 programs
+  const bool cont = (next >> j) & 1u;
+  const bool after = j > 0 && ((next >> (j - 1)) & 1u);
+  const bool tail_of_cond = after && ((cond >> (j - 1)) & 1u);  // the optional continuation: result stays in v8
+  if ((cont || after) && !tail_of_cond) o.movv(kJitChainOut + jit_chain_pos(next, j), kJitAcc);
+  if (!cont) {
+    o.w(kSetpcS30);
+    return;
+  }
+  if ((cond >> j) & 1u) {  // continue only when s46 != 0
+    o.w(kCmpS46Zero);
+    o.w(kBranchScc0Skip1);
+    o.w(kSetpcS30);
+  }
+}
+
+// words of the end of unit j (jit_unit_end)
+MTGP_JIT_HD inline int jit_unit_end_words(uint32_t next, uint32_t cond, int j) {
+  JitOut o{nullptr, 0};
+  jit_unit_end(o, next, cond, j);
+  return o.n;
+}
+
+// unit j is laid out right after unit j - 1 (no alignment padding in between)
+MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j) { return j < 32 && ((next >> j) & 1u) != 0u; }
+
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
-                                int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs) {
+                                int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
+                                uint32_t next = 0u, uint32_t cond = 0u) {
   JitOut o{out, 0};
   o.base = base;
   for (int g = 0; g < G; ++g) {
@@ -344,7 +394,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
       o.w(kSelHi);
     }
   }
-  o.w(kSetpcS30);
+  jit_unit_end(o, next, cond, j);
   return o.n;
 }
 
@@ -352,7 +402,8 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
 // that group, written at `out` (= byte offset `base` in the buffer), plus the unit's final
 // s_setpc when `last`.  jit_unit == the concatenation of its groups.
 MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
-                                      int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs) {
+                                      int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
+                                      uint32_t next = 0u, uint32_t cond = 0u) {
   JitOut o{out, 0};
   o.base = base;
   const int q = q0 + g;
@@ -369,7 +420,7 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
     o.w(kSelLo);
     o.w(kSelHi);
   }
-  if (last) o.w(kSetpcS30);
+  if (last) jit_unit_end(o, next, cond, j);
   return o.n;
 }
 

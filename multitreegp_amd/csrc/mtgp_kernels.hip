@@ -267,6 +267,8 @@ struct KArgs {
   const uint32_t* jit_off;  // [n_waves, n_prog] byte offset of each (wave, program) unit's code
   const int32_t* jit_info;  // mtgp_jit_plan info {status, total bytes} (device) or NULL
   uint64_t jit_cap;         // bytes of the code buffer
+  int32_t chain_state;      // the JIT code chains the state role (MtgpJitChain): one call per stage
+  int32_t chain_save;       // ... and continues it into the save-point readout on request (s46)
 };
 
 // per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
@@ -574,6 +576,29 @@ __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], 
   return acc;
 }
 
+// Call a role chain (mtgp_jit.h jit_unit_end, ABI v13): the chain's programs return in v26..v29
+// (position order), and with cont != 0 the optional continuation (the save-point readout)
+// runs too and returns in v8.
+struct ChainOut {
+  float v[mtgp::kJitChainMax];
+  float tail;
+};
+__device__ __forceinline__ ChainOut jit_call_chain(uint64_t addr_, const float d[kDMax], uint64_t& flag, int cont) {
+  const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr_ >> 32)) << 32;
+  const int c = __builtin_amdgcn_readfirstlane(cont);
+  ChainOut r;
+  asm volatile("s_swappc_b64 s[30:31], %[tgt]"
+               : "={v8}"(r.tail), "={v26}"(r.v[0]), "={v27}"(r.v[1]), "={v28}"(r.v[2]), "={v29}"(r.v[3]),
+                 "+{s[32:33]}"(flag)
+               : [tgt] "s"(addr), "{s46}"(c), "{v0}"(d[0]), "{v1}"(d[1]), "{v2}"(d[2]), "{v3}"(d[3]),
+                 "{v4}"(d[4]), "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
+               : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
+                 "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41",
+                 "s42", "s43", "s44", "s45", "vcc", "scc", "memory");
+  return r;
+}
+
 #ifndef MTGP_V_NOPROG
 #define MTGP_V_NOPROG 0
 #endif
@@ -627,12 +652,48 @@ __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L
 // Programs first .. first+M-1 of every live group -> out[0..M-1], each lane its own
 // individual's values.  JIT: one call per program to the wave's unit (mtgp_jit.h jit_unit);
 // the interpreter runs when there is no usable code or when a lane needs the slow sin/cos path.
+// chained: the role's code is one chain (A.chain_state, mtgp_jit.h jit_unit_end); with save_prog
+// >= 0 the chain's continuation (program save_prog, the save-point readout) runs too -> *save_v.
 template <bool JIT, int M>
 __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, int role, int first, DataVec<JIT>& D,
-                                         float (&out)[M]) {
+                                         float (&out)[M], bool chained = false, int save_prog = -1,
+                                         float* save_v = nullptr) {
   (void)role;
   bool interp = !JIT;
-  if (JIT) {
+  if (JIT && M <= mtgp::kJitChainMax && chained) {
+    if (__builtin_expect(L.jok, 1)) {
+      const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first);
+      uint64_t fl = 0;
+#if MTGP_V_NOPROG  // diagnostic only (A/B): no program call at all
+      (void)off;
+      const ChainOut r = {{0.0f, 0.0f, 0.0f, 0.0f}, 0.0f};
+#else
+      const ChainOut r = jit_call_chain(A.jit_base + off, D.v, fl, save_prog >= 0 ? 1 : 0);
+#endif
+#pragma unroll
+      for (int j = 0; j < M; ++j) out[j] = r.v[j < mtgp::kJitChainMax ? j : 0];
+      if (save_prog >= 0) *save_v = r.tail;
+      if (!MTGP_V_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // slow sin/cos lanes: re-run the chain's
+        bool spilled = false;                                      // programs for the groups concerned
+        for (int gi = 0; gi < ng; ++gi) {
+          if (!(fl & __ballot(L.g == gi && L.active))) continue;
+          if (!spilled) { D.spill(); spilled = true; }
+#pragma unroll
+          for (int j = 0; j < M; ++j) {
+            const float t = run_one_interp(A, L, gi, first + j, D.dcol, D.st);
+            out[j] = (L.g == gi) ? t : out[j];
+          }
+          if (save_prog >= 0) {
+            const float t = run_one_interp(A, L, gi, save_prog, D.dcol, D.st);
+            *save_v = (L.g == gi) ? t : *save_v;
+          }
+        }
+      }
+      return;
+    }
+    interp = true;
+    D.spill();
+  } else if (JIT) {
     if (__builtin_expect(L.jok, 1)) {
 #pragma unroll 1
       for (int q = 0; q < M; ++q) {
@@ -674,6 +735,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
     }
+    if (save_prog >= 0) *save_v = run_groups_interp(A, L, ng, save_prog, D.dcol, D.st, 0.0f);
   }
 }
 
@@ -798,20 +860,28 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, u);
-      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka);
+      // the save-point readout (dyn.py:101) reads this stage-0 data vector (y = f_obs(ts[k], x),
+      // a; u is folded to 0), so the state chain continues into it -- unless the save-point
+      // observation needs its own noise draw (ts[k] off the step grid)
+      bool redraw = false;
+      if (NOISE && stage == 0 && is_save)
+        redraw = __float_as_uint(A.ro.ts[step / save_every]) != __float_as_uint(t0 + (float)step * h);
+      const bool save_chain = JIT && A.chain_save && stage == 0 && is_save && diff_mask != 0 && !redraw;
+      float us_chain = u;
+      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0,
+                        save_chain ? A.m.prog_readout_save : -1, &us_chain);
       if (stage == 0) {
         if (is_save) {
           const int k = step / save_every;
           float us = u;
-          if (NOISE) {
-            const float tsk = A.ro.ts[k];
-            if (__float_as_uint(tsk) != __float_as_uint(t0 + (float)step * h)) {
-              ctl_obs<Env, true>(nzc, tsk, x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
+          if (NOISE && redraw) {
+            ctl_obs<Env, true>(nzc, A.ro.ts[k], x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
 #pragma unroll
-              for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-            }
+            for (int i = 0; i < NV; ++i) D.put(i, y[i]);
           }
-          if (JIT && diff_mask != 0) {  // the save-readout unit covers every group (equal programs give u again)
+          if (save_chain) {
+            us = us_chain;
+          } else if (JIT && diff_mask != 0) {  // the save-readout unit covers every group (equal programs give u again)
             float sr[1];
             run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
             us = sr[0];
@@ -1048,7 +1118,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, ur[0]);
       float ka[NAX];
-      run_role<JIT, NAX>(A, Ln, ng, 1, A.m.prog_state, D, ka);
+      run_role<JIT, NAX>(A, Ln, ng, 1, A.m.prog_state, D, ka, DYN && A.chain_state != 0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) ds[NV + j] = ka[j];
     } else {
@@ -1261,7 +1331,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], h, h2));
-      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
+      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
 #pragma unroll
       for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
@@ -1337,7 +1407,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
   // FSAL seed f0 = f(t0, y0)
 #pragma unroll
   for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-  run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
+  run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
 #pragma unroll
   for (int i = 0; i < NV; ++i) f[0][i] = kx[i];
   bool live = active && t < t_end && steps < max_steps;
@@ -1355,7 +1425,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
         y1[i] = yi;  // the stage-6 input is the step's solution
         D.put(i, yi);
       }
-      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx);
+      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
 #pragma unroll
       for (int j = 1; j < 7; ++j)
 #pragma unroll
@@ -1611,6 +1681,215 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       if (prev_ok && bad) pending = true;
       prev_ok = !bad;
     }
+  }
+  if (w == 0) finish_group(A, Ln, tot / (float)S);
+}
+
+// --------------------------------------------------------------------------------------
+// Wide-state SR (5 <= n_var <= 64) with adaptive Dopri5 + PIDController (SR_evaluator.py:57-94
+// with the notebook's solver, SymbolicRegression.ipynb:136): k_sr_wide's workgroup layout (wave w
+// owns components [8w, 8w + 8): their y, y1 and the seven stage derivatives stay in its VGPRs)
+// with k_sr_dopri5's per-lane step control.  Every per-lane decision (error norm, accept, step
+// size, event, save points) comes from quantities reduced over ALL components through LDS in
+// index order, so each lane's state is identical in every wave and all barriers are uniform:
+// the attempt loop, the save rounds and the +inf fill run while ANY lane needs them and commit
+// per lane.  LDS: two ping-pong stage vectors + one reduction vector (n_var columns each), the
+// waves' interpreter stacks and flag columns.
+template <bool TRAJ, bool JIT>
+__global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
+  extern __shared__ float wl[];
+  Lane Ln;
+  if (!lane_setup_wide(A, Ln)) return;  // uniform over the workgroup
+  if (JIT) asm volatile("s_icache_inv");
+  const int NV = A.m.n_var;
+  const int NW = (NV + kWideComp - 1) / kWideComp;
+  const int w = Ln.wave, lane = Ln.lane, r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  float* bufs[2] = {wl + lane, wl + (size_t)NV * kWave + lane};
+  float* red = wl + (size_t)2 * NV * kWave + lane;
+  float* st = wl + (size_t)(3 * NV + w * kSMax) * kWave + lane;
+  float* flags = wl + (size_t)(3 * NV + NW * kSMax) * kWave + lane;  // [NW] columns
+  const int S = A.m.n_save, max_steps = A.m.max_steps;
+  const float rtol = A.m.rtol, atol = A.m.atol, dtmin = A.m.dtmin, dtmax = A.m.dtmax;
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  const int c0 = w * kWideComp;
+  const float* __restrict__ ts = A.ro.ts;
+  const float t_end = ts[S - 1];
+  constexpr float E[7] = MTGP_DP_TABLE_E;
+  constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+  int buf = 0;
+
+  // this wave's trees on stage vector `in` -> kx (the G groups' programs, JIT or interpreted)
+  auto rhs = [&](const float* in, float* kx) __attribute__((always_inline)) {
+    if (JIT && Ln.jok) {
+      const uint32_t la = lds_address(in);
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) {
+        const int c = c0 + t;
+        if (c >= NV) break;
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c);
+        uint64_t fl = 0;
+        float v = jit_call_lds(A.jit_base + off, la, fl);
+        if (__builtin_expect(fl != 0, 0)) {
+          for (int gi = 0; gi < ng; ++gi) {
+            if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
+            const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, in, st);
+            v = (Ln.g == gi) ? tv : v;
+          }
+        }
+        kx[t] = v;
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) {
+        const int c = c0 + t;
+        if (c >= NV) break;
+        kx[t] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, in, st, 0.0f);
+      }
+    }
+  };
+  // sum over all components in index order of the values this wave puts in red (uniform barriers)
+  auto reduce = [&]() __attribute__((always_inline)) {
+    __syncthreads();
+    float s = red[0];
+    for (int d = 1; d < NV; ++d) s = s + red[d * kWave];
+    __syncthreads();
+    return s;
+  };
+  auto any_bad = [&](const float* v) __attribute__((always_inline)) {
+    bool b = false;
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) b = b || ((c0 + t < NV) && !mtgp_isfinite(v[t]));
+    flags[w * kWave] = b ? 1.0f : 0.0f;
+    __syncthreads();
+    bool all = false;
+    for (int q = 0; q < NW; ++q) all = all || (flags[q * kWave] != 0.0f);
+    __syncthreads();
+    return all;
+  };
+  float tot = 0.0f;
+  // MSE term of save point k for the lanes with `pend` (state v of this wave's components)
+  auto save = [&](int k, const float* v, bool pend) __attribute__((always_inline)) {
+    const int kk = k < S ? k : S - 1;
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) {
+      const int c = c0 + t;
+      if (c < NV) {
+        const float e = v[t] - A.ro.ys_true[((size_t)kk * NV + c) * R + rr];
+        red[c * kWave] = e * e;
+        if (TRAJ && pend && active && A.out.xs) store_row(A.out.xs, ((size_t)kk * NV + c) * PR, loff, v[t]);
+      }
+    }
+    const float sq = reduce();
+    if (pend) tot = tot + sq;
+  };
+
+  float y[kWideComp], y1[kWideComp], kx[kWideComp], f[7][kWideComp];
+#pragma unroll
+  for (int t = 0; t < kWideComp; ++t) {
+    y[t] = (c0 + t < NV) ? A.ro.x0[rr * NV + c0 + t] : 0.0f;
+    if (c0 + t < NV) bufs[0][(c0 + t) * kWave] = y[t];
+  }
+  save(0, y, true);  // (its barrier also publishes the stage vector)
+  int k = 1, steps = 0;
+  bool at_dtmin = false, prev_ok = !any_bad(y);
+  float t = ts[0];
+  float tnext = t + A.m.h;
+  tnext = tnext > t_end ? t_end : tnext;
+  rhs(bufs[0], kx);  // FSAL seed f0 = f(t0, y0)
+#pragma unroll
+  for (int i = 0; i < kWideComp; ++i) f[0][i] = kx[i];
+  bool live = active && t < t_end && steps < max_steps;
+  while (__any(live)) {  // identical in every wave of the workgroup
+    const float h = tnext - t;
+#pragma unroll 1
+    for (int s = 1; s <= 6; ++s) {
+      buf ^= 1;
+      float* in = bufs[buf];
+#pragma unroll
+      for (int i = 0; i < kWideComp; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 6; ++j)
+          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
+        const float yi = MTGP_FMAF(h, acc, y[i]);
+        y1[i] = yi;
+        if (c0 + i < NV) in[(c0 + i) * kWave] = yi;
+      }
+      __syncthreads();  // the other buffer is not read again before the next barrier
+      rhs(in, kx);
+#pragma unroll
+      for (int j = 1; j < 7; ++j)
+#pragma unroll
+        for (int i = 0; i < kWideComp; ++i) f[j][i] = (j == s) ? kx[i] : f[j][i];
+    }
+    // error norm: rms over all components (index order) of the scaled error estimate
+#pragma unroll
+    for (int i = 0; i < kWideComp; ++i) {
+      float acc = 0.0f;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
+      const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], rtol, atol);
+      if (c0 + i < NV) red[(c0 + i) * kWave] = sc * sc;
+    }
+    const float msum = reduce();
+    const float ms = msum / (float)NV;
+    const bool keep = (ms < 1.0f) || at_dtmin;
+    float dt = h * mtgp_dp_factor(ms, keep);
+    bool at_min_next = at_dtmin;
+    if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
+    if (dtmin > 0.0f) {
+      at_min_next = dt <= dtmin;
+      dt = dt < dtmin ? dtmin : dt;
+    }
+    const bool acc_step = live && keep;
+    // SaveAt(ts) through the dense output, in rounds over the lanes that pass save points
+    while (__any(acc_step && k < S && ts[k < S ? k : S - 1] <= tnext)) {
+      const bool pend = acc_step && k < S && ts[k < S ? k : S - 1] <= tnext;
+      const float th = (ts[k < S ? k : S - 1] - t) / h;
+      float v[kWideComp];
+#pragma unroll
+      for (int i = 0; i < kWideComp; ++i) {
+        float acc = 0.0f;
+#pragma unroll
+        for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, CM[j], f[j][i], j == 0);
+        const float ymid = MTGP_FMAF(h, acc, y[i]);
+        v[i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
+      }
+      save(k, v, pend);
+      if (pend) ++k;
+    }
+    if (acc_step) {
+      t = tnext;
+#pragma unroll
+      for (int i = 0; i < kWideComp; ++i) {
+        y[i] = y1[i];
+        f[0][i] = f[6][i];  // FSAL
+      }
+    }
+    const bool ok = !any_bad(y);
+    if (live) {
+      at_dtmin = at_min_next;
+      ++steps;
+      bool stop = false;
+      if (keep) {
+        stop = prev_ok && !ok;  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
+        prev_ok = ok;
+      }
+      if (stop || !(t < t_end) || steps >= max_steps) live = false;
+      else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+    }
+  }
+  if (w == 0 && active && A.out.steps) A.out.steps[loff] = steps;
+  float inf[kWideComp];
+#pragma unroll
+  for (int i = 0; i < kWideComp; ++i) inf[i] = kInf;
+  while (__any(active && k < S)) {  // unsaved points are +inf (throw=False)
+    const bool pend = active && k < S;
+    save(k, inf, pend);
+    if (pend) ++k;
   }
   if (w == 0) finish_group(A, Ln, tot / (float)S);
 }
@@ -1968,11 +2247,23 @@ struct JitUnitArgs {
   int n_prog, L, P, G, Rp, n_units;
   const int32_t* order;
   int mode;  // mtgp_jit.h kJitModeRegs / kJitModeLds
+  uint32_t next, cond;  // role chains (MtgpJitChain, mtgp_jit.h jit_unit_end)
 };
 
 __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
-  return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out, base);
+  return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out, base, mtgp::kJitModeRegs,
+                        U.next, U.cond);
+}
+
+// byte span of unit u in the layout: a unit that falls through into the next one (a chain member)
+// spans exactly its code, the next unit following directly; every other unit is padded so that
+// it ENDS on a 64-byte line (pre = bytes of the chain members packed in front of it), so every
+// unit that is called starts on one
+__device__ __forceinline__ uint32_t jit_unit_span(const JitUnitArgs& U, int u, int words, uint32_t pre = 0u) {
+  const int j = u % U.n_prog;
+  if (mtgp::jit_unit_packed(U.next, j)) return (uint32_t)words * 4u;
+  return ((pre + (uint32_t)words * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u)) - pre;
 }
 
 __global__ void __launch_bounds__(256) k_jit_count(JitUnitArgs U, uint32_t* __restrict__ offs,
@@ -1982,7 +2273,7 @@ __global__ void __launch_bounds__(256) k_jit_count(JitUnitArgs U, uint32_t* __re
   const int n = jit_unit_words(U, i, nullptr, 0u);
   // units start on 64-byte instruction-cache lines (measured: unaligned call targets made some
   // code shapes 2x slower, scripts/dispatch_cost.py k = 4)
-  offs[i] = n > 0 ? ((uint32_t)n * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u) : 0u;
+  offs[i] = n > 0 ? jit_unit_span(U, i, n) : 0u;
   if (n < 0) atomicMin(&info[0], n);
 }
 
@@ -2040,7 +2331,7 @@ __global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t*
 // offsets.  Replaces the k_jit_count translation pass + k_jit_scan.
 __device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const int32_t* __restrict__ jw, int u) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
-  int n = 1;  // s_setpc_b64
+  int n = mtgp::jit_unit_end_words(U.next, U.cond, j);  // s_setpc_b64 or the chain epilogue
   for (int g = 0; g < U.G; ++g) {
     const int q = wave * U.G + g;
     if (q >= U.P) break;
@@ -2058,7 +2349,14 @@ __global__ void __launch_bounds__(256) k_jit_sizes(JitUnitArgs U, const int32_t*
   const int u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= U.n_units) return;
   const int n = jit_unit_words_from(U, jw, u);
-  offs[u] = n > 0 ? ((uint32_t)n * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u) : (0x80000000u | (uint32_t)(-n));
+  uint32_t pre = 0u;  // the chain members packed in front of this unit
+  int bad = 0;
+  for (int v = u - 1; v >= 0 && v / U.n_prog == u / U.n_prog && mtgp::jit_unit_packed(U.next, v % U.n_prog); --v) {
+    const int m = jit_unit_words_from(U, jw, v);
+    if (m < 0) bad = m;
+    else pre += (uint32_t)m * 4u;
+  }
+  offs[u] = (n > 0 && bad == 0) ? jit_unit_span(U, u, n, pre) : (0x80000000u | (uint32_t)(-(n < 0 ? n : bad)));
 }
 
 // pass 2, one block: exclusive scan of the sizes in place (+ the shared templates in front),
@@ -2137,7 +2435,8 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
   }
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
   const uint32_t at = b + start * 4u;
-  mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode);
+  mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode,
+                       U.next, U.cond);
 }
 
 // the shared sin/cos subroutines at the start of the code buffer
@@ -2160,10 +2459,39 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
   U.G = kWave / Rp;
   U.order = order;
   U.mode = mtgp::kJitModeRegs;
+  U.next = U.cond = 0u;
   const long waves = ((long)P + U.G - 1) / U.G;
   if (waves * n_prog > INT32_MAX - 1) return false;
   U.n_units = (int)(waves * n_prog);
   return true;
+}
+
+// The role chain the evaluator kernels of `m` call (mtgp.h MtgpJitChain): the state role's
+// programs prog_state .. prog_state + M - 1 (M = state_size for the dynamic policy, n_var for
+// register-resident SR) as one chain when M >= 2, continued into the save-point readout when the
+// fixed-step dynamic kernel can use it (the readout_save program right after the state programs).
+MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
+  MtgpJitChain c{0u, 0u};
+  int first = m.prog_state, M = 0;
+  bool save = false;
+  if (m.model == MTGP_MODEL_SR) {
+    if (m.n_var > 4) return c;  // the wide-state kernel (LDS-data code) calls one program at a time
+    M = m.n_var;
+  } else if (m.model == MTGP_MODEL_DYNAMIC) {
+    M = m.state_size;
+    save = m.solver != MTGP_SOLVER_DOPRI5 && m.readout_save_same != 1 && m.prog_readout_save == first + M;
+  } else {
+    return c;
+  }
+  const int lim = n_prog < 32 ? n_prog : 32;
+  if (M < 1 || M > mtgp::kJitChainMax || first < 0 || first + M + (save ? 1 : 0) > lim) return c;
+  if (M == 1 && !save) return c;
+  for (int k = 0; k + 1 < M; ++k) c.next |= 1u << (first + k);
+  if (save) {
+    c.next |= 1u << (first + M - 1);
+    c.cond |= 1u << (first + M - 1);
+  }
+  return c;
 }
 
 // Executable device memory for the JIT (HSA pool allocation with the executable flag on the
@@ -2424,11 +2752,23 @@ int mtgp_jit_plan(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, i
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
+int mtgp_jit_chain(const MtgpModel* model, int32_t n_prog, MtgpJitChain* chain_out) {
+  if (!model || !chain_out || n_prog <= 0) return MTGP_ERR_ARG;
+  *chain_out = jit_chain_for(*model, n_prog);
+  return MTGP_OK;
+}
+
 int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t R, const int32_t* order,
                         uint32_t* offsets_out, int32_t* info_out, void* stream) {
+  return mtgp_jit_plan_words_chain(jit_words, P, n_prog, R, order, nullptr, offsets_out, info_out, stream);
+}
+
+int mtgp_jit_plan_words_chain(const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t R, const int32_t* order,
+                              const MtgpJitChain* chain, uint32_t* offsets_out, int32_t* info_out, void* stream) {
   JitUnitArgs U;
   static const MtgpInstr dummy = {0u, 0.0f};
   if (!jit_words || !offsets_out || !info_out || !jit_unit_args(&dummy, P, n_prog, 1, R, order, U)) return MTGP_ERR_ARG;
+  if (chain) { U.next = chain->next; U.cond = chain->cond; }
   hipStream_t s = (hipStream_t)stream;
   if (U.n_units == 0) {
     if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
@@ -2443,10 +2783,22 @@ int mtgp_jit_plan_words(const int32_t* jit_words, int32_t P, int32_t n_prog, int
 int mtgp_jit_emit_words(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t L,
                         int32_t R, const int32_t* order, const uint32_t* offsets, void* code, size_t code_bytes,
                         int32_t jit_mode, void* stream) {
+  return mtgp_jit_emit_words_chain(prog, jit_words, P, n_prog, L, R, order, nullptr, offsets, code, code_bytes,
+                                   jit_mode, stream);
+}
+
+int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, int32_t P, int32_t n_prog, int32_t L,
+                              int32_t R, const int32_t* order, const MtgpJitChain* chain, const uint32_t* offsets,
+                              void* code, size_t code_bytes, int32_t jit_mode, void* stream) {
   JitUnitArgs U;
   if (!jit_words || !offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
   if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   U.mode = jit_mode;
+  if (chain) {
+    if (jit_mode != mtgp::kJitModeRegs && (chain->next | chain->cond) != 0u) return MTGP_ERR_ARG;  // v26.. are preloads
+    U.next = chain->next;
+    U.cond = chain->cond;
+  }
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(k_jit_templates, dim3(1), dim3(256), 0, s, (uint32_t*)code, (uint64_t)code_bytes);
@@ -2478,19 +2830,33 @@ int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
-int mtgp_jit_unit_host_ex(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
-                          int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode) {
+static int jit_unit_host_impl(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                              const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode,
+                              uint32_t next, uint32_t cond) {
   JitUnitArgs U;
   if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
   if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   const int wave = unit / n_prog, j = unit - wave * n_prog;
-  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes, jit_mode);
+  const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes, jit_mode,
+                               next, cond);
   if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
   if (out) {
     if (n > max_words) return MTGP_ERR_ARG;
-    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode);
+    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode, next, cond);
   }
   return n;
+}
+
+int mtgp_jit_unit_host_ex(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
+                          int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode) {
+  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, jit_mode, 0u, 0u);
+}
+
+int mtgp_jit_unit_host_chain(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
+                             const int32_t* order, const MtgpJitChain* chain, int32_t unit, uint32_t* out,
+                             int32_t max_words) {
+  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, mtgp::kJitModeRegs,
+                            chain ? chain->next : 0u, chain ? chain->cond : 0u);
 }
 
 int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
@@ -2636,7 +3002,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
   if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;
   if (dopri5) {  // adaptive: save points come from ts, steps from the controller
-    if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > 4)) return MTGP_ERR_ARG;
+    if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > MTGP_MAX_DATA)) return MTGP_ERR_ARG;
     if (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f)) return MTGP_ERR_ARG;
     if (!(model->rtol >= 0.0f) || !(model->atol >= 0.0f)) return MTGP_ERR_ARG;
   } else {
@@ -2660,6 +3026,13 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   A.jit_off = jit ? jitc->offsets : nullptr;
   A.jit_info = jit ? jitc->info : nullptr;
   A.jit_cap = jit ? jitc->capacity : 0;
+  A.chain_state = A.chain_save = 0;
+  if (jit && (jitc->chain.next | jitc->chain.cond) != 0u) {  // chained code: must be the chain this model calls
+    const MtgpJitChain want = jit_chain_for(*model, n_prog);
+    if (want.next != jitc->chain.next || want.cond != jitc->chain.cond) return MTGP_ERR_ARG;
+    A.chain_state = 1;
+    A.chain_save = want.cond != 0u;
+  }
   // (the wide-state SR kernel keeps its data vector in LDS: its code is built in kJitModeLds)
   hipStream_t s = (hipStream_t)stream;
   int Rp = 1;
@@ -2686,8 +3059,18 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     if (model->n_var > 4) {
       if (model->n_var > MTGP_MAX_DATA || n_prog < model->prog_state + model->n_var) return MTGP_ERR_ARG;
       const int nw = (model->n_var + kWideComp - 1) / kWideComp;
-      const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
       const dim3 wgrid((unsigned)(((long)P + G - 1) / G)), wblock(kWave * nw);
+      if (dopri5) {  // + a reduction vector (error norm, MSE)
+        const size_t lds_dp = (size_t)(3 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+        return launch_timed([&] {
+          if (jit) {
+            if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, true>), wgrid, wblock, lds_dp, s, A);
+            else hipLaunchKernelGGL((k_sr_wide_dopri5<false, true>), wgrid, wblock, lds_dp, s, A);
+          } else if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, false>), wgrid, wblock, lds_dp, s, A);
+          else hipLaunchKernelGGL((k_sr_wide_dopri5<false, false>), wgrid, wblock, lds_dp, s, A);
+        }, s);
+      }
+      const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
       return launch_timed([&] {
         if (jit) {
           if (traj) hipLaunchKernelGGL((k_sr_wide<true, true>), wgrid, wblock, lds, s, A);

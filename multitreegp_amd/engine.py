@@ -47,8 +47,8 @@ class Flattened:
     order: Optional[torch.Tensor] = None  # int32 [P] evaluation schedule (mtgp_schedule)
     jit_words: Optional[torch.Tensor] = None  # int32 [P, n_prog] JIT code words per program (mtgp_flatten_ex)
     jit_cost: Optional[torch.Tensor] = None   # int32 [P, n_prog] schedule weight of the JIT code
-    jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity) of the JIT
-    jit_key: Optional[tuple] = None       # (R, order, engine id, arena slot, arena generation) of that code
+    jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity, chain) of the JIT
+    jit_key: Optional[tuple] = None       # (R, order, engine id, chain, arena slot, arena generation) of that code
 
 
 class DeviceEngine:
@@ -111,9 +111,10 @@ class DeviceEngine:
         without a host round trip: the buffer is sized from the code size per program seen in
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
-        key = (R, None if order is None else order.data_ptr(), id(self))
-        if fl.jit_key is not None and fl.jit_key[:3] == key:
-            slot, gen = fl.jit_key[3:]
+        chain = self.jit_chain(m, fl.n_prog) if fl.jit_words is not None else nat.MtgpJitChain(0, 0)
+        key = (R, None if order is None else order.data_ptr(), id(self), (chain.next, chain.cond))
+        if fl.jit_key is not None and fl.jit_key[:4] == key:
+            slot, gen = fl.jit_key[4:]
             if slot is None or self._arena_gen[slot] == gen:  # code still in place (or none was built)
                 return fl.jit
         fl.jit_key, fl.jit = key + (None, None), None
@@ -134,8 +135,8 @@ class DeviceEngine:
         info = torch.empty((3,), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         if fl.jit_words is not None:  # sizes from the flatten pass
-            rc = self.native.mtgp_jit_plan_words(fl.jit_words.data_ptr(), P, fl.n_prog, R, optr, offs.data_ptr(),
-                                                 info.data_ptr(), stream)
+            rc = self.native.mtgp_jit_plan_words_chain(fl.jit_words.data_ptr(), P, fl.n_prog, R, optr,
+                                                       ctypes.byref(chain), offs.data_ptr(), info.data_ptr(), stream)
         else:  # flattened without the sizing outputs: translate to size
             rc = self.native.mtgp_jit_plan(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(),
                                            info.data_ptr(), stream)
@@ -151,16 +152,28 @@ class DeviceEngine:
         per_unit = self._jit_bytes_per_unit or 1024.0 * G
         ptr, size = self._arena(int(n * per_unit) + 4096)
         if fl.jit_words is not None:
-            rc = self.native.mtgp_jit_emit_words(fl.prog.data_ptr(), fl.jit_words.data_ptr(), P, fl.n_prog, fl.L,
-                                                 R, optr, offs.data_ptr(), ptr, size, self._jit_mode(), stream)
+            rc = self.native.mtgp_jit_emit_words_chain(fl.prog.data_ptr(), fl.jit_words.data_ptr(), P, fl.n_prog,
+                                                       fl.L, R, optr, ctypes.byref(chain), offs.data_ptr(), ptr, size,
+                                                       self._jit_mode(), stream)
         else:
             rc = self.native.mtgp_jit_emit(fl.prog.data_ptr(), P, fl.n_prog, fl.L, R, optr, offs.data_ptr(), ptr,
                                            size, stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_emit failed: {rc}")
-        fl.jit = (ptr, offs, info, size)
+        fl.jit = (ptr, offs, info, size, chain)
         fl.jit_key = key + (self._arena_i, self._arena_gen[self._arena_i])
         return fl.jit
+
+    def jit_chain(self, m, n_prog: int) -> "nat.MtgpJitChain":
+        """The role chain the evaluator of model struct `m` calls (mtgp_jit_chain); none when
+        MTGP_JIT_CHAIN=0 (A/B switch) or in LDS-data mode."""
+        ch = nat.MtgpJitChain(0, 0)
+        if os.environ.get("MTGP_JIT_CHAIN", "1") == "0" or self._jit_mode() != nat.JIT_MODE_REGS:
+            return ch
+        rc = self.native.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch))
+        if rc != nat.OK:
+            raise RuntimeError(f"mtgp_jit_chain failed: {rc}")
+        return ch
 
     @staticmethod
     def jit_ok(fl: Flattened) -> bool:
@@ -390,6 +403,7 @@ class DeviceEngine:
         jc = nat.MtgpJitCode()
         if jit is not None:
             jc.code, jc.offsets, jc.info, jc.capacity = jit[0], jit[1].data_ptr(), jit[2].data_ptr(), jit[3]
+            jc.chain = jit[4]
         rc = self.native.mtgp_eval_rk4_jit(ctypes.byref(m), fl.prog.data_ptr(), fl.plen.data_ptr(), fl.n_prog, fl.L,
                                            fl.nodes.data_ptr(), P, ctypes.byref(ro), ctypes.byref(out),
                                            ctypes.byref(jc), stream)

@@ -302,10 +302,12 @@ class DynamicEvaluator(_ControlEvaluator):
         D = self.n_data()
         ymask = (1 << no) - 1
         umask = ((1 << nu) - 1) << (no + ss)
-        specs = [(t, D, 0) for t in range(ss)]                      # state equation [y, a, u, tg]
-        specs += [(ss + j, D, ymask | umask) for j in range(nu)]    # readout in _drift (dyn.py:113)
+        # order: readout | state equations | save-point readout, so that the JIT can chain the state
+        # programs into the save-point readout (mtgp.h MtgpJitChain: it must follow the state programs)
+        specs = [(ss + j, D, ymask | umask) for j in range(nu)]     # readout in _drift (dyn.py:113)
+        specs += [(t, D, 0) for t in range(ss)]                     # state equation [y, a, u, tg]
         specs += [(ss + j, D, umask) for j in range(nu)]            # readout at saves (dyn.py:101)
-        roles = dict(prog_state=0, prog_readout=ss, prog_readout_save=ss + nu, readout_save_same=-1)
+        roles = dict(prog_state=nu, prog_readout=0, prog_readout_save=ss + nu, readout_save_same=-1)
         return specs, roles
 
 
@@ -350,8 +352,6 @@ class SREvaluator(_CandidateAPI):
         if ys.shape[0] != R or ys.shape[2] != nv:
             raise ValueError("ys must be [R, S, n_var]")
         if self.solver_kind == "dopri5":  # save points straight from ts, steps from the controller
-            if nv > 4:
-                raise NotImplementedError("Dopri5 SR is implemented for n_var <= 4 (wide-state SR: RK4)")
             n_steps, save_every, S = adaptive_schedule(ts)
         else:
             n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)

@@ -33,11 +33,16 @@ def main():
                                obs_noise=0.0)
     env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
     dev = torch.device("cuda", 0)
-    engines = {}
+    engines, envs = {}, {}
     for v in a.variants.split(","):
-        path = nat.LIB_PATH if v == "prod" else os.path.join(ROOT, "multitreegp_amd", "lib", "variants",
-                                                             f"libmtgp_hip_{v}.so")
+        # "name@VAR=value[@VAR2=value]": the library `name` with environment overrides (engine switches
+        # such as MTGP_JIT_CHAIN=0) applied around each of its evaluations
+        name, *kv = v.split("@")
+        envs[v] = dict(x.split("=", 1) for x in kv)
+        path = nat.LIB_PATH if name == "prod" else os.path.join(ROOT, "multitreegp_amd", "lib", "variants",
+                                                                f"libmtgp_hip_{name}.so")
         engines[v] = DeviceEngine(ff, lib, 0.0, dev, native=nat.load(path))
+        engines[v].native.mtgp_set_timing(1)
     pop_dev = torch.from_numpy(pop).to(dev)
     first = next(iter(engines.values()))
     fl = first.flatten(pop_dev)
@@ -52,13 +57,22 @@ def main():
     first.check_status(fl)
     ref = None
     times = {v: [] for v in engines}
+    ktimes = {v: [] for v in engines}
     for r in range(a.rounds + 1):
         for v, eng in engines.items():
+            old = {k: os.environ.get(k) for k in envs[v]}
+            os.environ.update(envs[v])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=fl, check=False,
                                schedule=not a.no_schedule)
             e1.record()
+            for k, x in old.items():
+                if x is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = x
+            kms = eng.native.mtgp_last_kernel_ms()
             torch.cuda.synchronize()
             f = res["fitness"].cpu().numpy()
             if ref is None:
@@ -66,12 +80,14 @@ def main():
             same = bool(np.array_equal(f.view(np.uint32), ref.view(np.uint32)))
             if r > 0:
                 times[v].append(e0.elapsed_time(e1))
+                ktimes[v].append(kms)
             if not same:
                 print(f"WARNING variant {v} fitness differs from first variant", flush=True)
     units = a.pop * a.rollouts * a.ode_steps
     for v, t in times.items():
         print(json.dumps({"tag": a.tag, "variant": v, "pop": a.pop, "R": a.rollouts, "traj": not a.no_traj,
                           "median_ms": float(np.median(t)), "min_ms": float(np.min(t)),
+                          "kernel_median_ms": float(np.median(ktimes[v])), "kernel_min_ms": float(np.min(ktimes[v])),
                           "Gsteps_per_s": units / (np.median(t) / 1e3) / 1e9}), flush=True)
 
 

@@ -176,6 +176,59 @@ def test_gpu_dopri5_sr_bitexact(jit, n_var, tol, R):
     assert bits_equal(xs, ref["xs"]), mismatch_report(xs, ref["xs"], "xs")
 
 
+def test_dopri5_wide_sr_oracle_vs_fine_rk4():
+    """The checker of the wide-state Dopri5 kernel: the oracle's adaptive solve of 12-variable SR
+    candidates at a tight tolerance agrees with a fine fixed-step RK4 solve of the same trees
+    (where both stay finite and moderate), and starts every trajectory at x0."""
+    env, lib, ff, data, pop = sr_setup(P=8, R=3, n_save=11, save_every=4, h=0.01, depth=4, N=30, seed=2, n_var=12,
+                                       solver=(1e-6, 1e-6, 0.0001, 2000))
+    d = ff.prepare(data)
+    dp = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)["xs"]
+    x0, ts, ys, keys = data
+    fine = mt.SREvaluator(solver=mt.RK4(), dt0=0.0005)
+    d2 = fine.prepare(data)
+    rk = orc.evaluate(oracle_model(fine, d2), pop, lib, oracle_rollouts(d2), trajectories=True)["xs"]
+    assert np.array_equal(dp[:, :, 0, :], np.broadcast_to(x0, dp[:, :, 0, :].shape))
+    ok = np.isfinite(dp) & np.isfinite(rk) & (np.abs(rk) < 1e3)
+    assert ok.mean() > 0.5
+    # random trees include divisions: near-singular candidates force dtmin steps (accepted whatever
+    # their error), so only most candidates -- the smooth ones -- must agree closely
+    err = np.where(ok, np.abs(dp - rk) / (1e-3 + np.abs(rk)), 0.0).reshape(dp.shape[0], -1).max(axis=1)
+    assert (err < 1e-3).sum() >= dp.shape[0] // 2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+@pytest.mark.parametrize("n_var,tol,R,max_steps", [(5, 1e-5, 8, 300), (12, 1e-4, 4, 200), (64, 1e-4, 8, 150)])
+def test_gpu_dopri5_wide_sr_bitexact(jit, n_var, tol, R, max_steps):
+    """Wide-state SR (n_var > 4: the workgroup kernel, components spread over waves) with
+    Dopri5 + PIDController: per-lane adaptive steps whose error norm, event and save points are
+    reduced over all components -- fitness, per-rollout fitness, step counts and SaveAt(ts)
+    trajectories bit-identical to the oracle, with the JIT (LDS-data code) and the interpreter."""
+    import torch
+    from helpers import bits_equal, mismatch_report
+    from multitreegp_amd.engine import DeviceEngine
+    env, lib, ff, data, pop = sr_setup(P=21, R=R, n_save=26, save_every=4, h=0.01, depth=8, N=64,
+                                       seed=40 + n_var, n_var=n_var, solver=(tol, tol, 0.001, max_steps))
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=jit)
+    r = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=True, rollout_fitness=True, step_counts=True)
+    torch.cuda.synchronize()
+    assert DeviceEngine.jit_ok(r["_flat"]) == jit
+    res = {k: v.cpu().numpy() for k, v in r.items() if isinstance(v, torch.Tensor)}
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, S = pop.shape[0], d["n_save"]
+    xs = res["xs"].reshape(S, n_var, P, R).transpose(2, 3, 0, 1)
+    assert bits_equal(xs, ref["xs"]), mismatch_report(xs, ref["xs"], "xs")
+    if "steps" in ref:
+        assert np.array_equal(res["steps"], ref["steps"])
+    assert (res["steps"] >= 1).all() and (res["steps"] <= max_steps).all()
+    # the workload exercises more than one accept/reject pattern
+    assert len(np.unique(res["steps"])) > 3
+
+
 @pytest.mark.gpu
 def test_gpu_dopri5_fitness_only_matches_trajectory_mode():
     from helpers import bits_equal

@@ -58,8 +58,8 @@ def test_program_specs_dynamic():
     ev = mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05)
     specs, roles = ev.program_specs()
     # state equations see [y, a, u]; readout in the drift sees y = 0, u = 0; at saves u = 0
-    assert specs == [(0, 7, 0), (1, 7, 0), (2, 7, 0b1001111), (2, 7, 0b1000000)]
-    assert roles["prog_readout"] == 2 and roles["prog_readout_save"] == 3
+    assert specs == [(2, 7, 0b1001111), (0, 7, 0), (1, 7, 0), (2, 7, 0b1000000)]
+    assert roles["prog_readout"] == 0 and roles["prog_state"] == 1 and roles["prog_readout_save"] == 3
 
 
 def test_data_fingerprint_follows_content():

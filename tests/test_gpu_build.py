@@ -160,3 +160,88 @@ def test_lds_mode_units_match_host_units(R):
         # the units are laid out after the templates exactly as the host lays them out (PC-relative
         # calls aside, which SR has none of): equal words
         assert np.array_equal(code[o[u] // 4: o[u] // 4 + w], host[:w]), u
+
+
+@pytest.mark.parametrize("R", [4, 32])
+def test_chained_units_match_host_units(R):
+    """Role chains (ABI v13): the device plan packs a chain member's successor right behind it
+    (no alignment padding), every other unit starts on a 64-byte line, and the emitted code equals
+    the host-built chained units word for word (the PC-relative literal of each sin/cos call
+    aside: the host lays every unit out at the first code byte)."""
+    import torch
+    vl = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
+    lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
+    pop = sample_population(R, lib, 203, 1, max_init_depth=10, max_nodes=64)[0]
+    specs = [(2, 7, 0b1001111), (0, 7, 0), (1, 7, 0), (2, 7, 0b1000000)]  # readout | state | save readout
+    P, T, N, _ = pop.shape
+    n_prog = len(specs)
+    L = (2 * N + 8 + 3) // 4 * 4
+    prog, out = _flatten_ex(pop, lib, specs, L)
+    L_ = nat.load()
+    m = nat.MtgpModel()
+    m.model, m.state_size, m.n_var, m.solver = nat.MODEL_ACROBOT_DYNAMIC, 2, 4, nat.SOLVER_RK4
+    m.prog_state, m.prog_readout, m.prog_readout_save, m.readout_save_same = 1, 0, 3, -1
+    ch = nat.MtgpJitChain()
+    assert L_.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0 and ch.next == 0b110
+    order_np = np.random.default_rng(R).permutation(P).astype(np.int32)
+    order = torch.from_numpy(order_np).cuda()
+    n = L_.mtgp_jit_units(P, n_prog, R)
+    offs = torch.empty((n + 1,), dtype=torch.int32, device="cuda")
+    info = torch.zeros((2,), dtype=torch.int32, device="cuda")
+    assert L_.mtgp_jit_plan_words_chain(out["jw"].data_ptr(), P, n_prog, R, order.data_ptr(), ctypes.byref(ch),
+                                        offs.data_ptr(), info.data_ptr(), None) == 0
+    torch.cuda.synchronize()
+    inf = info.cpu().numpy()
+    assert inf[0] == 0
+    size = int(inf[1]) + 4096
+    buf = torch.zeros((size // 4,), dtype=torch.int32, device="cuda")
+    assert L_.mtgp_jit_emit_words_chain(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
+                                        ctypes.byref(ch), offs.data_ptr(), buf.data_ptr(), size, 0, None) == 0
+    torch.cuda.synchronize()
+    code = buf.cpu().numpy().view(np.uint32)
+    o = offs.cpu().numpy().view(np.uint32)
+    hp = prog[: P * n_prog * L * 2].cpu().numpy()
+    host = np.zeros(1 << 16, np.uint32)
+    for u in range(n):
+        j = u % n_prog
+        w = L_.mtgp_jit_unit_host_chain(hp.ctypes.data, P, n_prog, L, R, order_np.ctypes.data, ctypes.byref(ch), u,
+                                        host.ctypes.data, host.size)
+        assert w > 0
+        if ch.next >> j & 1:
+            assert o[u + 1] - o[u] == 4 * w, u  # the successor follows directly
+        else:  # every unit that is called starts on a 64-byte line, chain members follow directly
+            assert o[u] % 64 == 0 or (j > 0 and ch.next >> (j - 1) & 1), u
+            assert o[u + 1] % 64 == 0 and o[u + 1] - o[u] >= 4 * w, u
+        got = code[o[u] // 4: o[u] // 4 + w]
+        keep = np.ones(w, bool)
+        keep[1:] = got[:-1] != 0x802CFF2C  # s_add_u32 s44, literal: the PC-relative call offset
+        assert np.array_equal(got[keep], host[:w][keep]), u
+
+
+def test_chained_and_unchained_evaluations_agree():
+    """The same population evaluated with chained JIT code, one-call-per-program JIT code
+    (MTGP_JIT_CHAIN=0) and the interpreter: bit-identical fitness and trajectories (RK4 dynamic
+    policy with the save-point continuation, SR n_var 2 chain)."""
+    import os
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    env = mt.Acrobot(0.0, 0.0)
+    lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
+    ff = mt.DynamicEvaluator(env, 2, 0.05, solver=mt.RK4())
+    data = mt.control_data(env, 32, 0.05, None, seed=3, n_steps=60)
+    pop = torch.from_numpy(sample_population(11, lib, 130, 1, max_init_depth=10, max_nodes=64)[0]).cuda()
+    outs = []
+    for chain, jit in (("1", True), ("0", True), ("1", False)):
+        os.environ["MTGP_JIT_CHAIN"] = chain
+        try:
+            eng = DeviceEngine(ff, lib, 0.5, "cuda:0", jit=jit)
+            r = eng.evaluate(pop, data, trajectories=True)
+            if jit:
+                assert DeviceEngine.jit_ok(r["_flat"])
+                assert (r["_flat"].jit[4].next != 0) == (chain == "1")
+            outs.append({k: r[k].cpu().numpy().view(np.uint32) for k in ("fitness", "xs", "us", "acts", "ys")})
+        finally:
+            os.environ.pop("MTGP_JIT_CHAIN", None)
+    for o in outs[1:]:
+        for k in o:
+            assert np.array_equal(o[k], outs[0][k]), k

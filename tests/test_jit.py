@@ -8,6 +8,7 @@
   sin / cos / div templates as black boxes) reproduces the row-order oracle bit for bit on
   random trees and data, which pins operand order and the compile-time operand stack."""
 import os
+import ctypes
 import re
 import subprocess
 import sys
@@ -130,14 +131,27 @@ def _setup(kind):
     return lib, pop, 4, [0]
 
 
-def _emulate(words, data, full=False, lds=False):
+class FellThrough(Exception):
+    """The emulated unit ended without returning (a role-chain member falls into the next unit)."""
+
+    def __init__(self, regs):
+        super().__init__("fell through")
+        self.regs = regs
+
+
+def _emulate(words, data, full=False, lds=False, regs=None, s46=0):
     """Run emitted code on data [n_data, M] (float32 lanes, M <= 64); returns v8 (or all VGPRs).
     Honours the exec moves of per-wave units (VALU results only land in exec lanes).  lds: the
-    data vector is the LDS stage vector (LDS-data mode: ds_read_b32 from v0 + slot * 256)."""
+    data vector is the LDS stage vector (LDS-data mode: ds_read_b32 from v0 + slot * 256).
+    regs: VGPRs to start from (a chain's next unit); s46: the chain-continuation flag; a unit that
+    ends without returning raises FellThrough(regs)."""
     M = data.shape[1]
-    v = np.zeros((64, M), np.float32)
-    if not lds:
-        v[: data.shape[0]] = data
+    if regs is not None:
+        v = regs
+    else:
+        v = np.zeros((64, M), np.float32)
+        if not lds:
+            v[: data.shape[0]] = data
     i = 0
     lit = lambda k: np.full(M, np.array(words[k], np.uint32).view(np.float32), np.float32)  # noqa: E731
     exec_ = np.ones(M, bool)
@@ -148,9 +162,16 @@ def _emulate(words, data, full=False, lds=False):
         v[dst] = np.where(exec_, val, v[dst])
 
     while True:
+        if i >= len(words):
+            raise FellThrough(v)
         w = words[i]
         if w == SETPC:
             return v if full else v[8]
+        if words[i:i + 3] == [0xBF06802E, 0xBF840001, SETPC]:  # s_cmp_eq_u32 s46, 0; s_cbranch_scc0 +1; s_setpc
+            if s46 == 0:
+                return v if full else v[8]
+            i += 3
+            continue
         if (w & 0xFFFF0000) == 0xD86C0000:  # ds_read_b32 vdst, v0 offset:slot*256
             assert lds and (words[i + 1] & 0xFF) == 0, hex(words[i + 1])
             put(words[i + 1] >> 24, data[(w & 0xFFFF) // 256])
@@ -496,3 +517,109 @@ def test_lds_mode_translation_disassembles_and_emulates_to_oracle():
             assert same.all(), (p, t, got[~same][:4], want[~same][:4])
             checked += 1
     assert checked >= 600
+
+
+def _chain_model(kind):
+    m = nat.MtgpModel()
+    if kind == "dynamic":
+        m.model, m.state_size, m.n_var = nat.MODEL_ACROBOT_DYNAMIC, 2, 4
+        m.prog_state, m.prog_readout, m.prog_readout_save, m.readout_save_same = 1, 0, 3, -1
+    else:
+        m.model, m.n_var, m.prog_state = nat.MODEL_SR, 4, 0
+    m.solver = nat.SOLVER_RK4
+    return m
+
+
+def test_chain_masks():
+    """mtgp_jit_chain: the dynamic policy chains its state programs into the save-point readout
+    (conditional), register-resident SR its n_var trees; Dopri5 drops the save continuation,
+    wide SR and static policies have no chain."""
+    lib_n = nat.load()
+    ch = nat.MtgpJitChain()
+    m = _chain_model("dynamic")
+    assert lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch)) == 0
+    assert (ch.next, ch.cond) == (0b110, 0b100)
+    m.solver = nat.SOLVER_DOPRI5
+    lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch))
+    assert (ch.next, ch.cond) == (0b010, 0)
+    m = _chain_model("sr")
+    lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch))
+    assert (ch.next, ch.cond) == (0b0111, 0)
+    m.n_var = 12
+    lib_n.mtgp_jit_chain(ctypes.byref(m), 12, ctypes.byref(ch))
+    assert (ch.next, ch.cond) == (0, 0)
+    m.model, m.n_var, m.prog_state, m.prog_readout = nat.MODEL_ACROBOT_STATIC, 4, -1, 0
+    lib_n.mtgp_jit_chain(ctypes.byref(m), 1, ctypes.byref(ch))
+    assert (ch.next, ch.cond) == (0, 0)
+
+
+@pytest.mark.parametrize("kind,R", [("dynamic", 32), ("dynamic", 4), ("sr", 16)])
+def test_role_chain_units_emulate_to_oracle(kind, R):
+    """Role chains (ABI v13): the state programs of a wave run as one call -- each chain member
+    copies its result to v26 + k and falls into the next unit, the last returns, or (dynamic,
+    s46 != 0) continues into the save-point readout, which returns in v8.  Emulated unit by unit
+    and checked lane by lane against the oracle; the code disassembles and writes only v8-v29 /
+    the template SGPRs."""
+    if kind == "dynamic":
+        lib, pop, n_data, _ = _setup("dynamic")
+        ff = mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05)
+    else:
+        lib, pop, n_data, _ = _setup("sr")
+        ff = mt.SREvaluator(dt0=0.05)
+        ff._n_var = 4
+    prog, specs, roles, L = _host_flatten(ff, lib, pop[:24])
+    P, n_prog = prog.shape[:2]
+    order = np.random.default_rng(4).permutation(P).astype(np.int32)
+    lib_n = nat.load()
+    ch = nat.MtgpJitChain()
+    lib_n.mtgp_jit_chain(ctypes.byref(_chain_model(kind)), n_prog, ctypes.byref(ch))
+    first = roles["prog_state"]
+    members = [j for j in range(n_prog) if ch.next >> j & 1] + [j for j in range(n_prog) if
+                                                                 j > 0 and ch.next >> (j - 1) & 1 and
+                                                                 not ch.next >> j & 1]
+    members = sorted(set(members))
+    Rp = 1 << max(R - 1, 0).bit_length()
+    G = 64 // Rp
+    rng = np.random.default_rng(5)
+    out = np.zeros(1 << 16, np.uint32)
+    for wave in range(-(-P // G)):
+        data = (rng.standard_normal((8, 64)) * 2).astype(np.float32)
+        codes = {}
+        for j in members:
+            n = lib_n.mtgp_jit_unit_host_chain(prog.ctypes.data, P, n_prog, L, R, order.ctypes.data,
+                                               ctypes.byref(ch), wave * n_prog + j, out.ctypes.data, out.size)
+            assert n > 0, n
+            codes[j] = [int(x) for x in out[:n]]
+            for ln in _disassemble(codes[j]):
+                assert "invalid" not in ln.lower() and "exec" not in ln, ln
+                m = re.fullmatch(r"v_\w+ v(\d+),.*", ln)
+                if m:
+                    assert 8 <= int(m.group(1)) <= 29, ln
+        for s46 in ((0, 1) if ch.cond else (0,)):
+            regs = None
+            for j in members:
+                try:
+                    regs = _emulate(codes[j], data, full=True, regs=regs, s46=s46)
+                    break
+                except FellThrough as e:
+                    regs = e.regs
+            else:
+                raise AssertionError("the chain never returned")
+            n_state = len(members) - (1 if ch.cond else 0)
+            for lane in range(64):
+                q = wave * G + lane // Rp
+                if q >= P:
+                    continue
+                outs = [(26 + k, first + k) for k in range(n_state)]
+                if s46:
+                    outs.append((8, roles["prog_readout_save"]))
+                for reg, j in outs:
+                    t, nd, zm = specs[j]
+                    d = data[:n_data, lane].copy()
+                    for b in range(nd):
+                        if zm >> b & 1:
+                            d[b] = 0.0
+                    want = orc.eval_tree(pop[order[q], t], lib.fn_codes, lib.n_funcs, lib.var_start, d)
+                    got = regs[reg, lane]
+                    assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
+                        (np.isnan(got) and np.isnan(want)), (wave, lane, reg, got, want)
