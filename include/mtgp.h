@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 13
+#define MTGP_ABI_VERSION 14
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -269,10 +269,15 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  * the evaluator asks for it: the fixed-step dynamic kernel continues the state chain into the
  * save-point readout at save points).  mtgp_jit_chain gives the chain the evaluator kernels of
  * `model` call; code built with another non-zero chain is rejected (MTGP_ERR_ARG), code built
- * without one ({0, 0}) is called one program at a time as before. */
+ * without one ({0, 0, 0}) is called one program at a time as before.
+ * store (ABI v14): LDS store chains for the wide-state SR kernels (MTGP_JIT_MODE_LDS code): every
+ * unit j writes its result into the caller's LDS output vector (slot j) and falls through into
+ * unit j + 1 unless j + 1 is a multiple of `store` -- one call per wave (its `store` components)
+ * and stage. */
 typedef struct {
   uint32_t next;
   uint32_t cond;
+  uint32_t store;
 } MtgpJitChain;
 
 typedef struct {
@@ -281,7 +286,7 @@ typedef struct {
   const int32_t* info;      /* info[2] of mtgp_jit_plan, or NULL if the host checked it */
   uint64_t capacity;        /* bytes of `code`; the kernel interprets when info says the */
                             /* plan failed or the code did not fit (no host round trip) */
-  MtgpJitChain chain;       /* the chain the code was built with (ABI v13; {0, 0}: none) */
+  MtgpJitChain chain;       /* the chain the code was built with (ABI v13/14; {0, 0, 0}: none) */
 } MtgpJitCode;
 
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code);
@@ -312,7 +317,7 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
                               void* stream);
 int mtgp_jit_unit_host_chain(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                              const int32_t* order, const MtgpJitChain* chain, int32_t unit, uint32_t* out,
-                             int32_t max_words);
+                             int32_t max_words, int32_t jit_mode);
 /* host translation of one program (tests/tooling): number of code words, or < 0 */
 int mtgp_jit_translate_host(const MtgpInstr* prog, int32_t L, uint32_t* out, int32_t max_words);
 /* the same in either JIT mode (MTGP_JIT_MODE_*), for one program and for one unit */

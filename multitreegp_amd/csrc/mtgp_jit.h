@@ -331,7 +331,14 @@ constexpr uint32_t kSelHi = 0x00aa1119u;
 // s46 != 0 and returns otherwise; the unit after it (the save-point readout) then leaves its
 // result in v8 as a plain unit does.  Per chained call one fetch redirect replaces a return + a
 // call (two), and the call-site bookkeeping of the extra calls disappears.
+//
+// LDS store chains (ABI v14, chain.store = S > 0; the wide-state SR kernel in LDS-data mode):
+// every unit j ends with `ds_write_b32 v1, v8 offset:j*256` -- its result into the caller's LDS
+// output vector, v1 = that vector's slot-0 address -- and falls through into unit j + 1 unless
+// j + 1 is a multiple of S (or the last program): the S components a wave owns are one call.
 constexpr int kJitChainOut = 26, kJitChainMax = 4;
+constexpr uint32_t kDsWriteV1V8 = 0xd81a0000u;  // ds_write_b32 v1, v8 (word 0; | offset)
+constexpr uint32_t kDsWriteV1V8Hi = 0x00000801u;
 constexpr uint32_t kCmpS46Zero = 0xbf06802eu;  // s_cmp_eq_u32 s46, 0
 constexpr uint32_t kBranchScc0Skip1 = 0xbf840001u;  // s_cbranch_scc0 +1 (over the s_setpc)
 
@@ -343,8 +350,23 @@ MTGP_JIT_HD inline int jit_chain_pos(uint32_t next, int j) {
   return k;
 }
 
+// unit j of an LDS store chain falls through into unit j + 1
+MTGP_JIT_HD inline bool jit_store_cont(uint32_t store, int n_prog, int j) {
+  return store > 0u && ((uint32_t)(j + 1) % store) != 0u && j + 1 < n_prog;
+}
+
 // the end of unit j: s_setpc (plain unit), or the chain epilogue
-MTGP_JIT_HD inline void jit_unit_end(JitOut& o, uint32_t next, uint32_t cond, int j) {
+MTGP_JIT_HD inline void jit_unit_end(JitOut& o, uint32_t next, uint32_t cond, int j, uint32_t store = 0u,
+                                     int n_prog = 0) {
+  if (store > 0u) {  // LDS store chain
+    o.w(kDsWriteV1V8 | ((uint32_t)j * (uint32_t)MTGP_SLOT_BYTES & 0xffffu));
+    o.w(kDsWriteV1V8Hi);
+    if (!jit_store_cont(store, n_prog, j)) {
+      o.w(kWaitLgkm0);
+      o.w(kSetpcS30);
+    }
+    return;
+  }
   if (j >= 32) { o.w(kSetpcS30); return; }  // chains cover the first 32 programs
   const bool cont = (next >> j) & 1u;
   const bool after = j > 0 && ((next >> (j - 1)) & 1u);
@@ -362,19 +384,22 @@ MTGP_JIT_HD inline void jit_unit_end(JitOut& o, uint32_t next, uint32_t cond, in
 }
 
 // words of the end of unit j (jit_unit_end)
-MTGP_JIT_HD inline int jit_unit_end_words(uint32_t next, uint32_t cond, int j) {
+MTGP_JIT_HD inline int jit_unit_end_words(uint32_t next, uint32_t cond, int j, uint32_t store = 0u, int n_prog = 0) {
   JitOut o{nullptr, 0};
-  jit_unit_end(o, next, cond, j);
+  jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
 }
 
-// unit j is laid out right after unit j - 1 (no alignment padding in between)
-MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j) { return j < 32 && ((next >> j) & 1u) != 0u; }
+// unit j falls through into unit j + 1, which is laid out right behind it (no alignment padding)
+MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j, uint32_t store = 0u, int n_prog = 0) {
+  if (store > 0u) return jit_store_cont(store, n_prog, j);
+  return j < 32 && ((next >> j) & 1u) != 0u;
+}
 
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
                                 int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
-                                uint32_t next = 0u, uint32_t cond = 0u) {
+                                uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u) {
   JitOut o{out, 0};
   o.base = base;
   for (int g = 0; g < G; ++g) {
@@ -394,7 +419,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
       o.w(kSelHi);
     }
   }
-  jit_unit_end(o, next, cond, j);
+  jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
 }
 
@@ -403,7 +428,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
 // s_setpc when `last`.  jit_unit == the concatenation of its groups.
 MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
                                       int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
-                                      uint32_t next = 0u, uint32_t cond = 0u) {
+                                      uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u) {
   JitOut o{out, 0};
   o.base = base;
   const int q = q0 + g;
@@ -420,7 +445,7 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
     o.w(kSelLo);
     o.w(kSelHi);
   }
-  if (last) jit_unit_end(o, next, cond, j);
+  if (last) jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
 }
 

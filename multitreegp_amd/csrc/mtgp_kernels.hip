@@ -22,6 +22,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <atomic>
+#include <cstring>
 #include <mutex>
 #include <type_traits>
 #include "mtgp.h"
@@ -269,6 +270,7 @@ struct KArgs {
   uint64_t jit_cap;         // bytes of the code buffer
   int32_t chain_state;      // the JIT code chains the state role (MtgpJitChain): one call per stage
   int32_t chain_save;       // ... and continues it into the save-point readout on request (s46)
+  int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
 };
 
 // per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
@@ -832,9 +834,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 
   const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
   const int n_stages = euler ? 1 : 4;
+  int save_k = 0, save_ctr = 0;  // save index / steps since the last save (no per-step division)
   for (int step = 0;; ++step) {
     const bool last = step == n_steps;
-    const bool is_save = (step % save_every) == 0;
+    const bool is_save = save_ctr == 0;
+    const int ksave = save_k;
+    if (++save_ctr == save_every) {
+      save_ctr = 0;
+      ++save_k;
+    }
     bool stop = last;
 #if MTGP_V_UNROLL
 #pragma unroll
@@ -865,14 +873,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       // observation needs its own noise draw (ts[k] off the step grid)
       bool redraw = false;
       if (NOISE && stage == 0 && is_save)
-        redraw = __float_as_uint(A.ro.ts[step / save_every]) != __float_as_uint(t0 + (float)step * h);
+        redraw = __float_as_uint(A.ro.ts[ksave]) != __float_as_uint(t0 + (float)step * h);
       const bool save_chain = JIT && A.chain_save && stage == 0 && is_save && diff_mask != 0 && !redraw;
       float us_chain = u;
       run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0,
                         save_chain ? A.m.prog_readout_save : -1, &us_chain);
       if (stage == 0) {
         if (is_save) {
-          const int k = step / save_every;
+          const int k = ksave;
           float us = u;
           if (NOISE && redraw) {
             ctl_obs<Env, true>(nzc, A.ro.ts[k], x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
@@ -983,9 +991,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 
   const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
   const int n_stages = euler ? 1 : 4;
+  int save_k = 0, save_ctr = 0;  // save index / steps since the last save (no per-step division)
   for (int step = 0;; ++step) {
     const bool last = step == n_steps;
-    const bool is_save = (step % save_every) == 0;
+    const bool is_save = save_ctr == 0;
+    const int ksave = save_k;
+    if (++save_ctr == save_every) {
+      save_ctr = 0;
+      ++save_k;
+    }
     bool stop = last;
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
@@ -1004,7 +1018,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       env.drift(xt, u, kx);
       if (stage == 0) {
         if (is_save) {
-          const int k = step / save_every;
+          const int k = ksave;
           if (NOISE) {
             const float tsk = A.ro.ts[k];
             if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
@@ -1540,6 +1554,21 @@ __device__ __forceinline__ float jit_call_lds(uint64_t addr_, uint32_t lds_addr,
   return acc;
 }
 
+// Call an LDS store chain (mtgp_jit.h, ABI v14): the wave's components' programs back to back, each
+// result written to the output vector at v1 (slot j at + j * 256 B); the chain waits for its
+// writes before returning.
+__device__ __forceinline__ void jit_call_lds_store(uint64_t addr_, uint32_t lds_in, uint32_t lds_out, uint64_t& flag) {
+  const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr_ >> 32)) << 32;
+  asm volatile("s_swappc_b64 s[30:31], %[tgt]"
+               : "+{s[32:33]}"(flag)
+               : [tgt] "s"(addr), "{v0}"(lds_in), "{v1}"(lds_out)
+               : "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
+                 "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",
+                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "s30", "s31", "s34", "s35",
+                 "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "scc", "memory");
+}
+
 // LDS byte address of a pointer into shared memory
 __device__ __forceinline__ uint32_t lds_address(const float* p) {
   return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)p;
@@ -1631,7 +1660,22 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; k parks in nxt
-      if (JIT && Ln.jok) {  // one JIT unit call per component: the G groups' programs back to back
+      if (JIT && Ln.jok && A.chain_store) {  // one call: this wave's components' units, results into nxt
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c0);
+        uint64_t fl = 0;
+        jit_call_lds_store(A.jit_base + off, lds_address(cur), lds_address(nxt), fl);
+        if (__builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: interpret those groups
+          for (int t = 0; t < kWideComp; ++t) {
+            const int c = c0 + t;
+            if (c >= NV) break;
+            for (int gi = 0; gi < ng; ++gi) {
+              if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
+              const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, cur, st);
+              if (Ln.g == gi) nxt[c * kWave] = tv;
+            }
+          }
+        }
+      } else if (JIT && Ln.jok) {  // one JIT unit call per component: the G groups' programs back to back
         const uint32_t la = lds_address(cur);
         for (int t = 0; t < kWideComp; ++t) {
           const int c = c0 + t;
@@ -1723,7 +1767,24 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
 
   // this wave's trees on stage vector `in` -> kx (the G groups' programs, JIT or interpreted)
   auto rhs = [&](const float* in, float* kx) __attribute__((always_inline)) {
-    if (JIT && Ln.jok) {
+    if (JIT && Ln.jok && A.chain_store) {  // one call: results into the reduction vector, read back
+      const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c0);
+      uint64_t fl = 0;
+      jit_call_lds_store(A.jit_base + off, lds_address(in), lds_address(red), fl);
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) kx[t] = (c0 + t < NV) ? red[(c0 + t) * kWave] : 0.0f;
+      if (__builtin_expect(fl != 0, 0)) {
+        for (int t = 0; t < kWideComp; ++t) {
+          const int c = c0 + t;
+          if (c >= NV) break;
+          for (int gi = 0; gi < ng; ++gi) {
+            if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
+            const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, in, st);
+            kx[t] = (Ln.g == gi) ? tv : kx[t];
+          }
+        }
+      }
+    } else if (JIT && Ln.jok) {
       const uint32_t la = lds_address(in);
 #pragma unroll
       for (int t = 0; t < kWideComp; ++t) {
@@ -2177,6 +2238,290 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
   if (c != 0) atomicAdd(&nodes_out[p], c);
 }
 
+// Flatten, one WAVE per (individual, program spec): lane l owns rows l, l + 64, ... (NMAX / 64 per
+// lane), loaded with one coalesced 1-KB read per 64 rows.  The same two passes as k_flatten, but
+// level-synchronous over the tree instead of serial over the rows:
+//   pass 1: a row resolves (record, lengths, folded constant; mtgp_flatten_uniform.h) in the first
+//     round after its operand rows (j < i) have resolved -- rounds = the height of the dependency
+//     DAG, not N;
+//   pass 2: a reached row emits its word at the postorder position its parent assigned and
+//     assigns its children's -- rounds = the tree height.  A row reached twice (LDS atomic reach
+//     counter; only in arbitrary arrays) leaves the program to k_flatten_serial.
+// The tables are per wave in LDS (24 B per row), so the occupancy no longer falls with N (the
+// lane-per-tree kernel needs 16 B x N per LANE).  Output = k_flatten's word for word.
+template <int NMAX>
+__global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
+                                                     MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
+                                                     int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
+                                                     int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
+                                                     int32_t* jit_cost_out, int jit_mode) {
+  using namespace mtgp;
+  constexpr int RPL = NMAX / kWave;  // rows per lane
+  __shared__ uint32_t s_w[NMAX];   // packed row record (u_pack)
+  __shared__ uint32_t s_len[NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
+  __shared__ float s_cv[NMAX];     // folded constant
+  __shared__ float s_val[NMAX];    // the original value column (operands j >= i, gp.py:366-369)
+  __shared__ int32_t s_pos[NMAX];  // pass 2: first word of the node's code | push << 16
+  __shared__ uint32_t s_flag[NMAX];  // pass 1: resolved; pass 2: times reached
+  __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
+  __shared__ MtgpInstr s_prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
+  const int lane = threadIdx.x;
+  for (int k = lane; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
+  const long pj = blockIdx.x;
+  if (pj >= (long)P * n_prog) return;  // (uniform: one wave per block)
+  const int p = (int)(pj / n_prog), j = (int)(pj % n_prog);
+  const MtgpProgramSpec sp = specs[j];
+  const float4* tr = reinterpret_cast<const float4*>(pop + ((size_t)p * T + sp.tree) * N * 4);
+  MtgpInstr* out = prog_out + (size_t)pj * L;
+  const int cap = L - 1;
+  const int n_funcs = lib.n_funcs, var_start = lib.var_start, n_data = sp.n_data;
+  const uint64_t zmask = sp.zero_mask;
+  float4 row[RPL];
+  int cnt = 0;  // non-empty rows of this tree (gp.py:424)
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    const int i = k * kWave + lane;
+    row[k] = i < N ? tr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    s_val[i] = row[k].w;
+    cnt += __popcll(__ballot(i < N && row[k].x != 0.0f));
+  }
+  auto operand = [&](int jj, int i, uint32_t& w, ULeaf& lf, int& len, int& flen, bool& leaf) {
+    if (jj < i) {
+      w = s_w[jj];
+      const uint32_t ln = s_len[jj];
+      len = (int)(ln & 0xffffu);
+      flen = (int)(ln >> 16);
+      lf.isc = u_isc(w);
+      lf.v = s_cv[jj];
+      lf.slot = u_slot(w);
+      leaf = u_leaf(w);
+    } else {
+      w = u_pack(K_CONST, 0, 0, 1, 1, 0);
+      lf.isc = true;
+      lf.v = s_val[jj];
+      lf.slot = 0;
+      len = flen = 1;
+      leaf = true;
+    }
+  };
+  // ---- pass 1, round 0: leaves and empty rows resolve at once; operator rows note their operands
+  int fnr[RPL], ja[RPL], jb[RPL];
+  bool done[RPL];
+#pragma unroll
+  for (int k = 0; k < RPL; ++k) {
+    const int i = k * kWave + lane;
+    fnr[k] = -1;
+    ja[k] = jb[k] = -1;
+    done[k] = true;
+    if (i >= N) continue;
+    uint32_t kind = K_CONST, slot = 0, isc = 1;
+    float cv = 0.0f;
+    if (row[k].x == 1.0f) {  // coefficient (gp.py:372 select)
+      cv = row[k].w;
+    } else {
+      int32_t f = f2i_sat(row[k].x);
+      f = f < 0 ? 0 : (f > n_funcs - 1 ? n_funcs - 1 : f);
+      const int fn = s_fn[f];
+      if (fn == MTGP_FN_VAR) {
+        int sl = f - var_start;
+        if (sl > n_data - 1) sl = n_data - 1;
+        slot = (uint32_t)sl;
+        if (!((zmask >> sl) & 1ull)) { kind = K_VAR; isc = 0; }
+      } else if (fn_arity(fn) > 0) {
+        fnr[k] = fn;
+        ja[k] = norm_index(row[k].y, N);
+        if (fn_arity(fn) == 2) jb[k] = norm_index(row[k].z, N);
+        done[k] = false;
+      }  // else: empty node (gp.py:135) -> +0.0
+    }
+    if (done[k]) {
+      s_w[i] = u_pack(kind, MTGP_FN_ZERO, slot, isc, 1, 0);
+      s_len[i] = 1u | 1u << 16;
+      s_cv[i] = cv;
+    }
+    s_flag[i] = done[k] ? 1u : 0u;
+  }
+  // ---- pass 1, later rounds: an operator row resolves once its operand rows (j < i) have
+  for (;;) {
+    __syncthreads();
+    bool ready[RPL], pend = false;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const int i = k * kWave + lane;
+      ready[k] = !done[k] && (ja[k] >= i || s_flag[ja[k]] != 0u) && (jb[k] < 0 || jb[k] >= i || s_flag[jb[k]] != 0u);
+      pend = pend || (!done[k] && !ready[k]);
+    }
+    bool any_ready = false;
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) any_ready = any_ready || ready[k];
+    if (!__any(any_ready)) break;  // (a DAG: some row is always ready while any is pending)
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      if (!ready[k]) continue;
+      const int i = k * kWave + lane;
+      const int fn = fnr[k], ar = fn_arity(fn);
+      uint32_t kind = ar == 1 ? K_UNARY : K_BINARY, isc = 1, afirst = 1, need = 0;
+      int len = 1, flen = 1;
+      float cv = 0.0f;
+      uint32_t wa, wb = 0;
+      ULeaf la, lb;
+      lb.isc = true; lb.v = 0.0f; lb.slot = 0;
+      int lena, flena, lenb = 1, flenb = 1;
+      bool leafa, leafb = true;
+      operand(ja[k], i, wa, la, lena, flena, leafa);
+      if (ar == 2) operand(jb[k], i, wb, lb, lenb, flenb, leafb);
+      if (la.isc && lb.isc) {  // constant subtree: folded with the kernel's fp32 primitives
+        cv = apply_fn(fn, la.v, ar == 1 ? 0.0f : lb.v);
+      } else {
+        isc = 0;
+        if (ar == 1) {
+          if (leafa) { len = 2; flen = 1; }
+          else { len = lena + 1; flen = flena + 1; need = u_need(wa); }
+        } else if (leafa && leafb) {
+          len = 2; flen = 1;
+        } else if (leafb) {
+          len = lena + 1; flen = flena + 1; need = u_need(wa);
+        } else if (leafa) {
+          len = lenb + 1; flen = flenb + 1; need = u_need(wb);
+        } else {
+          const uint32_t pa = u_need(wa), qb = u_need(wb);
+          len = lena + lenb + 1;
+          flen = flena + flenb + 1;
+          if (pa >= qb) { afirst = 1; need = pa > qb + 1 ? pa : qb + 1; }
+          else { afirst = 0; need = qb > pa + 1 ? qb : pa + 1; }
+        }
+      }
+      s_w[i] = u_pack(kind, (uint32_t)fn, 0, isc, afirst, need > 31u ? 31u : need);
+      s_len[i] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
+      s_cv[i] = cv;
+    }
+    __syncthreads();  // every read of this round's flags precedes the new ones
+#pragma unroll
+    for (int k = 0; k < RPL; ++k)
+      if (ready[k]) {
+        s_flag[k * kWave + lane] = 1u;
+        done[k] = true;
+      }
+    (void)pend;
+  }
+  const uint32_t wr = s_w[N - 1], lr = s_len[N - 1];
+  int n;
+  if ((int)u_need(wr) > MTGP_STACK_MAX) n = -MTGP_ERR_STACK;
+  else if ((int)(lr & 0xffffu) > cap) n = -MTGP_ERR_PROG_TOO_LONG;
+  else n = (int)(lr >> 16);
+  // ---- pass 2: postorder positions top-down, one word per reached node, one level per round
+  bool shared = false;
+  if (n > 0) {
+    if (u_leaf(wr)) {  // the whole tree is one leaf
+      if (lane == 0) {
+        ULeaf x;
+        x.isc = u_isc(wr); x.v = s_cv[N - 1]; x.slot = u_slot(wr);
+        out[0] = s_prog[0] = u_load(x, false);
+      }
+    } else {
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) s_flag[k * kWave + lane] = 0u;
+      __syncthreads();
+      if (lane == 0) {
+        s_flag[N - 1] = 1u;
+        s_pos[N - 1] = 0;
+      }
+      bool emitted[RPL];
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) emitted[k] = false;
+      for (;;) {
+        __syncthreads();
+        bool go[RPL], any = false;
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+          const int i = k * kWave + lane;
+          go[k] = i < N && !emitted[k] && s_flag[i] != 0u;
+          any = any || go[k];
+        }
+        if (!__any(any)) break;
+        __syncthreads();  // every row's go decision precedes this round's visits
+#pragma unroll
+        for (int k = 0; k < RPL; ++k) {
+          if (!go[k]) continue;
+          emitted[k] = true;
+          const int i = k * kWave + lane;
+          const uint32_t w = s_w[i];
+          const int pp = s_pos[i], pos = pp & 0xffff;
+          const bool push = (pp >> 16) != 0;
+          const int fn = (int)u_fn(w);
+          uint32_t wa, wb;
+          ULeaf la, lb;
+          int lena, flena, lenb = 1, flenb = 1;
+          bool leafa, leafb = true;
+          const int ca = ja[k];
+          operand(ca, i, wa, la, lena, flena, leafa);
+          const int cb = u_kind(w) == K_BINARY ? jb[k] : 0;
+          if (u_kind(w) == K_BINARY) operand(cb, i, wb, lb, lenb, flenb, leafb);
+          auto visit = [&](int c, int cpos, bool cpush) {
+            s_pos[c] = cpos | (cpush ? 1 << 16 : 0);
+            shared = shared || atomicAdd(&s_flag[c], 1u) != 0u;  // a sub-DAG reached twice
+          };
+          MtgpInstr x;
+          auto emit = [&](int at, const MtgpInstr& v) {
+            out[at] = v;
+            s_prog[at] = v;
+          };
+          if (u_kind(w) == K_UNARY) {
+            const MtgpInstr un = u_instr(fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
+            if (leafa) { fuse_pair(u_load(la, push), un, &x); emit(pos, x); }
+            else { visit(ca, pos, push); emit(pos + flena, un); }
+          } else if (leafa && leafb) {
+            fuse_pair(u_load(la, push), u_op_leaf(fn, 0, lb), &x);
+            emit(pos, x);
+          } else if (leafb) {
+            visit(ca, pos, push);
+            emit(pos + flena, u_op_leaf(fn, 0, lb));
+          } else if (leafa) {
+            visit(cb, pos, push);
+            emit(pos + flenb, u_op_leaf(fn, 1, la));
+          } else {
+            const bool af = u_afirst(w) != 0;
+            const int f1 = af ? flena : flenb, f2 = af ? flenb : flena;
+            visit(af ? ca : cb, pos, push);
+            visit(af ? cb : ca, pos + f1, true);
+            emit(pos + f1 + f2, u_op_stack(fn, af ? 1 : 0));
+          }
+        }
+      }
+    }
+  }
+  shared = __any(shared);
+  __syncthreads();  // every lane's program words (LDS copy) precede the END and the JIT sizing
+  if (lane == 0) {
+    if (shared) {  // arbitrary arrays only: the serial walk duplicates the shared subtree
+      len_out[pj] = 0;
+      status_out[pj] = kFlatSerial;
+    } else {
+      MtgpInstr e;
+      e.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+      e.imm = 0.0f;
+      out[n > 0 ? n : 0] = e;
+      s_prog[n > 0 ? n : 0] = e;
+      len_out[pj] = n > 0 ? n : 0;
+      status_out[pj] = n > 0 ? 0 : -n;
+      flat_jit_size(s_prog, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
+    }
+  }
+  // node count (gp.py:424 parsimony): tree t of the individual is counted by its program t % n_prog
+  int c = 0;
+  for (int t = j; t < T; t += n_prog) {
+    if (t == sp.tree) { c += cnt; continue; }
+    const float4* tt = reinterpret_cast<const float4*>(pop + ((size_t)p * T + t) * N * 4);
+#pragma unroll
+    for (int k = 0; k < RPL; ++k) {
+      const int i = k * kWave + lane;
+      c += __popcll(__ballot(i < N && tt[i < N ? i : 0].x != 0.0f));
+    }
+  }
+  if (lane == 0 && c != 0) atomicAdd(&nodes_out[p], c);
+}
+
 // --------------------------------------------------------------------------------------
 // Schedule: counting sort of per-individual interpreter cost, then a slot permutation.
 struct SchedW {
@@ -2247,13 +2592,13 @@ struct JitUnitArgs {
   int n_prog, L, P, G, Rp, n_units;
   const int32_t* order;
   int mode;  // mtgp_jit.h kJitModeRegs / kJitModeLds
-  uint32_t next, cond;  // role chains (MtgpJitChain, mtgp_jit.h jit_unit_end)
+  uint32_t next, cond, store;  // role / LDS store chains (MtgpJitChain, mtgp_jit.h jit_unit_end)
 };
 
 __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
   return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out, base, mtgp::kJitModeRegs,
-                        U.next, U.cond);
+                        U.next, U.cond, U.store);
 }
 
 // byte span of unit u in the layout: a unit that falls through into the next one (a chain member)
@@ -2262,7 +2607,7 @@ __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint3
 // unit that is called starts on one
 __device__ __forceinline__ uint32_t jit_unit_span(const JitUnitArgs& U, int u, int words, uint32_t pre = 0u) {
   const int j = u % U.n_prog;
-  if (mtgp::jit_unit_packed(U.next, j)) return (uint32_t)words * 4u;
+  if (mtgp::jit_unit_packed(U.next, j, U.store, U.n_prog)) return (uint32_t)words * 4u;
   return ((pre + (uint32_t)words * 4u + kJitAlign - 1u) & ~(kJitAlign - 1u)) - pre;
 }
 
@@ -2331,7 +2676,7 @@ __global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t*
 // offsets.  Replaces the k_jit_count translation pass + k_jit_scan.
 __device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const int32_t* __restrict__ jw, int u) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
-  int n = mtgp::jit_unit_end_words(U.next, U.cond, j);  // s_setpc_b64 or the chain epilogue
+  int n = mtgp::jit_unit_end_words(U.next, U.cond, j, U.store, U.n_prog);  // s_setpc_b64 or the chain epilogue
   for (int g = 0; g < U.G; ++g) {
     const int q = wave * U.G + g;
     if (q >= U.P) break;
@@ -2351,7 +2696,7 @@ __global__ void __launch_bounds__(256) k_jit_sizes(JitUnitArgs U, const int32_t*
   const int n = jit_unit_words_from(U, jw, u);
   uint32_t pre = 0u;  // the chain members packed in front of this unit
   int bad = 0;
-  for (int v = u - 1; v >= 0 && v / U.n_prog == u / U.n_prog && mtgp::jit_unit_packed(U.next, v % U.n_prog); --v) {
+  for (int v = u - 1; v >= 0 && v / U.n_prog == u / U.n_prog && mtgp::jit_unit_packed(U.next, v % U.n_prog, U.store, U.n_prog); --v) {
     const int m = jit_unit_words_from(U, jw, v);
     if (m < 0) bad = m;
     else pre += (uint32_t)m * 4u;
@@ -2436,7 +2781,7 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
   const uint32_t at = b + start * 4u;
   mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode,
-                       U.next, U.cond);
+                       U.next, U.cond, U.store);
 }
 
 // the shared sin/cos subroutines at the start of the code buffer
@@ -2459,7 +2804,7 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
   U.G = kWave / Rp;
   U.order = order;
   U.mode = mtgp::kJitModeRegs;
-  U.next = U.cond = 0u;
+  U.next = U.cond = U.store = 0u;
   const long waves = ((long)P + U.G - 1) / U.G;
   if (waves * n_prog > INT32_MAX - 1) return false;
   U.n_units = (int)(waves * n_prog);
@@ -2471,11 +2816,14 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
 // register-resident SR) as one chain when M >= 2, continued into the save-point readout when the
 // fixed-step dynamic kernel can use it (the readout_save program right after the state programs).
 MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
-  MtgpJitChain c{0u, 0u};
+  MtgpJitChain c{0u, 0u, 0u};
   int first = m.prog_state, M = 0;
   bool save = false;
   if (m.model == MTGP_MODEL_SR) {
-    if (m.n_var > 4) return c;  // the wide-state kernel (LDS-data code) calls one program at a time
+    if (m.n_var > 4) {  // the wide-state kernels: one LDS store chain per wave (its kWideComp components)
+      if (m.prog_state == 0 && n_prog >= m.n_var) c.store = (uint32_t)kWideComp;
+      return c;
+    }
     M = m.n_var;
   } else if (m.model == MTGP_MODEL_DYNAMIC) {
     M = m.state_size;
@@ -2768,7 +3116,7 @@ int mtgp_jit_plan_words_chain(const int32_t* jit_words, int32_t P, int32_t n_pro
   JitUnitArgs U;
   static const MtgpInstr dummy = {0u, 0.0f};
   if (!jit_words || !offsets_out || !info_out || !jit_unit_args(&dummy, P, n_prog, 1, R, order, U)) return MTGP_ERR_ARG;
-  if (chain) { U.next = chain->next; U.cond = chain->cond; }
+  if (chain) { U.next = chain->next; U.cond = chain->cond; U.store = chain->store; }
   hipStream_t s = (hipStream_t)stream;
   if (U.n_units == 0) {
     if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
@@ -2796,8 +3144,10 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   U.mode = jit_mode;
   if (chain) {
     if (jit_mode != mtgp::kJitModeRegs && (chain->next | chain->cond) != 0u) return MTGP_ERR_ARG;  // v26.. are preloads
+    if (jit_mode != mtgp::kJitModeLds && chain->store != 0u) return MTGP_ERR_ARG;  // store chains: LDS-data code
     U.next = chain->next;
     U.cond = chain->cond;
+    U.store = chain->store;
   }
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -2832,31 +3182,32 @@ int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t
 
 static int jit_unit_host_impl(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                               const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode,
-                              uint32_t next, uint32_t cond) {
+                              uint32_t next, uint32_t cond, uint32_t store) {
   JitUnitArgs U;
   if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
   if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   const int wave = unit / n_prog, j = unit - wave * n_prog;
   const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes, jit_mode,
-                               next, cond);
+                               next, cond, store);
   if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
   if (out) {
     if (n > max_words) return MTGP_ERR_ARG;
-    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode, next, cond);
+    mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode, next, cond,
+                   store);
   }
   return n;
 }
 
 int mtgp_jit_unit_host_ex(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
                           int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode) {
-  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, jit_mode, 0u, 0u);
+  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, jit_mode, 0u, 0u, 0u);
 }
 
 int mtgp_jit_unit_host_chain(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                              const int32_t* order, const MtgpJitChain* chain, int32_t unit, uint32_t* out,
-                             int32_t max_words) {
-  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, mtgp::kJitModeRegs,
-                            chain ? chain->next : 0u, chain ? chain->cond : 0u);
+                             int32_t max_words, int32_t jit_mode) {
+  return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, jit_mode, chain ? chain->next : 0u,
+                            chain ? chain->cond : 0u, chain ? chain->store : 0u);
 }
 
 int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
@@ -2912,6 +3263,11 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
     const int v = e ? atoi(e) : MTGP_FLAT_LANES;
     return (v == 8 || v == 16 || v == 32) ? v : MTGP_FLAT_LANES;
   }();
+  // one wave per program (k_flatten_wave, default) or one lane per program (k_flatten): A/B knob
+  // MTGP_FLAT_MODE=lane at run time
+  const char* fm = getenv("MTGP_FLAT_MODE");
+  const bool wave_mode = !(fm && strcmp(fm, "lane") == 0);
+  if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
 #define MTGP_FLAT_ONE(NM, TP)                                                                                 \
   hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
                      T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
@@ -2919,10 +3275,14 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
 #define MTGP_FLAT_LAUNCH(NM)                                                                                \
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
-    if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                                    \
+    if (wave_mode)                                                                                          \
+      hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)total), dim3(kWave), 0, s, population, P, T, N, \
+                         libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,  \
+                         jit_cost_out, jit_mode);                                                           \
+    else if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                               \
     else if (tp >= 16) MTGP_FLAT_ONE(NM, 16);                                                               \
     else MTGP_FLAT_ONE(NM, 8);                                                                              \
-    hipLaunchKernelGGL(k_flatten_serial<NM>, dim3((unsigned)(total < 64 * 64 ? (total + 63) / 64 : 64)),   \
+    hipLaunchKernelGGL(k_flatten_serial<NM>, dim3((unsigned)(total < 256 * 64 ? (total + 63) / 64 : 256)), \
                        dim3(64), 0, s, population, P, T, N, libv, specs, n_prog, L, prog_out, len_out,     \
                        status_out, jit_words_out, jit_cost_out, jit_mode);                                  \
   } while (0)
@@ -3026,12 +3386,14 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   A.jit_off = jit ? jitc->offsets : nullptr;
   A.jit_info = jit ? jitc->info : nullptr;
   A.jit_cap = jit ? jitc->capacity : 0;
-  A.chain_state = A.chain_save = 0;
-  if (jit && (jitc->chain.next | jitc->chain.cond) != 0u) {  // chained code: must be the chain this model calls
+  A.chain_state = A.chain_save = A.chain_store = 0;
+  if (jit && (jitc->chain.next | jitc->chain.cond | jitc->chain.store) != 0u) {  // must be the chain this model calls
     const MtgpJitChain want = jit_chain_for(*model, n_prog);
-    if (want.next != jitc->chain.next || want.cond != jitc->chain.cond) return MTGP_ERR_ARG;
-    A.chain_state = 1;
+    if (want.next != jitc->chain.next || want.cond != jitc->chain.cond || want.store != jitc->chain.store)
+      return MTGP_ERR_ARG;
+    A.chain_state = (want.next | want.cond) != 0u;
     A.chain_save = want.cond != 0u;
+    A.chain_store = want.store != 0u;
   }
   // (the wide-state SR kernel keeps its data vector in LDS: its code is built in kJitModeLds)
   hipStream_t s = (hipStream_t)stream;

@@ -111,8 +111,8 @@ class DeviceEngine:
         without a host round trip: the buffer is sized from the code size per program seen in
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
-        chain = self.jit_chain(m, fl.n_prog) if fl.jit_words is not None else nat.MtgpJitChain(0, 0)
-        key = (R, None if order is None else order.data_ptr(), id(self), (chain.next, chain.cond))
+        chain = self.jit_chain(m, fl.n_prog) if fl.jit_words is not None else nat.MtgpJitChain(0, 0, 0)
+        key = (R, None if order is None else order.data_ptr(), id(self), (chain.next, chain.cond, chain.store))
         if fl.jit_key is not None and fl.jit_key[:4] == key:
             slot, gen = fl.jit_key[4:]
             if slot is None or self._arena_gen[slot] == gen:  # code still in place (or none was built)
@@ -167,8 +167,8 @@ class DeviceEngine:
     def jit_chain(self, m, n_prog: int) -> "nat.MtgpJitChain":
         """The role chain the evaluator of model struct `m` calls (mtgp_jit_chain); none when
         MTGP_JIT_CHAIN=0 (A/B switch) or in LDS-data mode."""
-        ch = nat.MtgpJitChain(0, 0)
-        if os.environ.get("MTGP_JIT_CHAIN", "1") == "0" or self._jit_mode() != nat.JIT_MODE_REGS:
+        ch = nat.MtgpJitChain(0, 0, 0)
+        if os.environ.get("MTGP_JIT_CHAIN", "1") == "0":
             return ch
         rc = self.native.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch))
         if rc != nat.OK:

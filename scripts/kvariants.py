@@ -26,10 +26,15 @@ def main():
     ap.add_argument("--ode-steps", type=int, default=200)
     ap.add_argument("--no-traj", action="store_true")
     ap.add_argument("--tag", default="")
+    ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
+    ap.add_argument("--reflatten", action="store_true", help="flatten inside every timed evaluation (A/B of the "
+                                                              "flattener; default: flatten once)")
     ap.add_argument("--order", default="orig", help="orig | pair (long with short) | sorted (host reorder)")
     ap.add_argument("--no-schedule", action="store_true", help="disable the device schedule (mtgp_schedule)")
     a = ap.parse_args()
-    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config="c3", solver="rk4",
+    if a.config != "c3" and a.pop == 8192 and a.rollouts == 32:  # the config's own sizes
+        a.pop, a.rollouts = {"c2": (1024, 16), "c5": (4096, 8)}[a.config]
+    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config=a.config, solver="rk4",
                                obs_noise=0.0)
     env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
     dev = torch.device("cuda", 0)
@@ -45,6 +50,7 @@ def main():
         engines[v].native.mtgp_set_timing(1)
     pop_dev = torch.from_numpy(pop).to(dev)
     first = next(iter(engines.values()))
+    first.prepare_data(data)  # (SR learns n_var from the data)
     fl = first.flatten(pop_dev)
     if a.order != "orig":
         cost = fl.plen.sum(dim=1).cpu().numpy()
@@ -64,7 +70,8 @@ def main():
             os.environ.update(envs[v])
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
-            res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=fl, check=False,
+            res = eng.evaluate(pop_dev, data, trajectories=not a.no_traj, flattened=None if a.reflatten else fl,
+                               check=False,
                                schedule=not a.no_schedule)
             e1.record()
             for k, x in old.items():

@@ -124,9 +124,12 @@ def test_word_based_jit_plan_and_emit_match_translation(kind, R):
     assert int((bufs[1] != 0).sum()) > size // 16
 
 
+@pytest.mark.parametrize("store", [0, 8])
 @pytest.mark.parametrize("R", [8, 64])
-def test_lds_mode_units_match_host_units(R):
-    """LDS-data mode (wide-state SR): the device-built units equal the host-built ones word for word."""
+def test_lds_mode_units_match_host_units(R, store):
+    """LDS-data mode (wide-state SR): the device-built units equal the host-built ones word for word,
+    plain or as LDS store chains (ABI v14: groups of 8 units packed back to back, each group ending
+    on a 64-byte line)."""
     import torch
     lib, pop, specs = _population("sr12", 129, seed=R)
     P, T, N, _ = pop.shape
@@ -139,24 +142,30 @@ def test_lds_mode_units_match_host_units(R):
     n = L_.mtgp_jit_units(P, n_prog, R)
     offs = torch.empty((n + 1,), dtype=torch.int32, device="cuda")
     info = torch.zeros((2,), dtype=torch.int32, device="cuda")
-    assert L_.mtgp_jit_plan_words(out["jw"].data_ptr(), P, n_prog, R, order.data_ptr(), offs.data_ptr(),
-                                  info.data_ptr(), None) == 0
+    ch = nat.MtgpJitChain(0, 0, store)
+    assert L_.mtgp_jit_plan_words_chain(out["jw"].data_ptr(), P, n_prog, R, order.data_ptr(), ctypes.byref(ch),
+                                        offs.data_ptr(), info.data_ptr(), None) == 0
     torch.cuda.synchronize()
     inf = info.cpu().numpy()
     assert inf[0] == 0
     size = int(inf[1]) + 4096
     buf = torch.zeros((size // 4,), dtype=torch.int32, device="cuda")
-    assert L_.mtgp_jit_emit_words(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
-                                  offs.data_ptr(), buf.data_ptr(), size, 1, None) == 0
+    assert L_.mtgp_jit_emit_words_chain(prog.data_ptr(), out["jw"].data_ptr(), P, n_prog, L, R, order.data_ptr(),
+                                        ctypes.byref(ch), offs.data_ptr(), buf.data_ptr(), size, 1, None) == 0
     torch.cuda.synchronize()
     code = buf.cpu().numpy().view(np.uint32)
     o = offs.cpu().numpy().view(np.uint32)
     hp = prog[: P * n_prog * L * 2].cpu().numpy()
     host = np.zeros(1 << 16, np.uint32)
     for u in range(0, n, max(1, n // 97)):
-        w = L_.mtgp_jit_unit_host_ex(hp.ctypes.data, P, n_prog, L, R, order_np.ctypes.data, u, host.ctypes.data,
-                                     host.size, 1)
+        w = L_.mtgp_jit_unit_host_chain(hp.ctypes.data, P, n_prog, L, R, order_np.ctypes.data, ctypes.byref(ch), u,
+                                        host.ctypes.data, host.size, 1)
         assert w > 0
+        j = u % n_prog
+        if store and (j + 1) % store != 0 and j + 1 < n_prog:
+            assert o[u + 1] - o[u] == 4 * w, u  # the next unit of the group follows directly
+        else:
+            assert o[u + 1] % 64 == 0, u
         # the units are laid out after the templates exactly as the host lays them out (PC-relative
         # calls aside, which SR has none of): equal words
         assert np.array_equal(code[o[u] // 4: o[u] // 4 + w], host[:w]), u
@@ -205,7 +214,7 @@ def test_chained_units_match_host_units(R):
     for u in range(n):
         j = u % n_prog
         w = L_.mtgp_jit_unit_host_chain(hp.ctypes.data, P, n_prog, L, R, order_np.ctypes.data, ctypes.byref(ch), u,
-                                        host.ctypes.data, host.size)
+                                        host.ctypes.data, host.size, 0)
         assert w > 0
         if ch.next >> j & 1:
             assert o[u + 1] - o[u] == 4 * w, u  # the successor follows directly

@@ -139,7 +139,7 @@ class FellThrough(Exception):
         self.regs = regs
 
 
-def _emulate(words, data, full=False, lds=False, regs=None, s46=0):
+def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None):
     """Run emitted code on data [n_data, M] (float32 lanes, M <= 64); returns v8 (or all VGPRs).
     Honours the exec moves of per-wave units (VALU results only land in exec lanes).  lds: the
     data vector is the LDS stage vector (LDS-data mode: ds_read_b32 from v0 + slot * 256).
@@ -179,6 +179,10 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0):
             continue
         if w == 0xBF8CC07F:  # s_waitcnt lgkmcnt(0)
             i += 1
+            continue
+        if (w & 0xFFFF0000) == 0xD81A0000 and words[i + 1] == 0x00000801:  # ds_write_b32 v1, v8 offset:j*256
+            lds_out[(w & 0xFFFF) // 256] = v[8].copy()
+            i += 2
             continue
         if w == GETPC_S44:  # getpc; s_add_u32 s44, lit; s_addc_u32 s45; s_swappc_b64 s[40:41], s[44:45]
             assert words[i + 1] == 0x802CFF2C and words[i + 4] == 0xBEA81E2C, [hex(x) for x in words[i:i + 5]]
@@ -587,7 +591,7 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
         codes = {}
         for j in members:
             n = lib_n.mtgp_jit_unit_host_chain(prog.ctypes.data, P, n_prog, L, R, order.ctypes.data,
-                                               ctypes.byref(ch), wave * n_prog + j, out.ctypes.data, out.size)
+                                               ctypes.byref(ch), wave * n_prog + j, out.ctypes.data, out.size, 0)
             assert n > 0, n
             codes[j] = [int(x) for x in out[:n]]
             for ln in _disassemble(codes[j]):
@@ -623,3 +627,54 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
                     got = regs[reg, lane]
                     assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
                         (np.isnan(got) and np.isnan(want)), (wave, lane, reg, got, want)
+
+
+@pytest.mark.parametrize("R", [8, 64])
+def test_lds_store_chain_units_emulate_to_oracle(R):
+    """LDS store chains (ABI v14, the wide-state SR kernels): each unit writes its result to the
+    output vector (ds_write_b32 v1, v8 offset:j*256) and falls into the next unit except at the
+    kWideComp boundaries, where it waits and returns; one call per wave runs its components.
+    Emulated per wave, every slot written equals the oracle of its lane's own individual."""
+    lib, pop, n_data = _lds_setup()
+    ff = mt.SREvaluator(dt0=0.05)
+    ff._n_var = n_data
+    prog, specs, roles, L = _host_flatten(ff, lib, pop[:20])
+    P, n_prog = prog.shape[:2]
+    order = np.random.default_rng(6).permutation(P).astype(np.int32)
+    lib_n = nat.load()
+    m = nat.MtgpModel()
+    m.model, m.n_var, m.prog_state, m.solver = nat.MODEL_SR, n_data, 0, nat.SOLVER_RK4
+    ch = nat.MtgpJitChain()
+    assert lib_n.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0
+    assert (ch.next, ch.cond, ch.store) == (0, 0, 8)
+    Rp = 1 << max(R - 1, 0).bit_length()
+    G = 64 // Rp
+    rng = np.random.default_rng(7)
+    out = np.zeros(1 << 16, np.uint32)
+    for wave in range(-(-P // G)):
+        data = (rng.standard_normal((n_data, 64)) * 2).astype(np.float32)
+        for c0 in range(0, n_prog, 8):
+            lds_out, regs = {}, None
+            for j in range(c0, min(c0 + 8, n_prog)):
+                n = lib_n.mtgp_jit_unit_host_chain(prog.ctypes.data, P, n_prog, L, R, order.ctypes.data,
+                                                   ctypes.byref(ch), wave * n_prog + j, out.ctypes.data, out.size, 1)
+                assert n > 0, n
+                words = [int(x) for x in out[:n]]
+                last = j == min(c0 + 8, n_prog) - 1
+                assert (words[-2:] == [0xBF8CC07F, SETPC]) == last, (j, [hex(x) for x in words[-3:]])
+                try:
+                    regs = _emulate(words, data, full=True, lds=True, regs=regs, lds_out=lds_out)
+                    assert last
+                except FellThrough as e:
+                    assert not last
+                    regs = e.regs
+            assert sorted(lds_out) == list(range(c0, min(c0 + 8, n_prog)))
+            for lane in range(64):
+                q = wave * G + lane // Rp
+                if q >= P:
+                    continue
+                for j, vals in lds_out.items():
+                    want = orc.eval_tree(pop[order[q], j], lib.fn_codes, lib.n_funcs, lib.var_start, data[:, lane])
+                    got = vals[lane]
+                    assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
+                        (np.isnan(got) and np.isnan(want)), (wave, lane, j, got, want)
