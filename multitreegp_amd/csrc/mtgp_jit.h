@@ -144,7 +144,14 @@ enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJit
 // Translate one END-terminated program (at most L instructions) into o; with `ret` the END
 // becomes s_setpc_b64 s[30:31], otherwise nothing (the code falls through).  Returns kJitOk
 // or a negative kJitErr* code.
-MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs) {
+// LDS-data mode in parts (the pipelined units, jit_unit_lds): part 1 emits only the program's
+// preloads (into v[pre_base..]; *npre_out = their number), part 2 only the rest -- the wait for
+// them (s_waitcnt lgkmcnt(wait_n): later loads may stay in flight) and the body; part 0 is both.
+constexpr int kJitPreB = 44;  // the second preload register set (v44..v59) of a pipelined unit
+MTGP_JIT_HD inline uint32_t jit_wait_lgkm(int n) { return kWaitLgkm0 | (uint32_t)(n > 15 ? 15 : n) << 8; }
+
+MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs,
+                                   int part = 0, int pre_base = kJitPre, int wait_n = 0, int* npre_out = nullptr) {
   int sp = 0;
   int pre[kJitPreSlots];
   int npre = 0;
@@ -177,17 +184,21 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
         if (!have && npre < kJitPreSlots) pre[npre++] = cand[k];
       }
     }
-    for (int q = 0; q < npre; ++q) {
-      o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
-      o.w((uint32_t)(kJitPre + q) << 24 | (uint32_t)kJitLdsAddr);
+    if (npre_out) *npre_out = npre;
+    if (part != 2) {
+      for (int q = 0; q < npre; ++q) {
+        o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
+        o.w((uint32_t)(pre_base + q) << 24 | (uint32_t)kJitLdsAddr);
+      }
     }
-    if (npre > 0) o.w(kWaitLgkm0);
+    if (part == 1) return kJitOk;
+    if (npre > 0) o.w(part == 2 ? jit_wait_lgkm(wait_n) : kWaitLgkm0);
   }
   // register holding data slot s: v0-v7 (register mode) or its preload / a load at the use
   auto vslot = [&](int s_, int tmp) -> int {
     if (mode != kJitModeLds) return kJitData + s_;
     for (int q = 0; q < npre; ++q)
-      if (pre[q] == s_) return kJitPre + q;
+      if (pre[q] == s_) return pre_base + q;
     o.w(kDsReadB32 | (uint32_t)(s_ * (int)MTGP_SLOT_BYTES));
     o.w((uint32_t)tmp << 24 | (uint32_t)kJitLdsAddr);
     o.w(kWaitLgkm0);
@@ -396,18 +407,56 @@ MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j, uint32_t store = 0
   return j < 32 && ((next >> j) & 1u) != 0u;
 }
 
+// LDS-data units are software-pipelined: the preloads of group g + 1's program are issued before
+// group g's body runs (alternating register sets v26.. / v44..), so the LDS latency of one
+// program hides behind the previous one's arithmetic.  Layout: [P_0] then per group g
+// [P_(g+1)] [v_mov v25, v8 (g > 0)] [wait for P_g + body_g] [select (g > 0)]; per group the same
+// words as the plain layout (preload, wait, body), only reordered, so group g (> 0) starts
+// 2 * npre(g) words after its plain position.  Register set of group g's preloads:
+MTGP_JIT_HD inline int jit_pre_set(int g) { return (g & 1) ? kJitPreB : kJitPre; }
+
+// words of the preloads of one LDS-mode program (< 0: untranslatable)
+MTGP_JIT_HD inline int jit_preload_words(const MtgpInstr* prog, int L) {
+  JitOut o{nullptr, 0};
+  const int rc = jit_program(o, prog, L, false, kJitModeLds, 1);
+  return rc < 0 ? rc : o.n;
+}
+
+// Region of group g of an LDS-mode unit (see above); `next` = the program of group g + 1 or null.
+MTGP_JIT_HD inline int jit_lds_region(JitOut& o, const MtgpInstr* cur, const MtgpInstr* next, int L, int g) {
+  if (g == 0) {
+    const int rc = jit_program(o, cur, L, false, kJitModeLds, 1, jit_pre_set(0));
+    if (rc < 0) return rc;
+  }
+  int np1 = 0;
+  if (next) {
+    const int rc = jit_program(o, next, L, false, kJitModeLds, 1, jit_pre_set(g + 1), 0, &np1);
+    if (rc < 0) return rc;
+  }
+  if (g > 0) o.movv(kJitKeep, kJitAcc);
+  return jit_program(o, cur, L, false, kJitModeLds, 2, jit_pre_set(g), np1);
+}
+
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
                                 int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
-                                uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u) {
+                                uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u, bool pipe = true) {
   JitOut o{out, 0};
   o.base = base;
   for (int g = 0; g < G; ++g) {
     const int q = wave * G + g;
     if (q >= P) break;
     const int ind = order ? order[q] : q;
-    if (g > 0) o.movv(kJitKeep, kJitAcc);
-    const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false, mode);
+    const MtgpInstr* cur = prog + ((size_t)ind * n_prog + j) * L;
+    int rc;
+    if (mode == kJitModeLds && pipe) {
+      const MtgpInstr* nxt = nullptr;
+      if (g + 1 < G && q + 1 < P) nxt = prog + ((size_t)(order ? order[q + 1] : q + 1) * n_prog + j) * L;
+      rc = jit_lds_region(o, cur, nxt, L, g);
+    } else {
+      if (g > 0) o.movv(kJitKeep, kJitAcc);
+      rc = jit_program(o, cur, L, false, mode);
+    }
     if (rc < 0) return rc;
     if (g > 0) {
       const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);  // g > 0 implies Rp < 64
@@ -428,13 +477,22 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
 // s_setpc when `last`.  jit_unit == the concatenation of its groups.
 MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
                                       int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
-                                      uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u) {
+                                      uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u,
+                                      bool pipe = true) {
   JitOut o{out, 0};
   o.base = base;
   const int q = q0 + g;
   const int ind = order ? order[q] : q;
-  if (g > 0) o.movv(kJitKeep, kJitAcc);
-  const int rc = jit_program(o, prog + ((size_t)ind * n_prog + j) * L, L, false, mode);
+  const MtgpInstr* cur = prog + ((size_t)ind * n_prog + j) * L;
+  int rc;
+  if (mode == kJitModeLds && pipe) {  // (the caller placed this region 2 * npre(g) words after the plain start)
+    const MtgpInstr* nxt = nullptr;
+    if (!last) nxt = prog + ((size_t)(order ? order[q + 1] : q + 1) * n_prog + j) * L;
+    rc = jit_lds_region(o, cur, nxt, L, g);
+  } else {
+    if (g > 0) o.movv(kJitKeep, kJitAcc);
+    rc = jit_program(o, cur, L, false, mode);
+  }
   if (rc < 0) return rc;
   if (g > 0) {
     const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);

@@ -217,6 +217,9 @@ __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, fl
   }
 }
 
+#ifndef MTGP_V_OBSFAST
+#define MTGP_V_OBSFAST 1
+#endif
 // y = C@x + nz with C = I (n_obs = n_var for every environment on this path): (C@x)_i + nz_i
 // equals x_i + nz_i when every x_j is finite (the +-0 terms 0*x_j cannot change the sum; with
 // nz = +0 a -0 becomes +0 either way), NaN otherwise (0*inf), then the environment's own
@@ -224,9 +227,20 @@ __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, fl
 template <class Env>
 __device__ __forceinline__ void ctl_obs_apply(const float x[Env::NV], const float nz[Env::NV], float y[Env::NV]) {
   constexpr int NV = Env::NV;
-  bool fin[NV];
+  bool fin[NV], all = true;
 #pragma unroll
-  for (int j = 0; j < NV; ++j) fin[j] = mtgp_isfinite(x[j]);
+  for (int j = 0; j < NV; ++j) {
+    fin[j] = mtgp_isfinite(x[j]);
+    all = all && fin[j];
+  }
+#if MTGP_V_OBSFAST
+  if (__builtin_expect(__all(all), 1)) {  // every lane's state finite (the common case): no NaN masking
+#pragma unroll
+    for (int i = 0; i < NV; ++i) y[i] = x[i] + nz[i];
+    Env::obs_transform(y);
+    return;
+  }
+#endif
   const float qn = mtgp_qnan();
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -535,6 +549,49 @@ __device__ __forceinline__ float stage_in(int stage, float s, float k, float h, 
 // RK4 accumulator: k1 + 2 k2 + 2 k3 + k4 (fma form shared with the oracle)
 __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
   return stage == 0 ? k : (stage == 3 ? acc + k : MTGP_FMAF(2.0f, k, acc));
+}
+
+// The same for a whole state vector, branching on the (wave-uniform) stage once instead of
+// selecting per component: the same operations, so the same bits.
+#ifndef MTGP_V_STAGEBR
+#define MTGP_V_STAGEBR 1
+#endif
+template <int N>
+__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&k)[N], float h, float h2,
+                                           float (&out)[N]) {
+#if MTGP_V_STAGEBR
+  const int st = uni(stage);
+  if (st == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = s[i];
+  } else {
+    const float c = st == 3 ? h : h2;
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = MTGP_FMAF(c, k[i], s[i]);
+  }
+#else
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = stage_in(stage, s[i], k[i], h, h2);
+#endif
+}
+template <int N>
+__device__ __forceinline__ void stage_acc_n(int stage, float (&acc)[N], const float (&k)[N]) {
+#if MTGP_V_STAGEBR
+  const int st = uni(stage);
+  if (st == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = k[i];
+  } else if (st == 3) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = acc[i] + k[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]);
+  }
+#else
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc[i] = stage_acc(stage, acc[i], k[i]);
+#endif
 }
 
 // --------------------------------------------------------------------------------------
@@ -851,10 +908,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #endif
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
-#pragma unroll
-      for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) at[j] = stage_in(stage, a[j], ka[j], h, h2);
+      stage_in_n<NV>(stage, x, kx, h, h2, xt);
+      stage_in_n<NA>(stage, a, ka, h, h2, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j) D.put(NV + j, at[j]);
       float ur[1];
@@ -929,10 +984,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (!TRAJ && __all(fit.settled || dead)) stop = true;
         if (stop) break;
       }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) aa[j] = stage_acc(stage, aa[j], ka[j]);
+      stage_acc_n<NV>(stage, ax, kx);
+      stage_acc_n<NA>(stage, aa, ka);
     }
     if (stop) break;
     if (!dead) {
@@ -1004,8 +1057,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
-#pragma unroll
-      for (int i = 0; i < NV; ++i) xt[i] = stage_in(stage, x[i], kx[i], h, h2);
+      stage_in_n<NV>(stage, x, kx, h, h2, xt);
       const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
       // stages 1 and 2 share the time t + h/2, hence the noise draw
       if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
@@ -1052,8 +1104,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
         if (!TRAJ && __all(fit.settled || dead)) stop = true;
         if (stop) break;
       }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
+      stage_acc_n<NV>(stage, ax, kx);
     }
     if (stop) break;
     if (!dead) {
@@ -1549,7 +1600,9 @@ __device__ __forceinline__ float jit_call_lds(uint64_t addr_, uint32_t lds_addr,
                : [tgt] "s"(addr), "{v0}"(lds_addr)
                : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
                  "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",
-                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "s30", "s31", "s34", "s35",
+                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47",
+                 "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "s30", "s31",
+                 "s34", "s35",
                  "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "memory");
   return acc;
 }
@@ -1565,7 +1618,9 @@ __device__ __forceinline__ void jit_call_lds_store(uint64_t addr_, uint32_t lds_
                : [tgt] "s"(addr), "{v0}"(lds_in), "{v1}"(lds_out)
                : "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
                  "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32", "v33", "v34",
-                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "s30", "s31", "s34", "s35",
+                 "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47",
+                 "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "s30", "s31",
+                 "s34", "s35",
                  "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "scc", "memory");
 }
 
@@ -2578,6 +2633,47 @@ __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict
   order[q] = p;
 }
 
+// The whole schedule in ONE block (P * n_prog <= kSchedFusedMax): histogram, exclusive scan and scatter in
+// LDS (no memset, no global atomics, one launch instead of three + a fill).  Same slot formula as
+// k_sched_scatter; ties are ordered arbitrarily as there.
+constexpr long kSchedFusedMax = 1 << 16;  // program entries (P * n_prog): C3 32768 -> fused, C5 262144 -> 3 kernels
+__global__ void __launch_bounds__(1024) k_sched_fused(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
+                                                      int G, int32_t* __restrict__ order) {
+  __shared__ int32_t hist[MTGP_SCHED_BINS];
+  __shared__ int32_t part[1024];
+  constexpr int kPer = MTGP_SCHED_BINS / 1024;
+  const int t = threadIdx.x;
+  for (int i = t; i < MTGP_SCHED_BINS; i += 1024) hist[i] = 0;
+  __syncthreads();
+  for (int p = t; p < P; p += 1024) atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
+  __syncthreads();
+  int loc[kPer], sum = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) { loc[i] = sum; sum += hist[t * kPer + i]; }
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the per-thread sums
+    const int v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const int base = part[t] - sum;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) hist[t * kPer + i] = base + loc[i];  // (each thread rewrites its own bins)
+  __syncthreads();
+  const int h = P / 2;
+  for (int p = t; p < P; p += 1024) {
+    const int sr = atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
+    int q;
+    if (G == 1) q = P - 1 - sr;
+    else if (sr < h) q = 2 * sr + 1;
+    else if (sr >= P - h) q = 2 * (P - 1 - sr);
+    else q = P - 1;  // middle element of an odd P
+    order[q] = p;
+  }
+}
+
 #endif  // MTGP_TU_MAIN
 
 #if MTGP_TU_MAIN
@@ -2593,6 +2689,7 @@ struct JitUnitArgs {
   const int32_t* order;
   int mode;  // mtgp_jit.h kJitModeRegs / kJitModeLds
   uint32_t next, cond, store;  // role / LDS store chains (MtgpJitChain, mtgp_jit.h jit_unit_end)
+  int pipe;                    // LDS-data units software-pipelined (mtgp_jit.h jit_lds_region)
 };
 
 __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
@@ -2760,6 +2857,62 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes(uint32_t* __restrict__ 
   }
 }
 
+// The same scan with every thread's PER sizes held in registers (one read, one write pass),
+// wave scans by shuffles and one barrier for the 16 wave totals (units <= 1024 * PER).
+template <int PER>
+__global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restrict__ offs, int total,
+                                                             int32_t* __restrict__ info) {
+  __shared__ uint64_t wsum[16];
+  __shared__ int32_t werr[16];
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  const int b = t * PER;
+  uint32_t v[PER];
+#pragma unroll
+  for (int k = 0; k < PER; ++k) v[k] = (b + k < total) ? offs[b + k] : 0u;
+  uint64_t sum = 0;
+  int bad = 0;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    const bool isbad = (v[k] & 0x80000000u) != 0u;
+    const int code = -(int)(v[k] & 0x7fffffffu);
+    bad = (isbad && code < bad) ? code : bad;
+    sum += isbad ? 0u : v[k];
+  }
+  uint64_t inc = sum;  // inclusive scan over the wave
+  for (int d = 1; d < kWave; d <<= 1) {
+    const uint64_t y = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += y;
+  }
+  int e = bad;
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int o = __shfl_xor(e, d, kWave);
+    e = o < e ? o : e;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  if (lane == 0) werr[w] = e;
+  __syncthreads();
+  uint64_t wbase = 0;
+  int err = 0;
+  for (int q = 0; q < 16; ++q) {
+    if (q < w) wbase += wsum[q];
+    err = werr[q] < err ? werr[q] : err;
+  }
+  uint64_t run = wbase + inc - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
+#pragma unroll
+  for (int k = 0; k < PER; ++k) {
+    if (b + k < total) {
+      offs[b + k] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+      run += (v[k] & 0x80000000u) ? 0u : v[k];
+    }
+  }
+  if (t == 1023) {
+    const uint64_t tot = wbase + inc + mtgp::kJitTemplateBytes;
+    offs[total] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+    info[0] = err;
+    info[1] = (int32_t)(tot < 0x7fffffffull ? tot : 0x7fffffffull);
+  }
+}
+
 // Emit with one thread per (unit, group): group g's code starts after groups 0..g-1 (sizes from
 // jit_words), so the G programs of a unit are translated in parallel.
 __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
@@ -2779,9 +2932,15 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
     start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (h > 0 ? 7u : 0u);
   }
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
+  if (U.mode == mtgp::kJitModeLds && U.pipe && g > 0) {  // pipelined LDS units: group g's region starts after its preloads
+    const int ind = U.order ? U.order[q] : q;
+    const int pw = mtgp::jit_preload_words(U.prog + ((size_t)ind * U.n_prog + j) * U.L, U.L);
+    if (pw < 0) return;
+    start += (uint32_t)pw;
+  }
   const uint32_t at = b + start * 4u;
   mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode,
-                       U.next, U.cond, U.store);
+                       U.next, U.cond, U.store, U.pipe != 0);
 }
 
 // the shared sin/cos subroutines at the start of the code buffer
@@ -2805,6 +2964,7 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
   U.order = order;
   U.mode = mtgp::kJitModeRegs;
   U.next = U.cond = U.store = 0u;
+  U.pipe = 1;
   const long waves = ((long)P + U.G - 1) / U.G;
   if (waves * n_prog > INT32_MAX - 1) return false;
   U.n_units = (int)(waves * n_prog);
@@ -3124,7 +3284,12 @@ int mtgp_jit_plan_words_chain(const int32_t* jit_words, int32_t P, int32_t n_pro
   }
   hipLaunchKernelGGL(k_jit_sizes, dim3((unsigned)((U.n_units + 255) / 256)), dim3(256), 0, s, U, jit_words,
                      offsets_out);
-  hipLaunchKernelGGL(k_jit_scan_sizes, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
+  if (U.n_units <= 1024 * 16)
+    hipLaunchKernelGGL(k_jit_scan_sizes_reg<16>, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
+  else if (U.n_units <= 1024 * 32)
+    hipLaunchKernelGGL(k_jit_scan_sizes_reg<32>, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
+  else
+    hipLaunchKernelGGL(k_jit_scan_sizes, dim3(1), dim3(1024), 0, s, offsets_out, U.n_units, info_out);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
@@ -3142,6 +3307,10 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   if (!jit_words || !offsets || !code || !jit_unit_args(prog, P, n_prog, L, R, order, U)) return MTGP_ERR_ARG;
   if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   U.mode = jit_mode;
+  {  // A/B knob: MTGP_JIT_LDS_PIPE=0 emits LDS-data units without the preload pipelining
+    const char* e = getenv("MTGP_JIT_LDS_PIPE");
+    U.pipe = !(e && strcmp(e, "0") == 0);
+  }
   if (chain) {
     if (jit_mode != mtgp::kJitModeRegs && (chain->next | chain->cond) != 0u) return MTGP_ERR_ARG;  // v26.. are preloads
     if (jit_mode != mtgp::kJitModeLds && chain->store != 0u) return MTGP_ERR_ARG;  // store chains: LDS-data code
@@ -3322,6 +3491,10 @@ int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t*
   while (Rp < R) Rp <<= 1;
   const int G = kWave / Rp;
   hipStream_t s = (hipStream_t)stream;
+  if ((long)P * n_prog <= kSchedFusedMax) {  // small populations: one block does it all
+    hipLaunchKernelGGL(k_sched_fused, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
+    return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  }
   int32_t* hist = scratch;
   int32_t* offs = scratch + MTGP_SCHED_BINS;
   if (hipMemsetAsync(hist, 0, MTGP_SCHED_BINS * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;

@@ -177,7 +177,7 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
             put(words[i + 1] >> 24, data[(w & 0xFFFF) // 256])
             i += 2
             continue
-        if w == 0xBF8CC07F:  # s_waitcnt lgkmcnt(0)
+        if (w & 0xFFFFF0FF) == 0xBF8CC07F:  # s_waitcnt lgkmcnt(n) (the emulator's loads complete at once)
             i += 1
             continue
         if (w & 0xFFFF0000) == 0xD81A0000 and words[i + 1] == 0x00000801:  # ds_write_b32 v1, v8 offset:j*256
