@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 14
+#define MTGP_ABI_VERSION 15
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -150,6 +150,13 @@ typedef struct {
   float rtol, atol;  /* PIDController tolerances                                         */
   float dtmin;       /* <= 0: None; else force_dtmin: steps at dtmin are always accepted */
   float dtmax;       /* <= 0: None                                                       */
+  /* ABI v15: a general PIDController (mtgp_dopri5.h mtgp_dp_factor_pid).  pid_custom == 0 (a
+   * zero-initialised struct): diffrax's defaults (pcoeff 0, icoeff 1, dcoeff 0, safety 0.9,
+   * factormin 0.2, factormax 10).  Otherwise pid_c1 = (icoeff + pcoeff + dcoeff) / 5,
+   * pid_c2 = -(pcoeff + 2 dcoeff) / 5, pid_c3 = dcoeff / 5 (error order 5), rounded to f32. */
+  int32_t pid_custom;
+  float pid_c1, pid_c2, pid_c3, pid_safety, pid_factormin, pid_factormax;
+  int32_t no_force_dtmin; /* 1: force_dtmin=False -- dt < dtmin ends the solve (dt_min_reached) */
 } MtgpModel;
 enum { MTGP_SOLVER_RK4 = 0, MTGP_SOLVER_DOPRI5 = 1, MTGP_SOLVER_EULER = 2 };
 

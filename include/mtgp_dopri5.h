@@ -97,6 +97,72 @@ MTGP_INLINE MTGP_HD float mtgp_dp_factor(float m, int keep) {
   return f > MTGP_DP_FACTORMAX ? MTGP_DP_FACTORMAX : f;
 }
 
+/* General PIDController (diffrax.PIDController(pcoeff, icoeff, dcoeff, safety, factormin,
+ * factormax)), restated from diffrax's published adapt_step_size: with error order 5,
+ *   c1 = (i + p + d) / 5, c2 = -(p + 2 d) / 5, c3 = d / 5,
+ *   factor = clip(safety * inv^c1 * prev^c2 * prev2^c3, keep ? 1 : factormin, factormax)
+ * (a factor with a zero exponent is 1, products left to right), inv = 1 / rms = m^(-1/2) of the
+ * mean square m, prev / prev2 the inverse errors of the last two ACCEPTED steps (initially 1; an
+ * inverse error of 0 or inf is stored as 1).  inv^c1 is exp(-(c1/2) log m) so that the default
+ * (c1 = 0.2, safety 0.9, factormin 0.2, factormax 10) reproduces mtgp_dp_factor bit for bit; the
+ * m == 0 / non-finite m rules are mtgp_dp_factor's. */
+typedef struct {
+  float c1, c2, c3, safety, factormin, factormax;
+} MtgpDpPid;
+
+MTGP_INLINE MTGP_HD float mtgp_dp_factor_pid(float m, int keep, float prev, float prev2, const MtgpDpPid* c) {
+  const float lo = keep ? 1.0f : c->factormin;
+  if (!(m == 0.0f) && !mtgp_isfinite(m)) return lo;
+  float f = c->safety;
+  if (c->c1 != 0.0f)  /* inv^c1; m == 0: inv = inf, so inf (c1 > 0) or 0 (c1 < 0) */
+    f = f * (m == 0.0f ? (c->c1 > 0.0f ? mtgp_u2f(0x7f800000u) : 0.0f) : mtgp_expf((-0.5f * c->c1) * mtgp_logf_pos(m)));
+  if (c->c2 != 0.0f) f = f * mtgp_expf(c->c2 * mtgp_logf_pos(prev));
+  if (c->c3 != 0.0f) f = f * mtgp_expf(c->c3 * mtgp_logf_pos(prev2));
+  f = f < lo ? lo : f;
+  return f > c->factormax ? c->factormax : f;
+}
+
+/* the inverse error carried to the next steps: 1 / rms of m, with 0 / inf (and NaN) stored as 1 */
+MTGP_INLINE MTGP_HD float mtgp_dp_inv_error(float m) {
+  if (!(m > 0.0f) || !mtgp_isfinite(m)) return 1.0f;
+  const float v = mtgp_expf(-0.5f * mtgp_logf_pos(m));
+  return (v == 0.0f || !mtgp_isfinite(v)) ? 1.0f : v;
+}
+
+/* Controller state of one solve (init {1, 1, 0}) and one controller decision after an attempt with
+ * mean squared scaled error ms and size h: keep (accept), the next dt after the factor, dtmax and
+ * dtmin, the state update (at_dtmin; on accept the inverse errors shift), and fail = 1 when
+ * force_dtmin is off and dt fell below dtmin (diffrax RESULTS.dt_min_reached: the solve ends after
+ * this attempt; with throw=False the unsaved points are +inf).  With the default coefficients and
+ * force_dtmin this is the round-1 rule bit for bit. */
+typedef struct {
+  float prev, prev2;
+  int at_dtmin;
+} MtgpDpCtl;
+
+MTGP_INLINE MTGP_HD float mtgp_dp_control(float ms, float h, float dtmin, float dtmax, int force_dtmin,
+                                          const MtgpDpPid* c, MtgpDpCtl* st, int* keep_out, int* fail_out) {
+  const int keep = (ms < 1.0f) || (force_dtmin && st->at_dtmin);
+  float dt = h * mtgp_dp_factor_pid(ms, keep, st->prev, st->prev2, c);
+  if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
+  int fail = 0;
+  if (dtmin > 0.0f) {
+    if (!force_dtmin && dt < dtmin) fail = 1;
+    st->at_dtmin = dt <= dtmin;
+    dt = dt < dtmin ? dtmin : dt;
+  }
+  if (keep && (c->c2 != 0.0f || c->c3 != 0.0f)) {
+    st->prev2 = st->prev;
+    st->prev = mtgp_dp_inv_error(ms);
+  }
+  *keep_out = keep;
+  *fail_out = fail;
+  return dt;
+}
+
+/* the default controller's coefficients (diffrax PIDController defaults) */
+#define MTGP_DP_PID_DEFAULT {0.2f, 0.0f, 0.0f, MTGP_DP_SAFETY, MTGP_DP_FACTORMIN, MTGP_DP_FACTORMAX}
+
 /* scaled error of one component: err / (atol + rtol * max(|y0|, |y1|)) */
 MTGP_INLINE MTGP_HD float mtgp_dp_scaled(float err, float y0, float y1, float rtol, float atol) {
   const float a0 = MTGP_FABSF(y0), a1 = MTGP_FABSF(y1);

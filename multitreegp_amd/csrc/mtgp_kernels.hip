@@ -1121,6 +1121,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 // Dormand-Prince a_ij (include/mtgp_dopri5.h), read with scalar loads by the rolled stage loops
 static __constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
 
+// the controller coefficients of model m (mtgp.h ABI v15; pid_custom == 0: diffrax's defaults)
+__device__ __forceinline__ MtgpDpPid dp_pid(const MtgpModel& m) {
+  if (!m.pid_custom) return MtgpDpPid MTGP_DP_PID_DEFAULT;
+  return MtgpDpPid{m.pid_c1, m.pid_c2, m.pid_c3, m.pid_safety, m.pid_factormin, m.pid_factormax};
+}
+
 // --------------------------------------------------------------------------------------
 // Control evaluators with adaptive Dopri5 + PIDController (the notebooks' solver,
 // DynamicPolicy.ipynb:105, StaticPolicy.ipynb:102; spec include/mtgp_dopri5.h).  NA > 0: the
@@ -1235,7 +1241,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   for (int j = NV; j < ND; ++j) y[j] = 0.0f;
   save_round(active, 0, y, false);
   int k = 1, steps = 0;
-  bool at_dtmin = false, prev_ok = !Env::bad(y, ND);
+  bool prev_ok = !Env::bad(y, ND);
+  MtgpDpCtl ctl{1.0f, 1.0f, 0};
+  const MtgpDpPid pid = dp_pid(A.m);
+  const int force_dtmin = !A.m.no_force_dtmin;
   float t = ts[0];
   float tnext = t + A.m.h;
   tnext = tnext > t_end ? t_end : tnext;
@@ -1261,7 +1270,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
 #pragma unroll
         for (int i = 0; i < ND; ++i) f[j][i] = (j == s) ? fs[i] : f[j][i];
     }
-    bool keep = false, stop = false;
+    bool keep = false, stop = false, fail = false;
     float dt = 0.0f;
     if (live) {
       float msum = 0.0f;
@@ -1274,13 +1283,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
         msum = (i == 0) ? sc * sc : msum + sc * sc;
       }
       const float ms = msum / (float)ND;
-      keep = (ms < 1.0f) || at_dtmin;
-      dt = h * mtgp_dp_factor(ms, keep);
-      if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
-      if (dtmin > 0.0f) {
-        at_dtmin = dt <= dtmin;
-        dt = dt < dtmin ? dtmin : dt;
-      }
+      int kp, fl;
+      dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &kp, &fl);
+      keep = kp != 0;
+      fail = fl != 0;
       ++steps;
     }
     // SaveAt(ts) through the dense output of the accepted steps, one save point per round
@@ -1314,7 +1320,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
         stop = prev_ok && !ok;  // Event(cond_fn_nan), dyn.py:94
         prev_ok = ok;
       }
-      if (stop || !(t < t_end) || steps >= max_steps || (!TRAJ && fit.settled)) live = false;
+      if (stop || fail || !(t < t_end) || steps >= max_steps || (!TRAJ && fit.settled)) live = false;
       else tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
   }
@@ -1465,7 +1471,10 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
   for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
   save(0, y);
   int k = 1, steps = 0;
-  bool at_dtmin = false, prev_ok = !bad(y);
+  bool prev_ok = !bad(y);
+  MtgpDpCtl ctl{1.0f, 1.0f, 0};
+  const MtgpDpPid pid = dp_pid(A.m);
+  const int force_dtmin = !A.m.no_force_dtmin;
   float t = ts[0];
   float tnext = t + A.m.h;
   tnext = tnext > t_end ? t_end : tnext;
@@ -1507,15 +1516,11 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
         msum = (i == 0) ? sc * sc : msum + sc * sc;
       }
       const float ms = msum / (float)NV;
-      const bool keep = (ms < 1.0f) || at_dtmin;
-      float dt = h * mtgp_dp_factor(ms, keep);
-      if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
-      if (dtmin > 0.0f) {
-        at_dtmin = dt <= dtmin;
-        dt = dt < dtmin ? dtmin : dt;
-      }
+      int kp, fl;
+      const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &kp, &fl);
+      const bool keep = kp != 0;
       ++steps;
-      bool stop = false;
+      bool stop = fl != 0;
       if (keep) {
         while (k < S && ts[k] <= tnext) {  // SaveAt(ts) through the dense output
           const float th = (ts[k] - t) / h;
@@ -1538,7 +1543,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
           f[0][i] = f[6][i];  // FSAL
         }
         const bool ok = !bad(y);
-        stop = prev_ok && !ok;  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
+        stop = stop || (prev_ok && !ok);  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
         prev_ok = ok;
       }
       if (stop || !(t < t_end) || steps >= max_steps) live = false;
@@ -1910,7 +1915,10 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
   }
   save(0, y, true);  // (its barrier also publishes the stage vector)
   int k = 1, steps = 0;
-  bool at_dtmin = false, prev_ok = !any_bad(y);
+  bool prev_ok = !any_bad(y);
+  MtgpDpCtl ctl{1.0f, 1.0f, 0};
+  const MtgpDpPid pid = dp_pid(A.m);
+  const int force_dtmin = !A.m.no_force_dtmin;
   float t = ts[0];
   float tnext = t + A.m.h;
   tnext = tnext > t_end ? t_end : tnext;
@@ -1952,14 +1960,10 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
     }
     const float msum = reduce();
     const float ms = msum / (float)NV;
-    const bool keep = (ms < 1.0f) || at_dtmin;
-    float dt = h * mtgp_dp_factor(ms, keep);
-    bool at_min_next = at_dtmin;
-    if (dtmax > 0.0f && dt > dtmax) dt = dtmax;
-    if (dtmin > 0.0f) {
-      at_min_next = dt <= dtmin;
-      dt = dt < dtmin ? dtmin : dt;
-    }
+    MtgpDpCtl nctl = ctl;  // committed by live lanes only
+    int kp, fl;
+    const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &nctl, &kp, &fl);
+    const bool keep = kp != 0;
     const bool acc_step = live && keep;
     // SaveAt(ts) through the dense output, in rounds over the lanes that pass save points
     while (__any(acc_step && k < S && ts[k < S ? k : S - 1] <= tnext)) {
@@ -1987,11 +1991,11 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
     }
     const bool ok = !any_bad(y);
     if (live) {
-      at_dtmin = at_min_next;
+      ctl = nctl;
       ++steps;
-      bool stop = false;
+      bool stop = fl != 0;
       if (keep) {
-        stop = prev_ok && !ok;  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
+        stop = stop || (prev_ok && !ok);  // Event(cond_fn_nan) (sr.py:93-94): terminate after this step
         prev_ok = ok;
       }
       if (stop || !(t < t_end) || steps >= max_steps) live = false;

@@ -353,6 +353,9 @@ class DeviceEngine:
         m.env = d.get("env", nat.ENV_ACROBOT)
         m.solver, m.max_steps = d.get("solver", nat.SOLVER_RK4), d.get("max_steps", 0)
         m.rtol, m.atol, m.dtmin, m.dtmax = d.get("rtol", 0.0), d.get("atol", 0.0), d.get("dtmin", 0.0), d.get("dtmax", 0.0)
+        for f in ("pid_custom", "pid_c1", "pid_c2", "pid_c3", "pid_safety", "pid_factormin", "pid_factormax",
+                  "no_force_dtmin"):
+            setattr(m, f, d.get(f, 0))
         return m
 
     @staticmethod

@@ -57,25 +57,43 @@ class Dopri5:
 
 
 class PIDController:
-    """diffrax.PIDController with its defaults (pcoeff 0, icoeff 1, dcoeff 0: an integral
-    controller; safety 0.9, factormin 0.2, factormax 10, force_dtmin True, rms norm)."""
+    """diffrax.PIDController (defaults: pcoeff 0, icoeff 1, dcoeff 0 -- an integral controller;
+    safety 0.9, factormin 0.2, factormax 10, force_dtmin True, rms norm).  Any coefficients run on
+    the GPU (include/mtgp_dopri5.h mtgp_dp_factor_pid, restated from diffrax's adapt_step_size);
+    force_dtmin=False ends a solve whose step falls below dtmin (RESULTS.dt_min_reached, the
+    remaining save points +inf as with throw=False)."""
     name = "PIDController"
 
     def __init__(self, rtol: float, atol: float, pcoeff: float = 0.0, icoeff: float = 1.0, dcoeff: float = 0.0,
                  dtmin: float = None, dtmax: float = None, force_dtmin: bool = True, factormin: float = 0.2,
                  factormax: float = 10.0, safety: float = 0.9):
-        if (pcoeff, icoeff, dcoeff) != (0.0, 1.0, 0.0) or (factormin, factormax, safety) != (0.2, 10.0, 0.9):
-            raise NotImplementedError("only the default PIDController coefficients are implemented on the GPU")
-        if not force_dtmin:
-            raise NotImplementedError("force_dtmin=False (error on dtmin) is not implemented")
         if rtol < 0 or atol < 0:
             raise ValueError("rtol and atol must be >= 0")
         self.rtol, self.atol = float(rtol), float(atol)
         self.dtmin = None if dtmin is None else float(dtmin)
         self.dtmax = None if dtmax is None else float(dtmax)
+        self.pcoeff, self.icoeff, self.dcoeff = float(pcoeff), float(icoeff), float(dcoeff)
+        self.factormin, self.factormax, self.safety = float(factormin), float(factormax), float(safety)
+        self.force_dtmin = bool(force_dtmin)
+
+    def is_default(self) -> bool:
+        return (self.pcoeff, self.icoeff, self.dcoeff, self.factormin, self.factormax, self.safety) == \
+            (0.0, 1.0, 0.0, 0.2, 10.0, 0.9)
+
+    def model_fields(self) -> dict:
+        """MtgpModel ABI v15 fields: error order 5 (Dopri5), exponents rounded to float32."""
+        out = dict(no_force_dtmin=0 if self.force_dtmin else 1, pid_custom=0)
+        if not self.is_default():
+            p, i, d = self.pcoeff, self.icoeff, self.dcoeff
+            out.update(pid_custom=1, pid_c1=float(np.float32((i + p + d) / 5.0)),
+                       pid_c2=float(np.float32(-(p + 2.0 * d) / 5.0)), pid_c3=float(np.float32(d / 5.0)),
+                       pid_safety=float(np.float32(self.safety)), pid_factormin=float(np.float32(self.factormin)),
+                       pid_factormax=float(np.float32(self.factormax)))
+        return out
 
     def __repr__(self):
-        return f"PIDController(rtol={self.rtol}, atol={self.atol}, dtmin={self.dtmin}, dtmax={self.dtmax})"
+        return (f"PIDController(rtol={self.rtol}, atol={self.atol}, pcoeff={self.pcoeff}, icoeff={self.icoeff}, "
+                f"dcoeff={self.dcoeff}, dtmin={self.dtmin}, dtmax={self.dtmax}, force_dtmin={self.force_dtmin})")
 
 
 def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
@@ -103,7 +121,7 @@ def _solver_fields(kind: str, controller, max_steps: int) -> dict:
         return dict(solver=nat.SOLVER_EULER if kind == "euler" else nat.SOLVER_RK4, max_steps=0, rtol=0.0, atol=0.0,
                     dtmin=0.0, dtmax=0.0)
     return dict(solver=nat.SOLVER_DOPRI5, max_steps=int(max_steps), rtol=controller.rtol, atol=controller.atol,
-                dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0)
+                dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0, **controller.model_fields())
 
 
 def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool = True) -> Tuple[int, int, int]:

@@ -105,6 +105,9 @@ typedef struct {
   int32_t solver;    /* 0 fixed-step RK4 (BASELINE.json), 1 Dopri5 + PIDController (notebooks), 2 Euler */
   int32_t max_steps; /* Dopri5: step attempts, accepted + rejected (diffeqsolve max_steps) */
   float rtol, atol, dtmin, dtmax; /* PIDController; dtmin / dtmax <= 0: None */
+  int32_t pid_custom;             /* 0: diffrax's default PID coefficients (mtgp.h ABI v15) */
+  float pid_c1, pid_c2, pid_c3, pid_safety, pid_factormin, pid_factormax;
+  int32_t no_force_dtmin;         /* 1: force_dtmin=False (dt < dtmin ends the solve) */
 } OrModel;
 
 enum { ENV_ACROBOT = 0, ENV_HARMONIC = 1, ENV_REACTOR = 2 };
@@ -352,12 +355,19 @@ static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float
   float y[OR_MAX_S], f[7][OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
   for (int i = 0; i < n; ++i) y[i] = s0[i];
   for (int i = 0; i < n; ++i) saved[i] = y[i];
-  int k = 1, steps = 0, at_dtmin = 0;
+  int k = 1, steps = 0;
   float t = ts[0];
   float tnext = t + m->h;
   if (tnext > t_end) tnext = t_end;
   float prev = cond_fn(m, y);
   rhs(c, t, y, f[0]);
+  const MtgpDpPid def_pid = MTGP_DP_PID_DEFAULT;
+  MtgpDpPid pid = def_pid;
+  if (m->pid_custom) {
+    pid.c1 = m->pid_c1; pid.c2 = m->pid_c2; pid.c3 = m->pid_c3;
+    pid.safety = m->pid_safety; pid.factormin = m->pid_factormin; pid.factormax = m->pid_factormax;
+  }
+  MtgpDpCtl ctl = {1.0f, 1.0f, 0};
   while (t < t_end && steps < m->max_steps) {
     const float h = tnext - t;
     for (int st = 1; st <= 6; ++st) {
@@ -377,15 +387,10 @@ static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float
       msum = (i == 0) ? sc * sc : msum + sc * sc;
     }
     const float ms = msum / (float)n;
-    const int keep = (ms < 1.0f) || at_dtmin;
-    float dt = h * mtgp_dp_factor(ms, keep);
-    if (m->dtmax > 0.0f && dt > m->dtmax) dt = m->dtmax;
-    if (m->dtmin > 0.0f) {
-      at_dtmin = dt <= m->dtmin;
-      if (dt < m->dtmin) dt = m->dtmin;
-    }
+    int keep, fail;
+    const float dt = mtgp_dp_control(ms, h, m->dtmin, m->dtmax, !m->no_force_dtmin, &pid, &ctl, &keep, &fail);
     ++steps;
-    int done = 0;
+    int done = fail; /* dt_min_reached: the solve ends after this attempt */
     if (keep) {
       const float t1 = tnext;
       while (k < S && ts[k] <= t1) { /* SaveAt(ts) by the dense output */

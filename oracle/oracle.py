@@ -32,9 +32,14 @@ class OrModel(ctypes.Structure):
                 ("h", ctypes.c_float), ("max_fitness", ctypes.c_float), ("parsimony", ctypes.c_float),
                 ("prng_impl", ctypes.c_int32), ("env", ctypes.c_int32),
                 ("solver", ctypes.c_int32), ("max_steps", ctypes.c_int32), ("rtol", ctypes.c_float),
-                ("atol", ctypes.c_float), ("dtmin", ctypes.c_float), ("dtmax", ctypes.c_float)]
+                ("atol", ctypes.c_float), ("dtmin", ctypes.c_float), ("dtmax", ctypes.c_float),
+                ("pid_custom", ctypes.c_int32), ("pid_c1", ctypes.c_float), ("pid_c2", ctypes.c_float),
+                ("pid_c3", ctypes.c_float), ("pid_safety", ctypes.c_float), ("pid_factormin", ctypes.c_float),
+                ("pid_factormax", ctypes.c_float), ("no_force_dtmin", ctypes.c_int32)]
 
-_MODEL_DEFAULTS = dict(prng_impl=0, env=0, solver=0, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0)
+_MODEL_DEFAULTS = dict(prng_impl=0, env=0, solver=0, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0,
+                       pid_custom=0, pid_c1=0.0, pid_c2=0.0, pid_c3=0.0, pid_safety=0.0, pid_factormin=0.0,
+                       pid_factormax=0.0, no_force_dtmin=0)
 
 
 class OrRollouts(ctypes.Structure):

@@ -82,7 +82,9 @@ def oracle_model(ff, d, parsimony=0.0):
                 n_save=d["n_save"], h=ff.dt0, max_fitness=ff.max_fitness, parsimony=parsimony,
                 prng_impl=d.get("prng_impl", 0), env=d.get("env", 0), solver=d.get("solver", 0),
                 max_steps=d.get("max_steps", 0), rtol=d.get("rtol", 0.0), atol=d.get("atol", 0.0),
-                dtmin=d.get("dtmin", 0.0), dtmax=d.get("dtmax", 0.0))
+                dtmin=d.get("dtmin", 0.0), dtmax=d.get("dtmax", 0.0),
+                **{f: d.get(f, 0) for f in ("pid_custom", "pid_c1", "pid_c2", "pid_c3", "pid_safety", "pid_factormin",
+                                            "pid_factormax", "no_force_dtmin")})
 
 
 def oracle_rollouts(d, data=None):

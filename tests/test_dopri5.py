@@ -53,6 +53,62 @@ def test_dopri5_oscillator_known_answer(tol, atol_err):
     np.testing.assert_allclose(xs, _exact(X0, TS), atol=atol_err)
 
 
+def _pid_model(S, tol, pid, dtmin=0.0, max_steps=4000):
+    m = _model(S, tol, tol, dtmin=dtmin, max_steps=max_steps)
+    m.update(pid.model_fields())
+    return m
+
+
+@pytest.mark.parametrize("coeffs", [dict(pcoeff=0.3, icoeff=0.4), dict(pcoeff=0.2, icoeff=0.5, dcoeff=0.1),
+                                    dict(icoeff=1.0, safety=0.8, factormin=0.3, factormax=5.0)])
+def test_dopri5_general_pid_known_answer(coeffs):
+    """PI / PID controllers (diffrax.PIDController coefficients) on the closed-form oscillator:
+    accurate to the tolerance scale, and (PI) a different step sequence from the integral default."""
+    lib, cand = _oscillator()
+    ro = dict(x0=X0, ts=TS, ys_true=np.zeros((3, len(TS), 2), np.float32))
+    pid = mt.PIDController(rtol=1e-6, atol=1e-6, dtmin=0.001, **coeffs)
+    out = orc.evaluate(_pid_model(len(TS), 1e-6, pid, dtmin=0.001), cand, lib, ro, trajectories=True)
+    np.testing.assert_allclose(out["xs"][0], _exact(X0, TS), atol=5e-5)
+    base = orc.evaluate(_model(len(TS), 1e-6, 1e-6, dtmin=0.001), cand, lib, ro, trajectories=True)
+    assert not np.array_equal(out["xs"], base["xs"])  # the controller changed the steps
+
+
+def test_dopri5_default_pid_fields_are_the_default_controller():
+    """Explicit default coefficients map to pid_custom = 0: the round-1 controller bit for bit."""
+    lib, cand = _oscillator()
+    ro = dict(x0=X0, ts=TS, ys_true=np.zeros((3, len(TS), 2), np.float32))
+    pid = mt.PIDController(rtol=1e-4, atol=1e-4, pcoeff=0.0, icoeff=1.0, dcoeff=0.0, dtmin=0.001)
+    a = orc.evaluate(_pid_model(len(TS), 1e-4, pid, dtmin=0.001), cand, lib, ro, trajectories=True)
+    b = orc.evaluate(_model(len(TS), 1e-4, 1e-4, dtmin=0.001), cand, lib, ro, trajectories=True)
+    assert np.array_equal(a["xs"].view(np.uint32), b["xs"].view(np.uint32))
+
+
+def test_dopri5_force_dtmin_false_ends_the_solve():
+    """force_dtmin=False: once the controller asks for a step below dtmin the solve stops
+    (diffrax RESULTS.dt_min_reached; with throw=False the remaining save points are +inf), while
+    force_dtmin=True keeps stepping at dtmin.  dx = x * x blows up at t = 1 for x0 = 1."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0"]], [1])
+    N = 3
+    cand = np.zeros((1, 1, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 2] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 0, N - 1] = [lib.string_to_node["*"], N - 2, N - 2, 0]
+    x0 = np.array([[1.0], [0.1]], np.float32)
+    ts = (np.arange(21) * np.float32(0.1)).astype(np.float32)
+    ro = dict(x0=x0, ts=ts, ys_true=np.zeros((2, len(ts), 1), np.float32))
+    outs = {}
+    for force in (True, False):
+        pid = mt.PIDController(rtol=1e-6, atol=1e-6, dtmin=0.01, force_dtmin=force)
+        m = _pid_model(len(ts), 1e-6, pid, dtmin=0.01, max_steps=4000)
+        m["n_var"] = 1
+        outs[force] = orc.evaluate(m, cand, lib, ro, trajectories=True)["xs"][0, :, :, 0]
+    soft, hard = outs[False], outs[True]
+    np.testing.assert_allclose(soft[1], hard[1])  # the smooth rollout never needs dtmin
+    stop = int(np.argmax(np.isinf(soft[0])))
+    assert 0 < stop < len(ts) - 1 and np.isinf(soft[0, stop:]).all() and np.isfinite(soft[0, :stop]).all()
+    assert np.isfinite(hard[0, :stop + 1]).all()  # forced steps go on past the point where the soft solve gave up
+
+
 def test_dopri5_vs_scipy_rk45():
     """scipy's RK45 is the same Dormand-Prince pair with an integral controller of the same
     exponent (-1/5), safety and clip range; step sequences and interpolants differ in detail, so
@@ -124,8 +180,10 @@ def test_solver_selection_api():
         _check_solver(mt.Dopri5(), pid)  # callers that do not opt in
     with pytest.raises(NotImplementedError):
         _check_solver(mt.Dopri5(), None, adaptive_ok=True)
-    with pytest.raises(NotImplementedError):
-        mt.PIDController(rtol=1e-3, atol=1e-3, pcoeff=0.3)
+    pid2 = mt.PIDController(rtol=1e-3, atol=1e-3, pcoeff=0.3, icoeff=0.4)  # PI controllers run too (ABI v15)
+    f = pid2.model_fields()
+    assert f["pid_custom"] == 1 and f["pid_c1"] == np.float32(0.7 / 5) and f["pid_c2"] == np.float32(-0.3 / 5)
+    assert mt.PIDController(rtol=1e-3, atol=1e-3).model_fields() == dict(no_force_dtmin=0, pid_custom=0)
     with pytest.raises(NotImplementedError):
         mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05, solver=mt.Dopri5(), stepsize_controller=mt.ConstantStepSize())
     env, lib, ff, data, pop = sr_setup(P=2, R=4, solver=(1e-6, 1e-6, 0.001, 500))
@@ -227,6 +285,39 @@ def test_gpu_dopri5_wide_sr_bitexact(jit, n_var, tol, R, max_steps):
     assert (res["steps"] >= 1).all() and (res["steps"] <= max_steps).all()
     # the workload exercises more than one accept/reject pattern
     assert len(np.unique(res["steps"])) > 3
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["sr2", "sr12", "dynamic"])
+def test_gpu_dopri5_general_pid_bitexact(kind):
+    """A PID controller (pcoeff 0.3, icoeff 0.4, dcoeff 0.1, safety 0.85) and force_dtmin=False
+    through every Dopri5 kernel (register SR, wide SR, dynamic control): fitness, step counts and
+    trajectories bit-identical to the oracle."""
+    import torch
+    from helpers import bits_equal, dynamic_setup, mismatch_report
+    from multitreegp_amd.engine import DeviceEngine
+    pid = mt.PIDController(rtol=1e-5, atol=1e-5, pcoeff=0.3, icoeff=0.4, dcoeff=0.1, safety=0.85, dtmin=0.002,
+                           force_dtmin=False)
+    if kind == "dynamic":
+        env, lib, ff, data, pop = dynamic_setup(P=21, R=8, n_steps=30, seed=4, solver=(1e-5, 1e-5, 0.002, 600))
+    else:
+        nv = 2 if kind == "sr2" else 12
+        env, lib, ff, data, pop = sr_setup(P=21, R=8, n_save=26, save_every=4, h=0.01, depth=6, N=40,
+                                           seed=70 + nv, n_var=nv, solver=(1e-5, 1e-5, 0.002, 600))
+    ff.stepsize_controller = pid
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    r = eng.evaluate(torch.from_numpy(pop).cuda(), data, trajectories=True, rollout_fitness=True, step_counts=True)
+    torch.cuda.synchronize()
+    res = {k: v.cpu().numpy() for k, v in r.items() if isinstance(v, torch.Tensor)}
+    d = eng.prepare_data(data)
+    assert d["pid_custom"] == 1 and d["no_force_dtmin"] == 1
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, S, R = pop.shape[0], d["n_save"], d["R"]
+    nv = res["xs"].shape[1]
+    xs = res["xs"].reshape(S, nv, P, R).transpose(2, 3, 0, 1)
+    assert bits_equal(xs, ref["xs"]), mismatch_report(xs, ref["xs"], "xs")
 
 
 @pytest.mark.gpu
