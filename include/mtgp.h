@@ -366,6 +366,10 @@ int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, 
  * hipEvents recorded on its stream around the launch; -1 if none.  Synchronises that event.
  * The on/off switch (mtgp_set_timing) is process-wide; events are per host thread and device. */
 float mtgp_last_kernel_ms(void);
+/* The durations (ms) of the calling thread's last n timed launches, oldest first, into out[n]
+ * (a ring of the last 1024 launches is kept): returns how many were written.  Lets a caller time
+ * a whole run with one synchronisation at the end instead of one per launch. */
+int mtgp_kernel_ms_history(float* out, int32_t n);
 int mtgp_set_timing(int enabled);
 
 #ifdef __cplusplus

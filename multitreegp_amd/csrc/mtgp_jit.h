@@ -150,9 +150,12 @@ enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJit
 constexpr int kJitPreB = 44;  // the second preload register set (v44..v59) of a pipelined unit
 MTGP_JIT_HD inline uint32_t jit_wait_lgkm(int n) { return kWaitLgkm0 | (uint32_t)(n > 15 ? 15 : n) << 8; }
 
+// sp_init: operand-stack depth before prog[0] (the per-instruction sizing of k_flatten_wave
+// translates a pop on its own with one element on the stack).
 MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs,
-                                   int part = 0, int pre_base = kJitPre, int wait_n = 0, int* npre_out = nullptr) {
-  int sp = 0;
+                                   int part = 0, int pre_base = kJitPre, int wait_n = 0, int* npre_out = nullptr,
+                                   int sp_init = 0) {
+  int sp = sp_init;
   int pre[kJitPreSlots];
   int npre = 0;
   if (mode == kJitModeLds) {  // preload the first kJitPreSlots distinct data slots the program reads
@@ -298,6 +301,21 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
     jit_binop(o, base_fn, x, y);
   }
   return kJitErrNoEnd;
+}
+
+// Operand-stack effect of one instruction in jit_program: +1 where it calls push() (LDCP, LDVP,
+// SINVP, COSVP, VCP_*, VVP_*), -1 for the stack-operand forms (kind 2: ADDS .. RDIVS), else 0.
+MTGP_JIT_HD inline int jit_stack_delta(uint32_t code) {
+  switch (code) {
+    case MTGP_OP_LDCP: case MTGP_OP_LDVP: case MTGP_OP_SINVP: case MTGP_OP_COSVP:
+    case MTGP_OP_VCP_ADD: case MTGP_OP_VCP_SUB: case MTGP_OP_VCP_RSUB: case MTGP_OP_VCP_MUL: case MTGP_OP_VCP_DIV:
+    case MTGP_OP_VCP_RDIV: case MTGP_OP_VVP_ADD: case MTGP_OP_VVP_SUB: case MTGP_OP_VVP_MUL: case MTGP_OP_VVP_DIV:
+      return 1;
+    case MTGP_OP_ADDS: case MTGP_OP_SUBS: case MTGP_OP_RSUBS: case MTGP_OP_MULS: case MTGP_OP_DIVS: case MTGP_OP_RDIVS:
+      return -1;
+    default:
+      return 0;
+  }
 }
 
 // One callable program: number of 32-bit code words (out == nullptr: count only) or < 0.

@@ -2061,6 +2061,100 @@ __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n
   }
 }
 
+// The same sizing by a whole wave (register-data mode).  In register mode the code of an
+// instruction depends on its opcode alone (operands only select registers / literals), apart from
+// the slot-range and stack checks, so jit_program's translation of every opcode is probed once on
+// the host into JitOpTable (jit_op_table) and lane l sizes instructions l, l + 64, ... by table
+// lookup (no divergent translation); a prefix sum of the stack effects gives the depth each push /
+// pop sees, and the first failing instruction in program order gives the status -- within one
+// instruction a slot / opcode error precedes a stack error, as in jit_program.  Identical outputs to
+// flat_jit_size (tests/test_gpu_build.py compares them with the host translation).
+struct JitOpTable {
+  uint8_t words[64];  // code words of the opcode's translation
+  uint8_t flags[64];  // kOpValid | kOpTrig | kOpIbSlot | kOpAxSlot | kOpPush | kOpPop
+};
+enum : uint8_t { kOpValid = 1, kOpTrig = 2, kOpIbSlot = 4, kOpAxSlot = 8, kOpPush = 16, kOpPop = 32 };
+static_assert(MTGP_OP_COUNT <= 64, "JitOpTable holds 64 opcodes");
+
+JitOpTable jit_op_table() {
+  JitOpTable t{};
+  MtgpInstr end;
+  end.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+  end.imm = 0.0f;
+  for (int code = 0; code < 64; ++code) {
+    if (code == MTGP_OP_END) continue;  // never sized (instructions before the END only)
+    const int d = mtgp::jit_stack_delta((uint32_t)code);
+    auto probe = [&](uint32_t ax, uint32_t ib, mtgp::JitOut& o) {
+      MtgpInstr p[2] = {{(uint32_t)code << MTGP_OP_SHIFT | ax, 0.0f}, end};
+      std::memcpy(&p[0].imm, &ib, 4);
+      return mtgp::jit_program(o, p, 2, false, mtgp::kJitModeRegs, 0, mtgp::kJitPre, 0, nullptr, d < 0 ? 1 : 0);
+    };
+    mtgp::JitOut o{nullptr, 0};
+    if (probe(0u, 0u, o) != mtgp::kJitOk) continue;  // not an opcode
+    uint8_t f = kOpValid | (o.trig ? kOpTrig : 0) | (d > 0 ? kOpPush : 0) | (d < 0 ? kOpPop : 0);
+    const uint32_t far = (uint32_t)mtgp::kJitMaxData * MTGP_SLOT_BYTES;
+    mtgp::JitOut o1{nullptr, 0}, o2{nullptr, 0};
+    if (probe(0u, far, o1) == mtgp::kJitErrSlot) f |= kOpIbSlot;
+    if (probe(far, 0u, o2) == mtgp::kJitErrSlot) f |= kOpAxSlot;
+    t.words[code] = (uint8_t)o.n;
+    t.flags[code] = f;
+  }
+  return t;
+}
+
+template <int KI>
+__device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n, const JitOpTable& T,
+                                                   int32_t* jit_words_out, int32_t* jit_cost_out, size_t pj, int lane) {
+  int words = 0, trig = 0, carry = 0, rc = 0;
+  bool failed = false;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int i = k * kWave + lane;
+    const bool in = i < n;
+    int d = 0, e = 0;
+    if (in) {
+      const MtgpInstr x = prog[i];
+      const uint32_t code = x.op >> MTGP_OP_SHIFT;
+      const uint32_t f = code < 64u ? T.flags[code] : 0u;
+      uint32_t ib;
+      __builtin_memcpy(&ib, &x.imm, 4);
+      const int sib = (int)(ib / MTGP_SLOT_BYTES), sax = (int)((x.op & 0xffffffu) / MTGP_SLOT_BYTES);
+      if (!(f & kOpValid)) e = mtgp::kJitErrOpcode;
+      else if (((f & kOpIbSlot) && sib >= mtgp::kJitMaxData) || ((f & kOpAxSlot) && sax >= mtgp::kJitMaxData))
+        e = mtgp::kJitErrSlot;
+      d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
+      words += code < 64u ? T.words[code] : 0;
+      trig += (f & kOpTrig) ? 1 : 0;
+    }
+    int incl = d;  // inclusive prefix sum of the stack effects over this chunk
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const int before = carry + incl - d;
+    if (in && e == 0 && ((d > 0 && before >= MTGP_STACK_MAX) || (d < 0 && before <= 0))) e = mtgp::kJitErrStack;
+    carry += __shfl(incl, kWave - 1);
+    const uint64_t bad = __ballot(in && e != 0);
+    if (!failed && bad) {
+      failed = true;
+      rc = __shfl(e, __ffsll((unsigned long long)bad) - 1);
+    }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    words += __shfl_xor(words, off);
+    trig += __shfl_xor(trig, off);
+  }
+  if (lane == 0) {
+    if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
+    if (jit_cost_out) {  // = flat_jit_size
+      const int c = failed ? rc : (words + 1 + mtgp::kJitTrigExecuted * trig);
+      jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
+    }
+  }
+}
+
 // The serial flatten_tree for the programs k_flatten flagged (a row reached from two parents):
 // a small grid strides over all programs, so the private row table it needs is allocated for few
 // waves only.
@@ -2313,7 +2407,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
                                                      MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                      int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                      int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
-                                                     int32_t* jit_cost_out, int jit_mode) {
+                                                     int32_t* jit_cost_out, int jit_mode, JitOpTable optab) {
   using namespace mtgp;
   constexpr int RPL = NMAX / kWave;  // rows per lane
   __shared__ uint32_t s_w[NMAX];   // packed row record (u_pack)
@@ -2564,12 +2658,16 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       s_prog[n > 0 ? n : 0] = e;
       len_out[pj] = n > 0 ? n : 0;
       status_out[pj] = n > 0 ? 0 : -n;
-      flat_jit_size(s_prog, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
+      if (jit_mode != kJitModeRegs) flat_jit_size(s_prog, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
     }
   }
-  // node count (gp.py:424 parsimony): tree t of the individual is counted by its program t % n_prog
+  if (!shared && jit_mode == kJitModeRegs && (jit_words_out || jit_cost_out))  // (shared: wave-uniform)
+    flat_jit_size_wave<(2 * NMAX + 8 + kWave - 1) / kWave>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
+  // node count (gp.py:424 parsimony): the individual's first program counts all T trees and
+  // stores the sum (no atomics, no zeroing pass before the launch)
+  if (j != 0) return;
   int c = 0;
-  for (int t = j; t < T; t += n_prog) {
+  for (int t = 0; t < T; ++t) {
     if (t == sp.tree) { c += cnt; continue; }
     const float4* tt = reinterpret_cast<const float4*>(pop + ((size_t)p * T + t) * N * 4);
 #pragma unroll
@@ -2578,7 +2676,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       c += __popcll(__ballot(i < N && tt[i < N ? i : 0].x != 0.0f));
     }
   }
-  if (lane == 0 && c != 0) atomicAdd(&nodes_out[p], c);
+  if (lane == 0) nodes_out[p] = c;
 }
 
 // --------------------------------------------------------------------------------------
@@ -2922,6 +3020,10 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restric
 __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
                                                         uint64_t code_bytes) {
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared sin/cos subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SIN_WORDS; k += blockDim.x) code[mtgp::kJitSinOffset / 4 + k] = mtgp_jit_sin_blob[k];
+    for (int k = threadIdx.x; k < MTGP_JIT_COS_WORDS; k += blockDim.x) code[mtgp::kJitCosOffset / 4 + k] = mtgp_jit_cos_blob[k];
+  }
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)U.n_units * U.G) return;
   const int u = (int)(i / U.G), g = (int)(i - (long)u * U.G);
@@ -3050,37 +3152,49 @@ hsa_status_t jit_find_pool(hsa_amd_memory_pool_t p, void* data) {
 
 #endif  // MTGP_TU_MAIN
 
-// Kernel timing (mtgp_set_timing / mtgp_last_kernel_ms): the switch is process-wide, the event
-// pair and the "last launch" record are per host thread and re-created when the thread moves to
-// another device, so concurrent callers on different threads / streams / devices never share
-// events.
+// Kernel timing (mtgp_set_timing / mtgp_last_kernel_ms / mtgp_kernel_ms_history): the switch is
+// process-wide; the event pairs (a ring of the last kTimingRing launches, so a caller can read the
+// durations of a whole run after one synchronisation instead of stalling the queue every launch)
+// are per host thread and re-created when the thread moves to another device, so concurrent callers
+// on different threads / streams / devices never share events.
 std::atomic<bool> g_timing{false};
+constexpr int kTimingRing = 1024;
 struct TimingState {
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t ev0[kTimingRing] = {}, ev1[kTimingRing] = {};
   int device = -1;
-  bool have = false;
+  long long count = 0;  // timed launches recorded on `device`
+  void reset(int dev) {
+    for (int i = 0; i < kTimingRing; ++i)
+      if (ev0[i]) { (void)hipEventDestroy(ev0[i]); (void)hipEventDestroy(ev1[i]); ev0[i] = ev1[i] = nullptr; }
+    device = dev;
+    count = 0;
+  }
 };
 thread_local TimingState t_timing;
+
+float timing_ms(const TimingState& ts, long long i) {
+  const int k = (int)(i % kTimingRing);
+  float ms = -1.0f;
+  (void)hipEventElapsedTime(&ms, ts.ev0[k], ts.ev1[k]);
+  return ms;
+}
 
 template <class F>
 int launch_timed(F&& launch, hipStream_t s) {
   const bool timing = g_timing.load(std::memory_order_relaxed);
   TimingState& ts = t_timing;
+  int k = 0;
   if (timing) {
     int dev = -1;
     (void)hipGetDevice(&dev);
-    if (!ts.ev0 || ts.device != dev) {
-      if (ts.ev0) { (void)hipEventDestroy(ts.ev0); (void)hipEventDestroy(ts.ev1); }
-      (void)hipEventCreate(&ts.ev0);
-      (void)hipEventCreate(&ts.ev1);
-      ts.device = dev;
-      ts.have = false;
-    }
-    (void)hipEventRecord(ts.ev0, s);
+    if (ts.device != dev) ts.reset(dev);
+    k = (int)(ts.count % kTimingRing);
+    if (!ts.ev0[k]) { (void)hipEventCreate(&ts.ev0[k]); (void)hipEventCreate(&ts.ev1[k]); }
+    (void)hipEventRecord(ts.ev0[k], s);
   }
   launch();
   if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
-  if (timing) { (void)hipEventRecord(ts.ev1, s); ts.have = true; }
+  if (timing) { (void)hipEventRecord(ts.ev1[k], s); ++ts.count; }
   return MTGP_OK;
 }
 
@@ -3324,8 +3438,7 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   }
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(k_jit_templates, dim3(1), dim3(256), 0, s, (uint32_t*)code, (uint64_t)code_bytes);
-  const long threads = (long)U.n_units * U.G;
+  const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
   hipLaunchKernelGGL(k_jit_emit_groups, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, U, jit_words, offsets,
                      (uint32_t*)code, (uint64_t)code_bytes);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
@@ -3410,11 +3523,22 @@ int mtgp_set_timing(int enabled) {
 
 float mtgp_last_kernel_ms(void) {
   const TimingState& ts = t_timing;  // this thread's last timed launch
-  if (!ts.have) return -1.0f;
-  float ms = -1.0f;
-  (void)hipEventSynchronize(ts.ev1);
-  (void)hipEventElapsedTime(&ms, ts.ev0, ts.ev1);
-  return ms;
+  if (ts.count == 0) return -1.0f;
+  (void)hipEventSynchronize(ts.ev1[(ts.count - 1) % kTimingRing]);
+  return timing_ms(ts, ts.count - 1);
+}
+
+int mtgp_kernel_ms_history(float* out, int32_t n) {
+  const TimingState& ts = t_timing;
+  if (!out || n < 0) return MTGP_ERR_ARG;
+  long long avail = ts.count < kTimingRing ? ts.count : kTimingRing;
+  if (n > avail) n = (int32_t)avail;
+  if (n == 0) return 0;
+  for (int32_t i = 0; i < n; ++i) {  // the launches may sit on different streams: wait for each
+    (void)hipEventSynchronize(ts.ev1[(ts.count - n + i) % kTimingRing]);
+    out[i] = timing_ms(ts, ts.count - n + i);
+  }
+  return n;
 }
 
 int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, const MtgpNodeLibrary* lib,
@@ -3430,7 +3554,6 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   hipStream_t s = (hipStream_t)stream;
   const long total = (long)P * n_prog;
   MtgpNodeLibrary libv = *lib;
-  if (hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
   static const int lanes_env = [] {  // A/B knob (scripts/): MTGP_FLAT_LANES=8|16|32 at run time
     const char* e = getenv("MTGP_FLAT_LANES");
     const int v = e ? atoi(e) : MTGP_FLAT_LANES;
@@ -3440,7 +3563,10 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   // MTGP_FLAT_MODE=lane at run time
   const char* fm = getenv("MTGP_FLAT_MODE");
   const bool wave_mode = !(fm && strcmp(fm, "lane") == 0);
+  static const JitOpTable optab = jit_op_table();  // (host probe of jit_program, once per process)
   if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
+  // the lane-per-program kernel sums node counts with atomics; the wave kernel stores them
+  if (!wave_mode && hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
 #define MTGP_FLAT_ONE(NM, TP)                                                                                 \
   hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
                      T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
@@ -3451,7 +3577,7 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
     if (wave_mode)                                                                                          \
       hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)total), dim3(kWave), 0, s, population, P, T, N, \
                          libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,  \
-                         jit_cost_out, jit_mode);                                                           \
+                         jit_cost_out, jit_mode, optab);                                                    \
     else if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                               \
     else if (tp >= 16) MTGP_FLAT_ONE(NM, 16);                                                               \
     else MTGP_FLAT_ONE(NM, 8);                                                                              \

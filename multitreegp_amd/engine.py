@@ -71,7 +71,8 @@ class DeviceEngine:
         self._arenas = [None, None]  # (pointer, bytes): a ring of two executable code buffers
         self._arena_i = 0
         self._arena_gen = [0, 0]     # bumped whenever a slot is (re)written: stale Flattened code is rebuilt
-        self._jit_last = None        # (pinned host info, event) of the previous build: capacity hint
+        self._jit_last = None        # (pinned host info, event, units) of a sampled build: capacity hint
+        self._jit_builds = 0
         self._jit_bytes_per_unit = None  # learnt from earlier plans (None: estimate from G)
 
     def __del__(self):
@@ -127,12 +128,13 @@ class DeviceEngine:
         if n < 0:
             return None
         optr = None if order is None else order.data_ptr()
-        if self._jit_last is not None and self._jit_last[1].query():  # previous plan done: learn its size
-            err, total, n_prev = (int(v) for v in self._jit_last[0].tolist())
-            if err == 0 and n_prev > 0:
-                self._jit_bytes_per_unit = total / n_prev * 1.5
+        if self._jit_last is not None and self._jit_last[1].query():  # previous readback done: learn its size
+            err, total = (int(v) for v in self._jit_last[0].tolist())
+            if err == 0 and self._jit_last[2] > 0:
+                self._jit_bytes_per_unit = total / self._jit_last[2] * 1.5
+            self._jit_last = None
         offs = torch.empty((n + 1,), dtype=torch.int32, device=self.device)
-        info = torch.empty((3,), dtype=torch.int32, device=self.device)
+        info = torch.empty((2,), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device).cuda_stream
         if fl.jit_words is not None:  # sizes from the flatten pass
             rc = self.native.mtgp_jit_plan_words_chain(fl.jit_words.data_ptr(), P, fl.n_prog, R, optr,
@@ -142,12 +144,15 @@ class DeviceEngine:
                                            info.data_ptr(), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_plan failed: {rc}")
-        info[2].fill_(n)
-        host = torch.empty((3,), dtype=torch.int32, pin_memory=True)
-        host.copy_(info, non_blocking=True)
-        ev = torch.cuda.Event()
-        ev.record()
-        self._jit_last = (host, ev)
+        self._jit_builds += 1
+        if self._jit_last is None and (self._jit_bytes_per_unit is None or self._jit_builds % 8 == 0):
+            # asynchronous readback of the plan's code size (every 8th build once learned: the
+            # device checks the capacity itself, this only tunes the arena estimate)
+            host = torch.empty((2,), dtype=torch.int32, pin_memory=True)
+            host.copy_(info, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            self._jit_last = (host, ev, n)
         G = 64 // (1 << max(R - 1, 0).bit_length())
         per_unit = self._jit_bytes_per_unit or 1024.0 * G
         ptr, size = self._arena(int(n * per_unit) + 4096)

@@ -100,3 +100,25 @@ def test_population_not_multiple_of_pack():
     d = eng.prepare_data(data)
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
     assert bits_equal(res["fitness"].cpu().numpy(), ref["fitness"])
+
+
+def test_kernel_timing_history():
+    """mtgp_kernel_ms_history: the durations of the last n timed evaluator launches, oldest first,
+    read with one synchronisation after the run (bench.py's timed loop never stalls the queue)."""
+    import ctypes
+    env, lib, ff, data, pop = dynamic_setup(P=16, R=8, n_steps=40)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    nat_lib = eng.native
+    nat_lib.mtgp_set_timing(1)
+    try:
+        pd = torch.from_numpy(pop).cuda()
+        for _ in range(3):
+            eng.evaluate(pd, data, check=False)
+        out = (ctypes.c_float * 5)()
+        assert nat_lib.mtgp_kernel_ms_history(out, 3) == 3
+        ms = list(out)[:3]
+        assert all(m > 0 for m in ms)
+        assert ms[-1] == nat_lib.mtgp_last_kernel_ms()
+        assert 3 <= nat_lib.mtgp_kernel_ms_history(out, 5) <= 5
+    finally:
+        nat_lib.mtgp_set_timing(0)
