@@ -3049,6 +3049,91 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
                        U.next, U.cond, U.store, U.pipe != 0);
 }
 
+// Register-data emit with one WAVE per (unit, group): as in k_flatten_wave's sizing, an
+// instruction's code depends only on its opcode, the operand-stack depth before it and its byte
+// address (the PC-relative sin/cos calls), so the lanes translate instructions l, l + 64, ... in
+// isolation (jit_program with that depth and base) at offsets from a prefix sum of the JitOpTable
+// word counts -- the same words jit_unit_group writes serially (tests/test_gpu_build.py).  Lane 0
+// writes the group's frame (the v25 keep, the lane-group select, the unit end).
+template <int KI>
+__global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int32_t* __restrict__ jw,
+                                                        const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
+                                                        uint64_t code_bytes, JitOpTable optab) {
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared sin/cos subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SIN_WORDS; k += blockDim.x) code[mtgp::kJitSinOffset / 4 + k] = mtgp_jit_sin_blob[k];
+    for (int k = threadIdx.x; k < MTGP_JIT_COS_WORDS; k += blockDim.x) code[mtgp::kJitCosOffset / 4 + k] = mtgp_jit_cos_blob[k];
+  }
+  const int lane = threadIdx.x & (kWave - 1);
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave;  // (wave-uniform)
+  if (i >= (long)U.n_units * U.G) return;
+  const int u = (int)(i / U.G), g = (int)(i - (long)u * U.G);
+  const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  const int q = wave * U.G + g;
+  if (q >= U.P) return;
+  const uint32_t b = offs[u], e = offs[u + 1];
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
+  uint32_t start = 0;  // words before group g inside the unit
+  for (int h = 0; h < g; ++h) {
+    const int ind = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
+    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (h > 0 ? 7u : 0u);
+  }
+  const bool last = (g == U.G - 1) || (q + 1 >= U.P);
+  const uint32_t at = b + start * 4u;  // byte address of the group's first word
+  uint32_t* out = code + at / 4;
+  const int ind = U.order ? U.order[q] : q;
+  const MtgpInstr* prog = U.prog + ((size_t)ind * U.n_prog + j) * U.L;
+  const int pre = g > 0 ? 1 : 0;  // v_mov v25, v8
+  MtgpInstr end;
+  end.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+  end.imm = 0.0f;
+  int woff = 0, sp = 0;  // words and stack depth before this chunk
+  bool ended = false;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    if (ended) break;  // (wave-uniform)
+    const int ii = k * kWave + lane;
+    const MtgpInstr x = ii < U.L ? prog[ii] : end;
+    const uint32_t c = x.op >> MTGP_OP_SHIFT;
+    const uint64_t ends = __ballot(c == (uint32_t)MTGP_OP_END);
+    const int first_end = ends ? __ffsll((unsigned long long)ends) - 1 : kWave;
+    const bool in = lane < first_end;
+    const uint32_t f = (in && c < 64u) ? optab.flags[c] : 0u;
+    const int w = (in && c < 64u) ? optab.words[c] : 0;
+    const int d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
+    int wi = w, di = d;  // inclusive prefix sums over the chunk
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int vw = __shfl_up(wi, off), vd = __shfl_up(di, off);
+      if (lane >= off) { wi += vw; di += vd; }
+    }
+    if (in) {
+      const MtgpInstr t[2] = {x, end};
+      mtgp::JitOut o{out + pre + woff + (wi - w), 0};
+      o.base = at + (uint32_t)(pre + woff + (wi - w)) * 4u;
+      (void)mtgp::jit_program(o, t, 2, false, mtgp::kJitModeRegs, 0, mtgp::kJitPre, 0, nullptr, sp + di - d);
+    }
+    woff += __shfl(wi, kWave - 1);
+    sp += __shfl(di, kWave - 1);
+    ended = ends != 0ull;
+  }
+  if (lane == 0) {
+    mtgp::JitOut o{out, 0};
+    o.base = at;
+    if (g > 0) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
+    o.n = pre + woff;
+    if (g > 0) {
+      const uint64_t mask = ((1ull << U.Rp) - 1ull) << (g * U.Rp);
+      o.w(mtgp::kMovS42);
+      o.w((uint32_t)mask);
+      o.w(mtgp::kMovS43);
+      o.w((uint32_t)(mask >> 32));
+      o.w(mtgp::kSelLo);
+      o.w(mtgp::kSelHi);
+    }
+    if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);
+  }
+}
+
 // the shared sin/cos subroutines at the start of the code buffer
 __global__ void __launch_bounds__(256) k_jit_templates(uint32_t* __restrict__ code, uint64_t code_bytes) {
   if (code_bytes < mtgp::kJitTemplateBytes) return;
@@ -3439,6 +3524,18 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
+  static const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread (one thread per group)
+  if (U.mode == mtgp::kJitModeRegs && !(ew && strcmp(ew, "thread") == 0) && U.L <= 5 * kWave) {
+    static const JitOpTable optab = jit_op_table();
+    const long wthreads = threads * kWave;
+    if (U.L <= 3 * kWave)
+      hipLaunchKernelGGL(k_jit_emit_waves<3>, dim3((unsigned)((wthreads + 255) / 256)), dim3(256), 0, s, U, jit_words,
+                         offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    else
+      hipLaunchKernelGGL(k_jit_emit_waves<5>, dim3((unsigned)((wthreads + 255) / 256)), dim3(256), 0, s, U, jit_words,
+                         offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  }
   hipLaunchKernelGGL(k_jit_emit_groups, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, U, jit_words, offsets,
                      (uint32_t*)code, (uint64_t)code_bytes);
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
