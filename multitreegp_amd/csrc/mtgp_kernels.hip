@@ -2402,26 +2402,46 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
 //     counter; only in arbitrary arrays) leaves the program to k_flatten_serial.
 // The tables are per wave in LDS (24 B per row), so the occupancy no longer falls with N (the
 // lane-per-tree kernel needs 16 B x N per LANE).  Output = k_flatten's word for word.
+// the kernel's waves are independent; LDS written by a wave is read back by the same wave
+// (in issue order), so only the compiler must not move LDS accesses across this point.  One wave
+// per block: with 4 per block the flatten took 90 us instead of 71 at C3 (a block's LDS and wave
+// slots stay allocated until its slowest program is done; r02/v18).
+constexpr int kFlatWaves = 1;
+__device__ __forceinline__ void flat_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 template <int NMAX>
-__global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
+__global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
                                                      MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                      int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                      int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
                                                      int32_t* jit_cost_out, int jit_mode, JitOpTable optab) {
   using namespace mtgp;
   constexpr int RPL = NMAX / kWave;  // rows per lane
-  __shared__ uint32_t s_w[NMAX];   // packed row record (u_pack)
-  __shared__ uint32_t s_len[NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
-  __shared__ float s_cv[NMAX];     // folded constant
-  __shared__ float s_val[NMAX];    // the original value column (operands j >= i, gp.py:366-369)
-  __shared__ int32_t s_pos[NMAX];  // pass 2: first word of the node's code | push << 16
-  __shared__ uint32_t s_flag[NMAX];  // pass 1: resolved; pass 2: times reached
-  __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
-  __shared__ MtgpInstr s_prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
-  const int lane = threadIdx.x;
+  // kFlatWaves independent waves per block, each with its own LDS tables (wave-level syncs only)
+  __shared__ uint32_t s_w_all[kFlatWaves][NMAX];   // packed row record (u_pack)
+  __shared__ uint32_t s_len_all[kFlatWaves][NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
+  __shared__ float s_cv_all[kFlatWaves][NMAX];     // folded constant
+  __shared__ float s_val_all[kFlatWaves][NMAX];    // the original value column (operands j >= i, gp.py:366-369)
+  __shared__ int32_t s_pos_all[kFlatWaves][NMAX];  // pass 2: first word of the node's code | push << 16
+  __shared__ uint32_t s_flag_all[kFlatWaves][NMAX];  // pass 1: resolved; pass 2: times reached
+  __shared__ int8_t s_fn_all[kFlatWaves][MTGP_MAX_FUNCS];
+  __shared__ MtgpInstr s_prog_all[kFlatWaves][NMAX + 8];  // the program as written (read back by the JIT sizing)
+  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
+  uint32_t* s_w = s_w_all[wv];
+  uint32_t* s_len = s_len_all[wv];
+  float* s_cv = s_cv_all[wv];
+  float* s_val = s_val_all[wv];
+  int32_t* s_pos = s_pos_all[wv];
+  uint32_t* s_flag = s_flag_all[wv];
+  int8_t* s_fn = s_fn_all[wv];
+  MtgpInstr* s_prog = s_prog_all[wv];
   for (int k = lane; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
-  const long pj = blockIdx.x;
-  if (pj >= (long)P * n_prog) return;  // (uniform: one wave per block)
+  const long pj = (long)blockIdx.x * kFlatWaves + wv;
+  if (pj >= (long)P * n_prog) return;  // (wave-uniform; no block-wide barrier below)
   const int p = (int)(pj / n_prog), j = (int)(pj % n_prog);
   const MtgpProgramSpec sp = specs[j];
   const float4* tr = reinterpret_cast<const float4*>(pop + ((size_t)p * T + sp.tree) * N * 4);
@@ -2496,7 +2516,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
   }
   // ---- pass 1, later rounds: an operator row resolves once its operand rows (j < i) have
   for (;;) {
-    __syncthreads();
+    flat_wave_sync();
     bool ready[RPL], pend = false;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
@@ -2548,7 +2568,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       s_len[i] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
       s_cv[i] = cv;
     }
-    __syncthreads();  // every read of this round's flags precedes the new ones
+    flat_wave_sync();  // every read of this round's flags precedes the new ones
 #pragma unroll
     for (int k = 0; k < RPL; ++k)
       if (ready[k]) {
@@ -2572,10 +2592,10 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
         out[0] = s_prog[0] = u_load(x, false);
       }
     } else {
-      __syncthreads();
+      flat_wave_sync();
 #pragma unroll
       for (int k = 0; k < RPL; ++k) s_flag[k * kWave + lane] = 0u;
-      __syncthreads();
+      flat_wave_sync();
       if (lane == 0) {
         s_flag[N - 1] = 1u;
         s_pos[N - 1] = 0;
@@ -2584,7 +2604,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
 #pragma unroll
       for (int k = 0; k < RPL; ++k) emitted[k] = false;
       for (;;) {
-        __syncthreads();
+        flat_wave_sync();
         bool go[RPL], any = false;
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
@@ -2593,7 +2613,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
           any = any || go[k];
         }
         if (!__any(any)) break;
-        __syncthreads();  // every row's go decision precedes this round's visits
+        flat_wave_sync();  // every row's go decision precedes this round's visits
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
           if (!go[k]) continue;
@@ -2645,7 +2665,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
     }
   }
   shared = __any(shared);
-  __syncthreads();  // every lane's program words (LDS copy) precede the END and the JIT sizing
+  flat_wave_sync();  // every lane's program words (LDS copy) precede the END and the JIT sizing
   if (lane == 0) {
     if (shared) {  // arbitrary arrays only: the serial walk duplicates the shared subtree
       len_out[pj] = 0;
@@ -3672,7 +3692,8 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
     if (wave_mode)                                                                                          \
-      hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)total), dim3(kWave), 0, s, population, P, T, N, \
+      hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)((total + kFlatWaves - 1) / kFlatWaves)),     \
+                         dim3(kWave * kFlatWaves), 0, s, population, P, T, N,                               \
                          libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,  \
                          jit_cost_out, jit_mode, optab);                                                    \
     else if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                               \
