@@ -2391,6 +2391,11 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
   if (c != 0) atomicAdd(&nodes_out[p], c);
 }
 
+// Trees per individual up to which k_flatten_wave stores node counts directly (see its end).
+// (Four independent waves per flatten block with wave-level syncs measured slower: 90 vs 71 us at
+// C3, a block holds its LDS and wave slots until its slowest program is done; r02/v18.)
+constexpr int kFlatDirectTrees = 8;
+
 // Flatten, one WAVE per (individual, program spec): lane l owns rows l, l + 64, ... (NMAX / 64 per
 // lane), loaded with one coalesced 1-KB read per 64 rows.  The same two passes as k_flatten, but
 // level-synchronous over the tree instead of serial over the rows:
@@ -2402,46 +2407,26 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
 //     counter; only in arbitrary arrays) leaves the program to k_flatten_serial.
 // The tables are per wave in LDS (24 B per row), so the occupancy no longer falls with N (the
 // lane-per-tree kernel needs 16 B x N per LANE).  Output = k_flatten's word for word.
-// the kernel's waves are independent; LDS written by a wave is read back by the same wave
-// (in issue order), so only the compiler must not move LDS accesses across this point.  One wave
-// per block: with 4 per block the flatten took 90 us instead of 71 at C3 (a block's LDS and wave
-// slots stay allocated until its slowest program is done; r02/v18).
-constexpr int kFlatWaves = 1;
-__device__ __forceinline__ void flat_wave_sync() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 template <int NMAX>
-__global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
+__global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
                                                      MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                      int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                      int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
                                                      int32_t* jit_cost_out, int jit_mode, JitOpTable optab) {
   using namespace mtgp;
   constexpr int RPL = NMAX / kWave;  // rows per lane
-  // kFlatWaves independent waves per block, each with its own LDS tables (wave-level syncs only)
-  __shared__ uint32_t s_w_all[kFlatWaves][NMAX];   // packed row record (u_pack)
-  __shared__ uint32_t s_len_all[kFlatWaves][NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
-  __shared__ float s_cv_all[kFlatWaves][NMAX];     // folded constant
-  __shared__ float s_val_all[kFlatWaves][NMAX];    // the original value column (operands j >= i, gp.py:366-369)
-  __shared__ int32_t s_pos_all[kFlatWaves][NMAX];  // pass 2: first word of the node's code | push << 16
-  __shared__ uint32_t s_flag_all[kFlatWaves][NMAX];  // pass 1: resolved; pass 2: times reached
-  __shared__ int8_t s_fn_all[kFlatWaves][MTGP_MAX_FUNCS];
-  __shared__ MtgpInstr s_prog_all[kFlatWaves][NMAX + 8];  // the program as written (read back by the JIT sizing)
-  const int lane = threadIdx.x & (kWave - 1), wv = threadIdx.x / kWave;
-  uint32_t* s_w = s_w_all[wv];
-  uint32_t* s_len = s_len_all[wv];
-  float* s_cv = s_cv_all[wv];
-  float* s_val = s_val_all[wv];
-  int32_t* s_pos = s_pos_all[wv];
-  uint32_t* s_flag = s_flag_all[wv];
-  int8_t* s_fn = s_fn_all[wv];
-  MtgpInstr* s_prog = s_prog_all[wv];
+  __shared__ uint32_t s_w[NMAX];   // packed row record (u_pack)
+  __shared__ uint32_t s_len[NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
+  __shared__ float s_cv[NMAX];     // folded constant
+  __shared__ float s_val[NMAX];    // the original value column (operands j >= i, gp.py:366-369)
+  __shared__ int32_t s_pos[NMAX];  // pass 2: first word of the node's code | push << 16
+  __shared__ uint32_t s_flag[NMAX];  // pass 1: resolved; pass 2: times reached
+  __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
+  __shared__ MtgpInstr s_prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
+  const int lane = threadIdx.x;
   for (int k = lane; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
-  const long pj = (long)blockIdx.x * kFlatWaves + wv;
-  if (pj >= (long)P * n_prog) return;  // (wave-uniform; no block-wide barrier below)
+  const long pj = blockIdx.x;
+  if (pj >= (long)P * n_prog) return;  // (uniform: one wave per block)
   const int p = (int)(pj / n_prog), j = (int)(pj % n_prog);
   const MtgpProgramSpec sp = specs[j];
   const float4* tr = reinterpret_cast<const float4*>(pop + ((size_t)p * T + sp.tree) * N * 4);
@@ -2516,7 +2501,7 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
   }
   // ---- pass 1, later rounds: an operator row resolves once its operand rows (j < i) have
   for (;;) {
-    flat_wave_sync();
+    __syncthreads();
     bool ready[RPL], pend = false;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
@@ -2568,7 +2553,7 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
       s_len[i] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
       s_cv[i] = cv;
     }
-    flat_wave_sync();  // every read of this round's flags precedes the new ones
+    __syncthreads();  // every read of this round's flags precedes the new ones
 #pragma unroll
     for (int k = 0; k < RPL; ++k)
       if (ready[k]) {
@@ -2592,10 +2577,10 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
         out[0] = s_prog[0] = u_load(x, false);
       }
     } else {
-      flat_wave_sync();
+      __syncthreads();
 #pragma unroll
       for (int k = 0; k < RPL; ++k) s_flag[k * kWave + lane] = 0u;
-      flat_wave_sync();
+      __syncthreads();
       if (lane == 0) {
         s_flag[N - 1] = 1u;
         s_pos[N - 1] = 0;
@@ -2604,7 +2589,7 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
 #pragma unroll
       for (int k = 0; k < RPL; ++k) emitted[k] = false;
       for (;;) {
-        flat_wave_sync();
+        __syncthreads();
         bool go[RPL], any = false;
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
@@ -2613,7 +2598,7 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
           any = any || go[k];
         }
         if (!__any(any)) break;
-        flat_wave_sync();  // every row's go decision precedes this round's visits
+        __syncthreads();  // every row's go decision precedes this round's visits
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
           if (!go[k]) continue;
@@ -2665,7 +2650,7 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
     }
   }
   shared = __any(shared);
-  flat_wave_sync();  // every lane's program words (LDS copy) precede the END and the JIT sizing
+  __syncthreads();  // every lane's program words (LDS copy) precede the END and the JIT sizing
   if (lane == 0) {
     if (shared) {  // arbitrary arrays only: the serial walk duplicates the shared subtree
       len_out[pj] = 0;
@@ -2683,11 +2668,14 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
   }
   if (!shared && jit_mode == kJitModeRegs && (jit_words_out || jit_cost_out))  // (shared: wave-uniform)
     flat_jit_size_wave<(2 * NMAX + 8 + kWave - 1) / kWave>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
-  // node count (gp.py:424 parsimony): the individual's first program counts all T trees and
-  // stores the sum (no atomics, no zeroing pass before the launch)
-  if (j != 0) return;
+  // node count (gp.py:424 parsimony).  Few trees (T <= kFlatDirectTrees): the individual's first
+  // program counts them all and stores the sum (no zeroing pass before the launch); many trees
+  // (C5: 64): tree t is counted by program t % n_prog and summed with atomics into the zeroed
+  // nodes_out, so no single wave walks the whole individual.
+  const bool direct = T <= kFlatDirectTrees;
+  if (direct && j != 0) return;
   int c = 0;
-  for (int t = 0; t < T; ++t) {
+  for (int t = direct ? 0 : j; t < T; t += direct ? 1 : n_prog) {
     if (t == sp.tree) { c += cnt; continue; }
     const float4* tt = reinterpret_cast<const float4*>(pop + ((size_t)p * T + t) * N * 4);
 #pragma unroll
@@ -2696,7 +2684,10 @@ __global__ void __launch_bounds__(64 * kFlatWaves) k_flatten_wave(const float* _
       c += __popcll(__ballot(i < N && tt[i < N ? i : 0].x != 0.0f));
     }
   }
-  if (lane == 0) nodes_out[p] = c;
+  if (lane == 0) {
+    if (direct) nodes_out[p] = c;
+    else if (c != 0) atomicAdd(&nodes_out[p], c);
+  }
 }
 
 // --------------------------------------------------------------------------------------
@@ -3682,8 +3673,9 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   const bool wave_mode = !(fm && strcmp(fm, "lane") == 0);
   static const JitOpTable optab = jit_op_table();  // (host probe of jit_program, once per process)
   if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
-  // the lane-per-program kernel sums node counts with atomics; the wave kernel stores them
-  if (!wave_mode && hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+  // node counts are summed with atomics into zeros, except by the wave kernel for few trees
+  if ((!wave_mode || T > kFlatDirectTrees) && hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess)
+    return MTGP_ERR_LAUNCH;
 #define MTGP_FLAT_ONE(NM, TP)                                                                                 \
   hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
                      T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
@@ -3692,8 +3684,7 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
     if (wave_mode)                                                                                          \
-      hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)((total + kFlatWaves - 1) / kFlatWaves)),     \
-                         dim3(kWave * kFlatWaves), 0, s, population, P, T, N,                               \
+      hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)total), dim3(kWave), 0, s, population, P, T, N, \
                          libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,  \
                          jit_cost_out, jit_mode, optab);                                                    \
     else if (tp >= 32) MTGP_FLAT_ONE(NM, 32);                                                               \
