@@ -50,38 +50,38 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-pmc", action="store_true",
                     help="skip the live rocprofv3 PMC passes (HBM traffic, VALU issue) of the dominant kernel")
+    ap.add_argument("--e2e-steps", type=int, default=20,
+                    help="timed GeneticProgramming.evaluate_population calls from host numpy (H2D + flatten + "
+                         "kernel + all-gather + D2H; SURVEY §8(d) end-to-end); 0 skips")
     a = ap.parse_args()
-    defaults = {"c2": (1024, 16), "c3": (8192, 32), "c5": (4096, 8)}[a.config]
-    a.pop = a.pop or defaults[0]
-    a.rollouts = a.rollouts or defaults[1]
+    apply_config_defaults(a)
+    return a
+
+
+# (individuals per GPU, rollouts) of each BASELINE configuration
+CONFIG_DEFAULTS = {"c2": (1024, 16), "c3": (8192, 32), "c5": (4096, 8)}
+
+
+def apply_config_defaults(a):
+    """--pop / --rollouts default to the configuration's own sizes (bench.py and scripts/kprof.py)"""
+    pop, R = CONFIG_DEFAULTS[a.config]
+    a.pop = a.pop or pop
+    a.rollouts = a.rollouts or R
     return a
 
 
 def _cached_population(name, make):
-    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mtgp_pop_{name}.npy")
+    """Sampled populations are cached under TMPDIR (the C5 population takes ~15 s to sample).
+    The sampler is vectorised (sampling.sample_trees_batch), so no worker pool is ever forked:
+    bench and scripts/kprof.py run under rocprofv3, whose signal handlers a forked pool inherits."""
+    cache = os.path.join(os.environ.get("TMPDIR", "/tmp"), f"mtgp_pop_v2_{name}.npy")
     if os.path.exists(cache):
         return np.load(cache)
     pop = make()
     os.makedirs(os.path.dirname(cache), exist_ok=True)
-    np.save(cache, pop)
+    np.save(cache + ".tmp.npy", pop)
+    os.replace(cache + ".tmp.npy", cache)
     return pop
-
-
-def _sample_block(job):
-    from multitreegp_amd.sampling import sample_population
-    seed, lib, n, depth, nodes = job
-    return sample_population(seed, lib, n, 1, max_init_depth=depth, max_nodes=nodes)[0]
-
-
-def _parallel_population(seed, lib, P, depth, nodes, block=256):
-    """Reference-distribution trees, sampled in blocks of `block` individuals (seed + block id)."""
-    import multiprocessing as mp
-    jobs = [(seed * 100003 + b, lib, min(block, P - b * block), depth, nodes) for b in range((P + block - 1) // block)]
-    workers = min(16, len(jobs), os.cpu_count() or 1)
-    if workers <= 1:
-        return np.concatenate([_sample_block(j) for j in jobs])
-    with mp.get_context("fork").Pool(workers) as pool:
-        return np.concatenate(pool.map(_sample_block, jobs))
 
 
 def setup_workload(args, rank):
@@ -97,7 +97,8 @@ def setup_workload(args, rank):
         ts = (np.arange(args.ode_steps + 1, dtype=np.float32) * np.float32(0.01)).astype(np.float32)
         data = (x0, ts, mt.ground_truth(env, x0, ts), np.zeros((args.rollouts, 2), np.uint32))
         pop = _cached_population(f"c5_{args.pop}_r{rank}",
-                                 lambda: _parallel_population(2000 + rank, lib, args.pop, 16, 128))
+                                 lambda: sample_population(2000 + rank, lib, args.pop, 1, max_init_depth=16,
+                                                           max_nodes=128)[0])
         return env, lib, ff, data, pop
     env = mt.Acrobot(0.0, getattr(args, "obs_noise", 0.0))
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
@@ -159,10 +160,19 @@ def pmc_passes(args, kernel_substr):
             cmd = ["timeout", "-s", "KILL", "90", rp, "--pmc", *counters, "-d", sub, "-o", "p",
                    "--output-format", "csv"] + cmd_tail
             try:
-                subprocess.run(cmd, check=True, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=120)
-            except Exception:
+                r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, timeout=120)
+            except Exception as e:  # the pass is reported (stderr), the field stays null
+                print(f"bench: PMC pass {counters} failed: {e!r}", file=sys.stderr)
                 return None
-            out.update(collect(sub, kernel_substr))
+            if r.returncode != 0:
+                tail = r.stdout.decode(errors="replace")[-1500:]
+                print(f"bench: PMC pass {counters} exited {r.returncode}:\n{tail}", file=sys.stderr)
+                return None
+            got = collect(sub, kernel_substr)
+            if not got.get("dispatches"):
+                print(f"bench: PMC pass {counters}: no dispatch of {kernel_substr!r} in the profile", file=sys.stderr)
+                return None
+            out.update(got)
     need = ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU", "GRBM_GUI_ACTIVE")
     return out if all(k in out for k in need) else None
 
@@ -196,6 +206,39 @@ def cpu_baseline(args, lib, ff, data, pop, steps=None):
                       f"{args.config.upper()} workload, "
                       f"trajectories on, oracle/mtgp_oracle.c row-order interpreter, {threads} OpenMP threads "
                       f"of {os.cpu_count()} on {cpu_model()}, {dt:.2f} s"}
+
+
+def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
+    """SURVEY §8(d) end-to-end rate: GeneticProgramming.evaluate_population (gp.py:403-433) on a
+    host numpy population of P*ws individuals, as the user's loop calls it -- H2D copy of this
+    rank's block, device flatten + schedule + JIT + fused kernel, fitness all-gather, D2H, argmin
+    and best-so-far bookkeeping.  Each rank's block is its own population (the array is the rank's
+    population tiled ws times), so the work per rank equals the kernel-resident line's."""
+    import torch
+    import torch.distributed as dist
+    from multitreegp_amd.genetic_programming import GeneticProgramming
+    P = pop.shape[0]
+    full = np.ascontiguousarray(np.concatenate([pop] * ws)[None]) if ws > 1 else pop[None]
+    gp = GeneticProgramming(1, P * ws, ff, lib.operator_list, lib.variable_list, lib.layer_sizes,
+                            max_nodes=pop.shape[2], migration_percentage=0.0, elite_percentage=0.0, device=dev,
+                            verbose=False)
+    for _ in range(3):
+        gp.evaluate_population(full, data)
+    if ws > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.e2e_steps):
+        fit, _ = gp.evaluate_population(full, data)  # returns host numpy: synchronous per call
+    torch.cuda.synchronize()
+    if ws > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if ws > 1:
+        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    return el * 1e3 / args.e2e_steps, fit
 
 
 def main():
@@ -337,6 +380,17 @@ def main():
             "RK4 h=0.05 x 0", "Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000")
         out["config"]["ode_steps"] = units_per_step / (P * R * ws)  # mean attempts per rollout
         out["config"]["solver"] = "dopri5"
+    if args.e2e_steps > 0:
+        e2e_ms, e2e_fit = end_to_end(args, ff, lib, data, pop, ws, rank, dev)
+        ok = bool(np.array_equal(e2e_fit.reshape(-1)[:P].view(np.uint32), res["fitness"].cpu().numpy().view(np.uint32)))
+        units = (units_per_step if not adaptive else float("nan"))
+        out["end_to_end"] = {
+            "what": "GeneticProgramming.evaluate_population from host numpy: H2D + flatten + schedule + JIT + "
+                    "kernel + fitness all-gather + D2H + best tracking (SURVEY §8(d))",
+            "ms_per_step": e2e_ms, "value": units / (e2e_ms / 1e3) if not adaptive else None,
+            "unit": "ODE-steps/s", "steps": args.e2e_steps, "trajectories": False,
+            "fitness_equal_to_kernel_line": ok,
+            "h2d_bytes_per_rank": int(pop.nbytes)}
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:

@@ -37,6 +37,8 @@ class NodeLibrary:
     def __init__(self, operator_list: Sequence, variable_list: Sequence[Sequence[str]],
                  layer_sizes: Sequence[int]):
         layer_sizes = [int(x) for x in np.asarray(layer_sizes).reshape(-1)]
+        self.operator_list = list(operator_list)  # the constructor arguments, kept for re-use
+        self.variable_list = [list(v) for v in variable_list]
         assert len(operator_list) > 0, "No operators were given"
         assert len(layer_sizes) == len(variable_list), \
             "There is not a set of expressions for every type of layer"

@@ -120,17 +120,82 @@ def sample_tree(rng: np.random.Generator, lib: NodeLibrary, var_mask: np.ndarray
     return out
 
 
+def sample_trees_batch(rng: np.random.Generator, lib: NodeLibrary, var_mask: np.ndarray, B: int,
+                       max_init_depth: int, max_nodes: int, coefficient_sd: float = 1.0,
+                       map_b_to_d: np.ndarray = None) -> np.ndarray:
+    """B independent trees of sample_tree's distribution (initialization.py:9-124), sampled
+    together: the breadth-first loop of sample_node runs once over all B trees with numpy
+    vector operations.  Only breadth-first indices below 2*max_nodes - 1 can hold a node: an
+    operator needs `open_slots < max_nodes - i - 1` (initialization.py:35), so operators sit at
+    i <= max_nodes - 2 and their children at i <= 2*max_nodes - 2 -- the loop stops there (or at
+    2**max_init_depth - 1, or when every tree has no open slot).  -> float32 [B, max_nodes, 4]"""
+    if map_b_to_d is None:
+        map_b_to_d = create_map_b_to_d(max_init_depth)
+    N = max_nodes
+    tree_size = 2 ** max_init_depth - 1
+    I = min(tree_size, 2 * N - 1)
+    slots = np.asarray(lib.slots, dtype=np.int64)
+    op_p = lib.operator_probabilities.astype(np.float64)
+    op_cdf = np.cumsum(op_p / op_p.sum())
+    var_p = np.asarray(var_mask, dtype=np.float64)
+    var_cdf = np.cumsum(var_p / var_p.sum())
+    var_idx = np.asarray(lib.variable_indices, dtype=np.int64)
+    op_idx = np.asarray(lib.operator_indices, dtype=np.int64)
+    f = np.zeros((B, I), dtype=np.int64)
+    coef = np.zeros((B, I), dtype=np.float32)
+    open_slots = np.ones(B, dtype=np.int64)
+    for i in range(I):
+        live = open_slots > 0
+        if not live.any():
+            break
+        c = (rng.standard_normal(B) * coefficient_sd).astype(np.float32)
+        u = rng.random((4, B))
+        depth = (i + 1).bit_length() - 1
+        leaf = np.where(u[0] < 0.5, 1,
+                        var_idx[np.minimum(np.searchsorted(var_cdf, u[1], side="right"), len(var_idx) - 1)])
+        can_op = (open_slots < N - i - 1) & (depth + 1 < max_init_depth) & (u[2] < 0.7 ** depth)
+        op = op_idx[np.minimum(np.searchsorted(op_cdf, u[3], side="right"), len(op_idx) - 1)]
+        index = np.where(can_op, op, leaf)
+        index = np.where(live, index, 0)
+        if i > 0:  # the parent's arity must reach this child (initialization.py:43)
+            pf = f[:, (i + (i % 2) - 2) // 2]
+            index = np.where(slots[pf] + i % 2 > 1, index, 0)
+        f[:, i] = index
+        coef[:, i] = np.where(index == 1, c, 0.0)
+        open_slots = np.where(index == 0, open_slots, np.maximum(0, open_slots + slots[index] - 1))
+    # prune (initialization.py:56-98): non-empty rows, highest depth-first row first, packed at the end
+    rows = map_b_to_d[:I]
+    key = np.where(f != 0, rows[None, :], -1)
+    order = np.argsort(-key, axis=1, kind="stable")
+    rank = np.empty_like(order)
+    np.put_along_axis(rank, order, np.arange(I)[None, :].repeat(B, 0), axis=1)
+    n_keep = (f != 0).sum(1)
+    assert int(n_keep.max(initial=0)) <= N
+    newpos = np.where(f != 0, N - 1 - rank, -1)
+    ch_a = np.minimum(2 * np.arange(I) + 1, I - 1)
+    ch_b = np.minimum(2 * np.arange(I) + 2, I - 1)
+    a_pos = np.where(slots[f] > 0, newpos[:, ch_a], -1)
+    b_pos = np.where(slots[f] > 1, newpos[:, ch_b], -1)
+    out = np.tile(np.array([0.0, -1.0, -1.0, 0.0], dtype=np.float32), (B, N, 1))
+    bb, ii = np.nonzero(f)
+    out[bb, newpos[bb, ii]] = np.stack([f[bb, ii], a_pos[bb, ii], b_pos[bb, ii], coef[bb, ii]], axis=1)
+    return out
+
+
 def sample_population(seed: int, lib: NodeLibrary, population_size: int, num_populations: int = 1,
                       max_init_depth: int = 4, max_nodes: int = 30,
                       coefficient_sd: float = 1.0) -> np.ndarray:
-    """[num_pop, pop, T, N, 4] float32 population (initialize_population, gp.py:298-308)."""
+    """[num_pop, pop, T, N, 4] float32 population (initialize_population, gp.py:298-308): each
+    tree position t sampled for the whole population at once (sample_trees_batch)."""
     rng = np.random.default_rng(seed)
     m = create_map_b_to_d(max_init_depth)
     T = lib.num_trees
-    out = np.zeros((num_populations, population_size, T, max_nodes, 4), dtype=np.float32)
-    for a in range(num_populations):
-        for b in range(population_size):
-            for t in range(T):
-                out[a, b, t] = sample_tree(rng, lib, lib.variable_array[t], max_init_depth, max_nodes,
-                                           coefficient_sd, m)
-    return out
+    B = num_populations * population_size
+    out = np.zeros((B, T, max_nodes, 4), dtype=np.float32)
+    chunk = 1 << 15  # bounded temporaries ([chunk, 2N] index tables)
+    for t in range(T):
+        for lo in range(0, B, chunk):
+            hi = min(B, lo + chunk)
+            out[lo:hi, t] = sample_trees_batch(rng, lib, lib.variable_array[t], hi - lo, max_init_depth,
+                                               max_nodes, coefficient_sd, m)
+    return out.reshape(num_populations, population_size, T, max_nodes, 4)

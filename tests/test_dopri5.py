@@ -237,22 +237,29 @@ def test_gpu_dopri5_sr_bitexact(jit, n_var, tol, R):
 def test_dopri5_wide_sr_oracle_vs_fine_rk4():
     """The checker of the wide-state Dopri5 kernel: the oracle's adaptive solve of 12-variable SR
     candidates at a tight tolerance agrees with a fine fixed-step RK4 solve of the same trees
-    (where both stay finite and moderate), and starts every trajectory at x0."""
-    env, lib, ff, data, pop = sr_setup(P=8, R=3, n_save=11, save_every=4, h=0.01, depth=4, N=30, seed=2, n_var=12,
+    wherever that solve is resolved (fp32 RK4 at h and h/2 agree to 2e-4: no near-singular division, no
+    blow-up), and starts every trajectory at x0."""
+    env, lib, ff, data, pop = sr_setup(P=16, R=3, n_save=11, save_every=4, h=0.01, depth=4, N=30, seed=2, n_var=12,
                                        solver=(1e-6, 1e-6, 0.0001, 2000))
-    d = ff.prepare(data)
+    pop = pop.copy()
+    pop[..., 0][pop[..., 0] == lib.string_to_node["/"]] = lib.string_to_node["*"]  # polynomial fields only:
+    d = ff.prepare(data)                                  # a division by a vanishing state is unresolvable
     dp = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)["xs"]
     x0, ts, ys, keys = data
-    fine = mt.SREvaluator(solver=mt.RK4(), dt0=0.0005)
-    d2 = fine.prepare(data)
-    rk = orc.evaluate(oracle_model(fine, d2), pop, lib, oracle_rollouts(d2), trajectories=True)["xs"]
+
+    def rk4(h):
+        fine = mt.SREvaluator(solver=mt.RK4(), dt0=h)
+        d2 = fine.prepare(data)
+        return orc.evaluate(oracle_model(fine, d2), pop, lib, oracle_rollouts(d2), trajectories=True)["xs"]
+
+    rk, rk2 = rk4(0.0005), rk4(0.00025)
     assert np.array_equal(dp[:, :, 0, :], np.broadcast_to(x0, dp[:, :, 0, :].shape))
-    ok = np.isfinite(dp) & np.isfinite(rk) & (np.abs(rk) < 1e3)
-    assert ok.mean() > 0.5
-    # random trees include divisions: near-singular candidates force dtmin steps (accepted whatever
-    # their error), so only most candidates -- the smooth ones -- must agree closely
-    err = np.where(ok, np.abs(dp - rk) / (1e-3 + np.abs(rk)), 0.0).reshape(dp.shape[0], -1).max(axis=1)
-    assert (err < 1e-3).sum() >= dp.shape[0] // 2, err
+    with np.errstate(all="ignore"):
+        resolved = (np.isfinite(rk).all(axis=(1, 2, 3)) & (np.abs(rk).max(axis=(1, 2, 3)) < 1e3) &
+                    (np.abs(rk - rk2) / (1e-3 + np.abs(rk2))).reshape(rk.shape[0], -1).max(axis=1).__lt__(2e-4))
+        err = (np.abs(dp - rk) / (1e-3 + np.abs(rk))).reshape(dp.shape[0], -1).max(axis=1)
+    assert resolved.sum() >= 3, resolved
+    assert np.all(err[resolved] < 1e-3), (err, resolved)
 
 
 @pytest.mark.gpu

@@ -57,3 +57,27 @@ def test_sampler_layout_invariants(depth, N):
                     assert tree[k, 1] == -1 and tree[k, 2] == -1
                 if f[k] >= lib.var_start:
                     assert lib.variable_array[t][f[k] - lib.var_start] == 1  # allowed variable only
+
+
+@pytest.mark.parametrize("depth,N", [(4, 30), (10, 64), (16, 128)])
+def test_batch_sampler_matches_tree_sampler_distribution(depth, N):
+    """sample_population samples all trees of a position together (sample_trees_batch); its
+    distribution must equal the per-tree restatement of initialization.py (sample_tree, which
+    the mutations use): node-count mean and quantiles, opcode frequencies."""
+    from multitreegp_amd.sampling import sample_tree
+    lib = mt.NodeLibrary(CONTROL_OPS, [["y1", "y2", "y3", "y4", "a1", "a2", "u"]], [1])
+    new = sample_population(3, lib, 4000, 1, max_init_depth=depth, max_nodes=N)[0, :, 0]
+    rng = np.random.default_rng(4)
+    m = create_map_b_to_d(depth)
+    old = np.stack([sample_tree(rng, lib, lib.variable_array[0], depth, N, 1.0, m) for _ in range(4000)])
+    cn, co = (new[..., 0] != 0).sum(1), (old[..., 0] != 0).sum(1)
+    assert abs(cn.mean() - co.mean()) < 0.05 * co.mean()
+    for q in (50, 90, 99):
+        assert abs(np.percentile(cn, q) - np.percentile(co, q)) <= max(2.0, 0.1 * np.percentile(co, q))
+    fn = np.bincount(new[..., 0].astype(int).ravel(), minlength=lib.n_funcs)[1:] / cn.sum()
+    fo = np.bincount(old[..., 0].astype(int).ravel(), minlength=lib.n_funcs)[1:] / co.sum()
+    np.testing.assert_allclose(fn, fo, atol=0.012)
+    # the coefficient leaves carry N(0, 1) values, every other row value 0
+    vals = new[..., 3][new[..., 0] == 1]
+    assert abs(vals.mean()) < 0.05 and abs(vals.std() - 1.0) < 0.05
+    assert np.all(new[..., 3][new[..., 0] != 1] == 0)
