@@ -1,0 +1,46 @@
+# GPU-box runner: bash scripts/gpu_run.sh TAG STEP [STEP ...]
+# Every step runs under its own time limit; the first failing step ends the call (no retries).
+# Outputs land in gpurun_out/TAG/ (merged back by gpurun).
+#   test        python -m pytest tests -m gpu (whole GPU suite)
+#   smoke       __graft_entry__.smoke()
+#   bench_c3    python bench.py (the driver's line: C3, PMC + CPU baseline + end-to-end)
+#   bench_c2 / bench_c5 / bench_dp / bench_dpn   other configs (dp = C3 Dopri5, dpn = + obs_noise 0.1)
+#   prof_c3 / prof_c2 / prof_c5 / prof_dp / prof_dpn   rocprofv3 --kernel-trace --stats of kprof (10 evaluations)
+set -o pipefail
+TAG=$1; shift
+O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+run() {  # name seconds cmd...
+  local n=$1 s=$2; shift 2
+  echo "== $n ($(date +%T))"
+  timeout -k 10 $s "$@" > $O/$n.log 2>&1
+  local rc=$?
+  echo "== $n exit $rc"
+  tail -3 $O/$n.log
+  return $rc
+}
+prof() {  # name config args...
+  local n=$1 c=$2; shift 2
+  run $n 240 rocprofv3 --kernel-trace --stats -d $O/$n -o $n -- python3 scripts/kprof.py --iters 10 --config $c "$@" || return 1
+  python3 scripts/kstats_db.py $(ls $O/$n/*/*.db 2>/dev/null | head -1) $O/${n}_kernel_stats.csv 2>/dev/null || \
+    cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats.csv
+  head -6 $O/${n}_kernel_stats.csv
+}
+for step in "$@"; do
+  case $step in
+    test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
+    bench_c3) run bench_c3 600 python bench.py || exit 1 ;;
+    bench_c2) run bench_c2 600 python bench.py --config c2 || exit 1 ;;
+    bench_c5) run bench_c5 600 python bench.py --config c5 || exit 1 ;;
+    bench_dp) run bench_dp 600 python bench.py --solver dopri5 --steps 20 --warmup 3 || exit 1 ;;
+    bench_dpn) run bench_dpn 600 python bench.py --solver dopri5 --obs-noise 0.1 --steps 10 --warmup 2 || exit 1 ;;
+    prof_c3) prof prof_c3 c3 || exit 1 ;;
+    prof_c2) prof prof_c2 c2 || exit 1 ;;
+    prof_c5) prof prof_c5 c5 || exit 1 ;;
+    prof_dp) prof prof_dp c3 --solver dopri5 || exit 1 ;;
+    prof_dpn) prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "all steps done"
