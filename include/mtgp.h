@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 15
+#define MTGP_ABI_VERSION 16
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -38,6 +38,7 @@ extern "C" {
 #define MTGP_MAX_DATA 64     /* data-vector length D seen by a tree            */
 #define MTGP_MAX_PROGRAMS 64 /* programs per individual (mtgp_schedule weights) */
 #define MTGP_STACK_MAX 8     /* operand-stack slots per lane (Sethi-Ullman)    */
+#define MTGP_MAX_ROLLOUTS 65536 /* rollouts R per individual (dyn.py:63 vmaps any batch) */
 
 /* ---------------------------------------------------------------- errors */
 #define MTGP_OK 0
@@ -70,11 +71,17 @@ typedef struct {
 
 /* One straight-line program to emit per individual: which tree, how long the data
  * vector is, and which data slots are known to hold +0.0 (e.g. the readout during the
- * ODE solve sees zeros for y and u, dyn.py:113). */
+ * ODE solve sees zeros for y and u, dyn.py:113).  ABI v16: the evaluator's data slot s (after
+ * the reference's clamp to n_data - 1, and after the zero_mask test) is placed at slot
+ * s + gap when s >= gap_at (gap 0: identity) -- the control kernels keep n_var observation
+ * slots, so with n_obs < n_var (C = eye(n_var)[:n_obs], control_environment_base.py:47) the
+ * slots after the observations move up by n_var - n_obs. */
 typedef struct {
   int32_t tree;
   int32_t n_data;
   uint64_t zero_mask;
+  int32_t gap_at;
+  int32_t gap;
 } MtgpProgramSpec;
 
 /* ------------------------------------------------------------ program format */
@@ -177,13 +184,21 @@ typedef struct {
   const uint32_t* obs_keys; /* [R, 2] obs_noise_keys (dyn.py:65) or NULL = noise-free */
   const float* obs_w;       /* [n_obs, n_obs] W (acrobot.py:49: obs_noise * I;          */
                             /*  reactor.py:43: obs_noise * I * [15, 15, 0.1])          */
+  /* ABI v16: lanes per individual (a lane set), a power of two >= R, or 0 = R rounded up to a
+   * power of two.  lanes <= 64: a wave holds 64 / lanes individuals (a wider set than R puts
+   * fewer individuals in each wave -- more waves, fewer program calls per wave; mtgp_schedule
+   * and the mtgp_jit_* functions must then be given lanes in place of R).  lanes > 64 (R > 64):
+   * every individual spans lanes / 64 waves, wave w running rollouts [64 w, 64 w + 64), and the
+   * fitness mean is formed by a second small kernel from MtgpOutputs.rollout_fitness, which is
+   * then required. */
+  int32_t lanes;
 } MtgpRollouts;
 
 /* Outputs.  Trajectories are time-major structure-of-arrays so that every save point
  * is one coalesced 256-B store per wave: xs[(k*n_var + c)*P*R + p*R + r]. */
 typedef struct {
   float* fitness;         /* [P] final fitness incl. parsimony (required)     */
-  float* rollout_fitness; /* [P, R] raw per-rollout fitness or NULL           */
+  float* rollout_fitness; /* [P, R] raw per-rollout fitness or NULL (required when R > 64) */
   float* xs;              /* [n_save, n_var, P*R] or NULL                     */
   float* ys;              /* [n_save, n_obs, P*R] or NULL (control models)    */
   float* us;              /* [n_save, n_control, P*R] or NULL                 */

@@ -165,8 +165,8 @@ class CoefficientOptimiser:
         for lo in range(0, max(n_max, 1), cap):
             pop, theta, nparam, K, libs = parameterise(cands, rows, eng.lib, n_data, lo, lo + cap)
             spec_arr = (nat.MtgpProgramSpec * len(specs))()
-            for i, (t, nd, z) in enumerate(specs):
-                spec_arr[i].tree, spec_arr[i].n_data, spec_arr[i].zero_mask = t, nd + K, z
+            for i, sp in enumerate(specs):
+                spec_arr[i].tree, spec_arr[i].n_data, spec_arr[i].zero_mask = sp[0], sp[1] + K, sp[2]
             spec_dev = torch.frombuffer(bytearray(bytes(spec_arr)), dtype=torch.uint8).to(dev)
             n_prog = len(specs)
             pop_dev = torch.from_numpy(pop).to(dev)

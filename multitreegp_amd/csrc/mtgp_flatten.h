@@ -91,7 +91,8 @@ MTGP_INLINE MTGP_HD bool zero_row(const float* tree, int i, const MtgpNodeLibrar
 // Resolve row i of `tree` ([N,4] f32) into info[i]; rows < i must be resolved already (or be
 // zero rows marked in zrows).
 MTGP_INLINE MTGP_HD void resolve_row(const float* tree, int N, int i, const MtgpNodeLibrary* lib,
-                                     int n_data, uint64_t zero_mask, RowInfo* info, const uint64_t* zrows) {
+                                     int n_data, uint64_t zero_mask, RowInfo* info, const uint64_t* zrows,
+                                     int gap_at = 0, int gap = 0) {
   RowInfo& r = info[i];
   const float fv = tree[4 * i + 0];
   r.afirst = 1;
@@ -112,7 +113,7 @@ MTGP_INLINE MTGP_HD void resolve_row(const float* tree, int N, int i, const Mtgp
   if (fn == MTGP_FN_VAR) {
     int slot = f - lib->var_start;
     if (slot > n_data - 1) slot = n_data - 1;  // (caller guarantees n_data >= V)
-    r.slot = (uint8_t)slot;
+    r.slot = (uint8_t)(slot >= gap_at ? slot + gap : slot);  // the evaluator's layout (MtgpProgramSpec.gap)
     if ((zero_mask >> slot) & 1ull) { r.kind = K_CONST; r.isconst = 1; r.cval = 0.0f; }
     else { r.kind = K_VAR; r.isconst = 0; r.cval = 0.0f; }
     return;
@@ -413,14 +414,14 @@ MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* o
 // -MTGP_ERR_*.
 MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNodeLibrary* lib,
                                           int n_data, uint64_t zero_mask, MtgpInstr* out, int cap,
-                                          RowInfo* info, int* stack_need) {
+                                          RowInfo* info, int* stack_need, int gap_at = 0, int gap = 0) {
   uint64_t zrows[(MTGP_MAX_NODES + 63) / 64] = {0};
   for (int i = 0; i < N; ++i) {
     if (i < N - 1 && zero_row(tree, i, lib)) {  // empty rows (most of a reference tree): no RowInfo
       zrows[i >> 6] |= 1ull << (i & 63);
       continue;
     }
-    resolve_row(tree, N, i, lib, n_data, zero_mask, info, zrows);
+    resolve_row(tree, N, i, lib, n_data, zero_mask, info, zrows, gap_at, gap);
     size_row(i, info);
   }
   const int need = info[N - 1].need;
@@ -438,9 +439,9 @@ MTGP_INLINE MTGP_HD int flatten_tree_body(const float* tree, int N, const MtgpNo
 // the slot holds a bare END (an empty program), so an evaluator never runs stale words.
 MTGP_INLINE MTGP_HD int flatten_tree(const float* tree, int N, const MtgpNodeLibrary* lib,
                                      int n_data, uint64_t zero_mask, MtgpInstr* out, int slots,
-                                     RowInfo* info, int* stack_need) {
+                                     RowInfo* info, int* stack_need, int gap_at = 0, int gap = 0) {
   if (slots < 1) return -MTGP_ERR_PROG_TOO_LONG;
-  const int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need);
+  const int n = flatten_tree_body(tree, N, lib, n_data, zero_mask, out, slots - 1, info, stack_need, gap_at, gap);
   const int at = n > 0 ? n : 0;
   out[at].op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
   out[at].imm = 0.0f;

@@ -172,11 +172,14 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
 // The key is per rollout (obs_noise_keys, dyn.py:65), W (acrobot.py:49: obs_noise * I;
 // reactor.py:43: obs_noise * I * [15, 15, 0.1]) is shared.  C@x and the noise product are
 // summed in index order exactly like the oracle.
+// NV = the environment's latent size; the observation has z.no <= NV components (C =
+// eye(n_var)[:n_obs], control_environment_base.py:47 / acrobot.py:48), W is [no, no].
 template <int NO>
 struct ObsNoise {
   uint32_t k0, k1;  // this lane's rollout key
-  const float* W;   // [NO, NO] row-major (read with scalar loads when used: no registers held)
+  const float* W;   // [no, no] row-major (read with scalar loads when used: no registers held)
   int impl;         // MTGP_PRNG_* random-bits layout
+  int no;           // observed components (MtgpModel.n_obs), wave-uniform
   bool diag;        // W diagonal with a non-zero diagonal: noise_j = n_j * W_jj exactly
 };
 
@@ -187,32 +190,58 @@ __device__ __forceinline__ ObsNoise<NO> obs_noise_setup(const MtgpModel& m, cons
   z.k1 = ro.obs_keys[2 * rr + 1];
   z.W = ro.obs_w;
   z.impl = m.prng_impl;
+  z.no = uni(m.n_obs);
+  const int no = z.no;
   bool diag = true;
 #pragma unroll
   for (int i = 0; i < NO; ++i)
 #pragma unroll
-    for (int j = 0; j < NO; ++j) diag = diag && ((i == j) ? (z.W[i * NO + j] != 0.0f) : (z.W[i * NO + j] == 0.0f));
+    for (int j = 0; j < NO; ++j)
+      if (i < no && j < no) diag = diag && ((i == j) ? (z.W[i * no + j] != 0.0f) : (z.W[i * no + j] == 0.0f));
   z.diag = uni((int)diag) != 0;
   return z;
 }
 
-// noise vector normal(fold_in(key, bitcast(t)), (NO,)) @ W (summed in index order).  With W
+// normal(fold_in(key, bitcast(t)), (no,)) for a wave-uniform no <= NO (the draw depends on the
+// shape): one compile-time instance per count, the rest of n[] zero
+template <int NO>
+__device__ __forceinline__ void obs_normals_n(uint32_t k0, uint32_t k1, float t, int no, int impl, float (&n)[NO]) {
+  if (no == NO) {
+    mtgp_obs_normals(k0, k1, t, NO, impl, n);
+    return;
+  }
+  if constexpr (NO > 1) {
+    float m[NO - 1];
+    obs_normals_n<NO - 1>(k0, k1, t, no, impl, m);
+#pragma unroll
+    for (int j = 0; j < NO - 1; ++j) n[j] = m[j];
+  }
+  n[NO - 1] = 0.0f;
+}
+
+// noise vector normal(fold_in(key, bitcast(t)), (no,)) @ W (summed in index order).  With W
 // diagonal and non-zero on the diagonal, the off-diagonal products are +-0 and the sum is
-// exactly n_j * W_jj (n_j is never 0: |u| > 0 always), so the product is skipped.
+// exactly n_j * W_jj (n_j is never 0: |u| > 0 always), so the product is skipped.  Components
+// j >= no (unobserved) are 0.
 template <int NO>
 __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, float nz[NO]) {
   float n[NO];
-  mtgp_obs_normals(z.k0, z.k1, t, NO, z.impl, n);
+  const int no = z.no;
+  obs_normals_n<NO>(z.k0, z.k1, t, no, z.impl, n);
   if (z.diag) {
 #pragma unroll
-    for (int j = 0; j < NO; ++j) nz[j] = n[j] * z.W[j * NO + j];
+    for (int j = 0; j < NO; ++j) nz[j] = j < no ? n[j] * z.W[j * no + j] : 0.0f;
     return;
   }
 #pragma unroll
   for (int j = 0; j < NO; ++j) {
-    float acc = n[0] * z.W[j];
+    float acc = 0.0f;
+    if (j < no) {
+      acc = n[0] * z.W[j];
 #pragma unroll
-    for (int i = 1; i < NO; ++i) acc = acc + n[i] * z.W[i * NO + j];
+      for (int i = 1; i < NO; ++i)
+        if (i < no) acc = acc + n[i] * z.W[i * no + j];
+    }
     nz[j] = acc;
   }
 }
@@ -220,7 +249,9 @@ __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, fl
 #ifndef MTGP_V_OBSFAST
 #define MTGP_V_OBSFAST 1
 #endif
-// y = C@x + nz with C = I (n_obs = n_var for every environment on this path): (C@x)_i + nz_i
+// y = C@x + nz with C = eye(n_var)[:n_obs]: all NV components are formed, the programs read only
+// the first n_obs (the flattener places the data slots after the observations behind all NV,
+// MtgpProgramSpec.gap) and only those are stored as ys.  (C@x)_i + nz_i
 // equals x_i + nz_i when every x_j is finite (the +-0 terms 0*x_j cannot change the sum; with
 // nz = +0 a -0 becomes +0 either way), NaN otherwise (0*inf), then the environment's own
 // observation transform (Acrobot: angle wrap, acrobot.py:29-32).
@@ -479,15 +510,20 @@ __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, i
 }
 
 // --------------------------------------------------------------------------------------
-// Wave layout.  A wave packs G = 64 / Rp individuals (Rp = R rounded up to a power of two):
-// lane = g * Rp + r -> schedule slot q0 + g, rollout r; the individual at slot q is
-// order[q] (identity without a schedule).  The environment (drift, observation, RK4 update,
-// fitness) is lane-parallel and runs once for all G individuals; only the tree programs
-// differ per individual, so they run once per group, each with a wave-uniform (scalar)
-// instruction stream.  A half-empty wave costs as much as a full one on gfx950 (measured: R=32
-// and R=64 take the same time), so packing is pure gain.
+// Wave layout.  A wave packs G = 64 / Rp individuals (Rp = the lane set: MtgpRollouts.lanes,
+// by default R rounded up to a power of two): lane = g * Rp + r -> schedule slot q0 + g,
+// rollout r; the individual at slot q is order[q] (identity without a schedule).  The
+// environment (drift, observation, RK4 update, fitness) is lane-parallel and runs once for all
+// G individuals; only the tree programs differ per individual, so they run once per group, each
+// with a wave-uniform (scalar) instruction stream.  A half-empty wave costs as much as a full
+// one on gfx950 (measured: R=32 and R=64 take the same time), so packing pays whenever the
+// launch has more waves than the chip has SIMDs; below that the host widens the lane set
+// (fewer individuals and program calls per wave, more waves).  A lane set wider than a wave
+// (R > 64) spans W = lanes / 64 consecutive waves of one individual, wave `part` running
+// rollouts [64 part, 64 part + 64); those waves share the individual's programs (and JIT unit).
 struct Lane {
   int wave, lane, Rp, G, q0, g, r, p, rr;
+  int W, part;  // waves per individual (1 unless R > 64) and this wave's part
   bool active;
   uint32_t ptab;  // lane gi (< G): byte offset of group gi's program block in A.prog
   uint32_t jtab;  // lane j < n_prog: JIT code offset of this wave's program-j unit
@@ -507,17 +543,41 @@ __device__ __forceinline__ uint32_t prog_table(const KArgs& A, const Lane& L) {
 
 __device__ __forceinline__ int sched_ind(const KArgs& A, int q) { return A.ro.order ? A.ro.order[q] : q; }
 
+// lanes per individual of this launch (MtgpRollouts.lanes, default R rounded up to a power of two)
+__device__ __forceinline__ int lane_set(const MtgpRollouts& ro) {
+  if (ro.lanes > 0) return ro.lanes;
+  int Rp = 1;
+  while (Rp < ro.R) Rp <<= 1;
+  return Rp;
+}
+
+// wave `wv` of the launch (or lane set `wv` of a workgroup-per-lane-set kernel) -> L.q0 / g / r
+__device__ __forceinline__ void lane_place(const KArgs& A, Lane& L, int wv) {
+  const int set = uni(lane_set(A.ro));
+  if (set <= kWave) {
+    L.Rp = set;
+    L.G = uni(kWave / set);
+    L.W = 1;
+    L.part = 0;
+    L.q0 = uni(wv * L.G);
+    L.g = L.lane / L.Rp;
+    L.r = L.lane - L.g * L.Rp;
+  } else {
+    L.Rp = kWave;
+    L.G = 1;
+    L.W = uni(set / kWave);
+    L.q0 = uni(wv / L.W);
+    L.part = uni(wv - L.q0 * L.W);
+    L.g = 0;
+    L.r = L.part * kWave + L.lane;
+  }
+}
+
 __device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
   L.wave = uni(threadIdx.x >> 6);
   L.lane = threadIdx.x & 63;
-  int Rp = 1;
-  while (Rp < A.ro.R) Rp <<= 1;
-  L.Rp = uni(Rp);
-  L.G = uni(kWave / Rp);
-  L.q0 = uni((blockIdx.x * kWavesPerBlock + L.wave) * L.G);
+  lane_place(A, L, (int)blockIdx.x * kWavesPerBlock + L.wave);
   if (L.q0 >= A.P) return false;
-  L.g = L.lane / L.Rp;
-  L.r = L.lane - L.g * L.Rp;
   const int q = L.q0 + L.g;
   L.p = q < A.P ? sched_ind(A, q) : A.P;  // A.P marks a padding group
   L.active = (L.r < A.ro.R) && (q < A.P);
@@ -804,6 +864,7 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
   MTGP_PROBE(L, 1);
   const float mx = A.m.max_fitness;
   if (A.out.rollout_fitness && L.active) A.out.rollout_fitness[(size_t)L.p * A.ro.R + L.r] = F;
+  if (L.W > 1) return;  // lane set over several waves: k_rollout_mean forms the fitness
   float v = L.active ? (mtgp_isfinite(F) ? F : mx) : 0.0f;
   // xor butterfly inside the group == pairwise tree in rollout order (mirrored by the oracle)
   for (int w = 1; w < L.Rp; w <<= 1) v = v + __shfl_xor(v, w, kWave);
@@ -812,6 +873,45 @@ __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, floa
     mean = mean < 0.0f ? 0.0f : (mean > mx ? mx : mean);
     A.out.fitness[L.p] = mean + A.m.parsimony * (float)A.nodes[L.p];
   }
+}
+
+// Fitness of individuals whose lane set spans several waves (R > 64): the same sum as
+// finish_group's butterfly -- per chunk of 64 rollouts the pairwise tree in rollout order (zeros
+// past R), then the pairwise tree over the chunks padded to a power of two (the oracle's
+// pairwise_sum) -- from the raw per-rollout fitness, then mean, clip and parsimony.  One thread
+// per individual; the pairwise trees are formed with a binary-counter stack.
+__global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ rf, int P, int R, float mx,
+                                                      float parsimony, const int32_t* __restrict__ nodes,
+                                                      float* __restrict__ fitness) {
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= P) return;
+  const float* v = rf + (size_t)p * R;
+  const int nch = (R + kWave - 1) / kWave;
+  int np2 = 1;
+  while (np2 < nch) np2 <<= 1;
+  float cst[24];
+  for (int c = 0; c < np2; ++c) {
+    float lst[8];
+    float sum = 0.0f;
+    for (int l = 0; l < kWave; ++l) {
+      const int r = c * kWave + l;
+      float x = (c < nch && r < R) ? v[r] : 0.0f;
+      if (c < nch && r < R && !mtgp_isfinite(x)) x = mx;
+      int lvl = 0;
+      for (; (l >> lvl) & 1; ++lvl) x = lst[lvl] + x;
+      lst[lvl] = x;
+      sum = x;  // after l = 63 the top of the stack holds the chunk's sum
+    }
+    float x = sum;
+    int lvl = 0;
+    for (; (c >> lvl) & 1; ++lvl) x = cst[lvl] + x;
+    cst[lvl] = x;
+  }
+  int top = 0;
+  while ((1 << top) < np2) ++top;
+  float mean = cst[top] / (float)R;
+  mean = mean < 0.0f ? 0.0f : (mean > mx ? mx : mean);
+  fitness[p] = mean + parsimony * (float)nodes[p];
 }
 
 // --------------------------------------------------------------------------------------
@@ -963,7 +1063,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
+              for (int i = 0; i < NV; ++i)
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
             }
             if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us);
             if (A.out.acts) {
@@ -1089,7 +1190,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             }
             if (A.out.ys) {
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
+              for (int i = 0; i < NV; ++i)
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
             }
             if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u);
           }
@@ -1224,7 +1326,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
       }
       if (A.out.ys) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) store_row(A.out.ys, ((size_t)k * NV + i) * PR, loff, y[i]);
+        for (int i = 0; i < NV; ++i)
+          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
       }
       if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, ur[0]);
       if (DYN && A.out.acts) {
@@ -1574,14 +1677,8 @@ constexpr int kWideComp = 8;  // components (trees) per wave
 __device__ __forceinline__ bool lane_setup_wide(const KArgs& A, Lane& L) {
   L.wave = uni(threadIdx.x >> 6);
   L.lane = threadIdx.x & 63;
-  int Rp = 1;
-  while (Rp < A.ro.R) Rp <<= 1;
-  L.Rp = uni(Rp);
-  L.G = uni(kWave / Rp);
-  L.q0 = uni(blockIdx.x * L.G);
+  lane_place(A, L, (int)blockIdx.x);  // one workgroup per lane set
   if (L.q0 >= A.P) return false;
-  L.g = L.lane / L.Rp;
-  L.r = L.lane - L.g * L.Rp;
   const int q = L.q0 + L.g;
   L.p = q < A.P ? sched_ind(A, q) : A.P;
   L.active = (L.r < A.ro.R) && (q < A.P);
@@ -2172,7 +2269,7 @@ __global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__
     MtgpInstr* out = prog_out + (size_t)pj * L;
     mtgp::RowInfo info[NMAX];
     const int n = mtgp::flatten_tree(pop + ((size_t)p * T + sp.tree) * N * 4, N, &lib, sp.n_data, sp.zero_mask, out,
-                                     L, info, nullptr);
+                                     L, info, nullptr, sp.gap_at, sp.gap);
     len_out[pj] = n > 0 ? n : 0;
     status_out[pj] = n > 0 ? 0 : -n;
     flat_jit_size(out, L, n, jit_words_out, jit_cost_out, (size_t)pj, jit_mode);
@@ -2264,7 +2361,7 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
         if (fn == MTGP_FN_VAR) {
           int sl = f - var_start;
           if (sl > n_data - 1) sl = n_data - 1;
-          slot = (uint32_t)sl;
+          slot = (uint32_t)(sl >= sp.gap_at ? sl + sp.gap : sl);  // MtgpProgramSpec.gap
           if (!((zmask >> sl) & 1ull)) { kind = K_VAR; isc = 0; }
         } else if (fn_arity(fn) > 0) {
           const int ar = fn_arity(fn);
@@ -2483,7 +2580,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       if (fn == MTGP_FN_VAR) {
         int sl = f - var_start;
         if (sl > n_data - 1) sl = n_data - 1;
-        slot = (uint32_t)sl;
+        slot = (uint32_t)(sl >= sp.gap_at ? sl + sp.gap : sl);  // MtgpProgramSpec.gap
         if (!((zmask >> sl) & 1ull)) { kind = K_VAR; isc = 0; }
       } else if (fn_arity(fn) > 0) {
         fnr[k] = fn;
@@ -3154,9 +3251,13 @@ __global__ void __launch_bounds__(256) k_jit_templates(uint32_t* __restrict__ co
 
 bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
                    JitUnitArgs& U) {
-  if (!prog || P < 0 || n_prog <= 0 || n_prog > MTGP_MAX_PROGRAMS || L <= 0 || R <= 0 || R > kWave) return false;
+  // R: the lane set (MtgpRollouts.lanes) or the rollout count; a set wider than a wave holds one
+  // individual, whose waves share its units
+  if (!prog || P < 0 || n_prog <= 0 || n_prog > MTGP_MAX_PROGRAMS || L <= 0 || R <= 0 || R > MTGP_MAX_ROLLOUTS)
+    return false;
   int Rp = 1;
   while (Rp < R) Rp <<= 1;
+  if (Rp > kWave) Rp = kWave;
   U.prog = prog;
   U.n_prog = n_prog;
   U.L = L;
@@ -3351,7 +3452,8 @@ template <class Env>
 int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, bool jit, bool noise, bool traj,
                dim3 grid, dim3 block, hipStream_t s) {
   constexpr int NV = Env::NV;
-  if (model->n_var != NV || model->n_obs != NV || model->n_control != 1 || !ro->params) return MTGP_ERR_ARG;
+  if (model->n_var != NV || model->n_obs < 1 || model->n_obs > NV || model->n_control != 1 || !ro->params)
+    return MTGP_ERR_ARG;
   if (model->n_targets < 0 || (model->n_targets > 0 && !ro->targets)) return MTGP_ERR_ARG;
   if (model->env != MTGP_ENV_ACROBOT && model->n_targets < 1) return MTGP_ERR_ARG;  // x_d needs the target
   if (model->model == MTGP_MODEL_STATIC) {
@@ -3722,13 +3824,13 @@ int mtgp_flatten_tree_host(const float* tree, int32_t N, const MtgpNodeLibrary* 
 int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t* weights, int32_t R,
                   int32_t* order_out, int32_t* scratch, void* stream) {
   if (!plen || !order_out || !scratch || P < 0 || n_prog <= 0 || n_prog > MTGP_MAX_PROGRAMS) return MTGP_ERR_ARG;
-  if (R <= 0 || R > kWave) return MTGP_ERR_ARG;
+  if (R <= 0 || R > MTGP_MAX_ROLLOUTS) return MTGP_ERR_ARG;  // R: the lane set (or the rollout count)
   if (P == 0) return MTGP_OK;
   SchedW W;
   for (int j = 0; j < MTGP_MAX_PROGRAMS; ++j) W.w[j] = (j < n_prog) ? (weights ? weights[j] : 1) : 0;
   int Rp = 1;
   while (Rp < R) Rp <<= 1;
-  const int G = kWave / Rp;
+  const int G = Rp >= kWave ? 1 : kWave / Rp;
   hipStream_t s = (hipStream_t)stream;
   if ((long)P * n_prog <= kSchedFusedMax) {  // small populations: one block does it all
     hipLaunchKernelGGL(k_sched_fused, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
@@ -3768,8 +3870,14 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
                       const MtgpOutputs* out, const MtgpJitCode* jitc, void* stream) {
   if (!model || !prog || !plen || !nodes || !rollouts || !out || !out->fitness) return MTGP_ERR_ARG;
   if (P < 0 || n_prog <= 0 || L <= 0 || (L & 3) != 0) return MTGP_ERR_ARG;
-  if (rollouts->R <= 0 || rollouts->R > kWave) return MTGP_ERR_ARG;
-  if ((int64_t)P * rollouts->R > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
+  if (rollouts->R <= 0 || rollouts->R > MTGP_MAX_ROLLOUTS) return MTGP_ERR_ARG;
+  const int set = rollouts->lanes > 0 ? rollouts->lanes : 0;
+  if (set && (set < rollouts->R || (set & (set - 1)) != 0 || set > 2 * MTGP_MAX_ROLLOUTS)) return MTGP_ERR_ARG;
+  int Rp = 1;
+  while (Rp < rollouts->R) Rp <<= 1;
+  if (set) Rp = set;
+  if (Rp > kWave && !out->rollout_fitness) return MTGP_ERR_ARG;  // the mean is formed from it
+  if ((int64_t)P * Rp > INT32_MAX) return MTGP_ERR_ARG;  // lane offsets are 32-bit
   if ((int64_t)P * n_prog * L * (int64_t)sizeof(MtgpInstr) > UINT32_MAX) return MTGP_ERR_ARG;  // 32-bit program offsets
   const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
   if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;
@@ -3809,16 +3917,16 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   }
   // (the wide-state SR kernel keeps its data vector in LDS: its code is built in kJitModeLds)
   hipStream_t s = (hipStream_t)stream;
-  int Rp = 1;
-  while (Rp < rollouts->R) Rp <<= 1;
-  const int G = kWave / Rp;  // individuals packed per wave
-  const long waves = ((long)P + G - 1) / G;
+  const int G = Rp >= kWave ? 1 : kWave / Rp;  // individuals packed per wave
+  const int Wset = Rp > kWave ? Rp / kWave : 1;  // waves per individual
+  const long waves = ((long)P + G - 1) / G * Wset;
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
   const bool noise = rollouts->obs_keys != nullptr;
   if (noise && (!rollouts->obs_w || model->model == MTGP_MODEL_SR)) return MTGP_ERR_ARG;
   if (model->prng_impl != MTGP_PRNG_THREEFRY_ORIGINAL && model->prng_impl != MTGP_PRNG_THREEFRY_PARTITIONABLE)
     return MTGP_ERR_ARG;
+  const int rc = [&]() -> int {
   if (model->model == MTGP_MODEL_DYNAMIC || model->model == MTGP_MODEL_STATIC) {
     switch (model->env) {
       case MTGP_ENV_ACROBOT: return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
@@ -3833,7 +3941,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     if (model->n_var > 4) {
       if (model->n_var > MTGP_MAX_DATA || n_prog < model->prog_state + model->n_var) return MTGP_ERR_ARG;
       const int nw = (model->n_var + kWideComp - 1) / kWideComp;
-      const dim3 wgrid((unsigned)(((long)P + G - 1) / G)), wblock(kWave * nw);
+      const dim3 wgrid((unsigned)(((long)P + G - 1) / G * Wset)), wblock(kWave * nw);
       if (dopri5) {  // + a reduction vector (error norm, MSE)
         const size_t lds_dp = (size_t)(3 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
         return launch_timed([&] {
@@ -3878,6 +3986,11 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
 #undef MTGP_SR
   }
   return MTGP_ERR_ARG;
+  }();
+  if (rc != MTGP_OK || Wset == 1) return rc;
+  hipLaunchKernelGGL(k_rollout_mean, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, s, out->rollout_fitness, P,
+                     rollouts->R, model->max_fitness, model->parsimony, nodes, out->fitness);
+  return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
 }  // extern "C"

@@ -49,13 +49,17 @@ class Flattened:
     jit_cost: Optional[torch.Tensor] = None   # int32 [P, n_prog] schedule weight of the JIT code
     jit: Optional[tuple] = None           # (code ptr, offsets [units+1], info [3], capacity, chain) of the JIT
     jit_key: Optional[tuple] = None       # (R, order, engine id, chain, arena slot, arena generation) of that code
+    order_lanes: Optional[int] = None     # lane set the schedule `order` was built for
 
 
 class DeviceEngine:
     """Binds one fitness-function config + node library to the HIP kernels."""
 
     def __init__(self, fitness_function, library: NodeLibrary, size_parsinomy: float = 0.0, device=None,
-                 native=None, jit: Optional[bool] = None):
+                 native=None, jit: Optional[bool] = None, lanes: Optional[int] = None):
+        """lanes: lanes per individual (MtgpRollouts.lanes); None = lane_set's occupancy policy,
+        0 = R rounded up to a power of two (the densest packing), else at least that many."""
+        self.lanes = lanes
         self.ff = fitness_function
         self.lib = library
         self.parsimony = float(size_parsinomy)
@@ -108,7 +112,8 @@ class DeviceEngine:
         return a
 
     def jit_build(self, fl: Flattened, m, R: int, order: Optional[torch.Tensor]) -> Optional[tuple]:
-        """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit),
+        """Translate the flattened programs to machine code once (mtgp_jit_plan + mtgp_jit_emit)
+        for lane set R (MtgpRollouts.lanes: 64 / R individuals per wave),
         without a host round trip: the buffer is sized from the code size per program seen in
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
@@ -153,7 +158,7 @@ class DeviceEngine:
             ev = torch.cuda.Event()
             ev.record()
             self._jit_last = (host, ev, n)
-        G = 64 // (1 << max(R - 1, 0).bit_length())
+        G = max(1, 64 // (1 << max(R - 1, 0).bit_length()))
         per_unit = self._jit_bytes_per_unit or 1024.0 * G
         ptr, size = self._arena(int(n * per_unit) + 4096)
         if fl.jit_words is not None:
@@ -232,8 +237,9 @@ class DeviceEngine:
         key = tuple(specs)
         if key != self._specs_key:
             arr = (nat.MtgpProgramSpec * len(specs))()
-            for i, (t, d, z) in enumerate(specs):
-                arr[i].tree, arr[i].n_data, arr[i].zero_mask = t, d, z
+            for i, sp in enumerate(specs):  # (tree, n_data, zero_mask[, gap_at, gap])
+                arr[i].tree, arr[i].n_data, arr[i].zero_mask = sp[:3]
+                arr[i].gap_at, arr[i].gap = sp[3:5] if len(sp) >= 5 else (0, 0)
             buf = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(self.device)
             self._specs_dev, self._specs_key = buf, key
         return specs, roles
@@ -247,7 +253,8 @@ class DeviceEngine:
         if N > nat.MAX_NODES:
             raise ValueError(f"max_nodes {N} > {nat.MAX_NODES}")
         specs, _ = self._specs()
-        for (t, _, _) in specs:
+        for sp in specs:
+            t = sp[0]
             if t >= T:
                 raise ValueError(f"candidate has {T} trees, the evaluator needs tree {t}")
         n_prog = len(specs)
@@ -320,7 +327,10 @@ class DeviceEngine:
         return cost
 
     def schedule(self, fl: Flattened, R: int) -> torch.Tensor:
-        """Build (once per flattened population) the wave schedule that balances per-wave work."""
+        """Build (once per flattened population and lane set R) the wave schedule that balances
+        per-wave work."""
+        if fl.order is not None and fl.order_lanes != R:
+            fl.order = None
         if fl.order is None:
             P = fl.plen.shape[0]
             order = torch.empty((P,), dtype=torch.int32, device=self.device)
@@ -334,6 +344,7 @@ class DeviceEngine:
             if rc != nat.OK:
                 raise RuntimeError(f"mtgp_schedule failed: {rc}")
             fl.order = order
+            fl.order_lanes = R
         return fl.order
 
     # ----------------------------------------------------------------- eval
@@ -363,14 +374,39 @@ class DeviceEngine:
             setattr(m, f, d.get(f, 0))
         return m
 
-    @staticmethod
-    def rollouts_struct(d: dict) -> "nat.MtgpRollouts":
-        """MtgpRollouts over the device copies of prepared data `d` (no schedule)."""
+    def rollouts_struct(self, d: dict, P: Optional[int] = None) -> "nat.MtgpRollouts":
+        """MtgpRollouts over the device copies of prepared data `d` (no schedule); lanes per
+        individual from lane_set(P, R) when P is given (else R rounded up to a power of two)."""
         ro = nat.MtgpRollouts()
         ro.x0, ro.params, ro.targets = _ptr(d["x0_dev"]), _ptr(d["params_dev"]), _ptr(d["targets_dev"])
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), d["R"]
         ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
+        ro.lanes = self.lane_set(P, d["R"]) if P is not None else 0
         return ro
+
+    def _simds(self) -> int:
+        if not hasattr(self, "_n_simds"):
+            self._n_simds = 4 * torch.cuda.get_device_properties(self.device).multi_processor_count
+        return self._n_simds
+
+    def lane_set(self, P: int, R: int) -> int:
+        """Lanes per individual (MtgpRollouts.lanes): R rounded up to a power of two, widened
+        (fewer individuals per wave, so fewer program calls per wave) while the launch would have
+        fewer waves than the GPU has SIMDs -- a wave alone on its SIMD runs at the same speed with
+        one individual's programs as with several, so at small P.R the spare SIMDs take the other
+        individuals instead (C2: 1024 x 16 rollouts -> 1024 waves of one individual instead of
+        256 waves of four).  MTGP_LANES overrides (A/B).  Results do not depend on the choice."""
+        Rp = 1 << max(R - 1, 0).bit_length()
+        if self.lanes is not None:
+            return max(Rp, 1 << max(int(self.lanes) - 1, 0).bit_length())
+        env = os.environ.get("MTGP_LANES")
+        if env:
+            return max(Rp, int(env))
+        if self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4:
+            return Rp  # the wide-state kernel runs a workgroup per lane set already
+        while Rp < 64 and (P + 64 // Rp - 1) // (64 // Rp) < self._simds():
+            Rp *= 2
+        return Rp
 
     def evaluate(self, pop: torch.Tensor, data, trajectories: bool = False, rollout_fitness: bool = False,
                  flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True,
@@ -383,16 +419,21 @@ class DeviceEngine:
         P = pop.shape[0]
         R, S = d["R"], d["n_save"]
         m = self.model_struct(d)
-        ro = self.rollouts_struct(d)
-        ro_order = self.schedule(fl, R) if schedule and P > 1 else None
+        ro = self.rollouts_struct(d, P)
+        lanes = ro.lanes
+        ro_order = self.schedule(fl, lanes) if schedule and P > 1 else None
         ro.order = _ptr(ro_order)
         dev = self.device
         res = {"fitness": torch.empty((P,), dtype=torch.float32, device=dev)}
         out = nat.MtgpOutputs()
         out.fitness = res["fitness"].data_ptr()
-        if rollout_fitness:
-            res["rollout_fitness"] = torch.empty((P, R), dtype=torch.float32, device=dev)
-            out.rollout_fitness = res["rollout_fitness"].data_ptr()
+        if rollout_fitness or lanes > 64:  # R > 64: the fitness mean is formed from it (mtgp.h)
+            rf = torch.empty((P, R), dtype=torch.float32, device=dev)
+            if rollout_fitness:
+                res["rollout_fitness"] = rf
+            else:
+                res["_rollout_fitness"] = rf
+            out.rollout_fitness = rf.data_ptr()
         if step_counts:  # Dopri5: step attempts per (individual, rollout)
             res["steps"] = torch.zeros((P, R), dtype=torch.int32, device=dev)
             out.steps = res["steps"].data_ptr()
@@ -407,7 +448,7 @@ class DeviceEngine:
                         res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
                         setattr(out, name, res[name].data_ptr())
         stream = torch.cuda.current_stream(dev).cuda_stream
-        jit = self.jit_build(fl, m, R, ro_order)
+        jit = self.jit_build(fl, m, lanes, ro_order)
         jc = nat.MtgpJitCode()
         if jit is not None:
             jc.code, jc.offsets, jc.info, jc.capacity = jit[0], jit[1].data_ptr(), jit[2].data_ptr(), jit[3]

@@ -243,8 +243,8 @@ class _ControlEvaluator(_CandidateAPI):
             # cond_fn_nan, which the reference evaluators require (dyn.py:94, ff.py:91)
             raise NotImplementedError(f"environment {name}: the MI355X path runs {sorted(ENVIRONMENTS)}")
         self.env_id, n_var, self.n_params = ENVIRONMENTS[name]
-        if env.n_obs != n_var:
-            raise NotImplementedError(f"{name} with n_obs != {n_var} (C = I only)")
+        if not 1 <= env.n_obs <= n_var:
+            raise ValueError(f"{name}: n_obs must be in [1, {n_var}] (C = eye(n_var)[:n_obs])")
         if env.n_control != 1 or (self.env_id != nat.ENV_ACROBOT and env.n_targets != 1):
             raise NotImplementedError(f"{name}: one control and one target only")
         self.env = env
@@ -255,6 +255,12 @@ class _ControlEvaluator(_CandidateAPI):
         self.solver = solver
         self.max_steps = max_steps
         self.stepsize_controller = stepsize_controller
+
+    def obs_gap(self) -> Tuple[int, int]:
+        """(gap_at, gap) of MtgpProgramSpec: the kernels hold all n_var observation slots, so with
+        n_obs < n_var (C = eye(n_var)[:n_obs], control_environment_base.py:47) the data slots after
+        the observations sit n_var - n_obs slots later than in the reference's data vector."""
+        return (self.obs_size, self.env.n_var - self.obs_size)
 
     def prepare(self, data) -> dict:
         """Reference data tuple (x0, ts, targets, process_keys, obs_keys, params) -> arrays.
@@ -322,9 +328,10 @@ class DynamicEvaluator(_ControlEvaluator):
         umask = ((1 << nu) - 1) << (no + ss)
         # order: readout | state equations | save-point readout, so that the JIT can chain the state
         # programs into the save-point readout (mtgp.h MtgpJitChain: it must follow the state programs)
-        specs = [(ss + j, D, ymask | umask) for j in range(nu)]     # readout in _drift (dyn.py:113)
-        specs += [(t, D, 0) for t in range(ss)]                     # state equation [y, a, u, tg]
-        specs += [(ss + j, D, umask) for j in range(nu)]            # readout at saves (dyn.py:101)
+        gap = self.obs_gap()
+        specs = [(ss + j, D, ymask | umask) + gap for j in range(nu)]     # readout in _drift (dyn.py:113)
+        specs += [(t, D, 0) + gap for t in range(ss)]                     # state equation [y, a, u, tg]
+        specs += [(ss + j, D, umask) + gap for j in range(nu)]            # readout at saves (dyn.py:101)
         roles = dict(prog_state=nu, prog_readout=0, prog_readout_save=ss + nu, readout_save_same=-1)
         return specs, roles
 
@@ -341,7 +348,7 @@ class FeedforwardEvaluator(_ControlEvaluator):
         return self.obs_size + self.env.n_targets
 
     def program_specs(self):
-        specs = [(j, self.n_data(), 0) for j in range(self.control_size)]
+        specs = [(j, self.n_data(), 0) + self.obs_gap() for j in range(self.control_size)]
         roles = dict(prog_state=-1, prog_readout=0, prog_readout_save=0, readout_save_same=1)
         return specs, roles
 

@@ -5,7 +5,7 @@
 #   smoke       __graft_entry__.smoke()
 #   bench_c3    python bench.py (the driver's line: C3, PMC + CPU baseline + end-to-end)
 #   bench_c2 / bench_c5 / bench_dp / bench_dpn   other configs (dp = C3 Dopri5, dpn = + obs_noise 0.1)
-#   prof_c3 / prof_c2 / prof_c5 / prof_dp / prof_dpn   rocprofv3 --kernel-trace --stats of kprof (10 evaluations)
+#   prof_c3 / prof_c2 / prof_c5 / prof_dp / prof_dpn   rocprofv3 --kernel-trace --stats of kprof (30 evaluations)
 set -o pipefail
 TAG=$1; shift
 O=gpurun_out/$TAG; mkdir -p $O
@@ -21,8 +21,8 @@ run() {  # name seconds cmd...
 }
 prof() {  # name config args...
   local n=$1 c=$2; shift 2
-  run $n 240 rocprofv3 --kernel-trace --stats -d $O/$n -o $n -- python3 scripts/kprof.py --iters 10 --config $c "$@" || return 1
-  python3 scripts/kstats_db.py $(ls $O/$n/*/*.db 2>/dev/null | head -1) $O/${n}_kernel_stats.csv 2>/dev/null || \
+  run $n 240 rocprofv3 --kernel-trace --stats -d $O/$n -o $n -- python3 scripts/kprof.py --iters 30 --config $c "$@" || return 1
+  python3 scripts/kstats_db.py $(find $O/$n -name "*.db" | head -1) $O/${n}_kernel_stats.csv 2>/dev/null || \
     cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats.csv
   head -6 $O/${n}_kernel_stats.csv
 }

@@ -26,12 +26,14 @@ def test_struct_layouts_match_header(tmp_path):
     src = tmp_path / "sz.c"
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mtgp.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(MtgpNodeLibrary), sizeof(MtgpProgramSpec), sizeof(MtgpInstr), sizeof(MtgpModel),'
-                   'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));return 0;}\n')
+                   'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));'
+                   'printf("%zu\\n", offsetof(MtgpRollouts, lanes));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(t) for t in (nat.MtgpNodeLibrary, nat.MtgpProgramSpec, nat.MtgpInstr, nat.MtgpModel,
-                                       nat.MtgpRollouts, nat.MtgpOutputs)] + [nat.MtgpModel.readout_save_same.offset]
+                                       nat.MtgpRollouts, nat.MtgpOutputs)] + [nat.MtgpModel.readout_save_same.offset,
+                                                                              nat.MtgpRollouts.lanes.offset]
     assert got == want
 
 
@@ -51,11 +53,20 @@ def test_argument_validation_without_gpu():
     out.fitness = one.ctypes.data
     assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 1, one.ctypes.data, 1,
                              ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
-    ro.R = 65  # more than one wave of rollouts per individual
     m.save_every = 2
     m.n_save = 6
-    assert lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 1, one.ctypes.data, 1,
-                             ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
+
+    def rk4():
+        return lib.mtgp_eval_rk4(ctypes.byref(m), one.ctypes.data, one.ctypes.data, 1, 4, one.ctypes.data, 1,
+                                 ctypes.byref(ro), ctypes.byref(out), None)
+    ro.R = 65  # lane set over two waves: the mean is formed from rollout_fitness, which is missing
+    assert rk4() == nat.ERR_ARG
+    ro.R, ro.lanes = 8, 4  # lane set narrower than R
+    assert rk4() == nat.ERR_ARG
+    ro.lanes = 24  # not a power of two
+    assert rk4() == nat.ERR_ARG
+    ro.R, ro.lanes = nat.MAX_ROLLOUTS + 1, 0
+    assert rk4() == nat.ERR_ARG
 
 
 def _define(text, name):
@@ -73,6 +84,7 @@ def test_constants_match_header():
     assert _define(text, "MTGP_SCHED_SCRATCH") == nat.SCHED_SCRATCH
     assert _define(text, "MTGP_MAX_PROGRAMS") == nat.MAX_PROGRAMS
     assert _define(text, "MTGP_STACK_MAX") == nat.STACK_MAX
+    assert _define(text, "MTGP_MAX_ROLLOUTS") == nat.MAX_ROLLOUTS
     ops = open(os.path.join(ROOT, "include", "mtgp_opcodes.h")).read()
     pairs = re.findall(r"MTGP_OP_(\w+) = (\d+),", ops)
     assert [n for n, _ in pairs] == nat.OP_NAMES and [int(v) for _, v in pairs] == list(range(len(pairs)))

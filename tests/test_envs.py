@@ -124,10 +124,14 @@ def test_other_env_termination_gives_max_fitness():
 
 
 def test_environment_configuration_checks():
-    with pytest.raises(NotImplementedError):
-        mt.DynamicEvaluator(mt.HarmonicOscillator(0, 0, n_obs=1), 1, 0.05, solver=mt.RK4())
-    with pytest.raises(NotImplementedError):
-        mt.FeedforwardEvaluator(mt.StirredTankReactor(0, 0, n_obs=2), 0.05, solver=mt.RK4())
+    with pytest.raises(ValueError):  # C = eye(n_var)[:n_obs] needs 1 <= n_obs <= n_var
+        mt.DynamicEvaluator(mt.HarmonicOscillator(0, 0, n_obs=3), 1, 0.05, solver=mt.RK4())
+    with pytest.raises(ValueError):
+        mt.FeedforwardEvaluator(mt.StirredTankReactor(0, 0, n_obs=0), 0.05, solver=mt.RK4())
+    # fewer observations than states: the data slots after y move up in the kernel's layout
+    ev = mt.DynamicEvaluator(mt.Acrobot(0, 0, n_obs=2), 2, 0.05, solver=mt.RK4())
+    assert ev.n_data() == 2 + 2 + 1 and ev.obs_gap() == (2, 2)
+    assert all(sp[3:] == (2, 2) for sp in ev.program_specs()[0])
 
     class CartPole:  # no cond_fn_nan in the reference: not runnable by its evaluators
         n_obs = n_var = 4

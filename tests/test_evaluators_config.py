@@ -58,7 +58,7 @@ def test_program_specs_dynamic():
     ev = mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05)
     specs, roles = ev.program_specs()
     # state equations see [y, a, u]; readout in the drift sees y = 0, u = 0; at saves u = 0
-    assert specs == [(2, 7, 0b1001111), (0, 7, 0), (1, 7, 0), (2, 7, 0b1000000)]
+    assert specs == [(2, 7, 0b1001111, 4, 0), (0, 7, 0, 4, 0), (1, 7, 0, 4, 0), (2, 7, 0b1000000, 4, 0)]
     assert roles["prog_readout"] == 0 and roles["prog_state"] == 1 and roles["prog_readout_save"] == 3
 
 

@@ -23,7 +23,7 @@ def _flatten_ex(pop, lib, specs, L, mode=0):
     dev = torch.device("cuda", 0)
     n_prog = len(specs)
     arr = (nat.MtgpProgramSpec * n_prog)()
-    for i, (t, d, z) in enumerate(specs):
+    for i, (t, d, z) in enumerate(s[:3] for s in specs):
         arr[i].tree, arr[i].n_data, arr[i].zero_mask = t, d, z
     sp = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(dev)
     pd = torch.from_numpy(np.ascontiguousarray(pop, np.float32)).to(dev)
@@ -71,7 +71,7 @@ def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
     word = np.zeros(4096, np.uint32)
     for p in range(P):
         assert nodes[p] == int((pop[p, ..., 0] != 0).sum())
-        for j, (t, d, z) in enumerate(specs):
+        for j, (t, d, z) in enumerate(s[:3] for s in specs):
             n = L_.mtgp_flatten_tree_host(pop[p, t].ctypes.data, N, ctypes.byref(libs), d, z, L, host.ctypes.data,
                                           None)
             assert plen[p, j] == max(n, 0) and status[p, j] == (0 if n > 0 else -n), (p, j)

@@ -17,8 +17,8 @@ from helpers import (bits_equal, dynamic_setup, mismatch_report, oracle_model, o
 pytestmark = pytest.mark.gpu
 
 
-def _run(ff, lib, data, pop, parsimony=0.0, traj=True):
-    eng = DeviceEngine(ff, lib, parsimony, "cuda:0")
+def _run(ff, lib, data, pop, parsimony=0.0, traj=True, lanes=None):
+    eng = DeviceEngine(ff, lib, parsimony, "cuda:0", lanes=lanes)
     res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=traj,
                        rollout_fitness=True)
     torch.cuda.synchronize()
@@ -79,10 +79,16 @@ def test_eval_programs_garbage_arrays():
     assert checked > 400
 
 
+# lanes: None = the engine's occupancy policy (small P: one individual per wave), 0 = the densest
+# packing (64 / R individuals per wave), 32 = an intermediate lane set
+LANES = [None, 0, 32]
+
+
+@pytest.mark.parametrize("lanes", LANES)
 @pytest.mark.parametrize("R", [8, 32])
-def test_dynamic_acrobot_bitexact(R):
+def test_dynamic_acrobot_bitexact(R, lanes):
     env, lib, ff, data, pop = dynamic_setup(P=40, R=R, n_steps=80)
-    res, ref, d = _run(ff, lib, data, pop)
+    res, ref, d = _run(ff, lib, data, pop, lanes=lanes)
     _check(res, ref, pop.shape[0], R, ["xs", "ys", "us", "acts"])
 
 
@@ -95,23 +101,51 @@ def test_dynamic_fitness_only_matches_trajectory_mode():
     assert bits_equal(a, b)
 
 
-def test_static_acrobot_bitexact():
+@pytest.mark.parametrize("lanes", LANES)
+def test_static_acrobot_bitexact(lanes):
     env, lib, ff, data, pop = static_setup(P=40, R=16, n_steps=80)
-    res, ref, d = _run(ff, lib, data, pop, parsimony=1.0)
+    res, ref, d = _run(ff, lib, data, pop, parsimony=1.0, lanes=lanes)
     _check(res, ref, pop.shape[0], 16, ["xs", "ys", "us"])
 
 
-def test_sr_vanderpol_bitexact():
+@pytest.mark.parametrize("lanes", LANES)
+def test_sr_vanderpol_bitexact(lanes):
     env, lib, ff, data, pop = sr_setup(P=40, R=16)
-    res, ref, d = _run(ff, lib, data, pop)
+    res, ref, d = _run(ff, lib, data, pop, lanes=lanes)
     _check(res, ref, pop.shape[0], 16, ["xs"])
 
 
+@pytest.mark.parametrize("lanes", [None, 0])
 @pytest.mark.parametrize("R", [1, 33, 64])
-def test_rollout_counts(R):
+def test_rollout_counts(R, lanes):
     env, lib, ff, data, pop = dynamic_setup(P=9, R=R, n_steps=30, seed=7)
-    res, ref, d = _run(ff, lib, data, pop)
+    res, ref, d = _run(ff, lib, data, pop, lanes=lanes)
     _check(res, ref, pop.shape[0], R, ["xs", "us"])
+
+
+@pytest.mark.parametrize("R", [65, 128, 200])
+@pytest.mark.parametrize("kind", ["dynamic", "static", "sr", "sr_wide", "dynamic_dopri5"])
+def test_more_than_64_rollouts(kind, R):
+    """R > 64 (dyn.py:63 vmaps any batch): an individual's lane set spans ceil(R/64) rounded up
+    to a power of two waves, the mean over rollouts is formed by k_rollout_mean in the
+    kernel's pairwise order -- fitness, per-rollout fitness and trajectories bit-exact."""
+    if kind == "dynamic":
+        env, lib, ff, data, pop = dynamic_setup(P=11, R=R, n_steps=24, seed=9)
+        names = ["xs", "ys", "us", "acts"]
+    elif kind == "dynamic_dopri5":
+        env, lib, ff, data, pop = dynamic_setup(P=7, R=R, n_steps=20, seed=9, solver=(1e-3, 1e-3, 0.001, 60))
+        names = ["xs", "us"]
+    elif kind == "static":
+        env, lib, ff, data, pop = static_setup(P=11, R=R, n_steps=24, seed=9)
+        names = ["xs", "ys", "us"]
+    elif kind == "sr":
+        env, lib, ff, data, pop = sr_setup(P=11, R=R, n_save=9, seed=9)
+        names = ["xs"]
+    else:
+        env, lib, ff, data, pop = sr_setup(P=5, R=R, n_save=7, seed=9, n_var=6)
+        names = ["xs"]
+    res, ref, d = _run(ff, lib, data, pop, parsimony=0.5)
+    _check(res, ref, pop.shape[0], R, names)
 
 
 @pytest.mark.parametrize("n_var,R,N,depth", [(5, 8, 30, 5), (12, 3, 64, 8), (64, 8, 128, 16)])
@@ -350,3 +384,34 @@ def test_euler_bitexact(kind, jit):
         c = ref[k].shape[-1]
         got = res[k].reshape(S, c, P, R).transpose(2, 3, 0, 1)
         assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+
+
+@pytest.mark.parametrize("case", ["acrobot_dyn_2", "acrobot_dyn_1_noise", "acrobot_static_3_noise", "harmonic_dyn_1",
+                                  "reactor_static_2_noise", "acrobot_dyn_2_dopri5"])
+def test_fewer_observations_than_states(case):
+    """n_obs < n_var: C = eye(n_var)[:n_obs] (control_environment_base.py:47, acrobot.py:48), noise
+    normal(key, (n_obs,)) @ W with W = obs_noise * eye(n_obs) -- the data vector [y(n_obs), a, u,
+    tg] of the reference reaches the kernel's n_var-slot layout through MtgpProgramSpec.gap."""
+    env_name, kind, no = case.split("_")[:3]
+    noise = 0.1 if case.endswith("noise") else 0.0
+    solver = (1e-3, 1e-3, 0.001, 80) if case.endswith("dopri5") else None
+    cls = {"acrobot": mt.Acrobot, "harmonic": mt.HarmonicOscillator, "reactor": mt.StirredTankReactor}[env_name]
+    env = cls(0.0, noise, n_obs=int(no))
+    from helpers import CONTROL_OPS, _ctl_solver, _mode
+    from multitreegp_amd.sampling import sample_population
+    ys = [f"y{i + 1}" for i in range(env.n_obs)]
+    tg = [f"tar{i + 1}" for i in range(env.n_targets)]
+    if kind == "dyn":
+        vl = [ys + ["a1", "a2", "u"] + tg, ["a1", "a2"] + tg]
+        lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
+        ff = mt.DynamicEvaluator(env, 2, 0.05, **_ctl_solver(solver))
+        names = ["xs", "ys", "us", "acts"]
+    else:
+        lib = mt.NodeLibrary(CONTROL_OPS, [ys + tg], [1])
+        ff = mt.FeedforwardEvaluator(env, 0.05, **_ctl_solver(solver))
+        names = ["xs", "ys", "us"]
+    data = mt.control_data(env, 8, 0.05, None, seed=3, n_steps=40, mode=_mode(env_name))
+    pop = sample_population(4, lib, 24, 1, max_init_depth=5, max_nodes=30)[0]
+    res, ref, d = _run(ff, lib, data, pop)
+    assert res["ys"].shape[1] == env.n_obs
+    _check(res, ref, pop.shape[0], 8, names)

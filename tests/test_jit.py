@@ -306,7 +306,7 @@ def _host_flatten(ff, lib, pop):
     L = (2 * N + 8 + 3) // 4 * 4
     prog = np.zeros((P, len(specs), L, 2), np.uint32)
     for p in range(P):
-        for j, (t, nd, zm) in enumerate(specs):
+        for j, (t, nd, zm) in enumerate(sp[:3] for sp in specs):
             raw = _raw_program(pop[p, t], nl, nd, zm)
             prog[p, j, : raw.shape[0]] = raw
     return prog, specs, roles, L
@@ -348,7 +348,7 @@ def test_wave_units_emulate_to_oracle(kind, R):
         data = (rng.standard_normal((8, 64)) * 2).astype(np.float32)
         regs = _emulate(words, data, full=True)
         wave, j = divmod(u, n_prog)
-        t, nd, zm = specs[j]
+        t, nd, zm = specs[j][:3]
         for lane in range(64):
             g = lane // Rp
             q = wave * G + g
@@ -618,7 +618,7 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
                 if s46:
                     outs.append((8, roles["prog_readout_save"]))
                 for reg, j in outs:
-                    t, nd, zm = specs[j]
+                    t, nd, zm = specs[j][:3]
                     d = data[:n_data, lane].copy()
                     for b in range(nd):
                         if zm >> b & 1:
