@@ -72,6 +72,6 @@ def test_schedule_rejects_bad_arguments():
     order = torch.empty((4,), dtype=torch.int32, device="cuda:0")
     plen = torch.ones((4, 2), dtype=torch.int32, device="cuda:0")
     w = (np.ctypeslib.ctypes.c_int32 * 2)(1, 1)
-    for P, n_prog, R in ((4, 0, 8), (4, nat.MAX_PROGRAMS + 1, 8), (4, 2, 0), (4, 2, 65), (-1, 2, 8)):
+    for P, n_prog, R in ((4, 0, 8), (4, nat.MAX_PROGRAMS + 1, 8), (4, 2, 0), (4, 2, nat.MAX_ROLLOUTS + 1), (-1, 2, 8)):
         assert lib.mtgp_schedule(plen.data_ptr(), P, n_prog, w, R, order.data_ptr(), scratch.data_ptr(),
                                  None) == nat.ERR_ARG
