@@ -164,6 +164,12 @@ typedef struct {
   int32_t pid_custom;
   float pid_c1, pid_c2, pid_c3, pid_safety, pid_factormin, pid_factormax;
   int32_t no_force_dtmin; /* 1: force_dtmin=False -- dt < dtmin ends the solve (dt_min_reached) */
+  /* ABI v16: Dopri5 control models in two launches.  dp_budget > 0: launch 1 runs every wave for at
+   * most dp_budget step attempts and parks the waves that are not done in MtgpOutputs.dp_state /
+   * dp_pending; launch 2 resumes only those (a wave runs until its slowest lane is done, so the
+   * few long solves otherwise hold whole waves and SIMDs).  Results are identical either way.
+   * 0: one launch. */
+  int32_t dp_budget;
 } MtgpModel;
 enum { MTGP_SOLVER_RK4 = 0, MTGP_SOLVER_DOPRI5 = 1, MTGP_SOLVER_EULER = 2 };
 
@@ -205,7 +211,11 @@ typedef struct {
   float* acts;            /* [n_save, state_size, P*R] or NULL (dynamic)      */
   int32_t* steps;         /* [P, R] Dopri5 step attempts (accepted + rejected) or NULL (ABI v9; */
                           /* the fixed-step RK4 kernels leave it untouched)                      */
+  /* ABI v16, required when MtgpModel.dp_budget > 0 (scratch, contents undefined afterwards):   */
+  float* dp_state;        /* [MTGP_DP_STATE_WORDS, waves * 64] f32, waves = mtgp_eval_waves()   */
+  int32_t* dp_pending;    /* [1 + waves] int32                                                  */
 } MtgpOutputs;
+#define MTGP_DP_STATE_WORDS 32
 
 /* ------------------------------------------------------------- entry points */
 int mtgp_abi_version(void);
@@ -261,6 +271,10 @@ int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t*
                   int32_t* order_out, int32_t* scratch, void* stream);
 
 /* Integrate every (individual, rollout) with fixed-step RK4 and reduce fitness. */
+/* Waves of the evaluator launch for P individuals with lane set `lanes` (MtgpRollouts.lanes, or
+ * the rollout count R when lanes == 0): sizes MtgpOutputs.dp_state / dp_pending. */
+int mtgp_eval_waves(int32_t P, int32_t R, int32_t lanes);
+
 int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen,
                   int32_t n_prog, int32_t L, const int32_t* nodes, int32_t P,
                   const MtgpRollouts* rollouts, const MtgpOutputs* out, void* stream);

@@ -316,6 +316,14 @@ struct KArgs {
   int32_t chain_state;      // the JIT code chains the state role (MtgpJitChain): one call per stage
   int32_t chain_save;       // ... and continues it into the save-point readout on request (s46)
   int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
+  // Dopri5 in two launches (ABI v16, MtgpModel.dp_budget): launch 1 runs every wave for at most
+  // dp_budget attempts and parks the lanes of waves that are not done (dp_state, word-major
+  // [kDpStateWords][waves * 64]) in the list dp_pending ([0] = count, then wave ids); launch 2
+  // resumes only those waves, each (mostly) alone on its SIMD.
+  int32_t dp_budget, dp_pass;
+  float* dp_state;
+  int32_t* dp_pending;
+  uint32_t dp_lanes;  // waves * 64 of the launch: the stride of a dp_state word
 };
 
 // per-lane online Acrobot fitness (acrobot.py:77-84 restated for a single pass)
@@ -504,9 +512,20 @@ struct EnvReactor {
 
 // store v at row `row` (wave-uniform element offset) + off (per lane): the 64-bit row base
 // stays in SGPRs, only the 32-bit lane offset is a VGPR
+// Trajectory rows are written once and never read by the kernel: non-temporal stores (`nt`), so
+// the streaming output (C3: 2.3 GB, C5: 1.7 GB per launch) does not evict the JIT code and the
+// rollout data from L2 -- C5's per-stage code footprint (~2 MB per XCD) is refetched every stage
+// when it does (PMC: FETCH_SIZE 20 GB per launch with plain stores).
+#ifndef MTGP_V_NTSTORE
+#define MTGP_V_NTSTORE 1
+#endif
 __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
   float* p = arr + row;
+#if MTGP_V_NTSTORE
+  __builtin_nontemporal_store(v, p + off);
+#else
   p[off] = v;
+#endif
 }
 
 // --------------------------------------------------------------------------------------
@@ -573,10 +592,11 @@ __device__ __forceinline__ void lane_place(const KArgs& A, Lane& L, int wv) {
   }
 }
 
-__device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L) {
+// wv < 0: this wave's own index in the launch
+__device__ __forceinline__ bool lane_setup(const KArgs& A, Lane& L, int wv = -1) {
   L.wave = uni(threadIdx.x >> 6);
   L.lane = threadIdx.x & 63;
-  lane_place(A, L, (int)blockIdx.x * kWavesPerBlock + L.wave);
+  lane_place(A, L, wv >= 0 ? wv : (int)blockIdx.x * kWavesPerBlock + L.wave);
   if (L.q0 >= A.P) return false;
   const int q = L.q0 + L.g;
   L.p = q < A.P ? sched_ind(A, q) : A.P;  // A.P marks a padding group
@@ -1237,6 +1257,54 @@ __device__ __forceinline__ MtgpDpPid dp_pid(const MtgpModel& m) {
 // six FSAL stages, then one call per round of pending save points, then the +inf fill) runs for
 // all lanes, and only the lanes concerned commit.  Save points: dense output of [x, a] at ts[k],
 // then f_obs(ts[k], x) and the save-time readout / policy (dyn.py:99-101, ff.py:96-97).
+// A lane's Dopri5 solve between the two launches (KArgs.dp_state, word-major): t, t_next, the
+// controller history, flags, save index, attempts, y and the FSAL derivative f0, the fitness
+// accumulator -- everything the attempt loop carries, so launch 2 continues bit for bit.
+constexpr int kDpStateWords = MTGP_DP_STATE_WORDS;
+template <int ND, class Fit>
+struct DpParked {
+  float* base;
+  uint32_t stride, gl;
+  static constexpr int kFitWords = (int)((sizeof(Fit) + 3) / 4);
+  static_assert(7 + 2 * ND + kFitWords <= kDpStateWords, "Dopri5 parked state too large");
+  __device__ __forceinline__ float& w(int i) const { return base[(size_t)i * stride + gl]; }
+  __device__ __forceinline__ void save(float t, float tn, const MtgpDpCtl& c, bool ok, bool live, int k, int steps,
+                                       const float (&y)[ND], const float (&f0)[ND], const Fit& fit) const {
+    w(0) = t;
+    w(1) = tn;
+    w(2) = c.prev;
+    w(3) = c.prev2;
+    w(4) = __int_as_float((c.at_dtmin != 0) | (ok ? 2 : 0) | (live ? 4 : 0));
+    w(5) = __int_as_float(k);
+    w(6) = __int_as_float(steps);
+#pragma unroll
+    for (int i = 0; i < ND; ++i) { w(7 + i) = y[i]; w(7 + ND + i) = f0[i]; }
+    uint32_t fw[kFitWords];
+    __builtin_memcpy(fw, &fit, sizeof(Fit));
+#pragma unroll
+    for (int i = 0; i < kFitWords; ++i) w(7 + 2 * ND + i) = __uint_as_float(fw[i]);
+  }
+  __device__ __forceinline__ void load(float& t, float& tn, MtgpDpCtl& c, bool& ok, bool& live, int& k, int& steps,
+                                       float (&y)[ND], float (&f0)[ND], Fit& fit) const {
+    t = w(0);
+    tn = w(1);
+    c.prev = w(2);
+    c.prev2 = w(3);
+    const int fl = __float_as_int(w(4));
+    c.at_dtmin = fl & 1;
+    ok = (fl & 2) != 0;
+    live = (fl & 4) != 0;
+    k = __float_as_int(w(5));
+    steps = __float_as_int(w(6));
+#pragma unroll
+    for (int i = 0; i < ND; ++i) { y[i] = w(7 + i); f0[i] = w(7 + ND + i); }
+    uint32_t fw[kFitWords];
+#pragma unroll
+    for (int i = 0; i < kFitWords; ++i) fw[i] = __float_as_uint(w(7 + 2 * ND + i));
+    __builtin_memcpy(&fit, fw, sizeof(Fit));
+  }
+};
+
 #ifndef MTGP_DP_WAVES
 #define MTGP_DP_WAVES 2  // register budget of the Dopri5 control kernels (A/B: 2 beats 4, C3 23 vs 28 ms)
 #endif
@@ -1248,7 +1316,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   constexpr int ND = NV + NA;  // integrated state
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
-  if (!lane_setup(A, Ln)) return;
+  int wv = (int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
+  if (A.dp_pass == 2) {  // resume a parked wave of launch 1
+    if (wv >= A.dp_pending[0]) return;
+    wv = uni(A.dp_pending[1 + wv]);
+  }
+  if (!lane_setup(A, Ln, wv)) return;
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -1338,22 +1411,36 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   };
 
   float y[ND], y1[ND], f[7][ND];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
-#pragma unroll
-  for (int j = NV; j < ND; ++j) y[j] = 0.0f;
-  save_round(active, 0, y, false);
   int k = 1, steps = 0;
-  bool prev_ok = !Env::bad(y, ND);
+  bool prev_ok;
   MtgpDpCtl ctl{1.0f, 1.0f, 0};
   const MtgpDpPid pid = dp_pid(A.m);
   const int force_dtmin = !A.m.no_force_dtmin;
-  float t = ts[0];
-  float tnext = t + A.m.h;
-  tnext = tnext > t_end ? t_end : tnext;
-  rhs(t, y, f[0]);
-  bool live = active && t < t_end && steps < max_steps;
-  while (__any(live)) {
+  float t, tnext;
+  bool live;
+  DpParked<ND, typename Env::Fit> park{A.dp_state, A.dp_lanes, (uint32_t)wv * kWave + (uint32_t)Ln.lane};
+  if (A.dp_pass == 2) {
+    park.load(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+  } else {
+#pragma unroll
+    for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
+#pragma unroll
+    for (int j = NV; j < ND; ++j) y[j] = 0.0f;
+    save_round(active, 0, y, false);
+    prev_ok = !Env::bad(y, ND);
+    t = ts[0];
+    tnext = t + A.m.h;
+    tnext = tnext > t_end ? t_end : tnext;
+    rhs(t, y, f[0]);
+    live = active && t < t_end && steps < max_steps;
+  }
+  const int budget = A.dp_pass == 1 ? A.dp_budget : 0x7fffffff;
+  for (int iter = 0; __any(live); ++iter) {
+    if (iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
+      park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+      if (Ln.lane == 0) A.dp_pending[1 + atomicAdd(A.dp_pending, 1)] = wv;
+      return;
+    }
     const float h = tnext - t;
 #pragma unroll 1
     for (int s = 1; s <= 6; ++s) {
@@ -3463,7 +3550,21 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
   }
   if (model->solver == MTGP_SOLVER_DOPRI5) {
     int rc = MTGP_OK;
-    const int lr = launch_timed([&] { rc = launch_dp_entry<Env>(&A, model, jit, noise, traj, grid.x, block.x, s); }, s);
+    const int lr = launch_timed([&] {
+      if (A.dp_budget <= 0) {
+        rc = launch_dp_entry<Env>(&A, model, jit, noise, traj, grid.x, block.x, s);
+        return;
+      }
+      // two launches: every wave for dp_budget attempts, then the parked waves (KArgs.dp_*)
+      if (hipMemsetAsync(A.dp_pending, 0, sizeof(int32_t), s) != hipSuccess) { rc = MTGP_ERR_LAUNCH; return; }
+      KArgs A1 = A;
+      A1.dp_pass = 1;
+      rc = launch_dp_entry<Env>(&A1, model, jit, noise, traj, grid.x, block.x, s);
+      if (rc != MTGP_OK) return;
+      KArgs A2 = A;
+      A2.dp_pass = 2;
+      rc = launch_dp_entry<Env>(&A2, model, jit, noise, traj, grid.x, block.x, s);
+    }, s);
     return rc != MTGP_OK ? rc : lr;
   }
   if (model->model == MTGP_MODEL_STATIC) return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_static, Env); }, s);
@@ -3859,6 +3960,19 @@ int mtgp_eval_programs(const MtgpInstr* prog, const int32_t* plen, int32_t n_pro
   return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
 }
 
+int mtgp_eval_waves(int32_t P, int32_t R, int32_t lanes) {
+  if (P < 0 || R <= 0 || R > MTGP_MAX_ROLLOUTS || lanes < 0) return MTGP_ERR_ARG;
+  int Rp = 1;
+  while (Rp < R) Rp <<= 1;
+  if (lanes > 0) {
+    if (lanes < R || (lanes & (lanes - 1)) != 0) return MTGP_ERR_ARG;
+    Rp = lanes;
+  }
+  const long G = Rp >= kWave ? 1 : kWave / Rp, W = Rp > kWave ? Rp / kWave : 1;
+  const long waves = (P + G - 1) / G * W;
+  return waves > INT32_MAX / kWave ? MTGP_ERR_ARG : (int)waves;
+}
+
 int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* plen, int32_t n_prog, int32_t L,
                   const int32_t* nodes, int32_t P, const MtgpRollouts* rollouts, const MtgpOutputs* out,
                   void* stream) {
@@ -3907,6 +4021,17 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   A.jit_info = jit ? jitc->info : nullptr;
   A.jit_cap = jit ? jitc->capacity : 0;
   A.chain_state = A.chain_save = A.chain_store = 0;
+  A.dp_budget = 0;
+  A.dp_pass = 0;
+  A.dp_state = nullptr;
+  A.dp_pending = nullptr;
+  A.dp_lanes = 0;
+  if (model->dp_budget > 0 && dopri5 && model->model != MTGP_MODEL_SR) {  // two launches (control models)
+    if (!out->dp_state || !out->dp_pending) return MTGP_ERR_ARG;
+    A.dp_budget = model->dp_budget;
+    A.dp_state = out->dp_state;
+    A.dp_pending = out->dp_pending;
+  }
   if (jit && (jitc->chain.next | jitc->chain.cond | jitc->chain.store) != 0u) {  // must be the chain this model calls
     const MtgpJitChain want = jit_chain_for(*model, n_prog);
     if (want.next != jitc->chain.next || want.cond != jitc->chain.cond || want.store != jitc->chain.store)
@@ -3920,6 +4045,8 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const int G = Rp >= kWave ? 1 : kWave / Rp;  // individuals packed per wave
   const int Wset = Rp > kWave ? Rp / kWave : 1;  // waves per individual
   const long waves = ((long)P + G - 1) / G * Wset;
+  if (waves * kWave > (long)UINT32_MAX) return MTGP_ERR_ARG;
+  A.dp_lanes = (uint32_t)(waves * kWave);
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
   const bool noise = rollouts->obs_keys != nullptr;

@@ -27,13 +27,14 @@ def test_struct_layouts_match_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mtgp.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(MtgpNodeLibrary), sizeof(MtgpProgramSpec), sizeof(MtgpInstr), sizeof(MtgpModel),'
                    'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));'
-                   'printf("%zu\\n", offsetof(MtgpRollouts, lanes));return 0;}\n')
+                   'printf("%zu %zu\\n", offsetof(MtgpRollouts, lanes), offsetof(MtgpModel, dp_budget));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(t) for t in (nat.MtgpNodeLibrary, nat.MtgpProgramSpec, nat.MtgpInstr, nat.MtgpModel,
                                        nat.MtgpRollouts, nat.MtgpOutputs)] + [nat.MtgpModel.readout_save_same.offset,
-                                                                              nat.MtgpRollouts.lanes.offset]
+                                                                              nat.MtgpRollouts.lanes.offset,
+                                                                              nat.MtgpModel.dp_budget.offset]
     assert got == want
 
 
@@ -67,6 +68,18 @@ def test_argument_validation_without_gpu():
     assert rk4() == nat.ERR_ARG
     ro.R, ro.lanes = nat.MAX_ROLLOUTS + 1, 0
     assert rk4() == nat.ERR_ARG
+    # launch geometry (sizes of the Dopri5 parked-state buffers)
+    assert lib.mtgp_eval_waves(8192, 32, 0) == 4096  # C3: two individuals per wave
+    assert lib.mtgp_eval_waves(1024, 16, 64) == 1024  # C2 lane set widened: one per wave
+    assert lib.mtgp_eval_waves(10, 128, 0) == 20      # R > 64: two waves per individual
+    assert lib.mtgp_eval_waves(7, 100, 0) == 14
+    assert lib.mtgp_eval_waves(5, 8, 4) == nat.ERR_ARG and lib.mtgp_eval_waves(5, 8, 12) == nat.ERR_ARG
+    ro.R, ro.lanes = 8, 0
+    ro.x0 = ro.ts = ro.params = one.ctypes.data
+    m.solver, m.dp_budget, m.max_steps, m.h, m.n_save = 1, 16, 10, 0.1, 4  # Dopri5 in two launches:
+    out.dp_state = None                                                     # the parked-state buffer is required
+    m.model, m.n_var, m.n_obs, m.n_control, m.state_size = 1, 4, 4, 1, 2  # otherwise a valid Acrobot model
+    assert rk4() == nat.ERR_ARG
 
 
 def _define(text, name):
@@ -85,6 +98,7 @@ def test_constants_match_header():
     assert _define(text, "MTGP_MAX_PROGRAMS") == nat.MAX_PROGRAMS
     assert _define(text, "MTGP_STACK_MAX") == nat.STACK_MAX
     assert _define(text, "MTGP_MAX_ROLLOUTS") == nat.MAX_ROLLOUTS
+    assert _define(text, "MTGP_DP_STATE_WORDS") == nat.DP_STATE_WORDS
     ops = open(os.path.join(ROOT, "include", "mtgp_opcodes.h")).read()
     pairs = re.findall(r"MTGP_OP_(\w+) = (\d+),", ops)
     assert [n for n, _ in pairs] == nat.OP_NAMES and [int(v) for _, v in pairs] == list(range(len(pairs)))

@@ -204,12 +204,12 @@ def test_dopri5_sr_population_oracle_is_deterministic():
 
 
 # ------------------------------------------------------------------ GPU parity (k_sr_dopri5)
-def _gpu_run(ff, lib, data, pop, jit, traj=True):
+def _gpu_run(ff, lib, data, pop, jit, traj=True, dp_budget=None, steps=False):
     import torch
     from multitreegp_amd.engine import DeviceEngine
-    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=jit)
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0", jit=jit, dp_budget=dp_budget)
     res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=traj,
-                       rollout_fitness=True)
+                       rollout_fitness=True, step_counts=steps)
     torch.cuda.synchronize()
     assert DeviceEngine.jit_ok(res["_flat"]) == jit
     return {k: v.cpu().numpy() for k, v in res.items() if isinstance(v, torch.Tensor)}, eng.prepare_data(data)
@@ -401,3 +401,34 @@ def test_gpu_dopri5_step_counts():
     st = a["steps"].cpu().numpy()
     assert st.shape == (40, 8) and st.min() >= 1 and st.max() <= 250
     assert bits_equal(a["rollout_fitness"].cpu().numpy(), b["rollout_fitness"].cpu().numpy())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("jit", [True, False])
+@pytest.mark.parametrize("budget", [0, 1, 7, 40])
+@pytest.mark.parametrize("kind", ["dynamic", "static_noise"])
+def test_gpu_dopri5_two_launches_bitexact(kind, budget, jit):
+    """MtgpModel.dp_budget: launch 1 parks every wave still integrating after `budget` attempts
+    (t, controller history, FSAL derivative, save index, fitness accumulator ...), launch 2 resumes
+    only those -- fitness, per-rollout fitness, step counts and trajectories identical to one
+    launch (budget 0) and to the oracle, including waves parked mid-way through their save points
+    and waves whose lanes all finished in launch 1."""
+    from helpers import bits_equal, dynamic_setup, mismatch_report, static_setup
+    solver = (1e-4, 1e-4, 0.001, 200)
+    if kind == "dynamic":
+        e, lib, ff, data, pop = dynamic_setup(P=37, R=12, n_steps=40, seed=8, solver=solver)
+    else:
+        e, lib, ff, data, pop = static_setup(P=37, R=12, n_steps=40, seed=8, obs_noise=0.1, solver=solver)
+    res, d = _gpu_run(ff, lib, data, pop, jit, dp_budget=budget, steps=True)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res[k], ref[k]), mismatch_report(res[k], ref[k], k)
+    P, R, S = pop.shape[0], d["R"], d["n_save"]
+    for k in ("xs", "ys", "us", "acts"):
+        if k in ref:
+            got = res[k].reshape(S, ref[k].shape[-1], P, R).transpose(2, 3, 0, 1)
+            assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+    one, _ = _gpu_run(ff, lib, data, pop, jit, dp_budget=0, steps=True)
+    assert np.array_equal(res["steps"], one["steps"])
+    if budget:  # the budget split the solves: some waves were parked
+        assert (one["steps"] > budget).any()
