@@ -391,6 +391,16 @@ int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, 
                  const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
                  float* scratch, float* loss_out, float* grad_out, void* stream);
 
+/* ABI v16: the same for the dynamic and static control models (dynamic_evaluate.py:37-118,
+ * feedforward_evaluate.py:36-110; value_and_grad of gp.py:253 / 435-452): every MTGP_ENV_*,
+ * MTGP_SOLVER_RK4 or MTGP_SOLVER_EULER, observation noise included, state_size <= 3, R <= 64.
+ * The programs read the reference's data vector [y(n_obs), a, u, targets] (MtgpProgramSpec gap 0)
+ * followed by the K parameter slots.  Tangent rules: include/mtgp_dual.h (the environment drift,
+ * f_obs, clip); the argmax step of the Acrobot fitness (acrobot.py:79) is piecewise constant. */
+int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                  const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
+                  float* scratch, float* loss_out, float* grad_out, void* stream);
+
 /* Wall time of the calling thread's last timed mtgp_eval_rk4 kernel (ms), measured with
  * hipEvents recorded on its stream around the launch; -1 if none.  Synchronises that event.
  * The on/off switch (mtgp_set_timing) is process-wide; events are per host thread and device. */

@@ -9,12 +9,15 @@ Every 5th generation after generation 10 the reference takes the 50 best candida
 * ``optimise`` (gp.py:454-473): the best loss over the epochs and the candidate it belongs to
   (first minimum).
 
-Here the loss and gradient come from ``mtgp_sr_grad`` (csrc/mtgp_grad.hip): forward-mode dual
-numbers through the same RK4 / Euler solve as the evaluator, one GPU lane per (candidate,
+Here the loss and gradient come from ``mtgp_sr_grad`` (the SR evaluator) and ``mtgp_ctl_grad``
+(the dynamic and static control evaluators, every environment; csrc/mtgp_grad.hip): forward-mode
+dual numbers through the same RK4 / Euler solve as the evaluator, one GPU lane per (candidate,
 parameter, rollout).  The parameters are the coefficient rows (``f == 1``) of every tree: the
-host turns the rows of one chunk into variable rows that read data slots ``n_var + k``, so the
-ordinary flattener produces the programs; other rows keep their reference meaning.  The
-optimiser is optax's Adam restated in float32 numpy (``adam``), applied on the host.
+host turns the rows of one chunk into variable rows that read data slots ``n_data + k`` (after
+the evaluator's data vector), so the ordinary flattener produces the programs; other rows keep
+their reference meaning.  The optimiser (optax's Adam restated in float32 numpy, ``adam``, or any
+object with optax's init / update) runs on the host with one state per candidate, as the
+reference's ``jax.vmap(self.optimiser.init)`` / ``jax.vmap(self.optimiser.update)`` do.
 
 Deviation (documented in DESIGN.md): JAX differentiates w.r.t. the whole value column, which
 also reaches entries read through a reference to a LATER row (the "original column" case of
@@ -133,10 +136,16 @@ class CoefficientOptimiser:
 
     @staticmethod
     def check_evaluator(ff):
-        if ff.model_id != nat.MODEL_SR or getattr(ff, "solver_kind", "") not in ("rk4", "euler"):
-            raise NotImplementedError("coefficient optimisation runs the SR evaluator with a fixed-step solver "
-                                      "(RK4 or Euler); control evaluators and the adaptive Dopri5 solve are not "
-                                      "differentiated here (SURVEY.md §8f row 4)")
+        if getattr(ff, "solver_kind", "") not in ("rk4", "euler"):
+            raise NotImplementedError("coefficient optimisation differentiates the fixed-step solves (RK4 or "
+                                      "Euler); the adaptive Dopri5 solve's step control is not differentiated here "
+                                      "(SURVEY.md §8f row 4)")
+        if ff.model_id != nat.MODEL_SR and getattr(ff, "state_size", 0) > 3:
+            raise NotImplementedError("coefficient optimisation of the dynamic evaluator: state_size <= 3")
+
+    def _grad_fn(self):
+        eng = self.engine
+        return eng.native.mtgp_sr_grad if eng.ff.model_id == nat.MODEL_SR else eng.native.mtgp_ctl_grad
 
     def param_cap(self, n_data: int) -> int:
         lib = self.engine.lib
@@ -161,11 +170,14 @@ class CoefficientOptimiser:
         m = eng.model_struct(d)
         ro = eng.rollouts_struct(d)
         R = d["R"]
-        L = (2 * N + 8 + 3) // 4 * 4
+        if R > 64:
+            raise NotImplementedError("coefficient optimisation with more than 64 rollouts")
+        L = eng.program_stride(N)
+        grad_fn = self._grad_fn()
         for lo in range(0, max(n_max, 1), cap):
             pop, theta, nparam, K, libs = parameterise(cands, rows, eng.lib, n_data, lo, lo + cap)
             spec_arr = (nat.MtgpProgramSpec * len(specs))()
-            for i, sp in enumerate(specs):
+            for i, sp in enumerate(specs):  # the reference's data vector + K parameter slots (no slot gap)
                 spec_arr[i].tree, spec_arr[i].n_data, spec_arr[i].zero_mask = sp[0], sp[1] + K, sp[2]
             spec_dev = torch.frombuffer(bytearray(bytes(spec_arr)), dtype=torch.uint8).to(dev)
             n_prog = len(specs)
@@ -187,11 +199,10 @@ class CoefficientOptimiser:
             scratch = torch.empty((B * K * R * 2,), dtype=torch.float32, device=dev)
             lo_d = torch.empty((B,), dtype=torch.float32, device=dev)
             gr_d = torch.empty((B, K), dtype=torch.float32, device=dev)
-            rc = eng.native.mtgp_sr_grad(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(),
-                                         npd.data_ptr(), K, ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(),
-                                         gr_d.data_ptr(), stream)
+            rc = grad_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
+                         ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), stream)
             if rc != nat.OK:
-                raise RuntimeError(f"mtgp_sr_grad rejected the configuration (code {rc})")
+                raise RuntimeError(f"{grad_fn.__name__} rejected the configuration (code {rc})")
             g = gr_d.cpu().numpy()
             if loss is None:
                 loss = lo_d.cpu().numpy()
@@ -211,16 +222,18 @@ class CoefficientOptimiser:
             return np.concatenate([c[b][r[:, 0], r[:, 1], 3] for b, r in enumerate(rows)] + [np.zeros(0, np.float32)])
 
         vals = values(cands).astype(np.float32)
-        state = opt.init(vals)
+        # one optimiser state per candidate (gp.py:468 vmaps init, gp.py:448 vmaps update): an
+        # optimiser with cross-element state (e.g. global-norm clipping) never couples candidates
+        states = [opt.init(vals[offs[b]: offs[b + 1]]) for b in range(len(rows))]
         hist_c, hist_l = [], []
         for _ in range(int(n_epoch)):
             loss, grads = self.loss_and_grad(cands, data, rows)
             hist_c.append(cands.copy())
             hist_l.append(loss)
-            g = np.concatenate(grads + [np.zeros(0, np.float32)]).astype(np.float32)
-            upd, state = opt.update(g, state, vals)
-            vals = (vals + np.asarray(upd, np.float32)).astype(np.float32)
             for b, r in enumerate(rows):
+                v = vals[offs[b]: offs[b + 1]]
+                upd, states[b] = opt.update(np.asarray(grads[b], np.float32), states[b], v)
+                vals[offs[b]: offs[b + 1]] = (v + np.asarray(upd, np.float32)).astype(np.float32)
                 cands[b][r[:, 0], r[:, 1], 3] = vals[offs[b]: offs[b + 1]]
         L = np.stack(hist_l)
         best = np.argmin(L, axis=0)

@@ -16,6 +16,8 @@
 #include <stdint.h>
 #include "mtgp.h"
 #include "mtgp_f32math.h"
+#include "mtgp_prng.h"
+#include "mtgp_dual.h"
 
 namespace {
 
@@ -82,9 +84,10 @@ __device__ __forceinline__ Dual slot_val(uint32_t off, const float* sv, const fl
   return {th[s - nv], (s - nv == kk) ? 1.0f : 0.0f};
 }
 
-// One program (mtgp.h format, every opcode incl. the fused forms) in dual numbers.
-template <int NV>
-__device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd, int nv, const float* th, int kk) {
+// One program (mtgp.h format, every opcode incl. the fused forms) in dual numbers; V(off) reads
+// data slot off / MTGP_SLOT_BYTES as a Dual.
+template <class Src>
+__device__ Dual run_dual_src(const MtgpInstr* code, Src V) {
   Dual acc = {0.0f, 0.0f};
   Dual stk[MTGP_STACK_MAX];
   int sp = 0;
@@ -93,7 +96,6 @@ __device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd
     const float imm = code[pc].imm;
     const uint32_t ib = __float_as_uint(imm);
     const Dual C = {imm, 0.0f};
-    auto V = [&](uint32_t off) { return slot_val<NV>(off, sv, sd, nv, th, kk); };
     auto push = [&]() { stk[sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1] = acc; ++sp; };
     auto pop = [&]() { --sp; return stk[sp < 0 ? 0 : (sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1)]; };
     switch (op) {
@@ -151,6 +153,11 @@ __device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd
       default: return acc;  // unknown word: the flattener never emits one
     }
   }
+}
+
+template <int NV>
+__device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd, int nv, const float* th, int kk) {
+  return run_dual_src(code, [&](uint32_t off) { return slot_val<NV>(off, sv, sd, nv, th, kk); });
 }
 
 // One (individual p, parameter k, rollout r) per lane; k_sr's integration in dual numbers.
@@ -284,7 +291,344 @@ __global__ void __launch_bounds__(256) k_grad_reduce(GradArgs A) {
   A.grad[gid] = k < A.nparam[p] ? dmean : 0.0f;
 }
 
+// ------------------------------------------------------------------------------------------
+// Control evaluators (dynamic_evaluate.py:37-118, feedforward_evaluate.py:36-110) with a
+// fixed-step solve: one (individual p, parameter k, rollout r) per lane, the evaluator's solve in
+// dual numbers -- f_obs (C @ x + noise, Acrobot wrap), the readout / policy and state programs
+// (parameterised: data slots D .. D + K - 1 are the coefficients), the environment drift in the
+// spec of include/mtgp_dual.h, RK4 / Euler, the Event, the save-point readout and an online
+// fitness whose every addition is the oracle's (oracle_ctl_grad; value = the evaluator's rollout
+// fitness bit for bit).  The data vector is the reference's [y(n_obs), a, u, tg] (no slot gap).
+__device__ __forceinline__ MtgpDual tod(Dual a) { return mtgp_dl(a.v, a.d); }
+__device__ __forceinline__ Dual frd(MtgpDual a) { return {a.v, a.d}; }
+
+template <int ENV>
+struct CtlEnv;
+template <>
+struct CtlEnv<0> {  // Acrobot
+  static constexpr int NV = 4, NP = 4;
+};
+template <>
+struct CtlEnv<1> {  // HarmonicOscillator
+  static constexpr int NV = 2, NP = 2;
+};
+template <>
+struct CtlEnv<2> {  // StirredTankReactor
+  static constexpr int NV = 3, NP = 8;
+};
+
+constexpr int kCtlData = 8;  // data slots of the control models (mtgp_kernels.hip kDMax)
+
+template <int ENV, int NA>
+__global__ void __launch_bounds__(256) k_ctl_grad(GradArgs A) {
+  constexpr int NV = CtlEnv<ENV>::NV, NP = CtlEnv<ENV>::NP, ND = NV + NA;
+  constexpr bool DYN = NA > 0;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int R = A.ro.R;
+  if (gid >= (long)A.P * A.K * R) return;
+  const int r = (int)(gid % R);
+  const long pk = gid / R;
+  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
+  float* out = A.part + (size_t)gid * 2;
+  const int np = A.nparam[p];
+  if (k > 0 && k >= np) {
+    out[0] = 0.0f;
+    out[1] = 0.0f;
+    return;
+  }
+  const int kk = k < np ? k : -1;
+  const float* th = A.theta + (size_t)p * A.K;
+  const int no = A.m.n_obs, nt = A.m.n_targets;
+  const int D = DYN ? no + NA + 1 + nt : no + nt;
+  const MtgpInstr* pr = A.prog + (size_t)p * A.n_prog * A.L;
+  const MtgpInstr* p_read = pr + (size_t)A.m.prog_readout * A.L;
+  const MtgpInstr* p_save = pr + (size_t)A.m.prog_readout_save * A.L;
+  const MtgpInstr* p_state = pr + (size_t)(A.m.prog_state < 0 ? 0 : A.m.prog_state) * A.L;
+  float prm[NP], tg[kCtlData];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) prm[i] = A.ro.params[(size_t)r * NP + i];
+  for (int i = 0; i < nt && i < kCtlData; ++i) tg[i] = A.ro.targets[(size_t)r * nt + i];
+  const uint32_t* key = A.ro.obs_keys ? A.ro.obs_keys + 2 * (size_t)r : nullptr;
+  // the data vector of a program call, and its reader
+  float dvv[kCtlData], dvd[kCtlData];
+  auto V = [&](uint32_t off) -> Dual {
+    const int sl = (int)(off / MTGP_SLOT_BYTES);
+    if (sl < D) {
+      float v = 0.0f, d = 0.0f;
+#pragma unroll
+      for (int i = 0; i < kCtlData; ++i) {
+        v = (i == sl) ? dvv[i] : v;
+        d = (i == sl) ? dvd[i] : d;
+      }
+      return {v, d};
+    }
+    return {th[sl - D], (sl - D == kk) ? 1.0f : 0.0f};
+  };
+  auto put = [&](int i, Dual x) {
+#pragma unroll
+    for (int j = 0; j < kCtlData; ++j) {
+      dvv[j] = (j == i) ? x.v : dvv[j];
+      dvd[j] = (j == i) ? x.d : dvd[j];
+    }
+  };
+  // f_obs (cbase.py:43-48, acrobot.py:29-32) in duals: the oracle's ctl_f_obs_dual
+  auto f_obs = [&](float t, const Dual* x, Dual* y) {
+    float nz[NV];
+#pragma unroll
+    for (int j = 0; j < NV; ++j) nz[j] = 0.0f;
+    if (key) {
+      float n[8];
+      mtgp_obs_normals(key[0], key[1], t, no, A.m.prng_impl, n);
+      for (int j = 0; j < no; ++j) {
+        float sacc = n[0] * A.ro.obs_w[0 * no + j];
+        for (int i = 1; i < no; ++i) sacc = sacc + n[i] * A.ro.obs_w[i * no + j];
+        nz[j] = sacc;
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      if (i >= no) { y[i] = {0.0f, 0.0f}; continue; }
+      MtgpDual sacc = mtgp_dl_cmul(i == 0 ? 1.0f : 0.0f, tod(x[0]));
+#pragma unroll
+      for (int j = 1; j < NV; ++j) sacc = mtgp_dl_add(sacc, mtgp_dl_cmul(i == j ? 1.0f : 0.0f, tod(x[j])));
+      y[i] = frd(mtgp_dl_addc(sacc, nz[i]));
+    }
+    if (ENV == 0) {
+      y[0] = frd(mtgp_dl_wrap_angle(tod(y[0])));
+      if (no > 1) y[1] = frd(mtgp_dl_wrap_angle(tod(y[1])));
+    }
+  };
+  auto drift = [&](const Dual* x, Dual u, Dual* dx) {
+    MtgpDual xx[NV], d[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) xx[i] = tod(x[i]);
+    if constexpr (ENV == 0) mtgp_dl_acro_drift(prm, xx, tod(u), d);
+    else if constexpr (ENV == 1) mtgp_dl_ho_drift(prm, xx, tod(u), d);
+    else mtgp_dl_reactor_drift(prm, xx, tod(u), d);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dx[i] = frd(d[i]);
+  };
+  // _drift (dyn.py:107-118 / ff.py:104-110) in duals
+  auto rhs = [&](float t, const Dual* st, Dual* ds) {
+    Dual y[NV];
+    f_obs(t, st, y);
+#pragma unroll
+    for (int j = 0; j < kCtlData; ++j) { dvv[j] = 0.0f; dvd[j] = 0.0f; }
+    if (DYN) {
+#pragma unroll
+      for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, st[NV + j]);
+      for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
+      const Dual u = run_dual_src(p_read, V);  // [0, a, 0, tg]
+      drift(st, u, ds);
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (i < no) put(i, y[i]);
+      put(no + NA, u);
+#pragma unroll
+      for (int j = 0; j < (DYN ? NA : 1); ++j) ds[NV + j] = run_dual_src(p_state + (size_t)j * A.L, V);
+    } else {
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        if (i < no) put(i, y[i]);
+      for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
+      const Dual u = run_dual_src(p_read, V);
+      drift(st, u, ds);
+    }
+  };
+  // online fitness over the save points (oracle_ctl_grad's full-array loop, addition for addition)
+  const int S = A.m.n_save;
+  const float* ts = A.ro.ts;
+  const float dts = ts[1] - ts[0];
+  bool settled = false;
+  int fs = 0;
+  MtgpDual cs = mtgp_dl(0.0f, 0.0f), c0 = mtgp_dl(0.0f, 0.0f);
+  auto save_point = [&](int q, const Dual* xq) {
+    Dual y[NV];
+    f_obs(ts[q], xq, y);
+#pragma unroll
+    for (int j = 0; j < kCtlData; ++j) { dvv[j] = 0.0f; dvd[j] = 0.0f; }
+#pragma unroll
+    for (int i = 0; i < NV; ++i)
+      if (i < no) put(i, y[i]);
+    Dual u;
+    if (DYN) {
+#pragma unroll
+      for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, xq[NV + j]);
+      for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
+      u = run_dual_src(p_save, V);  // dyn.py:101 [y, a, 0, tg]
+    } else {
+      for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
+      u = run_dual_src(p_read, V);  // ff.py:97
+    }
+    if constexpr (ENV == 0) {
+      const MtgpDual ud = tod(u);
+      const MtgpDual cost = mtgp_dl_mul(mtgp_dl_mulc(ud, 0.01f), ud);
+      const bool reached = ((-mtgp_cosf(xq[0].v)) - mtgp_cosf(xq[0].v + xq[1].v)) > 1.5f;
+      if (q == 0) {
+        const bool incl0 = !((ts[0] / dts) > 0.0f);
+        c0 = mtgp_dl_add(mtgp_dl(0.0f, 0.0f), incl0 ? cost : mtgp_dl(0.0f, 0.0f));
+        cs = mtgp_dl_add(mtgp_dl(0.0f, 0.0f), cost);
+        if (reached) { settled = true; fs = 0; cs = c0; }
+      } else if (settled) {
+        cs = mtgp_dl_add(cs, mtgp_dl(0.0f, 0.0f));
+      } else if (reached) {
+        fs = q;
+        cs = mtgp_dl_add(cs, ((ts[q] / dts) > (float)q) ? mtgp_dl(0.0f, 0.0f) : cost);
+        settled = true;
+      } else {
+        cs = mtgp_dl_add(cs, cost);
+      }
+    } else if constexpr (ENV == 1) {
+      const float Q[4] = {0.5f, 0.0f, 0.0f, 0.0f};
+      const float ud0 = (-0.0f * 0.0f + -1.0f * (-prm[0])) * tg[0] + ((-0.0f) * 1.0f + (-1.0f) * (-prm[1])) * 0.0f;
+      const MtgpDual e[2] = {mtgp_dl_subc(tod(xq[0]), tg[0]), mtgp_dl_subc(tod(xq[1]), 0.0f)};
+      const MtgpDual du = mtgp_dl_subc(tod(u), ud0);
+      cs = mtgp_dl_add(cs, mtgp_dl_add(mtgp_dl_quad_form(e, Q, 2), mtgp_dl_mul(mtgp_dl_mulc(du, 0.5f), du)));
+    } else {
+      const float Q[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.01f, 0.0f, 0.0f, 0.0f, 0.0f};
+      const MtgpDual e[3] = {mtgp_dl_subc(tod(xq[0]), 0.0f), mtgp_dl_subc(tod(xq[1]), tg[0]),
+                             mtgp_dl_subc(tod(xq[2]), 0.0f)};
+      cs = mtgp_dl_add(cs, mtgp_dl_add(mtgp_dl_quad_form(e, Q, 3), mtgp_dl_mul(mtgp_dl_mulc(tod(u), 0.0001f), tod(u))));
+    }
+  };
+  auto bad = [&](const Dual* st) {  // cond_fn (acrobot.py:86-87; the others: any non-finite)
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < ND; ++i) b = b || !mtgp_isfinite(st[i].v);
+    if (ENV == 0) {
+      b = b || (!mtgp_isnan(st[2].v) && __builtin_fabsf(st[2].v) > MTGP_8PI_F);
+      b = b || (!mtgp_isnan(st[3].v) && __builtin_fabsf(st[3].v) > MTGP_18PI_F);
+    }
+    return b;
+  };
+  Dual s[ND], kx[ND], acc[ND], tmp[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) s[i] = {i < NV ? A.ro.x0[(size_t)r * NV + i] : 0.0f, 0.0f};
+  save_point(0, s);
+  bool prev_ok = !bad(s), done = false;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ts[0];
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;
+  int q_saved = 0;
+  for (int step = 1; step <= A.m.n_steps && !done; ++step) {
+    const float t = t0 + (float)(step - 1) * h;
+    rhs(t, s, kx);
+    if (euler) {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) s[i] = {s[i].v + kx[i].v * h, s[i].d + kx[i].d * h};
+    } else {
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        acc[i] = kx[i];
+        tmp[i] = {MTGP_FMAF(h2, kx[i].v, s[i].v), MTGP_FMAF(h2, kx[i].d, s[i].d)};
+      }
+      rhs(t + h2, tmp, kx);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        acc[i] = {MTGP_FMAF(2.0f, kx[i].v, acc[i].v), MTGP_FMAF(2.0f, kx[i].d, acc[i].d)};
+        tmp[i] = {MTGP_FMAF(h2, kx[i].v, s[i].v), MTGP_FMAF(h2, kx[i].d, s[i].d)};
+      }
+      rhs(t + h2, tmp, kx);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        acc[i] = {MTGP_FMAF(2.0f, kx[i].v, acc[i].v), MTGP_FMAF(2.0f, kx[i].d, acc[i].d)};
+        tmp[i] = {MTGP_FMAF(h, kx[i].v, s[i].v), MTGP_FMAF(h, kx[i].d, s[i].d)};
+      }
+      rhs(t + h, tmp, kx);
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        acc[i] = {acc[i].v + kx[i].v, acc[i].d + kx[i].d};
+        s[i] = {MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d)};
+      }
+    }
+    if (step % A.m.save_every == 0) save_point(++q_saved, s);
+    const bool ok = !bad(s);
+    if (prev_ok && !ok) done = true;
+    prev_ok = ok;
+  }
+  // the +inf fill after the event (constants): Acrobot masks it (zero additions), the quadratic
+  // costs become non-finite
+  float F, dF;
+  if constexpr (ENV == 0) {
+    if (q_saved + 1 < S && settled) cs = mtgp_dl_add(cs, mtgp_dl(0.0f, 0.0f));
+    if (!settled) {
+      fs = 0;
+      cs = S > 1 ? mtgp_dl_add(c0, mtgp_dl(0.0f, 0.0f)) : c0;
+    }
+    const MtgpDual Fd = mtgp_dl_cadd((float)(fs + (fs == 0) * S), cs);
+    F = Fd.v;
+    dF = Fd.d;
+  } else {
+    F = q_saved + 1 < S ? mtgp_qnan() : cs.v;
+    dF = cs.d;
+  }
+  out[0] = F;
+  out[1] = dF;
+}
+
 }  // namespace
+
+static bool grad_args(GradArgs& A, const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                      const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro, float* scratch,
+                      float* loss_out, float* grad_out) {
+  A.m = *model;
+  A.prog = prog;
+  A.n_prog = n_prog;
+  A.L = L;
+  A.P = P;
+  A.K = K;
+  A.theta = theta;
+  A.nparam = nparam;
+  A.ro = *ro;
+  A.part = scratch;
+  A.loss = loss_out;
+  A.grad = grad_out;
+  return true;
+}
+
+extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                             const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
+                             float* scratch, float* loss_out, float* grad_out, void* stream) {
+  if (!model || !prog || !ro || !nparam || !scratch || !loss_out || !grad_out || P < 0 || K < 1 || L <= 0 ||
+      n_prog <= 0 || !theta)
+    return MTGP_ERR_ARG;
+  const bool dyn = model->model == MTGP_MODEL_DYNAMIC;
+  if (!dyn && model->model != MTGP_MODEL_STATIC) return MTGP_ERR_ARG;
+  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER) return MTGP_ERR_ARG;
+  const int nv = model->env == MTGP_ENV_ACROBOT ? 4 : (model->env == MTGP_ENV_HARMONIC_OSCILLATOR ? 2 : 3);
+  if (model->env < 0 || model->env > 2 || model->n_var != nv || model->n_obs < 1 || model->n_obs > nv ||
+      model->n_control != 1 || model->n_targets < 0 || model->n_targets > 8 || !ro->params || !ro->x0 || !ro->ts ||
+      (model->n_targets > 0 && !ro->targets) || (ro->obs_keys && !ro->obs_w) || ro->R < 1 || ro->R > 64 ||
+      model->save_every < 1 || model->n_save < 2 || model->n_steps < 0 || model->prog_readout < 0 ||
+      model->prog_readout >= n_prog)
+    return MTGP_ERR_ARG;
+  const int na = dyn ? model->state_size : 0;
+  const int D = model->n_obs + (dyn ? na + 1 : 0) + model->n_targets;
+  if (na < 0 || na > 3 || D > kCtlData || D + K > MTGP_MAX_DATA) return MTGP_ERR_ARG;
+  if (dyn && (model->prog_state < 0 || model->prog_state + na > n_prog || model->prog_readout_save < 0 ||
+              model->prog_readout_save >= n_prog))
+    return MTGP_ERR_ARG;
+  if (P == 0) return MTGP_OK;
+  GradArgs A;
+  grad_args(A, model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out);
+  hipStream_t s = (hipStream_t)stream;
+  const long lanes = (long)P * K * ro->R;
+  const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
+#define MTGP_CG(E)                                                                  \
+  switch (na) {                                                                     \
+    case 0: hipLaunchKernelGGL((k_ctl_grad<E, 0>), grid, block, 0, s, A); break;    \
+    case 1: hipLaunchKernelGGL((k_ctl_grad<E, 1>), grid, block, 0, s, A); break;    \
+    case 2: hipLaunchKernelGGL((k_ctl_grad<E, 2>), grid, block, 0, s, A); break;    \
+    default: hipLaunchKernelGGL((k_ctl_grad<E, 3>), grid, block, 0, s, A); break;   \
+  }
+  if (model->env == MTGP_ENV_ACROBOT) { MTGP_CG(0) }
+  else if (model->env == MTGP_ENV_HARMONIC_OSCILLATOR) { MTGP_CG(1) }
+  else { MTGP_CG(2) }
+#undef MTGP_CG
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(((long)P * K + 255) / 256)), dim3(256), 0, s, A);
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  return MTGP_OK;
+}
 
 extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
                             const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,

@@ -267,7 +267,7 @@ class DeviceEngine:
             if t >= T:
                 raise ValueError(f"candidate has {T} trees, the evaluator needs tree {t}")
         n_prog = len(specs)
-        L = (2 * N + 8 + 3) // 4 * 4  # multiple of 4: block-fetch fast path (mtgp.h)
+        L = self.program_stride(N)
         dev = self.device
         # one spare 32-byte block after the last program: a block prefetch never leaves the buffer
         prog_buf = torch.empty((P * n_prog * L * 2 + 8,), dtype=torch.int32, device=dev)
@@ -288,6 +288,12 @@ class DeviceEngine:
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_flatten failed: {rc}")
         return Flattened(prog, plen, nodes, status, L, n_prog, jit_words=jw, jit_cost=jc)
+
+    @staticmethod
+    def program_stride(N: int) -> int:
+        """Program slot L for max_nodes N: 2N + 7 instructions + END, rounded up to a multiple of 4
+        (the evaluators fetch four instructions per scalar load, mtgp.h)."""
+        return (2 * N + 8 + 3) // 4 * 4
 
     def _jit_usable(self) -> bool:
         """The program JIT serves every kernel: data vector in v0-v7 (control models, SR with

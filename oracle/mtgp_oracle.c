@@ -28,6 +28,7 @@
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_dopri5.h"
+#include "mtgp_dual.h"
 
 #define OR_MAX_N 256
 #define OR_MAX_D 64
@@ -846,6 +847,237 @@ int oracle_sr_grad(const OrModel* m, const float* pop, int P, int T, int N, int 
     if (c > m->max_fitness) { c = m->max_fitness; dmean = 0.0f; }
     else if (c == m->max_fitness) dmean = 0.5f * dmean;
     if (kq == 0) loss[p] = c;
+    grad[pk] = row < 0 ? 0.0f : dmean;
+  }
+  return 0;
+}
+
+/* ------------------------------------------------------- coefficient optimisation, control
+ * The same forward-mode derivative for the dynamic (dyn.py:37-118) and static (ff.py:36-110)
+ * evaluators with a fixed-step solve: dual numbers through the row-order interpreter, f_obs
+ * (C@x + noise, the Acrobot angle wrap), the environment drift (include/mtgp_dual.h, the spec of
+ * the tangent rules), RK4 / Euler, the Event, the save-point readout and the fitness function
+ * on the full saved arrays (acrobot.py:77-84 with first_success from the values -- argmax has no
+ * derivative -- harmonic_oscillator.py:71-77, reactor.py:73-78).  theta = the value entry of
+ * one coefficient row (tree pt, row pi), as in oracle_sr_grad. */
+static MtgpDual o2d(ODual a) { return mtgp_dl(a.v, a.d); }
+static ODual d2o(MtgpDual a) { return od(a.v, a.d); }
+
+static void ctl_f_obs_dual(const OrCtx* c, float t, const ODual* x, ODual* y) {
+  const int nv = c->m->n_var, no = c->m->n_obs;
+  float nz[OR_MAX_D];
+  if (c->key) {
+    float n[OR_MAX_D];
+    mtgp_obs_normals(c->key[0], c->key[1], t, no, c->m->prng_impl, n);
+    for (int j = 0; j < no; ++j) {
+      float s = n[0] * c->W[0 * no + j];
+      for (int i = 1; i < no; ++i) s = s + n[i] * c->W[i * no + j];
+      nz[j] = s;
+    }
+  } else {
+    for (int j = 0; j < no; ++j) nz[j] = 0.0f;
+  }
+  for (int i = 0; i < no; ++i) {  /* C@x: the literal index-order sum, in duals */
+    MtgpDual s = mtgp_dl_cmul(i == 0 ? 1.0f : 0.0f, o2d(x[0]));
+    for (int j = 1; j < nv; ++j) s = mtgp_dl_add(s, mtgp_dl_cmul(i == j ? 1.0f : 0.0f, o2d(x[j])));
+    y[i] = d2o(mtgp_dl_addc(s, nz[i]));
+  }
+  if (c->m->env == ENV_ACROBOT) {
+    y[0] = d2o(mtgp_dl_wrap_angle(o2d(y[0])));
+    if (no > 1) y[1] = d2o(mtgp_dl_wrap_angle(o2d(y[1])));
+  }
+}
+
+static void env_drift_dual(const OrCtx* c, const ODual* x, ODual u, ODual* dx) {
+  MtgpDual xx[OR_MAX_D], d[OR_MAX_D];
+  const int nv = c->m->n_var;
+  for (int i = 0; i < nv; ++i) xx[i] = o2d(x[i]);
+  if (c->m->env == ENV_HARMONIC) mtgp_dl_ho_drift(c->prm, xx, o2d(u), d);
+  else if (c->m->env == ENV_REACTOR) mtgp_dl_reactor_drift(c->prm, xx, o2d(u), d);
+  else mtgp_dl_acro_drift(c->prm, xx, o2d(u), d);
+  for (int i = 0; i < nv; ++i) dx[i] = d2o(d[i]);
+}
+
+/* the readout / policy tree j on a dual data vector */
+static ODual ctl_tree_dual(const OrCtx* c, int t, const ODual* data, int n_data, int pt, int pi) {
+  return tree_eval_dual(c->cand + (size_t)t * c->N * 4, c->N, &c->lib, data, n_data, t == pt ? pi : -1);
+}
+
+/* dyn.py:107-118 / ff.py:104-110 in duals */
+static void ctl_rhs_dual(const OrCtx* c, float t, const ODual* s, ODual* ds, int pt, int pi) {
+  const OrModel* m = c->m;
+  const int no = m->n_obs, nt = m->n_targets, nv = m->n_var;
+  ODual y[OR_MAX_D], data[OR_MAX_D];
+  ctl_f_obs_dual(c, t, s, y);
+  if (m->model == 1) {
+    const int na = m->state_size, nu = m->n_control, D = no + na + nu + nt;
+    for (int i = 0; i < D; ++i) data[i] = od(0.0f, 0.0f);
+    for (int i = 0; i < na; ++i) data[no + i] = s[nv + i];
+    for (int i = 0; i < nt; ++i) data[no + na + nu + i] = od(c->target[i], 0.0f);
+    ODual u[8];
+    for (int j = 0; j < nu; ++j) u[j] = ctl_tree_dual(c, na + j, data, D, pt, pi);  /* [0, a, 0, tg] */
+    env_drift_dual(c, s, u[0], ds);
+    for (int i = 0; i < no; ++i) data[i] = y[i];
+    for (int j = 0; j < nu; ++j) data[no + na + j] = u[j];
+    for (int i = 0; i < na; ++i) ds[nv + i] = ctl_tree_dual(c, i, data, D, pt, pi);  /* [y, a, u, tg] */
+  } else {
+    for (int i = 0; i < no; ++i) data[i] = y[i];
+    for (int i = 0; i < nt; ++i) data[no + i] = od(c->target[i], 0.0f);
+    const ODual u = ctl_tree_dual(c, 0, data, no + nt, pt, pi);
+    env_drift_dual(c, s, u, ds);
+  }
+}
+
+/* one rollout: F and dF / d theta (the evaluator's rollout fitness, before NaN/inf replacement) */
+static ODual ctl_rollout_dual(const OrCtx* c, const OrRollouts* ro, int r, int pt, int pi) {
+  const OrModel* m = c->m;
+  const int n = state_dim(m), nv = m->n_var, S = m->n_save;
+  ODual* saved = (ODual*)malloc(sizeof(ODual) * (size_t)S * n);
+  ODual s[OR_MAX_S], k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
+  for (int i = 0; i < n; ++i) s[i] = od(i < nv ? ro->x0[(size_t)r * nv + i] : 0.0f, 0.0f);
+  for (int i = 0; i < n; ++i) saved[i] = s[i];
+  float sv[OR_MAX_S];
+  for (int i = 0; i < n; ++i) sv[i] = s[i].v;
+  float prev = cond_fn(m, sv);
+  const float h = m->h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ro->ts[0];
+  int k_saved = 0, done = 0;
+  for (int step = 1; step <= m->n_steps && !done; ++step) {
+    const float t = t0 + (float)(step - 1) * h;
+    if (m->solver == 2) {
+      ctl_rhs_dual(c, t, s, k, pt, pi);
+      for (int i = 0; i < n; ++i) s[i] = od(s[i].v + k[i].v * h, s[i].d + k[i].d * h);
+    } else {
+      ctl_rhs_dual(c, t, s, k, pt, pi);
+      for (int i = 0; i < n; ++i) {
+        acc[i] = k[i];
+        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
+      }
+      ctl_rhs_dual(c, t + h2, tmp, k, pt, pi);
+      for (int i = 0; i < n; ++i) {
+        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
+        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
+      }
+      ctl_rhs_dual(c, t + h2, tmp, k, pt, pi);
+      for (int i = 0; i < n; ++i) {
+        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
+        tmp[i] = od(MTGP_FMAF(h, k[i].v, s[i].v), MTGP_FMAF(h, k[i].d, s[i].d));
+      }
+      ctl_rhs_dual(c, t + h, tmp, k, pt, pi);
+      for (int i = 0; i < n; ++i) {
+        acc[i] = od(acc[i].v + k[i].v, acc[i].d + k[i].d);
+        s[i] = od(MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d));
+      }
+    }
+    if (step % m->save_every == 0) {
+      ++k_saved;
+      for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];
+    }
+    for (int i = 0; i < n; ++i) sv[i] = s[i].v;
+    const float cur = cond_fn(m, sv);
+    if (prev > 0.0f && cur < 0.0f) done = 1;
+    prev = cur;
+  }
+  for (int q = k_saved + 1; q < S; ++q)  /* the +inf fill after the event: constants, no tangent */
+    for (int i = 0; i < n; ++i) saved[(size_t)q * n + i] = od(mtgp_u2f(0x7f800000u), 0.0f);
+  /* controls at the save points (dyn.py:99-101 / ff.py:96-97) */
+  ODual* us = (ODual*)malloc(sizeof(ODual) * (size_t)S);
+  const int no = m->n_obs, nt = m->n_targets;
+  for (int q = 0; q < S; ++q) {
+    const ODual* xq = saved + (size_t)q * n;
+    ODual y[OR_MAX_D], data[OR_MAX_D];
+    ctl_f_obs_dual(c, ro->ts[q], xq, y);
+    if (m->model == 1) {
+      const int na = m->state_size, nu = m->n_control, D = no + na + nu + nt;
+      for (int i = 0; i < no; ++i) data[i] = y[i];
+      for (int i = 0; i < na; ++i) data[no + i] = xq[nv + i];
+      for (int i = 0; i < nu; ++i) data[no + na + i] = od(0.0f, 0.0f);
+      for (int i = 0; i < nt; ++i) data[no + na + nu + i] = od(c->target[i], 0.0f);
+      us[q] = ctl_tree_dual(c, na, data, D, pt, pi);
+    } else {
+      for (int i = 0; i < no; ++i) data[i] = y[i];
+      for (int i = 0; i < nt; ++i) data[no + i] = od(c->target[i], 0.0f);
+      us[q] = ctl_tree_dual(c, 0, data, no + nt, pt, pi);
+    }
+  }
+  MtgpDual F = mtgp_dl(0.0f, 0.0f);
+  if (m->env == ENV_HARMONIC || m->env == ENV_REACTOR) {
+    const float tg = c->target[0];
+    for (int q = 0; q < S; ++q) {
+      const ODual* xq = saved + (size_t)q * n;
+      MtgpDual cost;
+      if (m->env == ENV_HARMONIC) {
+        const float Q[4] = {0.5f, 0.0f, 0.0f, 0.0f}, rr = 0.5f;
+        const MtgpDual e[2] = {mtgp_dl_subc(o2d(xq[0]), tg), mtgp_dl_subc(o2d(xq[1]), 0.0f)};
+        const MtgpDual du = mtgp_dl_subc(o2d(us[q]), ho_u_target(c->prm, tg));
+        cost = mtgp_dl_add(mtgp_dl_quad_form(e, Q, 2), mtgp_dl_mul(mtgp_dl_mulc(du, rr), du));
+      } else {
+        const float Q[9] = {0.0f, 0.0f, 0.0f, 0.0f, 0.01f, 0.0f, 0.0f, 0.0f, 0.0f}, rr = 0.0001f;
+        const MtgpDual e[3] = {mtgp_dl_subc(o2d(xq[0]), 0.0f), mtgp_dl_subc(o2d(xq[1]), tg),
+                               mtgp_dl_subc(o2d(xq[2]), 0.0f)};
+        cost = mtgp_dl_add(mtgp_dl_quad_form(e, Q, 3), mtgp_dl_mul(mtgp_dl_mulc(o2d(us[q]), rr), o2d(us[q])));
+      }
+      F = mtgp_dl_add(F, cost);
+    }
+  } else {  /* acrobot.py:77-84: first_success from the values, masked control costs in duals */
+    int fs = 0;
+    for (int q = 0; q < S; ++q) {
+      const float a1 = saved[(size_t)q * n + 0].v, a2 = saved[(size_t)q * n + 1].v;
+      if (((-mtgp_cosf(a1)) - mtgp_cosf(a1 + a2)) > 1.5f) { fs = q; break; }
+    }
+    const float dts = ro->ts[1] - ro->ts[0];
+    MtgpDual cs = mtgp_dl(0.0f, 0.0f);
+    for (int q = 0; q < S; ++q) {
+      const MtgpDual u = o2d(us[q]);
+      const MtgpDual cost = mtgp_dl_mul(mtgp_dl_mulc(u, 0.01f), u);
+      const MtgpDual masked = ((ro->ts[q] / dts) > (float)fs) ? mtgp_dl(0.0f, 0.0f) : cost;
+      cs = mtgp_dl_add(cs, masked);
+    }
+    F = mtgp_dl_cadd((float)(fs + (fs == 0) * S), cs);
+  }
+  free(saved);
+  free(us);
+  return d2o(F);
+}
+
+int oracle_ctl_grad(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
+                    const int8_t* fn, const OrRollouts* ro, const int32_t* prow, int K, float* loss, float* grad) {
+  if ((m->model != 1 && m->model != 2) || m->solver == 1 || N > OR_MAX_N || state_dim(m) > OR_MAX_S ||
+      ro->R > 64 || K < 1)
+    return -1;
+  const int R = ro->R;
+#pragma omp parallel for schedule(dynamic, 1)
+  for (long pk = 0; pk < (long)P * K; ++pk) {
+    const int p = (int)(pk / K), kq = (int)(pk % K);
+    const int row = prow[(size_t)p * K + kq];
+    if (row < 0 && kq > 0) { grad[pk] = 0.0f; continue; }
+    OrCtx c;
+    c.m = m;
+    c.cand = pop + (size_t)p * T * N * 4;
+    c.N = N;
+    c.lib.n_funcs = n_funcs;
+    c.lib.var_start = var_start;
+    c.lib.fn = fn;
+    c.W = ro->obs_w;
+    float v[64], dv[64];
+    for (int r = 0; r < R; ++r) {
+      c.target = ro->targets ? ro->targets + (size_t)r * m->n_targets : NULL;
+      static const float ones[8] = {1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f, 1.0f};
+      const int npar = m->env == ENV_HARMONIC ? 2 : (m->env == ENV_REACTOR ? 8 : 4);
+      c.prm = ro->params ? ro->params + (size_t)r * npar : ones;
+      c.key = ro->obs_keys ? ro->obs_keys + 2 * (size_t)r : NULL;
+      ODual F = ctl_rollout_dual(&c, ro, r, row < 0 ? -1 : row / N, row < 0 ? -1 : row % N);
+      if (!mtgp_isfinite(F.v)) F = od(m->max_fitness, 0.0f); /* dyn.py:49-50, derivative of where */
+      v[r] = F.v;
+      dv[r] = F.d;
+    }
+    const float mean = pairwise_sum(v, R) / (float)R;
+    float dmean = pairwise_sum(dv, R) / (float)R;
+    float cl = mean;
+    if (mean < 0.0f) { cl = 0.0f; dmean = 0.0f; }
+    else if (mean == 0.0f) dmean = 0.5f * dmean;
+    if (cl > m->max_fitness) { cl = m->max_fitness; dmean = 0.0f; }
+    else if (cl == m->max_fitness) dmean = 0.5f * dmean;
+    if (kq == 0) loss[p] = cl;
     grad[pk] = row < 0 ? 0.0f : dmean;
   }
   return 0;

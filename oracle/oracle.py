@@ -18,7 +18,7 @@ LIB = os.path.join(HERE, "build", "libmtgp_oracle.so")
 def build(force: bool = False) -> str:
     src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h"),
            os.path.join(HERE, "..", "include", "mtgp_prng.h"),
-           os.path.join(HERE, "..", "include", "mtgp_dopri5.h")]
+           os.path.join(HERE, "..", "include", "mtgp_dopri5.h"), os.path.join(HERE, "..", "include", "mtgp_dual.h")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
         subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
                        stdout=subprocess.DEVNULL)
@@ -84,6 +84,8 @@ def lib():
                                      ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(OrRollouts), vp, ctypes.c_int,
                                      vp, vp]
         L.oracle_sr_grad.restype = ctypes.c_int
+        L.oracle_ctl_grad.argtypes = L.oracle_sr_grad.argtypes
+        L.oracle_ctl_grad.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -262,6 +264,16 @@ def sr_grad(model: dict, pop: np.ndarray, library, rollouts: dict):
     """Loss [P] and d loss / d coefficient [P, K] of the SR evaluator (forward mode), one entry per
     coefficient row (f == 1) of each candidate in row-major (tree, row) order; K = the largest
     count (unused entries 0).  -> (loss, grad, rows: list of [(t, i)] per candidate)."""
+    return _grad("oracle_sr_grad", model, pop, library, rollouts)
+
+
+def ctl_grad(model: dict, pop: np.ndarray, library, rollouts: dict):
+    """sr_grad for the dynamic / static control evaluators (fixed-step RK4 / Euler, every
+    environment, observation noise included): loss = the evaluator's fitness without parsimony."""
+    return _grad("oracle_ctl_grad", model, pop, library, rollouts)
+
+
+def _grad(fname, model, pop, library, rollouts):
     pop = np.ascontiguousarray(pop, np.float32)
     P, T, N, _ = pop.shape
     rows = [np.argwhere(c[..., 0] == np.float32(1.0)) for c in pop]
@@ -273,13 +285,22 @@ def sr_grad(model: dict, pop: np.ndarray, library, rollouts: dict):
                    for k, _ in OrModel._fields_})
     x0 = np.ascontiguousarray(rollouts["x0"], np.float32)
     ts = np.ascontiguousarray(rollouts["ts"], np.float32)
-    yt = np.ascontiguousarray(rollouts["ys_true"], np.float32)
-    ro = OrRollouts(_p(x0).value, None, None, _p(ts).value, _p(yt).value, x0.shape[0], None, None)
+    yt = rollouts.get("ys_true")
+    yt = None if yt is None else np.ascontiguousarray(yt, np.float32)
+    prm = None if rollouts.get("params") is None else np.ascontiguousarray(rollouts["params"], np.float32)
+    tg = rollouts.get("targets")
+    tg = None if tg is None or np.asarray(tg).size == 0 else np.ascontiguousarray(tg, np.float32)
+    keys = rollouts.get("obs_keys")
+    keys = None if keys is None else np.ascontiguousarray(keys, np.uint32)
+    W = None if keys is None else np.ascontiguousarray(rollouts["obs_w"], np.float32)
+    ro = OrRollouts(_p(x0).value, None if prm is None else _p(prm).value, None if tg is None else _p(tg).value,
+                    _p(ts).value, None if yt is None else _p(yt).value, x0.shape[0],
+                    None if keys is None else _p(keys).value, None if W is None else _p(W).value)
     loss = np.empty(P, np.float32)
     grad = np.empty((P, K), np.float32)
     fn = np.ascontiguousarray(library.fn_codes, np.int8)
-    rc = lib().oracle_sr_grad(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
-                              ctypes.byref(ro), _p(prow), K, _p(loss), _p(grad))
+    rc = getattr(lib(), fname)(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
+                               ctypes.byref(ro), _p(prow), K, _p(loss), _p(grad))
     if rc != 0:
-        raise RuntimeError(f"oracle_sr_grad failed {rc}")
+        raise RuntimeError(f"{fname} failed {rc}")
     return loss, grad, rows
