@@ -64,3 +64,35 @@ def sharded_fitness(evaluate_shard: Callable[[int, int], torch.Tensor], P: int, 
     lo, hi, per = shard_bounds(P, ws, rank)
     local = evaluate_shard(lo, hi)
     return gather_fitness(local, P, per, group)
+
+
+def sharded_rows(compute: Callable[[int, int], Tuple["np.ndarray", "np.ndarray"]], n: int, row_shape: tuple,
+                 group=None):
+    """compute(lo, hi) -> (values [hi-lo] f32, rows [hi-lo, *row_shape] f32) of items [lo, hi)
+    on this rank; returns the full (values [n], rows [n, ...]) on every rank.  Items are split
+    into contiguous blocks like the population (shard_map's P('i'), gp.py:264-267 shard_optimise);
+    one all-gather of the padded blocks (values and rows packed together)."""
+    import numpy as np
+    rank, ws = world()
+    if ws == 1:
+        return compute(0, n)
+    lo, hi, per = shard_bounds(n, ws, rank)
+    vals, rows = compute(lo, hi)
+    width = 1 + int(np.prod(row_shape))
+    buf = np.zeros((per, width), np.float32)
+    m = hi - lo
+    if m > 0:
+        buf[:m, 0] = np.asarray(vals, np.float32)
+        buf[:m, 1:] = np.asarray(rows, np.float32).reshape(m, -1)
+    t = torch.from_numpy(buf)
+    if dist.get_backend(group) == "gloo":
+        parts = [torch.empty_like(t) for _ in range(ws)]
+        dist.all_gather(parts, t, group=group)
+        full = torch.cat(parts)
+    else:  # RCCL: device buffers
+        dev = local_device()
+        full = torch.empty((per * ws, width), dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(full, t.to(dev), group=group)
+        full = full.cpu()
+    full = full.numpy()[:n]
+    return full[:, 0].copy(), full[:, 1:].reshape(n, *row_shape).copy()

@@ -140,7 +140,8 @@ class GeneticProgramming:
         launch per rank, parsimony in-kernel, all-gather of fitness, best-so-far bookkeeping.
         With coefficient_optimisation, every 5th generation after generation 10 the 50 best
         candidates (by fitness before parsimony) get `gradient_steps` optimiser steps on their
-        coefficients (gp.py:418-422; multitreegp_amd.coefficients), replicated on every rank."""
+        coefficients (gp.py:418-422; multitreegp_amd.coefficients), split over the ranks like
+        shard_optimise (gp.py:264-267) and all-gathered."""
         pops = np.asarray(populations, dtype=np.float32)
         P = self.num_populations * self.population_size
         flat = pops.reshape(P, *pops.shape[2:])
@@ -149,8 +150,9 @@ class GeneticProgramming:
             raw = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data, 0.0), P)
             raw = raw.cpu().numpy()
             best_idx = np.argsort(raw, kind="stable")[:50]
-            opt = CoefficientOptimiser(self.vmap_foriloop.engine(self.fitness_function, 0.0))
-            opt_fit, opt_pop = opt.optimise(flat[best_idx], data, self.gradient_steps, self.optimiser)
+            # shard_optimise (gp.py:264-267): the candidates split over the ranks, one all-gather
+            opt_fit, opt_pop = mdist.sharded_rows(
+                lambda lo, hi: self._optimise_shard(flat[best_idx[lo:hi]], data), len(best_idx), flat.shape[1:])
             flat = flat.copy()
             flat[best_idx] = opt_pop
             raw[best_idx] = opt_fit
@@ -165,6 +167,13 @@ class GeneticProgramming:
             self.best_fitnesses[g] = fitness[best]
         return fitness.reshape(self.num_populations, self.population_size), \
             flat.reshape(self.num_populations, self.population_size, *flat.shape[1:])
+
+    def _optimise_shard(self, cands: np.ndarray, data):
+        """GeneticProgramming.optimise (gp.py:454-473) of this rank's candidates on its GPU."""
+        if len(cands) == 0:
+            return np.zeros(0, np.float32), cands
+        opt = CoefficientOptimiser(self.vmap_foriloop.engine(self.fitness_function, 0.0))
+        return opt.optimise(cands, data, self.gradient_steps, self.optimiser)
 
     def _evaluate_shard(self, flat: np.ndarray, lo: int, hi: int, data, parsimony=None) -> torch.Tensor:
         """Fitness of individuals [lo, hi) of the flattened population on this rank's GPU (one

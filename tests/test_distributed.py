@@ -145,3 +145,78 @@ def test_genetic_programming_evaluate_population_sharded(ws):
         fits, bf, bs, rcalls = res[r]
         assert fits == want_fit and bf == want_bf and bs == want_bs
         assert rcalls == [(9 * r, 9 * r + 9)] * 2  # contiguous block per rank, gp.py:259 P('i')
+
+
+def _opt_worker(rank, ws, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        import sys
+        sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+        q.put((rank, _opt_run()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _opt_run():
+    """Generation 14 of a coefficient-optimising run (gp.py:418-422) with the shard evaluator and
+    the shard optimiser injected (the CPU oracle's loss and gradients): the 50 best candidates
+    are split over the ranks (shard_optimise, gp.py:264-267) and all-gathered."""
+    from helpers import SR_OPS, oracle_model, oracle_rollouts, sr_setup
+    from multitreegp_amd import coefficients as co
+    from oracle import oracle as orc
+    import multitreegp_amd as mt
+    env, lib, ff, data, pop = sr_setup(P=60, R=4, n_save=9, save_every=2, h=0.05, depth=4, N=20, seed=9)
+    gp = mt.GeneticProgramming(20, 60, ff, SR_OPS, [["x0", "x1"]], [2], max_nodes=20, size_parsinomy=0.01,
+                               coefficient_optimisation=True, gradient_steps=3, verbose=False)
+    gp.current_generation = 14
+    d = ff.prepare(data)
+    d["h"] = ff.dt0
+    model, ro = oracle_model(ff, d), oracle_rollouts(d)
+
+    class OracleOpt(co.CoefficientOptimiser):
+        def __init__(self):
+            pass
+
+        def loss_and_grad(self, cands, data_, rows=None):
+            loss, grad, rws = orc.sr_grad(model, cands, lib, ro)
+            return loss, [grad[b, : len(r)].copy() for b, r in enumerate(rws)]
+
+    sizes = []
+
+    def opt_shard(cands, data_):
+        sizes.append(len(cands))
+        if len(cands) == 0:
+            return np.zeros(0, np.float32), cands
+        return OracleOpt().optimise(cands, data_, gp.gradient_steps, gp.optimiser)
+
+    gp._evaluate_shard = lambda flat, lo, hi, data_, parsimony=None: (
+        torch.empty(0) if hi <= lo else torch.from_numpy(
+            orc.evaluate(dict(model, parsimony=gp.size_parsinomy if parsimony is None else parsimony),
+                         flat[lo:hi], lib, ro)["fitness"]))
+    gp._optimise_shard = opt_shard
+    fit, back = gp.evaluate_population(pop[None], data)
+    return fit.tobytes(), back.tobytes(), gp.best_fitnesses.tobytes(), sizes
+
+
+def test_coefficient_optimisation_sharded():
+    """the optimisation of the 50 best candidates is split over the ranks and
+    all-gathered; fitness and population equal the single-process run bit for bit."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_opt_worker, args=(r, ws, port, q)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=300) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    want_fit, want_pop, want_bf, sizes = _opt_run()
+    assert sizes == [50]
+    for r in range(ws):
+        fit, back, bf, rsizes = res[r]
+        assert fit == want_fit and back == want_pop and bf == want_bf
+        assert rsizes == [25]

@@ -430,5 +430,5 @@ def test_gpu_dopri5_two_launches_bitexact(kind, budget, jit):
             assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
     one, _ = _gpu_run(ff, lib, data, pop, jit, dp_budget=0, steps=True)
     assert np.array_equal(res["steps"], one["steps"])
-    if budget:  # the budget split the solves: some waves were parked
+    if budget in (1, 7):  # these budgets split the solves (some waves were parked)
         assert (one["steps"] > budget).any()
