@@ -22,10 +22,19 @@ ap.add_argument("--budgets", default="0,64,128,256,512")
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--obs-noise", type=float, default=0.0)
 ap.add_argument("--config", default="c3", choices=["c2", "c3"])
+ap.add_argument("--legacy-pop", action="store_true",
+                help="the round-2 population: per-tree sampler (sampling.sample_tree), same seed -- A/B against "
+                     "round-2 measurements")
 a = ap.parse_args()
 args = bench.apply_config_defaults(argparse.Namespace(config=a.config, pop=None, rollouts=None, ode_steps=200,
                                                       solver="dopri5", obs_noise=a.obs_noise))
 env, lib, ff, data, pop = bench.setup_workload(args, 0)
+if a.legacy_pop:
+    from multitreegp_amd.sampling import create_map_b_to_d, sample_tree
+    rng = np.random.default_rng(1000)
+    m = create_map_b_to_d(10)
+    pop = np.stack([np.stack([sample_tree(rng, lib, lib.variable_array[t], 10, 64, 1.0, m) for t in range(3)])
+                    for _ in range(pop.shape[0])]).astype(np.float32)
 budgets = [int(b) for b in a.budgets.split(",")]
 engs = {b: DeviceEngine(ff, lib, 0.0, "cuda:0", dp_budget=b) for b in budgets}
 pd = torch.from_numpy(pop).cuda()

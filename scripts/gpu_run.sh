@@ -41,6 +41,8 @@ for step in "$@"; do
     prof_dp) prof prof_dp c3 --solver dopri5 || exit 1 ;;
     prof_dpn) prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
     dpab) run dpab 600 python scripts/dp_budget_ab.py || exit 1 ;;
+    dpab_legacy) run dpab_legacy 900 python scripts/dp_budget_ab.py --legacy-pop --budgets 0,500 --rounds 3 || exit 1 ;;
+    dpab_noise2) run dpab_noise2 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,384,512,640,768 --rounds 3 || exit 1 ;;
     dpab_noise) run dpab_noise 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,128,256,512 --rounds 3 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
