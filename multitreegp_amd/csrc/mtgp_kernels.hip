@@ -516,16 +516,22 @@ struct EnvReactor {
 // the streaming output (C3: 2.3 GB, C5: 1.7 GB per launch) does not evict the JIT code and the
 // rollout data from L2 -- C5's per-stage code footprint (~2 MB per XCD) is refetched every stage
 // when it does (PMC: FETCH_SIZE 20 GB per launch with plain stores).
+// The adaptive kernels' save points are divergent (each round writes one dword per lane into
+// different rows), so their partial lines are left to L2 to merge: plain stores there
+// (DP = true; non-temporal partial writes made the C3 Dopri5 kernel 44 % slower).
 #ifndef MTGP_V_NTSTORE
 #define MTGP_V_NTSTORE 1
 #endif
+template <bool DP = false>
 __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
   float* p = arr + row;
 #if MTGP_V_NTSTORE
-  __builtin_nontemporal_store(v, p + off);
-#else
-  p[off] = v;
+  if (!DP) {
+    __builtin_nontemporal_store(v, p + off);
+    return;
+  }
 #endif
+  p[off] = v;
 }
 
 // --------------------------------------------------------------------------------------
@@ -1395,17 +1401,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     if (TRAJ && active) {
       if (A.out.xs) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, sk[i]);
+        for (int i = 0; i < NV; ++i) store_row<true>(A.out.xs, ((size_t)k * NV + i) * PR, loff, sk[i]);
       }
       if (A.out.ys) {
 #pragma unroll
         for (int i = 0; i < NV; ++i)
-          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
+          if (i < A.m.n_obs) store_row<true>(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
       }
-      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, ur[0]);
+      if (A.out.us) store_row<true>(A.out.us, (size_t)k * PR, loff, ur[0]);
       if (DYN && A.out.acts) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NAX + j) * PR, loff, sk[NV + j]);
+        for (int j = 0; j < NA; ++j) store_row<true>(A.out.acts, ((size_t)k * NAX + j) * PR, loff, sk[NV + j]);
       }
     }
   };
@@ -1647,7 +1653,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
     tot = tot + sq;
     if (TRAJ && active && A.out.xs) {
 #pragma unroll
-      for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d]);
+      for (int d = 0; d < NV; ++d) store_row<true>(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d]);
     }
   };
   auto bad = [&](const float* v) __attribute__((always_inline)) {
@@ -2084,7 +2090,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
       if (c < NV) {
         const float e = v[t] - A.ro.ys_true[((size_t)kk * NV + c) * R + rr];
         red[c * kWave] = e * e;
-        if (TRAJ && pend && active && A.out.xs) store_row(A.out.xs, ((size_t)kk * NV + c) * PR, loff, v[t]);
+        if (TRAJ && pend && active && A.out.xs) store_row<true>(A.out.xs, ((size_t)kk * NV + c) * PR, loff, v[t]);
       }
     }
     const float sq = reduce();

@@ -26,6 +26,13 @@ prof() {  # name config args...
     cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats.csv
   head -6 $O/${n}_kernel_stats.csv
 }
+pmcsq() {  # name config: one pass of SQ stall / instruction counters over kprof (2 evaluations)
+  local n=$1 c=$2; shift 2
+  run $n 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+      SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_SALU -d $O/$n -o $n --output-format csv -- python3 scripts/kprof.py --iters 2 \
+      --config $c "$@" || return 1
+  python3 scripts/pmc_summary.py $O/$n ${KSUB:-k_} > $O/${n}.json; cat $O/${n}.json
+}
 for step in "$@"; do
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
@@ -42,8 +49,13 @@ for step in "$@"; do
     prof_dpn) prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
     dpab) run dpab 600 python scripts/dp_budget_ab.py || exit 1 ;;
     dpab_legacy) run dpab_legacy 900 python scripts/dp_budget_ab.py --legacy-pop --budgets 0,500 --rounds 3 || exit 1 ;;
+    dpab2) run dpab2 900 python scripts/dp_budget_ab.py --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab_noise2) run dpab_noise2 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,384,512,640,768 --rounds 3 || exit 1 ;;
     dpab_noise) run dpab_noise 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,128,256,512 --rounds 3 || exit 1 ;;
+    listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
+    pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
+    pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
+    pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
