@@ -59,6 +59,8 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kDMax = 8;  // data slots held in LDS by the small-state kernels
+constexpr int kDWide = 16;     // data slots of the runtime-state-size dynamic kernel (interpreter only)
+constexpr int kNaRuntime = 8;  // k_ctl_dynamic<Env, kNaRuntime, ...>: state_size 4 .. 8 at run time
 constexpr int kSMax = MTGP_STACK_MAX;
 constexpr int kLdsWaveWords = (kDMax + kSMax) * kWave;  // per wave: data columns | stack columns
 constexpr float kInf = __builtin_huge_valf();
@@ -694,7 +696,7 @@ struct DataVec {
     for (int k = 0; k < kDMax; ++k) v[k] = 0.0f;
   }
   __device__ __forceinline__ void put(int slot, float x) {
-    v[slot] = x;
+    if (JIT) v[slot] = x;  // (the register copy only feeds JIT calls: no dynamic index otherwise)
     if (!JIT) dcol[slot * kWave] = x;
   }
   __device__ __forceinline__ void spill() {
@@ -802,7 +804,7 @@ __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L
 template <bool JIT, int M>
 __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, int role, int first, DataVec<JIT>& D,
                                          float (&out)[M], bool chained = false, int save_prog = -1,
-                                         float* save_v = nullptr) {
+                                         float* save_v = nullptr, int mr = M) {
   (void)role;
   bool interp = !JIT;
   if (JIT && M <= mtgp::kJitChainMax && chained) {
@@ -875,7 +877,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
   }
   if (interp) {
 #pragma unroll 1
-    for (int q = 0; q < M; ++q) {
+    for (int q = 0; q < mr; ++q) {  // mr <= M: a runtime role size (state_size > 3, interpreter only)
       const float v = run_groups_interp(A, L, ng, first + q, D.dcol, D.st, 0.0f);
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
@@ -950,7 +952,11 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dynamic(KArgs A) {
   constexpr int NV = Env::NV;
-  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
+  // NA <= 3: the state size; NA = kNaRuntime: state_size 4 .. kNaRuntime at run time (interpreter
+  // only: the data vector has up to kDWide slots, beyond the JIT's register-data ABI)
+  constexpr int DM = NA > 3 ? kDWide : kDMax;
+  __shared__ float lds[kWavesPerBlock][(DM + kSMax) * kWave];
+  const int na = NA <= 3 ? NA : uni(A.m.state_size);
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
   MTGP_PROBE(Ln, 0);
@@ -958,7 +964,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const bool active = Ln.active;
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
-  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  float* st = &lds[Ln.wave][DM * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
   if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
 
@@ -970,14 +976,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
   for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
   if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
-  constexpr int uslot = NV + NA;
+  const int uslot = NV + na;
   Env env;
   env.load(A.ro, rr, A.m.n_targets);
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;  // element offset of this (individual, rollout) in a save row
 #pragma unroll
-  for (int t = 0; t < kDMax - uslot - 1; ++t)
-    if (t < A.m.n_targets) D.put(uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
+  for (int t = 0; t < DM - NV - 2; ++t)
+    if (t < A.m.n_targets && uslot + 1 + t < DM) D.put(uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
   // groups whose save-time readout differs from the drift readout (it reads y): bit per group
   uint64_t diff_mask = 0;
@@ -1000,7 +1006,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) a[j] = 0.0f;
+  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = 0.0f;
 
   typename Env::Fit fit = Env::fit_init(active);
   bool dead = !active;  // state frozen at +inf once the event state has been saved
@@ -1037,7 +1043,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       stage_in_n<NV>(stage, x, kx, h, h2, xt);
       stage_in_n<NA>(stage, a, ka, h, h2, at);
 #pragma unroll
-      for (int j = 0; j < NA; ++j) D.put(NV + j, at[j]);
+      for (int j = 0; j < NA; ++j)
+        if (j < na) D.put(NV + j, at[j]);
       float ur[1];
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       const float u = ur[0];
@@ -1058,7 +1065,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       const bool save_chain = JIT && A.chain_save && stage == 0 && is_save && diff_mask != 0 && !redraw;
       float us_chain = u;
       run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0,
-                        save_chain ? A.m.prog_readout_save : -1, &us_chain);
+                        save_chain ? A.m.prog_readout_save : -1, &us_chain, na);
       if (stage == 0) {
         if (is_save) {
           const int k = ksave;
@@ -1095,7 +1102,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
             if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us);
             if (A.out.acts) {
 #pragma unroll
-              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR, loff, a[j]);
+              for (int j = 0; j < NA; ++j)
+                if (j < na) store_row(A.out.acts, ((size_t)k * na + j) * PR, loff, a[j]);
             }
           }
         }
@@ -1121,7 +1129,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       for (int i = 0; i < NV; ++i) { x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
 #pragma unroll
       for (int j = 0; j < NA; ++j) { a[j] = euler ? a[j] + aa[j] * h : MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
-      const bool ok = !Env::bad(sn, NV + NA);
+      const bool ok = !Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
       if (prev_ok && !ok) pending = true;
       prev_ok = ok;
     }
@@ -3512,7 +3520,18 @@ int launch_timed(F&& launch, hipStream_t s) {
 
 template <class Env, int NA>
 int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
-  return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
+  if constexpr (NA > 3) {  // state_size 4 .. kNaRuntime: the interpreter (data vector beyond the JIT's 8 registers)
+    if (jit) return MTGP_ERR_ARG;
+    return launch_timed([&] {
+      if (noise) {
+        if (traj) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, true, false>), grid, block, 0, s, A);
+        else hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, true, false>), grid, block, 0, s, A);
+      } else if (traj) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, false, false>), grid, block, 0, s, A);
+      else hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, false, false>), grid, block, 0, s, A);
+    }, s);
+  } else {
+    return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
+  }
 }
 
 // adaptive Dopri5 variants (k_ctl_dopri5): static = NA 0
@@ -3551,6 +3570,10 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
   if (model->env != MTGP_ENV_ACROBOT && model->n_targets < 1) return MTGP_ERR_ARG;  // x_d needs the target
   if (model->model == MTGP_MODEL_STATIC) {
     if (NV + model->n_targets > kDMax) return MTGP_ERR_ARG;
+  } else if (model->state_size > 3) {  // runtime state size: the wide interpreter kernel, fixed-step solvers
+    if (model->state_size > kNaRuntime || NV + model->state_size + 1 + model->n_targets > kDWide || jit ||
+        model->solver == MTGP_SOLVER_DOPRI5)
+      return MTGP_ERR_ARG;
   } else if (NV + model->state_size + 1 + model->n_targets > kDMax) {
     return MTGP_ERR_ARG;
   }
@@ -3578,7 +3601,8 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
     case 1: return launch_dyn<Env, 1>(A, jit, noise, traj, grid, block, s);
     case 2: return launch_dyn<Env, 2>(A, jit, noise, traj, grid, block, s);
     case 3: return launch_dyn<Env, 3>(A, jit, noise, traj, grid, block, s);
-    default: return MTGP_ERR_ARG;
+    default: return model->state_size > 3 ? launch_dyn<Env, kNaRuntime>(A, jit, noise, traj, grid, block, s)
+                                          : MTGP_ERR_ARG;
   }
 }
 

@@ -314,6 +314,12 @@ class DynamicEvaluator(_ControlEvaluator):
                  stepsize_controller=None):
         super().__init__(env, dt0, solver, max_steps, stepsize_controller)
         self.state_size = int(state_size)
+        if self.state_size < 1:
+            raise ValueError("state_size must be >= 1")
+        if self.state_size > 3:  # the runtime-state-size interpreter kernel (mtgp_kernels.hip kNaRuntime)
+            if self.state_size > 8 or self.solver_kind == "dopri5":
+                raise NotImplementedError("state_size 4 .. 8 runs with the fixed-step solvers (RK4 / Euler); "
+                                          "state_size <= 3 with every solver")
 
     def n_trees(self) -> int:
         return self.state_size + self.control_size

@@ -415,3 +415,21 @@ def test_fewer_observations_than_states(case):
     res, ref, d = _run(ff, lib, data, pop)
     assert res["ys"].shape[1] == env.n_obs
     _check(res, ref, pop.shape[0], 8, names)
+
+
+@pytest.mark.parametrize("case", [("acrobot", 4, None, 0.0), ("acrobot", 6, "euler", 0.1), ("harmonic", 5, None, 0.0),
+                                  ("reactor", 8, None, 0.1)])
+def test_state_size_above_three(case):
+    """state_size 4 .. 8 (dyn.py:83 takes any): the data vector [y, a, u, tg] no longer fits the
+    JIT's eight data registers, so the wide interpreter kernel (k_ctl_dynamic<Env, kNaRuntime>,
+    runtime state size, 16 LDS data columns) runs it -- bit-exact vs the oracle."""
+    env_name, ss, solver, noise = case
+    from helpers import dynamic_setup
+    env, lib, ff, data, pop = dynamic_setup(P=21, R=8, n_steps=30, depth=5, N=30, seed=11, state_size=ss,
+                                            obs_noise=noise, env=env_name)
+    if solver == "euler":
+        ff = mt.DynamicEvaluator(env, ss, ff.dt0, solver=mt.Euler())
+    res, ref, d = _run(ff, lib, data, pop, parsimony=0.25)
+    assert not DeviceEngine.jit_ok(res["_flat"])  # (n_data > 8: interpreter)
+    _check(res, ref, pop.shape[0], 8, ["xs", "ys", "us", "acts"])
+    assert res["acts"].shape[1] == ss
