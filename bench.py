@@ -238,7 +238,14 @@ def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-    return el * 1e3 / args.e2e_steps, fit
+    # the host half of a generation: GeneticProgramming.evolve (gp.py:475-497) on the same
+    # population (native host library, include/mtgp_host.h)
+    ev = []
+    for i in range(4):
+        t1 = time.perf_counter()
+        gp.evolve(full, fit, 1000 + i)
+        ev.append((time.perf_counter() - t1) * 1e3)
+    return el * 1e3 / args.e2e_steps, fit, float(np.median(ev[1:]))
 
 
 def main():
@@ -381,7 +388,7 @@ def main():
         out["config"]["ode_steps"] = units_per_step / (P * R * ws)  # mean attempts per rollout
         out["config"]["solver"] = "dopri5"
     if args.e2e_steps > 0:
-        e2e_ms, e2e_fit = end_to_end(args, ff, lib, data, pop, ws, rank, dev)
+        e2e_ms, e2e_fit, evolve_ms = end_to_end(args, ff, lib, data, pop, ws, rank, dev)
         ok = bool(np.array_equal(e2e_fit.reshape(-1)[:P].view(np.uint32), res["fitness"].cpu().numpy().view(np.uint32)))
         units = (units_per_step if not adaptive else float("nan"))
         out["end_to_end"] = {
@@ -390,7 +397,10 @@ def main():
             "ms_per_step": e2e_ms, "value": units / (e2e_ms / 1e3) if not adaptive else None,
             "unit": "ODE-steps/s", "steps": args.e2e_steps, "trajectories": False,
             "fitness_equal_to_kernel_line": ok,
-            "h2d_bytes_per_rank": int(pop.nbytes)}
+            "h2d_bytes_per_rank": int(pop.nbytes),
+            "host_evolve_ms": evolve_ms,
+            "host_evolve_what": f"GeneticProgramming.evolve of the {P * ws}-candidate population (native host "
+                                f"library, MTGP_HOST_THREADS={os.environ.get('MTGP_HOST_THREADS', '8')}), median of 3"}
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:

@@ -77,7 +77,8 @@ class GeneticProgramming:
                  coefficient_optimisation: bool = False, gradient_steps: int = 10, optimiser=None,
                  selection_pressure_factors=(0.6, 0.9), reproduction_probability_factors=(1.0, 0.5),
                  crossover_probability_factors=(0.9, 0.4), mutation_probability_factors=(0.1, 0.5),
-                 sample_probability_factors=(0.0, 0.1), device=None, verbose: bool = True):
+                 sample_probability_factors=(0.0, 0.1), device=None, verbose: bool = True,
+                 evolve_backend: str = "native"):
         self.layer_sizes = np.asarray(layer_sizes)
         assert num_populations > 0, "The number of populations should be larger than 0"
         self.num_populations = num_populations
@@ -130,6 +131,10 @@ class GeneticProgramming:
         self.vmap_foriloop = TreeEvaluator(self.library, max_nodes, device)
         self.device = device
         self.operators = Operators(self.library, max_nodes, max_init_depth, coefficient_sd)
+        if evolve_backend not in ("native", "numpy"):
+            raise ValueError(f"evolve_backend must be 'native' or 'numpy', got {evolve_backend!r}")
+        self.evolve_backend = evolve_backend
+        self._evolver = None
 
     # ----------------------------------------------------------------- hot path
     def _engine(self) -> DeviceEngine:
@@ -192,9 +197,17 @@ class GeneticProgramming:
 
     def evolve(self, populations, fitness, key):
         """gp.py:475-497: optional ring migration, then per population elitism + tournament
-        selection + crossover / mutation / resampling (multitreegp_amd.genetic_operators, the
-        numpy restatement of genetic_operators/).  `key` seeds numpy's PCG64 (a JAX key's words
-        or an int)."""
+        selection + crossover / mutation / resampling.  evolve_backend "native" (default): the C++
+        host library (multitreegp_amd.host, include/mtgp_host.h) seeded with `key`; "numpy": the
+        numpy restatement (multitreegp_amd.genetic_operators) on PCG64 seeded with `key` (a JAX
+        key's words or an int)."""
+        if self.evolve_backend == "native":
+            if self._evolver is None:
+                from .host import HostEvolver
+                self._evolver = HostEvolver.for_strategy(self)
+            out = self._evolver.evolve(populations, fitness, _seed_of(key), self.current_generation)
+            self.current_generation += 1
+            return out
         rng = np.random.default_rng(_seed_of(key))
         out = evolve_populations(self.operators, np.asarray(populations, np.float32), np.asarray(fitness), rng,
                                  self.current_generation, self.migration_period, self.migration_size,
