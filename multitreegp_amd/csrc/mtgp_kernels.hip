@@ -2245,6 +2245,9 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
 // translation (jit_words: fall-through code words, < 0 if untranslatable; jit_cost: the schedule
 // weight), so the JIT build needs no translation pass of its own before the code is emitted.
 constexpr int32_t kFlatSerial = 0x7fff;  // status of a program left to k_flatten_serial
+#ifndef MTGP_V_LDS_SERIAL_SIZE
+#define MTGP_V_LDS_SERIAL_SIZE 0
+#endif
 
 // JIT sizing of one flattened program (mtgp_flatten_ex jit_words / jit_cost)
 __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n, int32_t* jit_words_out,
@@ -2344,6 +2347,104 @@ __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n,
     words += __shfl_xor(words, off);
     trig += __shfl_xor(trig, off);
   }
+  if (lane == 0) {
+    if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
+    if (jit_cost_out) {  // = flat_jit_size
+      const int c = failed ? rc : (words + 1 + mtgp::kJitTrigExecuted * trig);
+      jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
+    }
+  }
+}
+
+// The same sizing by a whole wave in LDS-data mode (the wide-state SR kernel's code).  An
+// instruction's code is its register-mode code (JitOpTable) plus, per data operand that is not
+// preloaded, a load at the use (ds_read_b32 + s_waitcnt: 3 words); the program starts with the
+// preloads of the first kJitPreSlots distinct slots it reads (2 words each) and one s_waitcnt.
+// "First distinct": each slot's first operand position (2 i + k, ib before ax) by an LDS atomicMin,
+// then a slot is preloaded iff fewer than kJitPreSlots slots occur before it.  Status as in
+// jit_program: a slot >= MTGP_MAX_DATA anywhere (its preload scan runs first), else the first
+// opcode / stack error in program order.  fpos: MTGP_MAX_DATA ints of this wave's LDS.
+template <int KI>
+__device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, int n, const JitOpTable& T,
+                                                       int32_t* jit_words_out, int32_t* jit_cost_out, size_t pj,
+                                                       int lane, int* fpos) {
+  static_assert(MTGP_MAX_DATA <= kWave, "one lane per data slot");
+  if (lane < MTGP_MAX_DATA) fpos[lane] = 0x7fffffff;
+  __syncthreads();
+  int sa[KI], sb[KI];  // this lane's data-operand slots per chunk (-1: none)
+  bool far = false;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int i = k * kWave + lane;
+    sa[k] = sb[k] = -1;
+    if (i < n) {
+      const MtgpInstr x = prog[i];
+      const uint32_t code = x.op >> MTGP_OP_SHIFT;
+      const uint32_t f = code < 64u ? T.flags[code] : 0u;
+      uint32_t ib;
+      __builtin_memcpy(&ib, &x.imm, 4);
+      if (f & kOpIbSlot) sa[k] = (int)(ib / MTGP_SLOT_BYTES);
+      if (f & kOpAxSlot) sb[k] = (int)((x.op & 0xffffffu) / MTGP_SLOT_BYTES);
+      far = far || sa[k] >= MTGP_MAX_DATA || sb[k] >= MTGP_MAX_DATA;
+      if (sa[k] >= 0 && sa[k] < MTGP_MAX_DATA) atomicMin(&fpos[sa[k]], 2 * i);
+      if (sb[k] >= 0 && sb[k] < MTGP_MAX_DATA) atomicMin(&fpos[sb[k]], 2 * i + 1);
+    }
+  }
+  __syncthreads();
+  const bool slot_err = __any(far);
+  // lane s: is slot s preloaded (fewer than kJitPreSlots slots first occur before it)
+  bool pre = false;
+  if (lane < MTGP_MAX_DATA) {
+    const int mine = fpos[lane];
+    int before = 0;
+#pragma unroll 8
+    for (int t = 0; t < MTGP_MAX_DATA; ++t) before += fpos[t] < mine ? 1 : 0;
+    pre = mine != 0x7fffffff && before < mtgp::kJitPreSlots;
+  }
+  const uint64_t pre_mask = __ballot(pre);
+  const int npre = __popcll(pre_mask);
+  int words = 0, trig = 0, carry = 0, rc = 0;
+  bool failed = false;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    const int i = k * kWave + lane;
+    const bool in = i < n;
+    int d = 0, e = 0;
+    if (in) {
+      const uint32_t code = prog[i].op >> MTGP_OP_SHIFT;
+      const uint32_t f = code < 64u ? T.flags[code] : 0u;
+      if (!(f & kOpValid)) e = mtgp::kJitErrOpcode;
+      d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
+      words += code < 64u ? T.words[code] : 0;
+      if (sa[k] >= 0 && sa[k] < MTGP_MAX_DATA && !((pre_mask >> sa[k]) & 1ull)) words += 3;
+      if (sb[k] >= 0 && sb[k] < MTGP_MAX_DATA && !((pre_mask >> sb[k]) & 1ull)) words += 3;
+      trig += (f & kOpTrig) ? 1 : 0;
+    }
+    int incl = d;
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int v = __shfl_up(incl, off);
+      if (lane >= off) incl += v;
+    }
+    const int before = carry + incl - d;
+    if (in && e == 0 && ((d > 0 && before >= MTGP_STACK_MAX) || (d < 0 && before <= 0))) e = mtgp::kJitErrStack;
+    carry += __shfl(incl, kWave - 1);
+    const uint64_t bad = __ballot(in && e != 0);
+    if (!failed && bad) {
+      failed = true;
+      rc = __shfl(e, __ffsll((unsigned long long)bad) - 1);
+    }
+  }
+#pragma unroll
+  for (int off = kWave / 2; off > 0; off >>= 1) {
+    words += __shfl_xor(words, off);
+    trig += __shfl_xor(trig, off);
+  }
+  if (slot_err) {
+    failed = true;
+    rc = mtgp::kJitErrSlot;
+  }
+  words += npre > 0 ? 2 * npre + 1 : 0;
   if (lane == 0) {
     if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
     if (jit_cost_out) {  // = flat_jit_size
@@ -2621,6 +2722,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
   __shared__ uint32_t s_flag[NMAX];  // pass 1: resolved; pass 2: times reached
   __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
   __shared__ MtgpInstr s_prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
+  __shared__ int s_fpos[MTGP_MAX_DATA];   // LDS-data sizing: first operand position per data slot
   const int lane = threadIdx.x;
   for (int k = lane; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
   const long pj = blockIdx.x;
@@ -2861,11 +2963,18 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       s_prog[n > 0 ? n : 0] = e;
       len_out[pj] = n > 0 ? n : 0;
       status_out[pj] = n > 0 ? 0 : -n;
+#if MTGP_V_LDS_SERIAL_SIZE  // A/B only: the LDS-data sizing by one lane (jit_program), round-2 behaviour
       if (jit_mode != kJitModeRegs) flat_jit_size(s_prog, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
+#endif
     }
   }
-  if (!shared && jit_mode == kJitModeRegs && (jit_words_out || jit_cost_out))  // (shared: wave-uniform)
-    flat_jit_size_wave<(2 * NMAX + 8 + kWave - 1) / kWave>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
+  if (!shared && (jit_words_out || jit_cost_out)) {  // (shared: wave-uniform)
+    constexpr int KI = (2 * NMAX + 8 + kWave - 1) / kWave;
+    if (jit_mode == kJitModeRegs)
+      flat_jit_size_wave<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
+    else if (!MTGP_V_LDS_SERIAL_SIZE)
+      flat_jit_size_wave_lds<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane, s_fpos);
+  }
   // node count (gp.py:424 parsimony).  Few trees (T <= kFlatDirectTrees): the individual's first
   // program counts them all and stores the sum (no zeroing pass before the launch); many trees
   // (C5: 64): tree t is counted by program t % n_prog and summed with atomics into the zeroed

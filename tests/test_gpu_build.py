@@ -46,6 +46,10 @@ def _population(kind, P, seed=0):
         lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
         pop = sample_population(seed, lib, P, 1, max_init_depth=10, max_nodes=64)[0]
         specs = [(0, 7, 0), (1, 7, 0), (2, 7, 0b1001111), (2, 7, 0b1000000)]
+    elif kind == "sr40":  # 40 variables, deep trees: programs read more than kJitPreSlots distinct slots
+        lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(40)]], [4])
+        pop = sample_population(seed, lib, P, 1, max_init_depth=9, max_nodes=128)[0]
+        specs = [(i, 40, 0) for i in range(4)]
     else:  # 12-variable SR: slots >= 8 are untranslatable -> negative jit words
         lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(12)]], [12])
         pop = sample_population(seed, lib, P, 1, max_init_depth=6, max_nodes=40)[0]
@@ -56,7 +60,7 @@ def _population(kind, P, seed=0):
     return lib, pop, specs
 
 
-@pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("sr12", 0), ("sr12", 1)])
+@pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("sr12", 0), ("sr12", 1), ("sr40", 1), ("dynamic", 1)])
 def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
     lib, pop, specs = _population(kind, 301)
     P, T, N, _ = pop.shape
@@ -85,6 +89,11 @@ def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
         assert np.array_equal(cost.cpu().numpy(), jc)
     if kind == "sr12":
         assert ((jw < 0).any() if mode == 0 else (jw >= 0).all()) and (jw > 0).any()
+    if kind == "sr40":  # some programs load slots at their use (more than 16 distinct slots)
+        sb = nat.SLOT_BYTES
+        distinct = [len({int(w) // sb for w in progs[p, j, :plen[p, j], 1].view(np.uint32) if w < 40 * sb})
+                    for p in range(P) for j in range(len(specs)) if status[p, j] == 0]
+        assert max(distinct) > 16
 
 
 @pytest.mark.parametrize("kind", ["dynamic", "sr12"])
