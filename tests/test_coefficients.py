@@ -16,7 +16,7 @@ import multitreegp_amd as mt
 from multitreegp_amd import coefficients as co
 from oracle import oracle as orc
 
-from helpers import SR_OPS, bits_equal, oracle_model, oracle_rollouts, sr_setup, tree_from_expr
+from helpers import SR_OPS, bits_equal, mismatch_report, oracle_model, oracle_rollouts, sr_setup, tree_from_expr
 
 
 # ------------------------------------------------------- independent complex-step restatement
@@ -81,8 +81,9 @@ def _sr_loss_c(cand, lib, d, prow_t, prow_i, eps=1e-30, euler=False):
     return m if 0 < m.real < 1e5 else complex(np.clip(m.real, 0, 1e5))
 
 
-def _setup(P=12, R=4, euler=False, seed=3):
-    env, lib, ff, data, pop = sr_setup(P=P, R=R, n_save=9, save_every=2, h=0.05, depth=4, N=20, seed=seed)
+def _setup(P=12, R=4, euler=False, seed=3, n_var=2):
+    env, lib, ff, data, pop = sr_setup(P=P, R=R, n_save=9, save_every=2, h=0.05, depth=4, N=20, seed=seed,
+                                       n_var=n_var)
     if euler:
         ff = mt.SREvaluator(solver=mt.Euler(), dt0=0.05)
     d = ff.prepare(data)
@@ -289,6 +290,27 @@ def test_gpu_sr_grad_bitexact(euler):
         assert bits_equal(g, rg[p, : len(g)]), p
     fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
     assert bits_equal(loss, fit)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_var,R", [(3, 5), (6, 8), (20, 3), (2, 5)])
+def test_gpu_sr_grad_bitexact_wide(n_var, R):
+    """The other k_sr_grad widths (n_var 3 -> 4 slots, 6 / 20 -> the 16 / 64-slot templates) and
+    non-power-of-two rollout counts: loss and gradients bit for bit vs the oracle, loss = the
+    evaluator's fitness."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    lib, ff, data, d, pop = _setup(P=24, R=R, seed=11 + n_var, n_var=n_var)
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    opt = co.CoefficientOptimiser(eng)
+    loss, grads = opt.loss_and_grad(pop, data)
+    rl, rg, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    assert sum(len(r) for r in rows) > 5
+    assert bits_equal(loss, rl), mismatch_report(loss, rl, "loss")
+    for p, g in enumerate(grads):
+        assert bits_equal(g, rg[p, : len(g)]), p
+    fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
+    assert bits_equal(loss, fit), mismatch_report(loss, fit, "fitness")
 
 
 @pytest.mark.gpu

@@ -11,7 +11,7 @@ import multitreegp_amd as mt
 from multitreegp_amd import _native as nat
 from multitreegp_amd.sampling import sample_population
 
-from helpers import CONTROL_OPS, SR_OPS, bits_equal, mismatch_report
+from helpers import CONTROL_OPS, SR_OPS, bits_equal, mismatch_report, tree_from_expr
 
 pytestmark = pytest.mark.gpu
 
@@ -50,6 +50,21 @@ def _population(kind, P, seed=0):
         lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(40)]], [4])
         pop = sample_population(seed, lib, P, 1, max_init_depth=9, max_nodes=128)[0]
         specs = [(i, 40, 0) for i in range(4)]
+        # the sampler's trees are small (operator probability 0.7^depth, initialization.py:35):
+        # every 7th individual gets balanced trees over 17-40 distinct variables
+        ops = ["+", "-", "*", "/"]
+
+        def balanced(vs, k=0):
+            if len(vs) == 1:
+                return vs[0]
+            h = len(vs) // 2
+            return (ops[k % 4], balanced(vs[:h], k + 1), balanced(vs[h:], k + 2))
+
+        for p in range(0, P, 7):
+            for t in range(4):
+                m = int(rng.integers(17, 41))
+                vs = [f"x{int(i)}" for i in rng.permutation(40)[:m]]
+                pop[p, t] = tree_from_expr(balanced(vs), lib, 128)
     else:  # 12-variable SR: slots >= 8 are untranslatable -> negative jit words
         lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(12)]], [12])
         pop = sample_population(seed, lib, P, 1, max_init_depth=6, max_nodes=40)[0]
