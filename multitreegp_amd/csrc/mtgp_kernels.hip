@@ -772,25 +772,48 @@ __device__ __forceinline__ void probe(const Lane& L, int what) {
 #define MTGP_PROBE(L, w)
 #endif
 
-// Run program `slot` of group gi (its individual's program, wave-uniform).
+// The interpreter as an out-of-line function for the JIT kernels' fallback sites (lanes that need
+// the slow sin/cos reduction, populations without usable code).  Inlined, its dispatch trees
+// make the C3 kernel 190 KB of code (19 KB out of line), but the call costs more than the
+// instruction fetch it saves: the call ABI spills SGPRs into VGPR lanes and a few VGPRs to
+// scratch inside the stage loop.  A/B in one process (profiles/r03/v5_ab_cold.log): C3 kernel
+// 2.60 ms out of line vs 2.30 inline, C2 1.06 vs 0.91, C5 7.51 vs 7.14.  Kept inline (0).
+#ifndef MTGP_COLD_INTERP
+#define MTGP_COLD_INTERP 0
+#endif
+typedef __attribute__((address_space(3))) float LdsFloat;
+__device__ __attribute__((noinline)) float run_prog_cold(const MtgpInstr* code, uint32_t dcol_lds, uint32_t st_lds) {
+  const float* dcol = (const float*)(LdsFloat*)(uintptr_t)dcol_lds;
+  float* st = (float*)(LdsFloat*)(uintptr_t)st_lds;
+  return run_prog(code, dcol, st);
+}
+__device__ __forceinline__ uint32_t lds_addr_of(const float* p) {
+  return (uint32_t)(uintptr_t)(const LdsFloat*)p;
+}
+
+// Run program `slot` of group gi (its individual's program, wave-uniform).  COLD: out of line.
+template <bool COLD = false>
 __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
                                                 float* st) {
 #if MTGP_V_PTAB
   const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.ptab, gi) +
                        (uint32_t)slot * (uint32_t)A.L * (uint32_t)sizeof(MtgpInstr);
-  return run_prog((const MtgpInstr*)((const char*)A.prog + off), dcol, st);
+  const MtgpInstr* code = (const MtgpInstr*)((const char*)A.prog + off);
 #else
   const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
-  return run_prog(A.prog + pj * A.L, dcol, st);
+  const MtgpInstr* code = A.prog + pj * A.L;
 #endif
+  if (COLD && MTGP_COLD_INTERP) return run_prog_cold(code, lds_addr_of(dcol), lds_addr_of(st));
+  return run_prog(code, dcol, st);
 }
 
 // interpreter: program `slot` of every live group on explicit LDS columns
+template <bool COLD = false>
 __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L, int ng, int slot, const float* dcol,
                                                    float* st, float dflt) {
   float v = dflt;
   for (int gi = 0; gi < ng; ++gi) {
-    const float t = run_one_interp(A, L, gi, slot, dcol, st);
+    const float t = run_one_interp<COLD>(A, L, gi, slot, dcol, st);
     v = (L.g == gi) ? t : v;
   }
   return v;
@@ -827,11 +850,11 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
           if (!spilled) { D.spill(); spilled = true; }
 #pragma unroll
           for (int j = 0; j < M; ++j) {
-            const float t = run_one_interp(A, L, gi, first + j, D.dcol, D.st);
+            const float t = run_one_interp<JIT>(A, L, gi, first + j, D.dcol, D.st);
             out[j] = (L.g == gi) ? t : out[j];
           }
           if (save_prog >= 0) {
-            const float t = run_one_interp(A, L, gi, save_prog, D.dcol, D.st);
+            const float t = run_one_interp<JIT>(A, L, gi, save_prog, D.dcol, D.st);
             *save_v = (L.g == gi) ? t : *save_v;
           }
         }
@@ -857,7 +880,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(L.g == gi && L.active))) continue;
             if (!spilled) { D.spill(); spilled = true; }
-            const float t = run_one_interp(A, L, gi, first + q, D.dcol, D.st);
+            const float t = run_one_interp<JIT>(A, L, gi, first + q, D.dcol, D.st);
             v = (L.g == gi) ? t : v;
           }
 #if MTGP_V_TIMING
@@ -878,11 +901,11 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
   if (interp) {
 #pragma unroll 1
     for (int q = 0; q < mr; ++q) {  // mr <= M: a runtime role size (state_size > 3, interpreter only)
-      const float v = run_groups_interp(A, L, ng, first + q, D.dcol, D.st, 0.0f);
+      const float v = run_groups_interp<JIT>(A, L, ng, first + q, D.dcol, D.st, 0.0f);
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
     }
-    if (save_prog >= 0) *save_v = run_groups_interp(A, L, ng, save_prog, D.dcol, D.st, 0.0f);
+    if (save_prog >= 0) *save_v = run_groups_interp<JIT>(A, L, ng, save_prog, D.dcol, D.st, 0.0f);
   }
 }
 
@@ -1928,7 +1951,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
             if (c >= NV) break;
             for (int gi = 0; gi < ng; ++gi) {
               if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-              const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, cur, st);
+              const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, cur, st);
               if (Ln.g == gi) nxt[c * kWave] = tv;
             }
           }
@@ -1944,7 +1967,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
           if (__builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: interpret those groups
             for (int gi = 0; gi < ng; ++gi) {
               if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-              const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, cur, st);
+              const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, cur, st);
               v = (Ln.g == gi) ? tv : v;
             }
           }
@@ -1954,7 +1977,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
         for (int t = 0; t < kWideComp; ++t) {
           const int c = c0 + t;
           if (c >= NV) break;
-          nxt[c * kWave] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+          nxt[c * kWave] = run_groups_interp<JIT>(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
         }
       }
 #pragma unroll
@@ -2037,7 +2060,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
           if (c >= NV) break;
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-            const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, in, st);
+            const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, in, st);
             kx[t] = (Ln.g == gi) ? tv : kx[t];
           }
         }
@@ -2054,7 +2077,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
         if (__builtin_expect(fl != 0, 0)) {
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-            const float tv = run_one_interp(A, Ln, gi, A.m.prog_state + c, in, st);
+            const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, in, st);
             v = (Ln.g == gi) ? tv : v;
           }
         }
@@ -2065,7 +2088,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
       for (int t = 0; t < kWideComp; ++t) {
         const int c = c0 + t;
         if (c >= NV) break;
-        kx[t] = run_groups_interp(A, Ln, ng, A.m.prog_state + c, in, st, 0.0f);
+        kx[t] = run_groups_interp<JIT>(A, Ln, ng, A.m.prog_state + c, in, st, 0.0f);
       }
     }
   };

@@ -44,8 +44,12 @@ def main():
         # such as MTGP_JIT_CHAIN=0) applied around each of its evaluations
         name, *kv = v.split("@")
         envs[v] = dict(x.split("=", 1) for x in kv)
-        path = nat.LIB_PATH if name == "prod" else os.path.join(ROOT, "multitreegp_amd", "lib", "variants",
-                                                                f"libmtgp_hip_{name}.so")
+        # variants/ is gpurun-ignored (never pushed wholesale): libraries for an A/B run are copied to lib/ab/
+        path = nat.LIB_PATH
+        if name != "prod":
+            path = os.path.join(ROOT, "multitreegp_amd", "lib", "ab", f"libmtgp_hip_{name}.so")
+            if not os.path.exists(path):
+                path = os.path.join(ROOT, "multitreegp_amd", "lib", "variants", f"libmtgp_hip_{name}.so")
         engines[v] = DeviceEngine(ff, lib, 0.0, dev, native=nat.load(path))
         engines[v].native.mtgp_set_timing(1)
     pop_dev = torch.from_numpy(pop).to(dev)
