@@ -781,6 +781,12 @@ __device__ __forceinline__ void probe(const Lane& L, int what) {
 #ifndef MTGP_COLD_INTERP
 #define MTGP_COLD_INTERP 0
 #endif
+// The Dopri5 kernels run at two waves per SIMD (183 VGPRs, no pressure from the call) and their
+// long tails are single waves whose hot loop competes for the instruction cache: there the
+// fallback interpreter is out of line (MTGP_DP_COLD).
+#ifndef MTGP_DP_COLD
+#define MTGP_DP_COLD 1
+#endif
 typedef __attribute__((address_space(3))) float LdsFloat;
 __device__ __attribute__((noinline)) float run_prog_cold(const MtgpInstr* code, uint32_t dcol_lds, uint32_t st_lds) {
   const float* dcol = (const float*)(LdsFloat*)(uintptr_t)dcol_lds;
@@ -803,7 +809,7 @@ __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, i
   const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
   const MtgpInstr* code = A.prog + pj * A.L;
 #endif
-  if (COLD && MTGP_COLD_INTERP) return run_prog_cold(code, lds_addr_of(dcol), lds_addr_of(st));
+  if (COLD) return run_prog_cold(code, lds_addr_of(dcol), lds_addr_of(st));
   return run_prog(code, dcol, st);
 }
 
@@ -824,7 +830,7 @@ __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L
 // the interpreter runs when there is no usable code or when a lane needs the slow sin/cos path.
 // chained: the role's code is one chain (A.chain_state, mtgp_jit.h jit_unit_end); with save_prog
 // >= 0 the chain's continuation (program save_prog, the save-point readout) runs too -> *save_v.
-template <bool JIT, int M>
+template <bool JIT, int M, bool COLD = (MTGP_COLD_INTERP != 0)>
 __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, int role, int first, DataVec<JIT>& D,
                                          float (&out)[M], bool chained = false, int save_prog = -1,
                                          float* save_v = nullptr, int mr = M) {
@@ -850,11 +856,11 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
           if (!spilled) { D.spill(); spilled = true; }
 #pragma unroll
           for (int j = 0; j < M; ++j) {
-            const float t = run_one_interp<JIT>(A, L, gi, first + j, D.dcol, D.st);
+            const float t = run_one_interp<JIT && COLD>(A, L, gi, first + j, D.dcol, D.st);
             out[j] = (L.g == gi) ? t : out[j];
           }
           if (save_prog >= 0) {
-            const float t = run_one_interp<JIT>(A, L, gi, save_prog, D.dcol, D.st);
+            const float t = run_one_interp<JIT && COLD>(A, L, gi, save_prog, D.dcol, D.st);
             *save_v = (L.g == gi) ? t : *save_v;
           }
         }
@@ -880,7 +886,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(L.g == gi && L.active))) continue;
             if (!spilled) { D.spill(); spilled = true; }
-            const float t = run_one_interp<JIT>(A, L, gi, first + q, D.dcol, D.st);
+            const float t = run_one_interp<JIT && COLD>(A, L, gi, first + q, D.dcol, D.st);
             v = (L.g == gi) ? t : v;
           }
 #if MTGP_V_TIMING
@@ -901,11 +907,11 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
   if (interp) {
 #pragma unroll 1
     for (int q = 0; q < mr; ++q) {  // mr <= M: a runtime role size (state_size > 3, interpreter only)
-      const float v = run_groups_interp<JIT>(A, L, ng, first + q, D.dcol, D.st, 0.0f);
+      const float v = run_groups_interp<JIT && COLD>(A, L, ng, first + q, D.dcol, D.st, 0.0f);
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
     }
-    if (save_prog >= 0) *save_v = run_groups_interp<JIT>(A, L, ng, save_prog, D.dcol, D.st, 0.0f);
+    if (save_prog >= 0) *save_v = run_groups_interp<JIT && COLD>(A, L, ng, save_prog, D.dcol, D.st, 0.0f);
   }
 }
 
@@ -1277,8 +1283,50 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   finish_group(A, Ln, Env::fit_final(fit, S));
 }
 
-// Dormand-Prince a_ij (include/mtgp_dopri5.h), read with scalar loads by the rolled stage loops
-static __constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
+// Dormand-Prince stage inputs (include/mtgp_dopri5.h): sum_{j<s} a_sj f_j, the fma chain of
+// mtgp_dp_term in ascending j with zero entries skipped, the tableau as compile-time constants.
+// The stage loops stay rolled (one copy of the RHS and its program call sites); one wave-uniform
+// switch on s selects the specialisation, and the stage derivative is filed into f[s] the same
+// way.  (Reading a_sj from a table by the dynamic s and filing f[s] with selects cost ~150 VALU
+// per stage: two thirds of a lone tail wave's arithmetic outside the RHS.)
+template <int S, int N>
+__device__ __forceinline__ void dp_stage_sum_s(const float (&f)[7][N], float (&acc)[N]) {
+  constexpr float a[7][6] = MTGP_DP_TABLE_A;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    float v = 0.0f;
+#pragma unroll
+    for (int j = 0; j < S; ++j) v = mtgp_dp_term(v, a[S][j], f[j][i], j == 0);
+    acc[i] = v;
+  }
+}
+template <int N>
+__device__ __forceinline__ void dp_stage_sum(int s, const float (&f)[7][N], float (&acc)[N]) {
+  switch (s) {
+    case 1: dp_stage_sum_s<1, N>(f, acc); break;
+    case 2: dp_stage_sum_s<2, N>(f, acc); break;
+    case 3: dp_stage_sum_s<3, N>(f, acc); break;
+    case 4: dp_stage_sum_s<4, N>(f, acc); break;
+    case 5: dp_stage_sum_s<5, N>(f, acc); break;
+    default: dp_stage_sum_s<6, N>(f, acc); break;
+  }
+}
+template <int S, int N>
+__device__ __forceinline__ void dp_file_s(float (&f)[7][N], const float (&k)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) f[S][i] = k[i];
+}
+template <int N>
+__device__ __forceinline__ void dp_file(int s, float (&f)[7][N], const float (&k)[N]) {
+  switch (s) {
+    case 1: dp_file_s<1, N>(f, k); break;
+    case 2: dp_file_s<2, N>(f, k); break;
+    case 3: dp_file_s<3, N>(f, k); break;
+    case 4: dp_file_s<4, N>(f, k); break;
+    case 5: dp_file_s<5, N>(f, k); break;
+    default: dp_file_s<6, N>(f, k); break;
+  }
+}
 
 // the controller coefficients of model m (mtgp.h ABI v15; pid_custom == 0: diffrax's defaults)
 __device__ __forceinline__ MtgpDpPid dp_pid(const MtgpModel& m) {
@@ -1395,19 +1443,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     if (DYN) {
 #pragma unroll
       for (int j = 0; j < NA; ++j) D.put(NV + j, s[NV + j]);
-      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // reads [0, a, 0, tar]
+      run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // reads [0, a, 0, tar]
       env.drift(s, ur[0], ds);
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, ur[0]);
       float ka[NAX];
-      run_role<JIT, NAX>(A, Ln, ng, 1, A.m.prog_state, D, ka, DYN && A.chain_state != 0);
+      run_role<JIT, NAX, MTGP_DP_COLD != 0>(A, Ln, ng, 1, A.m.prog_state, D, ka, DYN && A.chain_state != 0);
 #pragma unroll
       for (int j = 0; j < NA; ++j) ds[NV + j] = ka[j];
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+      run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       env.drift(s, ur[0], ds);
     }
   };
@@ -1423,9 +1471,9 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
 #pragma unroll
       for (int j = 0; j < NA; ++j) D.put(NV + j, sk[NV + j]);
       D.put(uslot, 0.0f);
-      run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, ur);  // readout([y, a, 0, tar]) dyn.py:101
+      run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 2, A.m.prog_readout_save, D, ur);  // readout([y, a, 0, tar]) dyn.py:101
     } else {
-      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // policy([y, tar]) ff.py:97
+      run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // policy([y, tar]) ff.py:97
     }
     if (!on) return;
     if (!fill) env.fit_update(fit, k, S, ts, ur[0], sk);
@@ -1481,21 +1529,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     const float h = tnext - t;
 #pragma unroll 1
     for (int s = 1; s <= 6; ++s) {
-      float yi[ND], fs[ND];
+      float yi[ND], fs[ND], acc[ND];
+      dp_stage_sum<ND>(s, f, acc);
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
-        yi[i] = MTGP_FMAF(h, acc, y[i]);
+        yi[i] = MTGP_FMAF(h, acc[i], y[i]);
         y1[i] = yi[i];
       }
       rhs(t + mtgp_dp_c(s) * h, yi, fs);
-#pragma unroll
-      for (int j = 1; j < 7; ++j)
-#pragma unroll
-        for (int i = 0; i < ND; ++i) f[j][i] = (j == s) ? fs[i] : f[j][i];
+      dp_file<ND>(s, f, fs);
     }
     bool keep = false, stop = false, fail = false;
     float dt = 0.0f;
@@ -1708,7 +1750,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
   // FSAL seed f0 = f(t0, y0)
 #pragma unroll
   for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-  run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
+  run_role<JIT, NV, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
 #pragma unroll
   for (int i = 0; i < NV; ++i) f[0][i] = kx[i];
   bool live = active && t < t_end && steps < max_steps;
@@ -1716,21 +1758,16 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
     const float h = tnext - t;
 #pragma unroll 1
     for (int s = 1; s <= 6; ++s) {  // stage s input y + h sum_{j<s} a_sj f_j (wave-uniform s)
+      float acc[NV];
+      dp_stage_sum<NV>(s, f, acc);
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
-        const float yi = MTGP_FMAF(h, acc, y[i]);
+        const float yi = MTGP_FMAF(h, acc[i], y[i]);
         y1[i] = yi;  // the stage-6 input is the step's solution
         D.put(i, yi);
       }
-      run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
-#pragma unroll
-      for (int j = 1; j < 7; ++j)
-#pragma unroll
-        for (int i = 0; i < NV; ++i) f[j][i] = (j == s) ? kx[i] : f[j][i];
+      run_role<JIT, NV, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
+      dp_file<NV>(s, f, kx);
     }
     if (live) {
       float msum = 0.0f;
@@ -1951,7 +1988,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
             if (c >= NV) break;
             for (int gi = 0; gi < ng; ++gi) {
               if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-              const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, cur, st);
+              const float tv = run_one_interp<JIT && MTGP_COLD_INTERP != 0>(A, Ln, gi, A.m.prog_state + c, cur, st);
               if (Ln.g == gi) nxt[c * kWave] = tv;
             }
           }
@@ -1967,7 +2004,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
           if (__builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: interpret those groups
             for (int gi = 0; gi < ng; ++gi) {
               if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-              const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, cur, st);
+              const float tv = run_one_interp<JIT && MTGP_COLD_INTERP != 0>(A, Ln, gi, A.m.prog_state + c, cur, st);
               v = (Ln.g == gi) ? tv : v;
             }
           }
@@ -1977,7 +2014,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
         for (int t = 0; t < kWideComp; ++t) {
           const int c = c0 + t;
           if (c >= NV) break;
-          nxt[c * kWave] = run_groups_interp<JIT>(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
+          nxt[c * kWave] = run_groups_interp<JIT && MTGP_COLD_INTERP != 0>(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
         }
       }
 #pragma unroll
@@ -2060,7 +2097,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
           if (c >= NV) break;
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-            const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, in, st);
+            const float tv = run_one_interp<JIT && MTGP_DP_COLD != 0>(A, Ln, gi, A.m.prog_state + c, in, st);
             kx[t] = (Ln.g == gi) ? tv : kx[t];
           }
         }
@@ -2077,7 +2114,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
         if (__builtin_expect(fl != 0, 0)) {
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(Ln.g == gi && Ln.active))) continue;
-            const float tv = run_one_interp<JIT>(A, Ln, gi, A.m.prog_state + c, in, st);
+            const float tv = run_one_interp<JIT && MTGP_DP_COLD != 0>(A, Ln, gi, A.m.prog_state + c, in, st);
             v = (Ln.g == gi) ? tv : v;
           }
         }
@@ -2088,7 +2125,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
       for (int t = 0; t < kWideComp; ++t) {
         const int c = c0 + t;
         if (c >= NV) break;
-        kx[t] = run_groups_interp<JIT>(A, Ln, ng, A.m.prog_state + c, in, st, 0.0f);
+        kx[t] = run_groups_interp<JIT && MTGP_DP_COLD != 0>(A, Ln, ng, A.m.prog_state + c, in, st, 0.0f);
       }
     }
   };
@@ -2153,22 +2190,17 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
     for (int s = 1; s <= 6; ++s) {
       buf ^= 1;
       float* in = bufs[buf];
+      float acc[kWideComp];
+      dp_stage_sum<kWideComp>(s, f, acc);
 #pragma unroll
       for (int i = 0; i < kWideComp; ++i) {
-        float acc = 0.0f;
-#pragma unroll
-        for (int j = 0; j < 6; ++j)
-          if (j < s) acc = mtgp_dp_term(acc, kDpA[s][j], f[j][i], j == 0);
-        const float yi = MTGP_FMAF(h, acc, y[i]);
+        const float yi = MTGP_FMAF(h, acc[i], y[i]);
         y1[i] = yi;
         if (c0 + i < NV) in[(c0 + i) * kWave] = yi;
       }
       __syncthreads();  // the other buffer is not read again before the next barrier
       rhs(in, kx);
-#pragma unroll
-      for (int j = 1; j < 7; ++j)
-#pragma unroll
-        for (int i = 0; i < kWideComp; ++i) f[j][i] = (j == s) ? kx[i] : f[j][i];
+      dp_file<kWideComp>(s, f, kx);
     }
     // error norm: rms over all components (index order) of the scaled error estimate
 #pragma unroll
