@@ -781,11 +781,11 @@ __device__ __forceinline__ void probe(const Lane& L, int what) {
 #ifndef MTGP_COLD_INTERP
 #define MTGP_COLD_INTERP 0
 #endif
-// The Dopri5 kernels run at two waves per SIMD (183 VGPRs, no pressure from the call) and their
-// long tails are single waves whose hot loop competes for the instruction cache: there the
-// fallback interpreter is out of line (MTGP_DP_COLD).
+// The Dopri5 kernels (two waves per SIMD, 183 VGPRs) can take the fallback out of line too
+// (MTGP_DP_COLD=1); measured on C3 Dopri5 (profiles/r03/v8_dptail.log vs v6): full population
+// 21.4 vs 20.2 ms, a lone tail wave 10.6 vs 9.9 us per attempt -- inline kept.
 #ifndef MTGP_DP_COLD
-#define MTGP_DP_COLD 1
+#define MTGP_DP_COLD 0
 #endif
 typedef __attribute__((address_space(3))) float LdsFloat;
 __device__ __attribute__((noinline)) float run_prog_cold(const MtgpInstr* code, uint32_t dcol_lds, uint32_t st_lds) {

@@ -54,6 +54,8 @@ for step in "$@"; do
     dpab_noise) run dpab_noise 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,128,256,512 --rounds 3 || exit 1 ;;
     dptail) run dptail 600 python scripts/dp_tail.py || exit 1 ;;
     dptail_noise) run dptail_noise 600 python scripts/dp_tail.py --obs-noise 0.1 --tail 990 || exit 1 ;;
+    ab_c5_union) run ab_c5_union 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,prod@MTGP_JIT_LDS_PIPE=1" --tag c5_union || exit 1 ;;
+    dpprof) run dpprof 700 bash scripts/dpprof.sh || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
