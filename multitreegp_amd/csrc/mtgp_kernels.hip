@@ -1893,6 +1893,11 @@ __device__ __forceinline__ uint32_t lds_address(const float* p) {
 }
 
 
+// The per-save MSE (components summed in index order, sr.py:24) is needed by wave 0 only, which
+// writes the fitness; the other waves skip the 64 LDS reads (MTGP_V_MSE0=0: every wave sums).
+#ifndef MTGP_V_MSE0
+#define MTGP_V_MSE0 1
+#endif
 template <bool TRAJ, bool JIT>
 __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   extern __shared__ float wl[];
@@ -1955,9 +1960,11 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
         }
       }
       __syncthreads();
-      float sq = nxt[0];
-      for (int d = 1; d < NV; ++d) sq = sq + nxt[d * kWave];
-      tot = tot + sq;
+      if (!MTGP_V_MSE0 || w == 0) {  // (only wave 0 reports the fitness: finish_group)
+        float sq = nxt[0];
+        for (int d = 1; d < NV; ++d) sq = sq + nxt[d * kWave];
+        tot = tot + sq;
+      }
       __syncthreads();
     }
     if (pending) {
@@ -1981,7 +1988,13 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       if (JIT && Ln.jok && A.chain_store) {  // one call: this wave's components' units, results into nxt
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c0);
         uint64_t fl = 0;
+#if MTGP_V_NOPROG  // diagnostic only (A/B): the stage glue without the program calls
+        (void)off;
+        for (int t = 0; t < kWideComp; ++t)
+          if (c0 + t < NV) nxt[(c0 + t) * kWave] = 0.0f;
+#else
         jit_call_lds_store(A.jit_base + off, lds_address(cur), lds_address(nxt), fl);
+#endif
         if (__builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: interpret those groups
           for (int t = 0; t < kWideComp; ++t) {
             const int c = c0 + t;
@@ -2539,6 +2552,11 @@ __global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__
 #define MTGP_FLAT_LANES 16
 #endif
 
+// The lane-per-program flattener is the round-1 design, kept for A/B runs only: built with
+// -DMTGP_AB_FLAT_LANE=1 (MTGP_FLAT_MODE=lane then selects it); the product launches k_flatten_wave.
+#ifndef MTGP_AB_FLAT_LANE
+#define MTGP_AB_FLAT_LANE 0
+#endif
 template <int NMAX, int TPB>
 __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, int P, int T, int N,
                                                             MtgpNodeLibrary lib,
@@ -4067,16 +4085,20 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   // one wave per program (k_flatten_wave, default) or one lane per program (k_flatten): A/B knob
   // MTGP_FLAT_MODE=lane at run time
   const char* fm = getenv("MTGP_FLAT_MODE");
-  const bool wave_mode = !(fm && strcmp(fm, "lane") == 0);
+  const bool wave_mode = !MTGP_AB_FLAT_LANE || !(fm && strcmp(fm, "lane") == 0);
   static const JitOpTable optab = jit_op_table();  // (host probe of jit_program, once per process)
   if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
   // node counts are summed with atomics into zeros, except by the wave kernel for few trees
   if ((!wave_mode || T > kFlatDirectTrees) && hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess)
     return MTGP_ERR_LAUNCH;
+#if MTGP_AB_FLAT_LANE
 #define MTGP_FLAT_ONE(NM, TP)                                                                                 \
   hipLaunchKernelGGL((k_flatten<NM, TP>), dim3((unsigned)((total + TP - 1) / TP)), dim3(TP), 0, s, population, P, \
                      T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,      \
                      jit_cost_out, jit_mode)
+#else
+#define MTGP_FLAT_ONE(NM, TP) (void)0
+#endif
 #define MTGP_FLAT_LAUNCH(NM)                                                                                \
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \

@@ -33,6 +33,12 @@ pmcsq() {  # name config: one pass of SQ stall / instruction counters over kprof
       --config $c "$@" || return 1
   python3 scripts/pmc_summary.py $O/$n ${KSUB:-k_} > $O/${n}.json; cat $O/${n}.json
 }
+pmcic() {  # name config: one pass of instruction-cache counters over kprof (2 evaluations)
+  local n=$1 c=$2; shift 2
+  run $n 120 timeout -s KILL 90 rocprofv3 --pmc SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE \
+      -d $O/$n -o $n --output-format csv -- python3 scripts/kprof.py --iters 2 --config $c "$@" || return 1
+  python3 scripts/pmc_summary.py $O/$n ${KSUB:-k_} > $O/${n}.json; cat $O/${n}.json
+}
 for step in "$@"; do
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
@@ -56,10 +62,16 @@ for step in "$@"; do
     dptail_noise) run dptail_noise 600 python scripts/dp_tail.py --obs-noise 0.1 --tail 990 || exit 1 ;;
     ab_c5_union) run ab_c5_union 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,prod@MTGP_JIT_LDS_PIPE=1" --tag c5_union || exit 1 ;;
     dpprof) run dpprof 700 bash scripts/dpprof.sh || exit 1 ;;
+    ab_c5_mse) run ab_c5_mse 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,mseall,noprog" --tag c5_mse || exit 1 ;;
+    ab_c3_noprog) run ab_c3_noprog 400 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod,noprog" --tag c3_noprog || exit 1 ;;
+    ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;
+    pmcic_c5) KSUB=k_sr_wide pmcic pmcic_c5 c5 || exit 1 ;;
+    pmcic_c3) KSUB=k_ctl_dynamic pmcic pmcic_c3 c3 || exit 1 ;;
+    pmcic_c2) KSUB=k_ctl_static pmcic pmcic_c2 c2 || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
