@@ -60,8 +60,19 @@ enum {
   MTGP_FN_MUL = 4,  /* "*"  x * y                                                  */
   MTGP_FN_DIV = 5,  /* "/"  x / y   (IEEE, unprotected: SymbolicRegression.ipynb)  */
   MTGP_FN_SIN = 6,  /* "sin" f(x)                                  gp.py:24-25    */
-  MTGP_FN_COS = 7   /* "cos"                                                       */
+  MTGP_FN_COS = 7,  /* "cos"                                                       */
+  /* round 3: further unary operators a reference operator_list may name (gp.py:143-162
+   * accepts any lambda; these follow jnp.exp / log / sqrt / tanh / abs in f32, specs in
+   * mtgp_f32math.h).  The program JIT does not translate them: a population that uses one is
+   * evaluated by the interpreter (bit-identical, slower). */
+  MTGP_FN_EXP = 8,  /* "exp"  mtgp_expf                                            */
+  MTGP_FN_LOG = 9,  /* "log"  mtgp_logf  (x < 0: NaN, 0: -inf)                     */
+  MTGP_FN_SQRT = 10, /* "sqrt" IEEE sqrt (correctly rounded; x < 0: NaN)           */
+  MTGP_FN_TANH = 11, /* "tanh" mtgp_tanhf                                          */
+  MTGP_FN_ABS = 12   /* "abs"  |x| (sign bit cleared)                              */
 };
+/* unary function codes: SIN .. ABS except the binary ones */
+#define MTGP_FN_IS_UNARY(fn) ((fn) == MTGP_FN_SIN || (fn) == MTGP_FN_COS || ((fn) >= MTGP_FN_EXP && (fn) <= MTGP_FN_ABS))
 
 typedef struct {
   int32_t n_funcs;   /* 2 + K + V: lax.switch branch count (index is clamped)       */

@@ -16,6 +16,7 @@
 #ifndef MTGP_DUAL_H
 #define MTGP_DUAL_H
 
+#include "mtgp.h"
 #include "mtgp_f32math.h"
 
 typedef struct {
@@ -53,6 +54,33 @@ MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_cos(MtgpDual a) { return mtgp_dl(mtgp_cosf(
 MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_exp(MtgpDual a) {
   const float e = mtgp_expf(a.v);
   return mtgp_dl(e, e * a.d);
+}
+/* the round-3 unary tree operators, tangents as jax.lax defines their JVPs:
+ * log: g / x;  sqrt: g * (0.5 / ans);  tanh: (g + g * ans) * (1 - ans);  abs: sign(x) * g */
+MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_log(MtgpDual a) { return mtgp_dl(mtgp_logf(a.v), a.d / a.v); }
+MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_sqrt(MtgpDual a) {
+  const float s = mtgp_sqrtf(a.v);
+  return mtgp_dl(s, a.d * (0.5f / s));
+}
+MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_tanh(MtgpDual a) {
+  const float t = mtgp_tanhf(a.v);
+  return mtgp_dl(t, (a.d + a.d * t) * (1.0f - t));
+}
+MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_abs(MtgpDual a) {
+  const float sg = a.v > 0.0f ? 1.0f : (a.v < 0.0f ? -1.0f : a.v);  /* jnp.sign: +-0 -> +-0, NaN -> NaN */
+  return mtgp_dl(mtgp_absf(a.v), sg * a.d);
+}
+/* one of the unary tree operators by function code (MTGP_FN_*): sin .. abs */
+MTGP_INLINE MTGP_HD MtgpDual mtgp_dl_unary(int fn, MtgpDual a) {
+  switch (fn) {
+    case MTGP_FN_SIN: return mtgp_dl_sin(a);
+    case MTGP_FN_COS: return mtgp_dl_cos(a);
+    case MTGP_FN_EXP: return mtgp_dl_exp(a);
+    case MTGP_FN_LOG: return mtgp_dl_log(a);
+    case MTGP_FN_SQRT: return mtgp_dl_sqrt(a);
+    case MTGP_FN_TANH: return mtgp_dl_tanh(a);
+    default: return mtgp_dl_abs(a);
+  }
 }
 
 /* jnp.clip(u, lo, hi) = minimum(maximum(u, lo), hi): value as mtgp_clip (NaN propagates), tangent

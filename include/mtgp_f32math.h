@@ -36,6 +36,7 @@
 #define MTGP_RINT(a) __builtin_rint(a)
 #define MTGP_TRUNCF(a) __builtin_truncf(a)
 #define MTGP_FABSF(a) __builtin_fabsf(a)
+#define MTGP_SQRTF(a) __builtin_sqrtf(a) /* correctly rounded (HIP's default f32 sqrt) */
 #else
 #include <math.h>
 #define MTGP_HD
@@ -45,6 +46,7 @@
 #define MTGP_RINT(a) rint(a)
 #define MTGP_TRUNCF(a) truncf(a)
 #define MTGP_FABSF(a) fabsf(a)
+#define MTGP_SQRTF(a) sqrtf(a)
 #endif
 
 /* wave-uniform "does any lane need the rare path" test: a single scalar branch on the GPU,
@@ -301,6 +303,77 @@ MTGP_INLINE MTGP_HD float mtgp_expf(float x) {
   const int ni = (int)n, n1 = ni / 2, n2 = ni - n1; /* |n1|, |n2| <= 75: normal powers of two */
   y = y * mtgp_u2f((uint32_t)(n1 + 127) << 23);
   return y * mtgp_u2f((uint32_t)(n2 + 127) << 23);
+}
+
+/* ---- log, fdlibm-style (FreeBSD e_logf.c polynomial), basic operations only ---- */
+/* log(u) for finite u > 0 (u == 1 -> 0). */
+MTGP_INLINE MTGP_HD float mtgp_logf_pos(float u) {
+  uint32_t ix = mtgp_f2u(u);
+  int k = 0;
+  if (ix < 0x00800000u) { /* subnormal: scale by 2^25 (exact) */
+    u = u * 33554432.0f;
+    ix = mtgp_f2u(u);
+    k = -25;
+  }
+  k += (int)(ix >> 23) - 127;
+  ix &= 0x007fffffu;
+  /* normalise m into [sqrt(2)/2, sqrt(2)): i = 0x800000 when the mantissa is >= ~sqrt(2)
+   * (0x800000 - 0x4afb20 = 0x3504e0, sqrt(2) = 0x3fb504f3), then m is halved */
+  const uint32_t i = (ix + 0x4afb20u) & 0x800000u;
+  const float m = mtgp_u2f(ix | (i ^ 0x3f800000u)); /* m or m/2 */
+  k += (int)(i >> 23);
+  const float f = m - 1.0f;
+  const float s = f / (2.0f + f);
+  const float z = s * s;
+  const float w = z * z;
+  const float t1 = w * (0.40000972152f + w * 0.24279078841f);
+  const float t2 = z * (0.66666662693f + w * 0.28498786688f);
+  const float R = t2 + t1;
+  const float hfsq = 0.5f * f * f;
+  const float dk = (float)k;
+  /* ln2 split: hi has 16 trailing zero bits so dk * hi is exact */
+  return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
+}
+
+
+/* ---- further unary operators a reference operator_list may name (round 3) ----
+ * Each is one fixed f32 algorithm of basic IEEE operations (plus mtgp_expf / mtgp_logf_pos), so
+ * the kernels and the oracle agree bit for bit; the accuracy vs float64 is tested in
+ * tests/test_f32math.py (XLA's own exp / log / tanh may differ in the last bits: unpinnable here). */
+
+/* jnp.log: NaN -> NaN, x < 0 -> NaN, +-0 -> -inf, +inf -> +inf, else mtgp_logf_pos */
+MTGP_INLINE MTGP_HD float mtgp_logf(float x) {
+  if (mtgp_isnan(x)) return x;
+  if (x < 0.0f) return mtgp_qnan();
+  if (x == 0.0f) return -__builtin_huge_valf();
+  if (!mtgp_isfinite(x)) return x;
+  return mtgp_logf_pos(x);
+}
+
+/* jnp.sqrt: the correctly rounded IEEE square root (x < 0 -> NaN, -0 -> -0) */
+MTGP_INLINE MTGP_HD float mtgp_sqrtf(float x) { return MTGP_SQRTF(x); }
+
+/* jnp.abs: the sign bit cleared */
+MTGP_INLINE MTGP_HD float mtgp_absf(float x) { return mtgp_u2f(mtgp_f2u(x) & 0x7fffffffu); }
+
+/* jnp.tanh (Cephes tanhf): |x| < 0.625: x + x^3 P(x^2) (degree-4 P, fma chain); otherwise
+ * sign(x) * (1 - 2 / (exp(2|x|) + 1)) (exp overflow -> +-1).  NaN -> NaN, -0 -> -0. */
+MTGP_INLINE MTGP_HD float mtgp_tanhf(float x) {
+  if (mtgp_isnan(x)) return x;
+  const float a = MTGP_FABSF(x);
+  if (a >= 0.625f) {
+    const float e = mtgp_expf(a + a);
+    const float t = 1.0f - 2.0f / (e + 1.0f);
+    return x < 0.0f ? -t : t;
+  }
+  if (a == 0.0f) return x; /* +-0 */
+  const float z = x * x;
+  float p = -5.70498872745e-3f;
+  p = MTGP_FMAF(p, z, 2.06390887954e-2f);
+  p = MTGP_FMAF(p, z, -5.37397155531e-2f);
+  p = MTGP_FMAF(p, z, 1.33314422036e-1f);
+  p = MTGP_FMAF(p, z, -3.33332819422e-1f);
+  return MTGP_FMAF(p * z, x, x);
 }
 
 #endif /* MTGP_F32MATH_H */

@@ -93,36 +93,7 @@ MTGP_INLINE MTGP_HD uint32_t mtgp_random_bits_word(uint32_t k0, uint32_t k1, int
   return i < half ? y0 : y1;
 }
 
-/* ---- log1p, fdlibm-style (FreeBSD e_logf.c polynomial), basic operations only ---- */
-/* log(u) for finite u > 0 (u == 1 -> 0). */
-MTGP_INLINE MTGP_HD float mtgp_logf_pos(float u) {
-  uint32_t ix = mtgp_f2u(u);
-  int k = 0;
-  if (ix < 0x00800000u) { /* subnormal: scale by 2^25 (exact) */
-    u = u * 33554432.0f;
-    ix = mtgp_f2u(u);
-    k = -25;
-  }
-  k += (int)(ix >> 23) - 127;
-  ix &= 0x007fffffu;
-  /* normalise m into [sqrt(2)/2, sqrt(2)): i = 0x800000 when the mantissa is >= ~sqrt(2)
-   * (0x800000 - 0x4afb20 = 0x3504e0, sqrt(2) = 0x3fb504f3), then m is halved */
-  const uint32_t i = (ix + 0x4afb20u) & 0x800000u;
-  const float m = mtgp_u2f(ix | (i ^ 0x3f800000u)); /* m or m/2 */
-  k += (int)(i >> 23);
-  const float f = m - 1.0f;
-  const float s = f / (2.0f + f);
-  const float z = s * s;
-  const float w = z * z;
-  const float t1 = w * (0.40000972152f + w * 0.24279078841f);
-  const float t2 = z * (0.66666662693f + w * 0.28498786688f);
-  const float R = t2 + t1;
-  const float hfsq = 0.5f * f * f;
-  const float dk = (float)k;
-  /* ln2 split: hi has 16 trailing zero bits so dk * hi is exact */
-  return dk * 6.9313812256e-01f - ((hfsq - (s * (hfsq + R) + dk * 9.0580006145e-06f)) - f);
-}
-
+/* ---- log1p on mtgp_logf_pos (include/mtgp_f32math.h) ---- */
 /* log1p(a) for a >= -1 (jnp.log1p semantics at the edges: -1 -> -inf, nan -> nan). */
 MTGP_INLINE MTGP_HD float mtgp_log1pf(float a) {
   if (mtgp_isnan(a)) return a;

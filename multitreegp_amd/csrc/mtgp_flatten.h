@@ -67,12 +67,34 @@ MTGP_INLINE MTGP_HD float apply_fn(int fn, float x, float y) {
     case MTGP_FN_DIV: return x / y;
     case MTGP_FN_SIN: return mtgp_sinf(x);
     case MTGP_FN_COS: return mtgp_cosf(x);
+    case MTGP_FN_EXP: return mtgp_expf(x);
+    case MTGP_FN_LOG: return mtgp_logf(x);
+    case MTGP_FN_SQRT: return mtgp_sqrtf(x);
+    case MTGP_FN_TANH: return mtgp_tanhf(x);
+    case MTGP_FN_ABS: return mtgp_absf(x);
     default: return 0.0f;
   }
 }
 
 MTGP_INLINE MTGP_HD int fn_arity(int fn) {
-  return (fn >= MTGP_FN_ADD && fn <= MTGP_FN_DIV) ? 2 : ((fn == MTGP_FN_SIN || fn == MTGP_FN_COS) ? 1 : 0);
+  return (fn >= MTGP_FN_ADD && fn <= MTGP_FN_DIV) ? 2 : (MTGP_FN_IS_UNARY(fn) ? 1 : 0);
+}
+
+// a unary function whose leaf operand fuses into one instruction (SINV / COSV and their push
+// forms); the other unary functions are a load followed by the operation
+MTGP_INLINE MTGP_HD bool unary_fuses(int fn) { return fn == MTGP_FN_SIN || fn == MTGP_FN_COS; }
+
+// program opcode of a unary function (acc = f(acc))
+MTGP_INLINE MTGP_HD uint32_t unary_op(int fn) {
+  switch (fn) {
+    case MTGP_FN_SIN: return MTGP_OP_SIN;
+    case MTGP_FN_COS: return MTGP_OP_COS;
+    case MTGP_FN_EXP: return MTGP_OP_EXP;
+    case MTGP_FN_LOG: return MTGP_OP_LOG;
+    case MTGP_FN_SQRT: return MTGP_OP_SQRT;
+    case MTGP_FN_TANH: return MTGP_OP_TANH;
+    default: return MTGP_OP_ABS;
+  }
 }
 
 // Rows whose value is the constant 0.0 without any lookup: f != 1.0 and int(f) (clamped) an
@@ -355,13 +377,13 @@ MTGP_INLINE MTGP_HD int emit_program(int root, const RowInfo* info, MtgpInstr* o
     if (r.kind == K_UNARY) {
       if (ph == 0 && al) {
         em.load(r.a, info);
-        em.put(r.fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
+        em.put(unary_op(r.fn), 0, 0.0f);
         --top;
       } else if (ph == 0) {
         fr_ph[top] = 1;
         ++top; fr_row[top] = r.a.row; fr_ph[top] = 0;
       } else {
-        em.put(r.fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
+        em.put(unary_op(r.fn), 0, 0.0f);
         --top;
       }
       continue;

@@ -66,17 +66,29 @@ MTGP_INLINE MTGP_HD MtgpInstr u_op_stack(int fn, int rev) {
   return u_instr(fam_op(FK_S, idx), 0, 0.0f);
 }
 
-// packed row record: kind 2 | fn 3 | slot 8 | isconst 1 | afirst 1 | need 5 (bits, low to high)
+// packed row record: kind 2 | fn 4 | slot 8 | isconst 1 | afirst 1 | need 5 (bits, low to high)
 MTGP_INLINE MTGP_HD uint32_t u_pack(uint32_t kind, uint32_t fn, uint32_t slot, uint32_t isc, uint32_t afirst,
                                     uint32_t need) {
-  return kind | fn << 2 | slot << 5 | isc << 13 | afirst << 14 | need << 15;
+  return kind | fn << 2 | slot << 6 | isc << 14 | afirst << 15 | need << 16;
 }
 MTGP_INLINE MTGP_HD uint32_t u_kind(uint32_t w) { return w & 3u; }
-MTGP_INLINE MTGP_HD uint32_t u_fn(uint32_t w) { return (w >> 2) & 7u; }
-MTGP_INLINE MTGP_HD uint32_t u_slot(uint32_t w) { return (w >> 5) & 255u; }
-MTGP_INLINE MTGP_HD bool u_isc(uint32_t w) { return (w >> 13) & 1u; }
-MTGP_INLINE MTGP_HD uint32_t u_afirst(uint32_t w) { return (w >> 14) & 1u; }
-MTGP_INLINE MTGP_HD uint32_t u_need(uint32_t w) { return (w >> 15) & 31u; }
+MTGP_INLINE MTGP_HD uint32_t u_fn(uint32_t w) { return (w >> 2) & 15u; }
+MTGP_INLINE MTGP_HD uint32_t u_slot(uint32_t w) { return (w >> 6) & 255u; }
+MTGP_INLINE MTGP_HD bool u_isc(uint32_t w) { return (w >> 14) & 1u; }
+MTGP_INLINE MTGP_HD uint32_t u_afirst(uint32_t w) { return (w >> 15) & 1u; }
+MTGP_INLINE MTGP_HD uint32_t u_need(uint32_t w) { return (w >> 16) & 31u; }
+
+// a unary node over a leaf: its word(s) at pos (one fused word for sin / cos, else load + op)
+MTGP_INLINE MTGP_HD int u_unary_leaf(int fn, const ULeaf& la, bool push, MtgpInstr* w) {
+  const MtgpInstr un = u_instr(unary_op(fn), 0, 0.0f);
+  if (unary_fuses(fn)) {
+    fuse_pair(u_load(la, push), un, &w[0]);
+    return 1;
+  }
+  w[0] = u_load(la, push);
+  w[1] = un;
+  return 2;
+}
 MTGP_INLINE MTGP_HD bool u_leaf(uint32_t w) { return u_isc(w) || u_kind(w) == K_VAR; }
 
 // per-lane bit set over NMAX rows kept in registers (selects, never a dynamic index)

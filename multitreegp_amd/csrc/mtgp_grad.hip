@@ -38,6 +38,12 @@ __device__ __forceinline__ Dual d_div(Dual a, Dual b) {
 __device__ __forceinline__ Dual d_sin(Dual a) { return {mtgp_sinf(a.v), mtgp_cosf(a.v) * a.d}; }
 __device__ __forceinline__ Dual d_cos(Dual a) { return {mtgp_cosf(a.v), -mtgp_sinf(a.v) * a.d}; }
 
+// the round-3 unary operators: include/mtgp_dual.h's rules (shared with the oracle)
+__device__ __forceinline__ Dual d_unary(int fn, Dual a) {
+  const MtgpDual r = mtgp_dl_unary(fn, mtgp_dl(a.v, a.d));
+  return {r.v, r.d};
+}
+
 // family member: 0 ADD, 1 SUB (acc - o), 2 RSUB (o - acc), 3 MUL, 4 DIV (acc / o), 5 RDIV (o / acc)
 __device__ __forceinline__ Dual d_fam(int f, Dual acc, Dual o) {
   switch (f) {
@@ -128,6 +134,11 @@ __device__ Dual run_dual_src(const MtgpInstr* code, Src V) {
       case MTGP_OP_COSV: acc = d_cos(V(ib)); break;
       case MTGP_OP_SINVP: push(); acc = d_sin(V(ib)); break;
       case MTGP_OP_COSVP: push(); acc = d_cos(V(ib)); break;
+      case MTGP_OP_EXP: acc = d_unary(MTGP_FN_EXP, acc); break;
+      case MTGP_OP_LOG: acc = d_unary(MTGP_FN_LOG, acc); break;
+      case MTGP_OP_SQRT: acc = d_unary(MTGP_FN_SQRT, acc); break;
+      case MTGP_OP_TANH: acc = d_unary(MTGP_FN_TANH, acc); break;
+      case MTGP_OP_ABS: acc = d_unary(MTGP_FN_ABS, acc); break;
       // VC_f: acc = f(v[aux], imm); VCP: push first
       case MTGP_OP_VC_ADD: acc = d_fam(0, V(ax), C); break;
       case MTGP_OP_VC_SUB: acc = d_fam(1, V(ax), C); break;

@@ -2654,7 +2654,7 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
           } else {
             isc = 0;
             if (ar == 1) {
-              if (leafa) { len = 2; flen = 1; }
+              if (leafa) { len = 2; flen = unary_fuses(fn) ? 1 : 2; }
               else { len = lena + 1; flen = flena + 1; need = u_need(wa); }
             } else if (leafa && leafb) {
               len = 2; flen = 1;
@@ -2719,9 +2719,12 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
         };
         MtgpInstr x;
         if (u_kind(w) == K_UNARY) {
-          const MtgpInstr un = u_instr(fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
-          if (leafa) { fuse_pair(u_load(la, push), un, &x); out[pos] = x; }
-          else { visit(ja, pos, push); out[pos + flena] = un; }
+          const MtgpInstr un = u_instr(mtgp::unary_op(fn), 0, 0.0f);
+          if (leafa) {
+            MtgpInstr w2[2];
+            const int nw = u_unary_leaf(fn, la, push, w2);
+            for (int q = 0; q < nw; ++q) out[pos + q] = w2[q];
+          } else { visit(ja, pos, push); out[pos + flena] = un; }
         } else if (leafa && leafb) {
           fuse_pair(u_load(la, push), u_op_leaf(fn, 0, lb), &x);
           out[pos] = x;
@@ -2906,7 +2909,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       } else {
         isc = 0;
         if (ar == 1) {
-          if (leafa) { len = 2; flen = 1; }
+          if (leafa) { len = 2; flen = unary_fuses(fn) ? 1 : 2; }
           else { len = lena + 1; flen = flena + 1; need = u_need(wa); }
         } else if (leafa && leafb) {
           len = 2; flen = 1;
@@ -2999,9 +3002,12 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
             s_prog[at] = v;
           };
           if (u_kind(w) == K_UNARY) {
-            const MtgpInstr un = u_instr(fn == MTGP_FN_SIN ? MTGP_OP_SIN : MTGP_OP_COS, 0, 0.0f);
-            if (leafa) { fuse_pair(u_load(la, push), un, &x); emit(pos, x); }
-            else { visit(ca, pos, push); emit(pos + flena, un); }
+            const MtgpInstr un = u_instr(mtgp::unary_op(fn), 0, 0.0f);
+            if (leafa) {
+              MtgpInstr w2[2];
+              const int nw = u_unary_leaf(fn, la, push, w2);
+              for (int q = 0; q < nw; ++q) emit(pos + q, w2[q]);
+            } else { visit(ca, pos, push); emit(pos + flena, un); }
           } else if (leafa && leafb) {
             fuse_pair(u_load(la, push), u_op_leaf(fn, 0, lb), &x);
             emit(pos, x);

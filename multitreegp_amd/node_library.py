@@ -4,8 +4,10 @@ Opcodes: 0 = empty node, 1 = coefficient, 2 .. 2+K-1 = operators in ``operator_l
 (first occurrence of a name wins), then variables in first-appearance order over
 ``variable_list``.  ``slots`` is the arity per opcode and ``variable_array`` the per-tree mask
 of allowed variables.  Operators are identified by NAME: the kernel implements the fixed set
-``+ - * / sin cos`` with IEEE fp32 semantics; any other name is rejected here,
-at construction, instead of failing inside the evaluator.
+``+ - * / sin cos`` (the reference's notebooks) and, since round 3, ``exp log sqrt tanh abs``
+(jnp semantics in float32, specs in include/mtgp_f32math.h; the program JIT does not translate
+these five, so a population using them runs in the interpreter); any other name is rejected
+here, at construction, instead of failing inside the evaluator.
 """
 from __future__ import annotations
 
@@ -23,6 +25,11 @@ SUPPORTED_OPERATORS = {
     "/": (nat.FN_DIV, 2),
     "sin": (nat.FN_SIN, 1),
     "cos": (nat.FN_COS, 1),
+    "exp": (nat.FN_EXP, 1),
+    "log": (nat.FN_LOG, 1),
+    "sqrt": (nat.FN_SQRT, 1),
+    "tanh": (nat.FN_TANH, 1),
+    "abs": (nat.FN_ABS, 1),
 }
 
 

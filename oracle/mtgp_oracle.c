@@ -35,7 +35,8 @@
 #define OR_MAX_S 64 /* state dims */
 
 /* node-function codes (same numbering as include/mtgp.h MTGP_FN_*) */
-enum { FN_ZERO = 0, FN_VAR = 1, FN_ADD = 2, FN_SUB = 3, FN_MUL = 4, FN_DIV = 5, FN_SIN = 6, FN_COS = 7 };
+enum { FN_ZERO = 0, FN_VAR = 1, FN_ADD = 2, FN_SUB = 3, FN_MUL = 4, FN_DIV = 5, FN_SIN = 6, FN_COS = 7,
+       FN_EXP = 8, FN_LOG = 9, FN_SQRT = 10, FN_TANH = 11, FN_ABS = 12 };
 
 typedef struct {
   int32_t n_funcs, var_start;
@@ -87,6 +88,11 @@ float oracle_eval_tree(const float* tree, int N, int n_funcs, int var_start, con
         case FN_DIV: v = x / y; break;
         case FN_SIN: v = mtgp_sinf(x); break;
         case FN_COS: v = mtgp_cosf(x); break;
+        case FN_EXP: v = mtgp_expf(x); break;
+        case FN_LOG: v = mtgp_logf(x); break;
+        case FN_SQRT: v = mtgp_sqrtf(x); break;
+        case FN_TANH: v = mtgp_tanhf(x); break;
+        case FN_ABS: v = mtgp_absf(x); break;
         default: v = 0.0f; break;
       }
     }
@@ -627,6 +633,14 @@ int oracle_abi_version(void) { return 1; }
 void oracle_sincos(const float* x, float* s, float* c, long n) {
   for (long i = 0; i < n; ++i) { s[i] = mtgp_sinf(x[i]); c[i] = mtgp_cosf(x[i]); }
 }
+/* the unary tree operators by function code (FN_SIN .. FN_ABS) and their tangents (include/mtgp_dual.h) */
+void oracle_unary(int fn, const float* x, const float* dx, float* y, float* dy, long n) {
+  for (long i = 0; i < n; ++i) {
+    const MtgpDual r = mtgp_dl_unary(fn, mtgp_dl(x[i], dx ? dx[i] : 0.0f));
+    y[i] = r.v;
+    if (dy) dy[i] = r.d;
+  }
+}
 void oracle_wrap(const float* x, float* o, long n) {
   for (long i = 0; i < n; ++i) o[i] = mtgp_wrap_angle(x[i]);
 }
@@ -740,6 +754,11 @@ static ODual tree_eval_dual(const float* tree, int N, const OrLib* lib, const OD
         case FN_DIV: v = od_div(x, y); break;
         case FN_SIN: v = od_sin(x); break;
         case FN_COS: v = od_cos(x); break;
+        case FN_EXP: case FN_LOG: case FN_SQRT: case FN_TANH: case FN_ABS: {
+          const MtgpDual r = mtgp_dl_unary(lib->fn[k], mtgp_dl(x.v, x.d));  /* include/mtgp_dual.h */
+          v = od(r.v, r.d);
+          break;
+        }
         default: v = od(0.0f, 0.0f); break;
       }
     }

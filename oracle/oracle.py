@@ -65,6 +65,7 @@ def lib():
         L.oracle_eval.restype = ctypes.c_int
         L.oracle_sincos.argtypes = [vp, vp, vp, ctypes.c_long]
         L.oracle_wrap.argtypes = [vp, vp, ctypes.c_long]
+        L.oracle_unary.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
         L.oracle_acro_drift.argtypes = [vp, vp, ctypes.c_float, vp]
         L.oracle_acro_f_obs.argtypes = [vp, vp]
         L.oracle_expf.argtypes = [vp, vp, ctypes.c_long]
@@ -110,6 +111,20 @@ def sincos(x: np.ndarray):
     s, c = np.empty_like(x), np.empty_like(x)
     lib().oracle_sincos(_p(x), _p(s), _p(c), x.size)
     return s, c
+
+
+def unary(fn: int, x, dx=None):
+    """The unary tree operator `fn` (MTGP_FN_SIN .. MTGP_FN_ABS, include/mtgp_f32math.h specs) on
+    float32 x; with dx also its tangent (include/mtgp_dual.h) -> y or (y, dy)."""
+    x = np.ascontiguousarray(x, np.float32)
+    y = np.empty_like(x)
+    if dx is None:
+        lib().oracle_unary(int(fn), _p(x), None, _p(y), None, x.size)
+        return y
+    dx = np.ascontiguousarray(dx, np.float32)
+    dy = np.empty_like(x)
+    lib().oracle_unary(int(fn), _p(x), _p(dx), _p(y), _p(dy), x.size)
+    return y, dy
 
 
 def wrap(x: np.ndarray):

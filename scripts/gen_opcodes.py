@@ -46,6 +46,11 @@ def ops():
             pre = "POP " if k == "S" else ""
             out.append((f + k, pre + "acc = " + e.format(x="acc", y=src) + ";", k if k != "S" else "-"))
     out += [("SIN", "acc = mtgp_sinf(acc);", "-"), ("COS", "acc = mtgp_cosf(acc);", "-")]
+    # further unary operators (round 3; include/mtgp_f32math.h specs): acc forms only, at the
+    # floor weight (the JIT does not translate them, populations using them are interpreted)
+    out += [("EXP", "acc = mtgp_expf(acc);", "-"), ("LOG", "acc = mtgp_logf(acc);", "-"),
+            ("SQRT", "acc = mtgp_sqrtf(acc);", "-"), ("TANH", "acc = mtgp_tanhf(acc);", "-"),
+            ("ABS", "acc = mtgp_absf(acc);", "-")]
     # superinstructions: a leaf load fused with the leaf operation that follows it
     for p in ("", "P"):
         push = "PUSH " if p else ""

@@ -35,7 +35,9 @@ def eval_tree(tree, lib, data):
                     v = data[min(k - lib.var_start, len(data) - 1)]
                 else:
                     v = {"+": lambda: x + y, "-": lambda: x - y, "*": lambda: x * y, "/": lambda: x / y,
-                         "sin": lambda: np.sin(x), "cos": lambda: np.cos(x)}[name]()
+                         "sin": lambda: np.sin(x), "cos": lambda: np.cos(x), "exp": lambda: np.exp(x),
+                         "log": lambda: np.log(x), "sqrt": lambda: np.sqrt(x), "tanh": lambda: np.tanh(x),
+                         "abs": lambda: np.abs(x)}[name]()
             val[i] = v
     return val[N - 1]
 

@@ -17,6 +17,13 @@ def _cos(x):
     return orc.sincos(np.array([x], np.float32))[1][0]
 
 
+_UNARY = {"EXP": 8, "LOG": 9, "SQRT": 10, "TANH": 11, "ABS": 12}  # MTGP_FN_* of the round-3 operators
+
+
+def _unary(name, x):
+    return orc.unary(_UNARY[name], np.array([x], np.float32))[0]
+
+
 _FAM = {"ADD": lambda x, y: x + y, "SUB": lambda x, y: x - y, "RSUB": lambda x, y: y - x,
         "MUL": lambda x, y: x * y, "DIV": lambda x, y: x / y, "RDIV": lambda x, y: y / x}
 
@@ -38,6 +45,8 @@ def run(prog, data):
                 acc = _sin(acc)
             elif name == "COS":
                 acc = _cos(acc)
+            elif name in _UNARY:
+                acc = _unary(name, acc)
             elif name in ("SINV", "SINVP"):
                 acc = _sin(d[a])
             elif name in ("COSV", "COSVP"):

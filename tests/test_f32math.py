@@ -77,3 +77,59 @@ def test_wrap_angle_bit_exact(lo, hi):
         ref = (_jax_remainder((y + pi).astype(np.float32), b) - pi).astype(np.float32)
     same = (got.view(np.uint32) == ref.view(np.uint32)) | (np.isnan(got) & np.isnan(ref))
     assert same.all(), (y[~same][:5], got[~same][:5], ref[~same][:5])
+
+
+# ---- the round-3 unary tree operators (include/mtgp_f32math.h, MTGP_FN_EXP .. MTGP_FN_ABS) ----
+FN_EXP, FN_LOG, FN_SQRT, FN_TANH, FN_ABS = 8, 9, 10, 11, 12
+
+
+def test_log_within_1ulp_and_edges():
+    rng = np.random.default_rng(5)
+    x = np.concatenate([np.exp(rng.uniform(-87, 88, 600)), rng.uniform(0.5, 2.0, 300),
+                        np.array([1e-40, 1e-45, 3.4e38], np.float64)]).astype(np.float32)
+    x = x[x > 0]
+    assert _ulp_err(x, orc.unary(FN_LOG, x), mpmath.log) <= 1.0
+    e = np.array([0.0, -0.0, -1.0, np.inf, -np.inf, np.nan, 1.0], np.float32)
+    y = orc.unary(FN_LOG, e)
+    assert y[0] == -np.inf and y[1] == -np.inf and np.isnan(y[2]) and y[3] == np.inf and np.isnan(y[4])
+    assert np.isnan(y[5]) and y[6] == 0.0
+
+
+def test_sqrt_and_abs_are_ieee():
+    rng = np.random.default_rng(6)
+    x = np.concatenate([np.exp(rng.uniform(-100, 88, 4000)), np.array([0.0, -0.0, np.inf, 1e-45])]).astype(np.float32)
+    assert np.array_equal(orc.unary(FN_SQRT, x).view(np.uint32), np.sqrt(x).view(np.uint32))  # correctly rounded
+    assert np.isnan(orc.unary(FN_SQRT, np.array([-1.0, -np.inf, np.nan], np.float32))).all()
+    z = (rng.standard_normal(2000) * 10).astype(np.float32)
+    z[:3] = [-0.0, np.inf, -np.inf]
+    assert np.array_equal(orc.unary(FN_ABS, z).view(np.uint32), np.abs(z).view(np.uint32))
+
+
+@pytest.mark.parametrize("lo,hi", [(-0.7, 0.7), (-12, 12), (-60, 60)])
+def test_tanh_within_3ulp(lo, hi):
+    rng = np.random.default_rng(int(hi))
+    x = rng.uniform(lo, hi, 600).astype(np.float32)
+    assert _ulp_err(x, orc.unary(FN_TANH, x), mpmath.tanh) <= 3.0
+    e = orc.unary(FN_TANH, np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e-30], np.float32))
+    assert e.view(np.uint32)[1] == 0x80000000 and e[0] == 0.0 and e[2] == 1.0 and e[3] == -1.0
+    assert np.isnan(e[4]) and e[5] == np.float32(1e-30)
+
+
+def test_exp_through_the_operator_code():
+    x = np.random.default_rng(7).uniform(-80, 80, 2000).astype(np.float32)
+    assert np.array_equal(orc.unary(FN_EXP, x).view(np.uint32), orc.expf(x).view(np.uint32))
+    assert _ulp_err(x[:400], orc.unary(FN_EXP, x[:400]), mpmath.exp) <= 1.0
+
+
+def test_unary_tangents_match_finite_differences():
+    """include/mtgp_dual.h's JVP rules (the coefficient optimiser's forward mode): d/dx f vs a
+    float64 central difference of the float64 function."""
+    x = np.array([0.3, 1.7, 2.5, 0.05, 4.0], np.float32)
+    fns = {FN_EXP: np.exp, FN_LOG: np.log, FN_SQRT: np.sqrt, FN_TANH: np.tanh, FN_ABS: np.abs}
+    for fn, f in fns.items():
+        y, dy = orc.unary(fn, x, np.ones_like(x))
+        xd = x.astype(np.float64)
+        fd = (f(xd + 1e-6) - f(xd - 1e-6)) / 2e-6
+        assert np.allclose(dy, fd, rtol=1e-5, atol=1e-6), (fn, dy, fd)
+    _, d = orc.unary(FN_ABS, np.array([-2.0, 0.0], np.float32), np.array([1.0, 1.0], np.float32))
+    assert d[0] == -1.0 and d[1] == 0.0  # jnp.sign(0) = 0

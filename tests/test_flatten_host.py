@@ -10,16 +10,23 @@ from oracle import oracle as orc
 from helpers import CONTROL_OPS, SR_OPS
 
 
-def _lib():
-    return mt.NodeLibrary(SR_OPS + [("sin", None, 1), ("cos", None, 1)], [["x0", "x1", "x2", "x3"]], [3])
+# the round-3 unary operators (node_library.SUPPORTED_OPERATORS): load + op, no fused forms
+EXT_OPS = [("exp", None, 1, 0.1), ("log", None, 1, 0.1), ("sqrt", None, 1, 0.1), ("tanh", None, 1, 0.1),
+           ("abs", None, 1, 0.1)]
+
+
+def _lib(ext=False):
+    return mt.NodeLibrary(SR_OPS + [("sin", None, 1), ("cos", None, 1)] + (EXT_OPS if ext else []),
+                          [["x0", "x1", "x2", "x3"]], [3])
 
 
 def _same(a, b):
     return a.view(np.uint32) == b.view(np.uint32) or (np.isnan(a) and np.isnan(b))
 
 
-def test_reference_distribution_trees_bit_exact():
-    lib = _lib()
+@pytest.mark.parametrize("ext", [False, True])
+def test_reference_distribution_trees_bit_exact(ext):
+    lib = _lib(ext)
     nl = lib.native()
     pop = sample_population(9, lib, 120, 1, max_init_depth=7, max_nodes=48)[0]
     rng = np.random.default_rng(0)
@@ -32,8 +39,9 @@ def test_reference_distribution_trees_bit_exact():
                 assert _same(progsim.run(prog, d), orc.eval_tree(tree, lib.fn_codes, lib.n_funcs, lib.var_start, d))
 
 
-def test_garbage_arrays_follow_body_fun():
-    lib = _lib()
+@pytest.mark.parametrize("ext", [False, True])
+def test_garbage_arrays_follow_body_fun(ext):
+    lib = _lib(ext)
     nl = lib.native()
     rng = np.random.default_rng(1)
     n = 0
@@ -95,3 +103,34 @@ def test_stack_limit_and_length_errors():
     # the length cap applies to the program as emitted (before fusion)
     with pytest.raises(ValueError, match=str(-nat.ERR_PROG_TOO_LONG)):
         nat.flatten_tree_host(t[:8], nl, 4, L=64)
+
+
+def test_extended_unary_ops_flatten_to_load_and_op():
+    """exp / log / sqrt / tanh / abs over a leaf are two words (no fused forms), over a subtree one;
+    constant subtrees fold with the same fp32 specs; the program JIT declines them (the population
+    is then interpreted)."""
+    from helpers import tree_from_expr
+    lib = _lib(True)
+    nl = lib.native()
+    names = {}
+    for op in ("exp", "log", "sqrt", "tanh", "abs"):
+        prog, _ = nat.flatten_tree_host(tree_from_expr((op, "x1"), lib, 10), nl, 4)
+        names[op] = [p[0] for p in prog]
+        assert names[op] == ["LDV", op.upper()], names[op]
+        prog, _ = nat.flatten_tree_host(tree_from_expr((op, ("+", "x0", "x2")), lib, 10), nl, 4)
+        assert [p[0] for p in prog] == ["VV_ADD", op.upper()]
+        c = np.float32(0.7)
+        prog, _ = nat.flatten_tree_host(tree_from_expr(("*", (op, float(c)), "x3"), lib, 10), nl, 4)
+        want = orc.unary(lib.fn_codes[lib.string_to_node[op]], np.array([c], np.float32))[0]
+        assert len(prog) == 1 and prog[0][0] == "VC_MUL" and np.float32(prog[0][2]).view(np.uint32) == want.view(np.uint32)
+    import ctypes
+    for op in ("exp", "log", "sqrt", "tanh", "abs"):
+        L = 28
+        out = (nat.MtgpInstr * L)()
+        need = ctypes.c_int32(0)
+        t = np.ascontiguousarray(tree_from_expr((op, "x1"), lib, 10), np.float32)
+        n = nat.load().mtgp_flatten_tree_host(t.ctypes.data, 10, ctypes.byref(nl), 4, 0, L, ctypes.addressof(out),
+                                              ctypes.byref(need))
+        assert n == 2
+        for mode in (0, 1):  # register-data and LDS-data translation both decline (kJitErrOpcode)
+            assert nat.load().mtgp_jit_translate_host_ex(ctypes.addressof(out), L, None, 0, mode) == -101

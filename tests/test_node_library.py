@@ -27,7 +27,12 @@ def test_duplicates_and_unknown_operators():
     lib = mt.NodeLibrary([("+", None, 2), ("+", None, 2), ("/", None, 2)], [["x0", "x1"]], [2])
     assert lib.string_to_node == {"+": 2, "/": 3, "x0": 4, "x1": 5}
     with pytest.raises(NotImplementedError):
-        mt.NodeLibrary([("exp", None, 1)], [["x"]], [1])
+        mt.NodeLibrary([("erf", None, 1)], [["x"]], [1])
+    ext = mt.NodeLibrary([("exp", None, 1), ("log", None, 1), ("sqrt", None, 1), ("tanh", None, 1), ("abs", None, 1)],
+                         [["x"]], [1])  # round 3: jnp's exp / log / sqrt / tanh / abs
+    assert list(ext.fn_codes[2:7]) == [nat.FN_EXP, nat.FN_LOG, nat.FN_SQRT, nat.FN_TANH, nat.FN_ABS]
+    with pytest.raises(ValueError):
+        mt.NodeLibrary([("exp", None, 2)], [["x"]], [1])
     with pytest.raises(ValueError):
         mt.NodeLibrary([("sin", None, 2)], [["x"]], [1])
 
