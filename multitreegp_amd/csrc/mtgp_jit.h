@@ -350,6 +350,27 @@ constexpr uint32_t kMovS42 = 0xbeaa00ffu;   // s_mov_b32 s42, literal
 constexpr uint32_t kMovS43 = 0xbeab00ffu;   // s_mov_b32 s43, literal
 constexpr uint32_t kSelLo = 0xd1000008u;    // v_cndmask_b32_e64 v8, v25, v8, s[42:43]
 constexpr uint32_t kSelHi = 0x00aa1119u;
+constexpr uint32_t kLshlS42 = 0x8eaa002au;  // s_lshl_b64 s[42:43], s[42:43], inline constant (| (128 + n) << 8)
+
+// The merge frame of group g > 0: `v_mov v25, v8` before its program, the lane mask of its Rp
+// lanes in s[42:43] and `v_cndmask v8, v25, v8, s[42:43]` after it.  Group 1 sets the mask with
+// two literal moves; group g >= 2 shifts the previous group's mask by Rp (s[42:43] survives the
+// programs: the sin/cos/div templates never write it), 4 words instead of 7 -- at C5 (8 groups per
+// unit) the merges were a quarter of the code and most of the SALU instructions.
+MTGP_JIT_HD inline int jit_merge_words(int g) { return g <= 0 ? 0 : (g == 1 ? 7 : 4); }
+MTGP_JIT_HD inline void jit_merge_tail(JitOut& o, int g, int Rp) {
+  if (g == 1) {
+    const uint64_t mask = ((1ull << Rp) - 1ull) << Rp;  // g > 0 implies Rp < 64
+    o.w(kMovS42);
+    o.w((uint32_t)mask);
+    o.w(kMovS43);
+    o.w((uint32_t)(mask >> 32));
+  } else {
+    o.w(kLshlS42 | (uint32_t)(128 + Rp) << 8);
+  }
+  o.w(kSelLo);
+  o.w(kSelHi);
+}
 
 // ---- role chains (ABI v13, MtgpJitChain) ---------------------------------------------------
 // A role that runs several programs back to back (the state equations of a dynamic policy, the
@@ -476,15 +497,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
       rc = jit_program(o, cur, L, false, mode);
     }
     if (rc < 0) return rc;
-    if (g > 0) {
-      const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);  // g > 0 implies Rp < 64
-      o.w(kMovS42);
-      o.w((uint32_t)mask);
-      o.w(kMovS43);
-      o.w((uint32_t)(mask >> 32));
-      o.w(kSelLo);
-      o.w(kSelHi);
-    }
+    if (g > 0) jit_merge_tail(o, g, Rp);
   }
   jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
@@ -512,15 +525,7 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
     rc = jit_program(o, cur, L, false, mode);
   }
   if (rc < 0) return rc;
-  if (g > 0) {
-    const uint64_t mask = ((1ull << Rp) - 1ull) << (g * Rp);
-    o.w(kMovS42);
-    o.w((uint32_t)mask);
-    o.w(kMovS43);
-    o.w((uint32_t)(mask >> 32));
-    o.w(kSelLo);
-    o.w(kSelHi);
-  }
+  if (g > 0) jit_merge_tail(o, g, Rp);
   if (last) jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
 }

@@ -719,7 +719,7 @@ __device__ __forceinline__ float jit_call(uint64_t addr_, const float d[kDMax], 
                  "{v5}"(d[5]), "{v6}"(d[6]), "{v7}"(d[7])
                : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
                  "v22", "v23", "v24", "v25", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41",
-                 "s42", "s43", "s44", "s45", "vcc", "memory");
+                 "s42", "s43", "s44", "s45", "vcc", "scc", "memory");  // (SCC: the templates' and merges' SALU ops)
   return acc;
 }
 
@@ -1866,7 +1866,7 @@ __device__ __forceinline__ float jit_call_lds(uint64_t addr_, uint32_t lds_addr,
                  "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46", "v47",
                  "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "v57", "v58", "v59", "s30", "s31",
                  "s34", "s35",
-                 "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "memory");
+                 "s36", "s37", "s38", "s39", "s40", "s41", "s42", "s43", "s44", "s45", "vcc", "scc", "memory");
   return acc;
 }
 
@@ -3267,7 +3267,7 @@ __global__ void __launch_bounds__(256) k_jit_emit(JitUnitArgs U, const uint32_t*
 }
 
 // Unit layout from the flatten's per-program code sizes (mtgp_flatten_ex jit_words): unit
-// (wave, j) = its G groups' programs + (G_live - 1) * 7 merge words + s_setpc (mtgp_jit.h
+// (wave, j) = its G groups' programs + the merge words of groups 1.. (mtgp_jit.h jit_merge_words) + s_setpc (mtgp_jit.h
 // jit_unit), 64-byte aligned; a grid sizes the units, one block scans the sizes into byte
 // offsets.  Replaces the k_jit_count translation pass + k_jit_scan.
 __device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const int32_t* __restrict__ jw, int u) {
@@ -3279,7 +3279,7 @@ __device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const i
     const int ind = U.order ? U.order[q] : q;
     const int w = jw[(size_t)ind * U.n_prog + j];
     if (w < 0) return w;
-    n += w + (g > 0 ? 7 : 0);
+    n += w + mtgp::jit_merge_words(g);
   }
   return n;
 }
@@ -3432,7 +3432,7 @@ __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int
   uint32_t start = 0;  // words before group g inside the unit
   for (int h = 0; h < g; ++h) {
     const int ind = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
-    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (h > 0 ? 7u : 0u);
+    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (uint32_t)mtgp::jit_merge_words(h);
   }
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
   if (U.mode == mtgp::kJitModeLds && U.pipe && g > 0) {  // pipelined LDS units: group g's region starts after its preloads
@@ -3472,7 +3472,7 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   uint32_t start = 0;  // words before group g inside the unit
   for (int h = 0; h < g; ++h) {
     const int ind = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
-    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (h > 0 ? 7u : 0u);
+    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (uint32_t)mtgp::jit_merge_words(h);
   }
   const bool last = (g == U.G - 1) || (q + 1 >= U.P);
   const uint32_t at = b + start * 4u;  // byte address of the group's first word
@@ -3518,15 +3518,7 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
     o.base = at;
     if (g > 0) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
     o.n = pre + woff;
-    if (g > 0) {
-      const uint64_t mask = ((1ull << U.Rp) - 1ull) << (g * U.Rp);
-      o.w(mtgp::kMovS42);
-      o.w((uint32_t)mask);
-      o.w(mtgp::kMovS43);
-      o.w((uint32_t)(mask >> 32));
-      o.w(mtgp::kSelLo);
-      o.w(mtgp::kSelHi);
-    }
+    if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp);
     if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);
   }
 }

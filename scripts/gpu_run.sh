@@ -64,6 +64,10 @@ for step in "$@"; do
     dpprof) run dpprof 700 bash scripts/dpprof.sh || exit 1 ;;
     ab_c5_mse) run ab_c5_mse 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,mseall,noprog" --tag c5_mse || exit 1 ;;
     ab_c3_noprog) run ab_c3_noprog 400 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod,noprog" --tag c3_noprog || exit 1 ;;
+    ab_dp_waves) run ab_dp_waves 600 python scripts/kvariants.py --solver dopri5 --rounds 4 --variants "prod,dpw3,dpw4" --tag dp_waves || exit 1 ;;
+    ab_dpn_waves) run ab_dpn_waves 600 python scripts/kvariants.py --solver dopri5 --obs-noise 0.1 --rounds 3 --variants "prod,dpw3,dpw4" --tag dpn_waves || exit 1 ;;
+    ab_c5_merge) run ab_c5_merge 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,premerge" --tag c5_merge || exit 1 ;;
+    ab_c3_merge) run ab_c3_merge 400 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod,premerge" --tag c3_merge || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;

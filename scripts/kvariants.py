@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--no-traj", action="store_true")
     ap.add_argument("--tag", default="")
     ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
+    ap.add_argument("--solver", default="rk4", choices=["rk4", "dopri5"])
+    ap.add_argument("--obs-noise", type=float, default=0.0)
     ap.add_argument("--reflatten", action="store_true", help="flatten inside every timed evaluation (A/B of the "
                                                               "flattener; default: flatten once)")
     ap.add_argument("--order", default="orig", help="orig | pair (long with short) | sorted (host reorder)")
@@ -34,8 +36,8 @@ def main():
     a = ap.parse_args()
     if a.config != "c3" and a.pop == 8192 and a.rollouts == 32:  # the config's own sizes
         a.pop, a.rollouts = {"c2": (1024, 16), "c5": (4096, 8)}[a.config]
-    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config=a.config, solver="rk4",
-                               obs_noise=0.0)
+    bargs = argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps, config=a.config, solver=a.solver,
+                               obs_noise=a.obs_noise)
     env, lib, ff, data, pop = bench.setup_workload(bargs, 0)
     dev = torch.device("cuda", 0)
     engines, envs = {}, {}

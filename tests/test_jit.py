@@ -213,6 +213,11 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
             else:
                 raise AssertionError(hex(w))
             continue
+        if (w & 0xFFFF00FF) == 0x8EAA002A:  # s_lshl_b64 s[42:43], s[42:43], n: the next group's lane mask
+            m64 = ((sel[0] | sel[1] << 32) << (((w >> 8) & 0xFF) - 128)) & 0xFFFFFFFFFFFFFFFF
+            sel = [m64 & 0xFFFFFFFF, m64 >> 32]
+            i += 1
+            continue
         if words[i:i + 2] == [0xD1000008, 0x00AA1119]:  # v_cndmask_b32_e64 v8, v25, v8, s[42:43]
             m64 = sel[0] | sel[1] << 32
             lanes = np.array([bool(m64 >> lane & 1) for lane in range(M)])
