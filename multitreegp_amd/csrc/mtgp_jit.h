@@ -351,24 +351,23 @@ constexpr uint32_t kMovS43 = 0xbeab00ffu;   // s_mov_b32 s43, literal
 constexpr uint32_t kSelLo = 0xd1000008u;    // v_cndmask_b32_e64 v8, v25, v8, s[42:43]
 constexpr uint32_t kSelHi = 0x00aa1119u;
 constexpr uint32_t kLshlS42 = 0x8eaa002au;  // s_lshl_b64 s[42:43], s[42:43], inline constant (| (128 + n) << 8)
+constexpr uint32_t kBfmS42 = 0x91aa0000u;   // s_bfm_b64 s[42:43], width, offset (inline constants)
 
-// The merge frame of group g > 0: `v_mov v25, v8` before its program, the lane mask of its Rp
-// lanes in s[42:43] and `v_cndmask v8, v25, v8, s[42:43]` after it.  Group 1 sets the mask with
-// two literal moves; group g >= 2 shifts the previous group's mask by Rp (s[42:43] survives the
-// programs: the sin/cos/div templates never write it), 4 words instead of 7 -- at C5 (8 groups per
-// unit) the merges were a quarter of the code and most of the SALU instructions.
-MTGP_JIT_HD inline int jit_merge_words(int g) { return g <= 0 ? 0 : (g == 1 ? 7 : 4); }
-MTGP_JIT_HD inline void jit_merge_tail(JitOut& o, int g, int Rp) {
-  if (g == 1) {
-    const uint64_t mask = ((1ull << Rp) - 1ull) << Rp;  // g > 0 implies Rp < 64
-    o.w(kMovS42);
-    o.w((uint32_t)mask);
-    o.w(kMovS43);
-    o.w((uint32_t)(mask >> 32));
-  } else {
-    o.w(kLshlS42 | (uint32_t)(128 + Rp) << 8);
-  }
-  o.w(kSelLo);
+// The merge of the G groups' results of a unit (round 3; was 7 words per group g > 0): the
+// running result lives in v25 -- `v_mov v25, v8` after group 0 (emitted before group 1's program),
+// `v_cndmask v25, v25, v8, s[42:43]` after every later group, except that the LAST group selects
+// into v8 (`v_cndmask v8, v25, v8, s[42:43]`), where the unit's result is expected.  The lane
+// mask of group g's Rp lanes: group 1 forms it with one s_bfm_b64 (Rp ones at bit Rp), group
+// g >= 2 shifts the previous one by Rp (s[42:43] survives the programs: the sin/cos/div templates
+// never write it).  Words per group: 4 for g = 1, 3 for g >= 2 -- at C5 (8 groups per unit) the
+// literal-move merges were a quarter of the code and most of the SALU instructions.
+constexpr uint32_t kSelLoRun = 0xd1000019u;  // v_cndmask_b32_e64 v25, v25, v8, s[42:43] (+ kSelHi)
+MTGP_JIT_HD inline int jit_merge_words(int g) { return g <= 0 ? 0 : (g == 1 ? 4 : 3); }
+MTGP_JIT_HD inline bool jit_merge_keep(int g) { return g == 1; }  // `v_mov v25, v8` before group g's program
+MTGP_JIT_HD inline void jit_merge_tail(JitOut& o, int g, int Rp, bool last) {
+  const uint32_t r = (uint32_t)(128 + Rp);  // inline integer constant Rp (1 .. 32: g > 0 implies Rp < 64)
+  o.w(g == 1 ? (kBfmS42 | r << 8 | r) : (kLshlS42 | r << 8));
+  o.w(last ? kSelLo : kSelLoRun);
   o.w(kSelHi);
 }
 
@@ -472,7 +471,7 @@ MTGP_JIT_HD inline int jit_lds_region(JitOut& o, const MtgpInstr* cur, const Mtg
     const int rc = jit_program(o, next, L, false, kJitModeLds, 1, jit_pre_set(g + 1), 0, &np1);
     if (rc < 0) return rc;
   }
-  if (g > 0) o.movv(kJitKeep, kJitAcc);
+  if (jit_merge_keep(g)) o.movv(kJitKeep, kJitAcc);
   return jit_program(o, cur, L, false, kJitModeLds, 2, jit_pre_set(g), np1);
 }
 
@@ -493,11 +492,11 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
       if (g + 1 < G && q + 1 < P) nxt = prog + ((size_t)(order ? order[q + 1] : q + 1) * n_prog + j) * L;
       rc = jit_lds_region(o, cur, nxt, L, g);
     } else {
-      if (g > 0) o.movv(kJitKeep, kJitAcc);
+      if (jit_merge_keep(g)) o.movv(kJitKeep, kJitAcc);
       rc = jit_program(o, cur, L, false, mode);
     }
     if (rc < 0) return rc;
-    if (g > 0) jit_merge_tail(o, g, Rp);
+    if (g > 0) jit_merge_tail(o, g, Rp, g == G - 1 || q + 1 >= P);
   }
   jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
@@ -521,11 +520,11 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
     if (!last) nxt = prog + ((size_t)(order ? order[q + 1] : q + 1) * n_prog + j) * L;
     rc = jit_lds_region(o, cur, nxt, L, g);
   } else {
-    if (g > 0) o.movv(kJitKeep, kJitAcc);
+    if (jit_merge_keep(g)) o.movv(kJitKeep, kJitAcc);
     rc = jit_program(o, cur, L, false, mode);
   }
   if (rc < 0) return rc;
-  if (g > 0) jit_merge_tail(o, g, Rp);
+  if (g > 0) jit_merge_tail(o, g, Rp, last);
   if (last) jit_unit_end(o, next, cond, j, store, n_prog);
   return o.n;
 }

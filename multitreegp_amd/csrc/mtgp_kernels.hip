@@ -3479,7 +3479,7 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   uint32_t* out = code + at / 4;
   const int ind = U.order ? U.order[q] : q;
   const MtgpInstr* prog = U.prog + ((size_t)ind * U.n_prog + j) * U.L;
-  const int pre = g > 0 ? 1 : 0;  // v_mov v25, v8
+  const int pre = mtgp::jit_merge_keep(g) ? 1 : 0;  // v_mov v25, v8
   MtgpInstr end;
   end.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
   end.imm = 0.0f;
@@ -3516,9 +3516,9 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   if (lane == 0) {
     mtgp::JitOut o{out, 0};
     o.base = at;
-    if (g > 0) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
+    if (mtgp::jit_merge_keep(g)) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
     o.n = pre + woff;
-    if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp);
+    if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp, last);
     if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);
   }
 }

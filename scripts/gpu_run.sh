@@ -68,6 +68,8 @@ for step in "$@"; do
     ab_dpn_waves) run ab_dpn_waves 600 python scripts/kvariants.py --solver dopri5 --obs-noise 0.1 --rounds 3 --variants "prod,dpw3,dpw4" --tag dpn_waves || exit 1 ;;
     ab_c5_merge) run ab_c5_merge 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,premerge" --tag c5_merge || exit 1 ;;
     ab_c3_merge) run ab_c3_merge 400 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod,premerge" --tag c3_merge || exit 1 ;;
+    ab_c5_bfm) run ab_c5_bfm 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,shift" --tag c5_bfm || exit 1 ;;
+    ab_c3_bfm) run ab_c3_bfm 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,shift" --tag c3_bfm || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;

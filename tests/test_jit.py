@@ -213,10 +213,22 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
             else:
                 raise AssertionError(hex(w))
             continue
+        if (w & 0xFFFF0000) == 0x91AA0000:  # s_bfm_b64 s[42:43], width, offset: group 1's lane mask
+            width, off = (w & 0xFF) - 128, ((w >> 8) & 0xFF) - 128
+            m64 = (((1 << width) - 1) << off) & 0xFFFFFFFFFFFFFFFF
+            sel = [m64 & 0xFFFFFFFF, m64 >> 32]
+            i += 1
+            continue
         if (w & 0xFFFF00FF) == 0x8EAA002A:  # s_lshl_b64 s[42:43], s[42:43], n: the next group's lane mask
             m64 = ((sel[0] | sel[1] << 32) << (((w >> 8) & 0xFF) - 128)) & 0xFFFFFFFFFFFFFFFF
             sel = [m64 & 0xFFFFFFFF, m64 >> 32]
             i += 1
+            continue
+        if words[i:i + 2] == [0xD1000019, 0x00AA1119]:  # v_cndmask_b32_e64 v25, v25, v8, s[42:43] (running result)
+            m64 = sel[0] | sel[1] << 32
+            lanes = np.array([bool(m64 >> lane & 1) for lane in range(M)])
+            put(25, np.where(lanes, v[8], v[25]))
+            i += 2
             continue
         if words[i:i + 2] == [0xD1000008, 0x00AA1119]:  # v_cndmask_b32_e64 v8, v25, v8, s[42:43]
             m64 = sel[0] | sel[1] << 32
