@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 16
+#define MTGP_ABI_VERSION 17
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -209,6 +209,14 @@ typedef struct {
    * fitness mean is formed by a second small kernel from MtgpOutputs.rollout_fitness, which is
    * then required. */
   int32_t lanes;
+  /* ABI v17, Acrobot only: the fitness mask `ts / (ts[1] - ts[0]) > first_success` (acrobot.py:82)
+   * as a count table, fit_kof[f] = #{k : f32(ts[k] / (ts[1] - ts[0])) <= (float)f} for f in [0, S)
+   * (the mask keeps a prefix of the save points when the ratio is non-decreasing).  NULL: the ratio
+   * of save k lies in (k - 1, k + 1] for every k (ts starting at 0 on a uniform grid), which the
+   * kernels' one-pass fitness assumes.  Given, the kernels keep the running cost prefix and settle
+   * each rollout at prefix fit_kof[first_success]; MtgpOutputs.fit_hist is then required when some
+   * f in [1, S) has 1 <= fit_kof[f] <= f (the prefix lies behind the first success). */
+  const int32_t* fit_kof;
 } MtgpRollouts;
 
 /* Outputs.  Trajectories are time-major structure-of-arrays so that every save point
@@ -225,6 +233,9 @@ typedef struct {
   /* ABI v16, required when MtgpModel.dp_budget > 0 (scratch, contents undefined afterwards):   */
   float* dp_state;        /* [MTGP_DP_STATE_WORDS, waves * 64] f32, waves = mtgp_eval_waves()   */
   int32_t* dp_pending;    /* [1 + waves] int32                                                  */
+  /* ABI v17 (scratch): [n_save, P*R] f32 running cost prefixes of the general Acrobot mask, or NULL */
+  /* (see MtgpRollouts.fit_kof)                                                                     */
+  float* fit_hist;
 } MtgpOutputs;
 #define MTGP_DP_STATE_WORDS 32
 

@@ -159,6 +159,10 @@ class CoefficientOptimiser:
         B, T, N, _ = cands.shape
         rows = coefficient_rows(cands) if rows is None else rows
         d = eng.prepare_data(data)
+        if d.get("fit_kof") is not None:
+            raise NotImplementedError("coefficient optimisation of Acrobot with ts off the one-pass mask "
+                                      "(ts / (ts[1] - ts[0]) outside (k - 1, k + 1]): the general mask is not "
+                                      "differentiated")
         n_data = eng.ff.n_data()
         specs, _ = eng._specs()
         cap = self.param_cap(n_data)

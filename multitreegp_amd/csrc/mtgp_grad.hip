@@ -610,7 +610,7 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
       model->n_control != 1 || model->n_targets < 0 || model->n_targets > 8 || !ro->params || !ro->x0 || !ro->ts ||
       (model->n_targets > 0 && !ro->targets) || (ro->obs_keys && !ro->obs_w) || ro->R < 1 || ro->R > 64 ||
       model->save_every < 1 || model->n_save < 2 || model->n_steps < 0 || model->prog_readout < 0 ||
-      model->prog_readout >= n_prog)
+      model->prog_readout >= n_prog || ro->fit_kof)  // (the general Acrobot mask is not differentiated)
     return MTGP_ERR_ARG;
   const int na = dyn ? model->state_size : 0;
   const int D = model->n_obs + (dyn ? na + 1 : 0) + model->n_targets;

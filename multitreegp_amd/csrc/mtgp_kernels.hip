@@ -37,7 +37,8 @@
 // (__graft_entry__.build_hip): MTGP_TU=0 holds the C ABI, the Acrobot / SR / JIT / flatten /
 // schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor RK4
 // control kernels, MTGP_TU=3 / 4 / 5 the Dopri5 control kernels of Acrobot / HarmonicOscillator /
-// StirredTankReactor, behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
+// StirredTankReactor, MTGP_TU=6 the Acrobot kernels of the general cost mask (EnvAcrobotMask),
+// behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
 #ifndef MTGP_TU
 #define MTGP_TU_MAIN 1
 #define MTGP_TU_HARMONIC 1
@@ -45,6 +46,7 @@
 #define MTGP_TU_ACRO_DOPRI5 1
 #define MTGP_TU_HARMONIC_DOPRI5 1
 #define MTGP_TU_REACTOR_DOPRI5 1
+#define MTGP_TU_ACRO_MASK 1
 #else
 #define MTGP_TU_MAIN (MTGP_TU == 0)
 #define MTGP_TU_HARMONIC (MTGP_TU == 1)
@@ -52,6 +54,7 @@
 #define MTGP_TU_ACRO_DOPRI5 (MTGP_TU == 3)
 #define MTGP_TU_HARMONIC_DOPRI5 (MTGP_TU == 4)
 #define MTGP_TU_REACTOR_DOPRI5 (MTGP_TU == 5)
+#define MTGP_TU_ACRO_MASK (MTGP_TU == 6)
 #endif
 
 namespace {
@@ -358,6 +361,47 @@ __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool i
   }
 }
 
+// The general mask (MtgpRollouts.fit_kof given: ts / (ts[1] - ts[0]) is not within one of the save
+// index, e.g. ts starting at t > 0): the cost sum is the prefix of the first kof[first_success]
+// costs (acrobot.py:82 keeps ratio <= first_success, a prefix of the non-decreasing ratio) summed
+// left to right, the masked zeros adding nothing.  Per lane: csum = running prefix (hist row k when
+// the prefix can lie behind the first success), c0incl = the prefix kof[0] (first_success 0: never
+// reached, or reached at save 0), F = first success + 1 as int bits until settled (0 = none yet).
+// The +inf fill after a termination never reaches (cos(inf) is NaN) but its costs (the policy on
+// the fill) still count when the prefix runs past it; the last save point settles every lane.
+__device__ __forceinline__ void acro_fit_general(AcroFit& f, int k, int S, const int32_t* __restrict__ kof,
+                                                 float* hist, size_t PR, int loff, bool dead, float u,
+                                                 float x0, float x1) {
+  if (f.settled) return;
+  const float P = f.csum + (u * 0.01f) * u;  // save 0: 0 + cost = cost
+  f.csum = P;
+  if (hist) hist[(size_t)k * PR + loff] = P;  // read back by this lane only (below)
+  if (k + 1 == kof[0]) f.c0incl = P;
+  int fs1 = __float_as_int(f.F);
+  if (fs1 == 0) {
+    bool reached = false;
+    if (!dead) {
+      const float x01 = x0 + x1;
+      reached = ((-mtgp_cosf(x0)) - mtgp_cosf(x01)) > 1.5f;
+    }
+    fs1 = reached ? k + 1 : ((dead || k == S - 1) ? 1 : 0);  // argmax of all-false = 0
+  }
+  if (fs1 == 0) return;
+  const int fs = fs1 - 1, K = kof[fs];
+  if (K > k + 1) {  // the prefix runs on past this save point
+    f.F = __int_as_float(fs1);
+    return;
+  }
+  float v = 0.0f;
+  if (K > 0) {
+    if (fs == 0) v = f.c0incl;
+    else if (K == k + 1) v = P;
+    else v = __hip_atomic_load(hist + (size_t)(K - 1) * PR + loff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  f.settled = true;
+  f.F = (float)(fs + (fs == 0) * S) + v;
+}
+
 __device__ __forceinline__ bool save_incl(const float* ts, int k) {
   const float dts = ts[1] - ts[0];
   return !((ts[k] / dts) > (float)k);
@@ -379,6 +423,7 @@ __device__ __forceinline__ bool save_incl(const float* ts, int k) {
 // Acrobot (acrobot.py:7-87)
 struct EnvAcrobot {
   static constexpr int NV = 4;
+  static constexpr bool kMask = false;  // the one-pass fitness (MtgpRollouts.fit_kof NULL)
   // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
   // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
   float l1, l2, m1, m2;
@@ -402,10 +447,24 @@ struct EnvAcrobot {
   __device__ __forceinline__ void fit_update(Fit& f, int k, int S, const float* ts, float u, const float x[4]) const {
     acro_fit_update(f, k, S, save_incl(ts, k), u, x[0], x[1]);
   }
+
   __device__ __forceinline__ static void fit_kill(Fit& f) { (void)f; }  // fs/cost mask ignore the fill
   __device__ __forceinline__ static float fit_final(Fit& f, int S) {
     if (!f.settled) { f.settled = true; f.F = (float)S + f.c0incl; }
     return f.F;
+  }
+};
+
+// Acrobot with the general cost mask (MtgpRollouts.fit_kof): kernels of its own (translation unit
+// 6, trajectory variants only: no early exit on settled lanes), so that the one-pass kernels keep
+// their registers -- a run-time switch inside them held the mask's pointers live through the loop
+// and cost the C3 kernel 1.3 % more VALU (SGPR spills) and 1.1 % time.
+struct EnvAcrobotMask : EnvAcrobot {
+  static constexpr bool kMask = true;
+  // one save point (dead: a point of the +inf fill)
+  __device__ __forceinline__ void fit_save(Fit& f, int k, int S, const KArgs& A, size_t PR, int loff, bool dead,
+                                           float u, const float x[4]) const {
+    acro_fit_general(f, k, S, A.ro.fit_kof, A.out.fit_hist, PR, loff, dead, u, x[0], x[1]);
   }
 };
 
@@ -441,6 +500,7 @@ struct QuadFit {
 // u_d = -pinv(b) A x_d with pinv(b) = [[0, 1]] exactly, Q = [[0.5, 0], [0, 0]], R = [[0.5]].
 struct EnvHarmonic {
   static constexpr int NV = 2;
+  static constexpr bool kMask = false;
   float a10, a11, tg, ud;
   typedef QuadFit Fit;
   __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
@@ -474,6 +534,7 @@ struct EnvHarmonic {
 // Cost: x_d = [0, target, 0], Q = diag(0, 0.01, 0) (full 3x3), r = [[1e-4]].
 struct EnvReactor {
   static constexpr int NV = 3;
+  static constexpr bool kMask = false;
   float qV, Tf, mdHrCp, UAVCp, Volc, Tcf, UAVcCp, tg;
   typedef QuadFit Fit;
   __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
@@ -1117,7 +1178,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               us = (Ln.g == gi) ? t : us;
             }
           }
-          if (!dead) env.fit_update(fit, k, S, A.ro.ts, us, x);
+          if constexpr (Env::kMask) {
+            if (active) env.fit_save(fit, k, S, A, PR, loff, dead, us, x);
+          } else if (!dead) {
+            env.fit_update(fit, k, S, A.ro.ts, us, x);
+          }
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
@@ -1245,7 +1310,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
               u = ur[0];
             }
           }
-          if (!dead) env.fit_update(fit, k, S, A.ro.ts, u, x);
+          if constexpr (Env::kMask) {
+            if (active) env.fit_save(fit, k, S, A, PR, loff, dead, u, x);
+          } else if (!dead) {
+            env.fit_update(fit, k, S, A.ro.ts, u, x);
+          }
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
@@ -1476,7 +1545,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
       run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // policy([y, tar]) ff.py:97
     }
     if (!on) return;
-    if (!fill) env.fit_update(fit, k, S, ts, ur[0], sk);
+    if constexpr (Env::kMask) env.fit_save(fit, k, S, A, PR, loff, fill, ur[0], sk);
+    else if (!fill) env.fit_update(fit, k, S, ts, ur[0], sk);
     if (TRAJ && active) {
       if (A.out.xs) {
 #pragma unroll
@@ -1597,7 +1667,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   // unsaved points are +inf (throw=False); their fitness terms follow Env::fit_kill
   bool fl = active && k < S;
   if (fl && !fit.settled) Env::fit_kill(fit);  // (settled: the fitness is already final)
-  if (TRAJ) {
+  if (TRAJ) {  // (EnvAcrobotMask: trajectory variants only -- the general mask counts the fill's costs)
     float sk[ND];
 #pragma unroll
     for (int i = 0; i < ND; ++i) sk[i] = kInf;
@@ -3678,23 +3748,30 @@ int launch_timed(F&& launch, hipStream_t s) {
 
 }  // namespace
 
-// the eight (TRAJ, NOISE, JIT) variants of one control kernel
+// the eight (TRAJ, NOISE, JIT) variants of one control kernel; an Env with kMask (EnvAcrobotMask)
+// has the four TRAJ variants only (the caller passes traj = true)
+template <class E, int... N>
+constexpr bool kTrajOnly = E::kMask;
 #define MTGP_CTL_VARIANTS(KERNEL, ...)                                                                   \
   do {                                                                                                  \
     if (jit) {                                                                                          \
       if (noise) {                                                                                      \
         if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, true>), grid, block, 0, s, A);    \
-        else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, true>), grid, block, 0, s, A);        \
+        else if constexpr (!kTrajOnly<__VA_ARGS__>)                                                     \
+          hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, true>), grid, block, 0, s, A);           \
       } else {                                                                                          \
         if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, true>), grid, block, 0, s, A);   \
-        else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, true>), grid, block, 0, s, A);       \
+        else if constexpr (!kTrajOnly<__VA_ARGS__>)                                                     \
+          hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, true>), grid, block, 0, s, A);          \
       }                                                                                                 \
     } else if (noise) {                                                                                 \
       if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true, false>), grid, block, 0, s, A);     \
-      else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, false>), grid, block, 0, s, A);         \
+      else if constexpr (!kTrajOnly<__VA_ARGS__>)                                                       \
+        hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true, false>), grid, block, 0, s, A);            \
     } else {                                                                                            \
       if (traj) hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false, false>), grid, block, 0, s, A);    \
-      else hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, false>), grid, block, 0, s, A);        \
+      else if constexpr (!kTrajOnly<__VA_ARGS__>)                                                       \
+        hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false, false>), grid, block, 0, s, A);           \
     }                                                                                                   \
   } while (0)
 
@@ -3705,9 +3782,12 @@ int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 
     return launch_timed([&] {
       if (noise) {
         if (traj) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, true, false>), grid, block, 0, s, A);
-        else hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, true, false>), grid, block, 0, s, A);
-      } else if (traj) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, false, false>), grid, block, 0, s, A);
-      else hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, false, false>), grid, block, 0, s, A);
+        else if constexpr (!Env::kMask) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, true, false>), grid, block, 0, s, A);
+      } else if (traj) {
+        hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, false, false>), grid, block, 0, s, A);
+      } else if constexpr (!Env::kMask) {
+        hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, false, false>), grid, block, 0, s, A);
+      }
     }, s);
   } else {
     return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
@@ -3734,7 +3814,8 @@ __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic_dopri5(MTGP_TU
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor_dopri5(MTGP_TU_DP_ARGS);
 template <class Env>
 int launch_dp_entry(MTGP_TU_DP_ARGS) {
-  if constexpr (std::is_same<Env, EnvAcrobot>::value) return mtgp_tu_launch_acrobot_dopri5(A, model, jit, noise, traj, grid, block, s);
+  if constexpr (Env::kMask) return launch_ctl_dp<Env>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
+  else if constexpr (std::is_same<Env, EnvAcrobot>::value) return mtgp_tu_launch_acrobot_dopri5(A, model, jit, noise, traj, grid, block, s);
   else if constexpr (std::is_same<Env, EnvHarmonic>::value) return mtgp_tu_launch_harmonic_dopri5(A, model, jit, noise, traj, grid, block, s);
   else return mtgp_tu_launch_reactor_dopri5(A, model, jit, noise, traj, grid, block, s);
 }
@@ -3793,6 +3874,13 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
       unsigned grid, unsigned block, hipStream_t s
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS);
+#if MTGP_TU_ACRO_MASK
+int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS) {  // every solver; the trajectory variants (traj unused)
+  (void)traj;
+  return launch_ctl<EnvAcrobotMask>(*(const KArgs*)A, model, ro, jit, noise, true, dim3(grid), dim3(block), s);
+}
+#endif
 #if MTGP_TU_ACRO_DOPRI5
 int mtgp_tu_launch_acrobot_dopri5(MTGP_TU_DP_ARGS) {
   return launch_ctl_dp<EnvAcrobot>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
@@ -4218,6 +4306,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
   }
   if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;
+  if (rollouts->fit_kof && (model->model == MTGP_MODEL_SR || model->env != MTGP_ENV_ACROBOT)) return MTGP_ERR_ARG;
   if (P == 0) return MTGP_OK;
   KArgs A;
   A.m = *model;
@@ -4270,7 +4359,10 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   const int rc = [&]() -> int {
   if (model->model == MTGP_MODEL_DYNAMIC || model->model == MTGP_MODEL_STATIC) {
     switch (model->env) {
-      case MTGP_ENV_ACROBOT: return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
+      case MTGP_ENV_ACROBOT:
+        if (rollouts->fit_kof)  // the general cost mask: its own kernels (EnvAcrobotMask, TU 6)
+          return launch_tu([&] { return mtgp_tu_launch_acrobot_mask(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
+        return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
       case MTGP_ENV_HARMONIC_OSCILLATOR:
         return launch_tu([&] { return mtgp_tu_launch_harmonic(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
       case MTGP_ENV_STIRRED_TANK_REACTOR:

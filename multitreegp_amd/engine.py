@@ -242,7 +242,7 @@ class DeviceEngine:
             return self._data
         host = self.ff.prepare(data)
         dev = {}
-        for name in ("x0", "params", "targets", "ts", "ys_true", "obs_keys", "obs_w"):
+        for name in ("x0", "params", "targets", "ts", "ys_true", "obs_keys", "obs_w", "fit_kof"):
             a = host.get(name)
             a = None if a is None else np.asarray(a)
             dev[name] = None if a is None or a.size == 0 else torch.from_numpy(np.ascontiguousarray(a)).to(self.device)
@@ -411,6 +411,7 @@ class DeviceEngine:
         ro.ts, ro.ys_true, ro.R = _ptr(d["ts_dev"]), _ptr(d["ys_true_dev"]), d["R"]
         ro.obs_keys, ro.obs_w = _ptr(d.get("obs_keys_dev")), _ptr(d.get("obs_w_dev"))
         ro.lanes = self.lane_set(P, d["R"]) if P is not None else 0
+        ro.fit_kof = _ptr(d.get("fit_kof_dev"))
         return ro
 
     def _simds(self) -> int:
@@ -479,6 +480,9 @@ class DeviceEngine:
                                  torch.empty((1 + waves,), dtype=torch.int32, device=dev))
             m.dp_budget = budget
             out.dp_state, out.dp_pending = self._dp_bufs[0].data_ptr(), self._dp_bufs[1].data_ptr()
+        if d.get("fit_need_hist"):  # the general Acrobot mask's cost prefixes (mtgp.h fit_hist)
+            res["_fit_hist"] = torch.empty((S * P * R,), dtype=torch.float32, device=dev)
+            out.fit_hist = res["_fit_hist"].data_ptr()
         if trajectories:
             PR = P * R
             if self.ff.model_id == nat.MODEL_SR:

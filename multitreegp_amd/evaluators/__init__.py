@@ -15,7 +15,7 @@ evaluators (every environment) and for ``SREvaluator``.
 """
 from __future__ import annotations
 
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 
@@ -124,11 +124,8 @@ def _solver_fields(kind: str, controller, max_steps: int) -> dict:
                 dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0, **controller.model_fields())
 
 
-def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool = True) -> Tuple[int, int, int]:
-    """Map (ts, dt0) to (n_steps, save_every, n_save) for save points on step ends.
-
-    With acrobot_mask, also checks the Acrobot fitness-mask regularity ts[k]/(ts[1]-ts[0]) in
-    (k-1, k+1] that the kernel's one-pass fitness relies on (acrobot.py:82)."""
+def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
+    """Map (ts, dt0) to (n_steps, save_every, n_save) for save points on step ends."""
     ts = np.asarray(ts, dtype=np.float32)
     S = int(ts.shape[0])
     if S < 2:
@@ -140,30 +137,43 @@ def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int, acrobot_mask: bool 
     expect = np.float64(ts[0]) + np.arange(S) * dts
     if np.max(np.abs(ts.astype(np.float64) - expect)) > 1e-4 * max(abs(float(ts[-1])), 1.0):
         raise ValueError("ts must be uniformly spaced (fixed-step RK4 saves on step ends)")
-    ratio = ts / np.float32(ts[1] - ts[0])
-    k = np.arange(S, dtype=np.float32)
-    if acrobot_mask and not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
-        raise NotImplementedError("ts with an offset start (ts[0] != 0 style masks) is not supported")
     n_steps = (S - 1) * save_every
     if n_steps > max_steps:
         raise ValueError(f"{n_steps} RK4 steps exceed max_steps={max_steps}")
     return n_steps, save_every, S
 
 
-def adaptive_schedule(ts: np.ndarray, acrobot_mask: bool = False) -> Tuple[int, int, int]:
-    """Dopri5: save points straight from ts (SaveAt(ts)), any non-decreasing grid; with
-    acrobot_mask the one-pass Acrobot fitness needs ts[k]/(ts[1]-ts[0]) in (k-1, k+1] as for RK4.
+def adaptive_schedule(ts: np.ndarray) -> Tuple[int, int, int]:
+    """Dopri5: save points straight from ts (SaveAt(ts)), any non-decreasing grid.
     -> (n_steps 0, save_every 1, n_save)."""
     ts = np.asarray(ts, dtype=np.float32)
     S = int(ts.shape[0])
     if S < 2 or np.any(np.diff(ts) < 0):
         raise ValueError("ts needs at least two non-decreasing save points")
-    if acrobot_mask:
-        ratio = ts / np.float32(ts[1] - ts[0])
-        k = np.arange(S, dtype=np.float32)
-        if not (np.all(ratio > k - 1) and np.all(ratio <= k + 1)):
-            raise NotImplementedError("ts with an offset start (ts[0] != 0 style masks) is not supported")
     return 0, 1, S
+
+
+def acrobot_mask(ts: np.ndarray) -> Optional[Tuple[np.ndarray, bool]]:
+    """The Acrobot cost mask `ts / (ts[1] - ts[0]) > first_success` (acrobot.py:82) as the count
+    table MtgpRollouts.fit_kof: kof[f] = #{k : f32(ts[k] / (ts[1] - ts[0])) <= f32(f)} -- the mask
+    keeps the first kof[first_success] costs when the ratio is non-decreasing.  None when the ratio
+    of save k lies in (k - 1, k + 1] for every k (ts from 0 on a uniform grid: the kernels' one-pass
+    fitness).  -> (kof int32 [S], need_hist: some f >= 1 has 1 <= kof[f] <= f, so the kernels keep
+    the per-save cost prefixes in MtgpOutputs.fit_hist)."""
+    ts = np.asarray(ts, dtype=np.float32)
+    S = int(ts.shape[0])
+    with np.errstate(divide="ignore", invalid="ignore"):
+        ratio = ts / np.float32(ts[1] - ts[0])
+    k = np.arange(S, dtype=np.float32)
+    if np.all(ratio > k - 1) and np.all(ratio <= k + 1):
+        return None
+    if np.any(np.isnan(ratio)) or np.any(np.diff(ratio) < 0):
+        raise NotImplementedError("Acrobot fitness mask: ts / (ts[1] - ts[0]) must be non-decreasing "
+                                  "(the mask is then a prefix of the save points)")
+    kof = np.searchsorted(ratio, np.arange(S, dtype=np.float32), side="right").astype(np.int32)
+    f = np.arange(S)
+    need_hist = bool(np.any((f >= 1) & (kof >= 1) & (kof <= f)))
+    return kof, need_hist
 
 
 def _f32(a) -> np.ndarray:
@@ -285,14 +295,16 @@ class _ControlEvaluator(_CandidateAPI):
         tg = _f32(targets).reshape(R, -1)
         if tg.shape[1] != self.env.n_targets:
             raise ValueError(f"targets must be [R, {self.env.n_targets}]")
-        acro = self.env_id == nat.ENV_ACROBOT
         if self.solver_kind == "dopri5":
-            n_steps, save_every, S = adaptive_schedule(ts, acrobot_mask=acro)
+            n_steps, save_every, S = adaptive_schedule(ts)
         else:
-            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps, acrobot_mask=acro)
+            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+        mask = acrobot_mask(ts) if self.env_id == nat.ENV_ACROBOT else None
         out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R, n_var=nv, env=self.env_id,
                    n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code(),
                    **_solver_fields(self.solver_kind, self.stepsize_controller, self.max_steps))
+        if mask is not None:  # ts off the one-pass mask: the general prefix form (mtgp.h fit_kof)
+            out["fit_kof"], out["fit_need_hist"] = mask
         obs_noise = float(getattr(self.env, "obs_noise", 0.0))
         if obs_noise != 0.0:
             keys = np.ascontiguousarray(np.asarray(obs_keys), dtype=np.uint32)
@@ -408,4 +420,4 @@ class SREvaluator(_CandidateAPI):
 
 
 __all__ = ["RK4", "Euler", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
-           "rk4_schedule", "adaptive_schedule"]
+           "rk4_schedule", "adaptive_schedule", "acrobot_mask"]

@@ -50,8 +50,37 @@ def test_schedule_errors():
         rk4_schedule(np.array([0.0, 0.1, 0.3], np.float32), 0.05, 100)  # non-uniform
     with pytest.raises(ValueError):
         rk4_schedule(np.arange(0, 10, 0.1, dtype=np.float32), 0.05, 10)  # max_steps
+    assert rk4_schedule(np.array([5.0, 5.1, 5.2], np.float32), 0.05, 100) == (4, 2, 3)  # offset start
+
+
+@pytest.mark.parametrize("t0,dt,S", [(0.0, 0.2, 250), (5.0, 0.1, 40), (0.05, 0.1, 30), (-0.35, 0.05, 50),
+                                     (-3.0, 0.2, 12), (100.0, 0.5, 20)])
+def test_acrobot_mask_table(t0, dt, S):
+    """acrobot_mask restates `ts / (ts[1] - ts[0]) > first_success` (acrobot.py:82): for every
+    first_success f the kept costs are exactly the first kof[f] save points."""
+    from multitreegp_amd.evaluators import acrobot_mask
+    ts = (np.float32(t0) + np.arange(S, dtype=np.float32) * np.float32(dt)).astype(np.float32)
+    r = acrobot_mask(ts)
+    ratio = ts / np.float32(ts[1] - ts[0])
+    k = np.arange(S, dtype=np.float32)
+    if np.all(ratio > k - 1) and np.all(ratio <= k + 1):  # ts[0] = 0, or an offset below one spacing
+        assert r is None and abs(t0 / dt) < 1  # the kernels' one-pass form
+        return
+    kof, need_hist = r
+    assert kof.dtype == np.int32 and kof.shape == (S,)
+    for f in range(S):
+        keep = ~(ratio > np.float32(f))
+        assert np.all(keep[:kof[f]]) and not np.any(keep[kof[f]:])
+    assert need_hist == any(1 <= kof[f] <= f for f in range(1, S))
+    assert need_hist == (t0 > 0 and t0 / dt < S - 1)  # a positive offset puts the prefix behind fs
+    assert t0 / dt >= 1 or t0 / dt <= -1
+
+
+def test_acrobot_mask_rejects_non_monotone_ratio():
+    from multitreegp_amd.evaluators import acrobot_mask
     with pytest.raises(NotImplementedError):
-        rk4_schedule(np.array([5.0, 5.1, 5.2], np.float32), 0.05, 100)  # offset start breaks the mask
+        acrobot_mask(np.array([0.0, 0.0, 0.1], np.float32))  # 0 / 0
+    assert acrobot_mask(np.array([0.0, 0.1, 0.2], np.float32)) is None
 
 
 def test_program_specs_dynamic():

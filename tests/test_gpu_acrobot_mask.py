@@ -1,0 +1,78 @@
+"""Acrobot fitness mask with ts off the one-pass form (acrobot.py:82): `ts / (ts[1] - ts[0]) >
+first_success` for a grid that does not start at 0 -- positive offsets (the kept cost prefix lies
+behind the first success: MtgpOutputs.fit_hist), fractional offsets, negative offsets (the prefix
+runs past the first success, into the +inf fill of terminated rollouts).  RK4, Euler and Dopri5,
+dynamic and static policies, fitness and trajectories bit-identical to the oracle; fitness-only
+launches (early exit, Dopri5 fill rounds) equal to trajectory launches."""
+import numpy as np
+import pytest
+import torch
+
+from multitreegp_amd.engine import DeviceEngine, to_reference_layout
+from multitreegp_amd.evaluators import acrobot_mask
+from oracle import oracle as orc
+from helpers import bits_equal, dynamic_setup, mismatch_report, oracle_model, oracle_rollouts, static_setup
+
+pytestmark = pytest.mark.gpu
+
+
+def _swing_data(data, t0, seed):
+    """The setup's data with ts shifted by t0 and initial states spread over all angles and fast
+    spins, so that rollouts reach the goal at save 0, later or never, and some terminate."""
+    x0, ts, *rest = data
+    R = x0.shape[0]
+    rng = np.random.default_rng(seed)
+    x0 = np.concatenate([rng.uniform(-np.pi, np.pi, (R, 2)), rng.uniform(-6.0, 6.0, (R, 2))], 1).astype(np.float32)
+    ts = (np.asarray(ts, np.float32) + np.float32(t0)).astype(np.float32)
+    return (x0, ts, *rest)
+
+
+def _first_success(xs):
+    """argmax of the reached flags per rollout (acrobot.py:78-79) from oracle trajectories [P, R, S, 4]."""
+    t1, t2 = xs[..., 0].astype(np.float64), xs[..., 1].astype(np.float64)
+    with np.errstate(invalid="ignore"):
+        reached = (-np.cos(t1) - np.cos(t1 + t2)) > 1.5
+    return np.where(reached.any(-1), reached.argmax(-1), -1)
+
+
+def _run(ff, lib, data, pop, traj):
+    eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
+    res = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=traj,
+                       rollout_fitness=True)
+    torch.cuda.synchronize()
+    return eng, {k: v for k, v in res.items() if isinstance(v, torch.Tensor)}
+
+
+# (policy, solver, ts[0]) on ts = ts[0] + 0.05 k, k < 61: ratio = k + ts[0] / 0.05; 5.0 masks every cost
+CASES = [("dynamic", "rk4", 1.0), ("dynamic", "rk4", 0.07), ("dynamic", "rk4", -0.35), ("static", "rk4", 2.5),
+         ("static", "rk4", 5.0), ("static", "euler", -1.0), ("dynamic", "dopri5", 1.5), ("dynamic", "dopri5", -0.4),
+         ("static", "dopri5", 0.3)]
+
+
+@pytest.mark.parametrize("kind,solver,t0", CASES)
+def test_acrobot_offset_ts_bitexact(kind, solver, t0):
+    sol = (1e-5, 1e-5, 0.002, 800) if solver == "dopri5" else None
+    setup = dynamic_setup if kind == "dynamic" else static_setup
+    env, lib, ff, data, pop = setup(P=48, R=16, n_steps=60, seed=11, solver=sol)
+    if solver == "euler":
+        import multitreegp_amd as mt
+        ff = mt.FeedforwardEvaluator(env, 0.05, solver=mt.Euler())
+    data = _swing_data(data, t0, seed=int(abs(t0) * 100) + 3)
+    mask = acrobot_mask(data[1])
+    assert mask is not None and mask[1] == (0 < t0 / 0.05 < 60)  # the general form; fit_hist for positive offsets
+    eng, res = _run(ff, lib, data, pop, True)
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    P, R = pop.shape[0], d["R"]
+    for k in ("fitness", "rollout_fitness"):
+        got = res[k].cpu().numpy()
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+    names = ["xs", "ys", "us"] + (["acts"] if kind == "dynamic" else [])
+    for k in names:
+        got = to_reference_layout(res[k], P, R)
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+    fs = _first_success(ref["xs"])
+    assert (fs > 0).sum() >= 8 and (fs == -1).sum() >= 8  # later successes and none both exercised
+    _, res_f = _run(ff, lib, data, pop, False)  # fitness-only launch
+    for k in ("fitness", "rollout_fitness"):
+        assert bits_equal(res_f[k].cpu().numpy(), res[k].cpu().numpy()), k
