@@ -76,3 +76,31 @@ def test_acrobot_offset_ts_bitexact(kind, solver, t0):
     _, res_f = _run(ff, lib, data, pop, False)  # fitness-only launch
     for k in ("fitness", "rollout_fitness"):
         assert bits_equal(res_f[k].cpu().numpy(), res[k].cpu().numpy()), k
+
+
+# the other kernel shapes of the mask's translation unit: the run-time state-size interpreter
+# kernel, an individual over several waves (R > 64) and observation noise keyed on the offset times
+SHAPES = [dict(state_size=5, R=16, obs_noise=0.0, t0=1.0), dict(state_size=2, R=100, obs_noise=0.0, t0=-0.5),
+          dict(state_size=2, R=16, obs_noise=0.1, t0=0.65), dict(state_size=1, R=16, obs_noise=0.1, t0=-0.2, dopri5=True)]
+
+
+@pytest.mark.parametrize("case", SHAPES, ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_acrobot_offset_ts_kernel_shapes(case):
+    sol = (1e-5, 1e-5, 0.002, 800) if case.get("dopri5") else None
+    env, lib, ff, data, pop = dynamic_setup(P=24, R=case["R"], n_steps=60, seed=17, state_size=case["state_size"],
+                                            obs_noise=case["obs_noise"], solver=sol)
+    t0 = case["t0"]
+    data = _swing_data(data, t0, seed=29)
+    assert acrobot_mask(data[1]) is not None
+    eng, res = _run(ff, lib, data, pop, True)
+    d = eng.prepare_data(data)
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d), trajectories=True)
+    P, R = pop.shape[0], d["R"]
+    for k in ("fitness", "rollout_fitness"):
+        got = res[k].cpu().numpy()
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+    for k in ("xs", "us", "acts"):
+        got = to_reference_layout(res[k], P, R)
+        assert bits_equal(got, ref[k]), mismatch_report(got, ref[k], k)
+    fs = _first_success(ref["xs"])
+    assert (fs > 0).sum() >= 4
