@@ -407,8 +407,10 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
  * theta[P, K]: parameter values; nparam[P] (<= K): parameters in use per individual.
  * scratch: device float [P, K, R, 2].  loss_out[P]: the evaluator's fitness without parsimony
  *   (bit-identical to mtgp_eval_rk4's with parsimony 0); grad_out[P, K] (0 beyond nparam).
- * model: MTGP_MODEL_SR with MTGP_SOLVER_RK4 or MTGP_SOLVER_EULER, n_var + K <= MTGP_MAX_DATA,
- * R <= 64; anything else returns MTGP_ERR_ARG. */
+ * model: MTGP_MODEL_SR with MTGP_SOLVER_RK4, MTGP_SOLVER_EULER or (ABI v17) MTGP_SOLVER_DOPRI5,
+ * n_var + K <= MTGP_MAX_DATA, R <= 64; anything else returns MTGP_ERR_ARG.  Dopri5: the adaptive
+ * solve (include/mtgp_dopri5.h, rollouts->ts the save points) in dual numbers with the step sizes,
+ * accept / reject decisions and the event held at their primal values. */
 int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
                  const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
                  float* scratch, float* loss_out, float* grad_out, void* stream);

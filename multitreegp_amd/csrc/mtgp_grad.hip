@@ -18,6 +18,7 @@
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_dual.h"
+#include "mtgp_dopri5.h"
 
 namespace {
 
@@ -259,6 +260,145 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
     if (prev_ok && !ok) pending = true;
     prev_ok = ok;
   }
+  out[0] = tot / (float)S;
+  out[1] = dtot / (float)S;
+}
+
+// k_sr_grad for the adaptive solve (SR_evaluator.py:76-79 with Dopri5 + PIDController): k_sr_dopri5's
+// integration (include/mtgp_dopri5.h) in dual numbers, the step sizes, accept / reject decisions and
+// the event held at their primal values (oracle sr_rollout_dual_dp: the derivative of the discrete
+// solution along the step sequence the solve took).  The value half is the evaluator's MSE of the
+// saved points bit for bit.  Lanes run independently (no wave-uniform program calls: the grad
+// launch is small, one lane per (individual, parameter, rollout)).
+template <int NV>
+__global__ void __launch_bounds__(256) k_sr_grad_dp(GradArgs A) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int R = A.ro.R;
+  if (gid >= (long)A.P * A.K * R) return;
+  const int r = (int)(gid % R);
+  const long pk = gid / R;
+  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
+  float* out = A.part + (size_t)gid * 2;
+  const int np = A.nparam[p];
+  if (k > 0 && k >= np) {  // unused parameter slot of this individual
+    out[0] = 0.0f;
+    out[1] = 0.0f;
+    return;
+  }
+  const int kk = k < np ? k : -1;
+  const int nv = A.m.n_var;
+  const float* th = A.theta + (size_t)p * A.K;
+  const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
+  const int S = A.m.n_save, max_steps = A.m.max_steps;
+  const float rtol = A.m.rtol, atol = A.m.atol, dtmin = A.m.dtmin, dtmax = A.m.dtmax;
+  const float* __restrict__ ts = A.ro.ts;
+  const float t_end = ts[S - 1];
+  constexpr float TA[7][6] = MTGP_DP_TABLE_A;
+  constexpr float E[7] = MTGP_DP_TABLE_E;
+  constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+  float yv[NV], yd[NV], y1v[NV], y1d[NV], fv[7][NV], fd[7][NV], sv[NV], sd[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    yv[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
+    yd[i] = 0.0f;
+  }
+  auto bad = [&]() {
+    bool b = false;
+#pragma unroll
+    for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(yv[i]));
+    return b;
+  };
+  auto rhs = [&](const float* xv, const float* xd, float* ov, float* od) {
+    for (int i = 0; i < nv; ++i) {
+      const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk);
+      ov[i] = o.v;
+      od[i] = o.d;
+    }
+  };
+  float tot = 0.0f, dtot = 0.0f;
+  auto mse = [&](int ks, const float* xv, const float* xd) {  // SR_evaluator.py:24, save point ks
+    float sq = 0.0f, dsq = 0.0f;
+    for (int d = 0; d < nv; ++d) {
+      const float e = xv[d] - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
+      const float de = xd[d] * (2.0f * e);
+      sq = (d == 0) ? e * e : sq + e * e;
+      dsq = (d == 0) ? de : dsq + de;
+    }
+    tot = tot + sq;
+    dtot = dtot + dsq;
+  };
+  mse(0, yv, yd);
+  int ks = 1, steps = 0;
+  float t = ts[0];
+  float tnext = t + A.m.h;
+  tnext = tnext > t_end ? t_end : tnext;
+  bool prev_ok = !bad();
+  rhs(yv, yd, fv[0], fd[0]);
+  const MtgpDpPid pid = A.m.pid_custom ? MtgpDpPid{A.m.pid_c1, A.m.pid_c2, A.m.pid_c3, A.m.pid_safety,
+                                                   A.m.pid_factormin, A.m.pid_factormax}
+                                       : MtgpDpPid MTGP_DP_PID_DEFAULT;
+  MtgpDpCtl ctl{1.0f, 1.0f, 0};
+  const int force_dtmin = !A.m.no_force_dtmin;
+  while (t < t_end && steps < max_steps) {
+    const float h = tnext - t;
+    for (int st = 1; st <= 6; ++st) {
+      for (int i = 0; i < nv; ++i) {
+        float acc = 0.0f, dacc = 0.0f;
+        for (int j = 0; j < st; ++j) {
+          acc = mtgp_dp_term(acc, TA[st][j], fv[j][i], j == 0);
+          dacc = mtgp_dp_term(dacc, TA[st][j], fd[j][i], j == 0);
+        }
+        sv[i] = MTGP_FMAF(h, acc, yv[i]);
+        sd[i] = MTGP_FMAF(h, dacc, yd[i]);
+        if (st == 6) { y1v[i] = sv[i]; y1d[i] = sd[i]; }
+      }
+      rhs(sv, sd, fv[st], fd[st]);
+    }
+    float msum = 0.0f;
+    for (int i = 0; i < nv; ++i) {
+      float acc = 0.0f;
+      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], fv[j][i], j == 0);
+      const float sc = mtgp_dp_scaled(h * acc, yv[i], y1v[i], rtol, atol);
+      msum = (i == 0) ? sc * sc : msum + sc * sc;
+    }
+    const float ms = msum / (float)nv;
+    int keep, fail;
+    const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &keep, &fail);
+    ++steps;
+    bool done = fail != 0;
+    if (keep) {
+      const float t1 = tnext;
+      while (ks < S && ts[ks] <= t1) {  // SaveAt(ts) by the dense output at the primal theta
+        const float thk = (ts[ks] - t) / h;
+        for (int i = 0; i < nv; ++i) {
+          float acc = 0.0f, dacc = 0.0f;
+          for (int j = 0; j < 7; ++j) {
+            acc = mtgp_dp_term(acc, CM[j], fv[j][i], j == 0);
+            dacc = mtgp_dp_term(dacc, CM[j], fd[j][i], j == 0);
+          }
+          const float ymid = MTGP_FMAF(h, acc, yv[i]), dymid = MTGP_FMAF(h, dacc, yd[i]);
+          sv[i] = mtgp_dp_interp(yv[i], y1v[i], ymid, h * fv[0][i], h * fv[6][i], thk);
+          sd[i] = mtgp_dp_interp(yd[i], y1d[i], dymid, h * fd[0][i], h * fd[6][i], thk);
+        }
+        mse(ks, sv, sd);
+        ++ks;
+      }
+      t = t1;
+      for (int i = 0; i < nv; ++i) {
+        yv[i] = y1v[i];
+        yd[i] = y1d[i];
+        fv[0][i] = fv[6][i];  // FSAL
+        fd[0][i] = fd[6][i];
+      }
+      const bool ok = !bad();
+      if (prev_ok && !ok) done = true;  // the NaN event (sr.py:93-94)
+      prev_ok = ok;
+    }
+    if (done) break;
+    tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+  }
+  // unsaved points are +inf: the squared error is +inf (NaN stays NaN)
+  if (ks < S && mtgp_isfinite(tot)) tot = kInf;
   out[0] = tot / (float)S;
   out[1] = dtot / (float)S;
 }
@@ -651,7 +791,9 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
       model->n_var + K > MTGP_MAX_DATA || ro->R < 1 || ro->R > 64 || !ro->x0 || !ro->ys_true ||
       model->save_every < 1 || model->n_save < 1 || model->prog_state < 0 || model->prog_state + model->n_var > n_prog)
     return MTGP_ERR_ARG;
-  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER) return MTGP_ERR_ARG;
+  const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
+  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;
+  if (dopri5 && (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f) || !ro->ts)) return MTGP_ERR_ARG;
   if (P == 0) return MTGP_OK;
   GradArgs A;
   A.m = *model;
@@ -670,7 +812,12 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
   const long lanes = (long)P * K * ro->R;
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
   const int nv = model->n_var;
-  if (nv <= 2) hipLaunchKernelGGL(k_sr_grad<2>, grid, block, 0, s, A);
+  if (dopri5) {
+    if (nv <= 2) hipLaunchKernelGGL(k_sr_grad_dp<2>, grid, block, 0, s, A);
+    else if (nv <= 4) hipLaunchKernelGGL(k_sr_grad_dp<4>, grid, block, 0, s, A);
+    else if (nv <= 16) hipLaunchKernelGGL(k_sr_grad_dp<16>, grid, block, 0, s, A);
+    else hipLaunchKernelGGL(k_sr_grad_dp<64>, grid, block, 0, s, A);
+  } else if (nv <= 2) hipLaunchKernelGGL(k_sr_grad<2>, grid, block, 0, s, A);
   else if (nv <= 4) hipLaunchKernelGGL(k_sr_grad<4>, grid, block, 0, s, A);
   else if (nv <= 16) hipLaunchKernelGGL(k_sr_grad<16>, grid, block, 0, s, A);
   else hipLaunchKernelGGL(k_sr_grad<64>, grid, block, 0, s, A);

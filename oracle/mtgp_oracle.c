@@ -834,11 +834,123 @@ static ODual sr_rollout_dual(const OrModel* m, const float* cand, int N, const O
   return od(tot.v / (float)S, tot.d / (float)S);
 }
 
+/* sr_rollout_dual for the adaptive solve: solve_dopri5 (include/mtgp_dopri5.h) in dual numbers
+ * with the step sizes, the accept / reject decisions and the event held at their primal values --
+ * the derivative of the discrete solution along the step sequence the solve took.  (Whether
+ * diffrax's DirectAdjoint also differentiates the controller's next-step size is not pinned here:
+ * that term is of the order of the local error tolerance.)  The value half is solve_dopri5 + the
+ * evaluator's MSE of the saved points bit for bit; the tangent half applies the same linear maps
+ * (stage fma chains, dense output at the primal theta) to the tangents. */
+static ODual sr_rollout_dual_dp(const OrModel* m, const float* cand, int N, const OrLib* lib, const OrRollouts* ro,
+                                int r, int pt, int pi) {
+  static const float A[7][6] = MTGP_DP_TABLE_A;
+  static const float E[7] = MTGP_DP_TABLE_E;
+  static const float CM[7] = MTGP_DP_TABLE_CMID;
+  const int nv = m->n_var, S = m->n_save;
+  const float* ts = ro->ts;
+  const float t_end = ts[S - 1];
+  ODual y[OR_MAX_S], f[7][OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  float sv[OR_MAX_S];
+  ODual tot = od(0.0f, 0.0f);
+#define OR_DP_RHS(in, out)                                                                          \
+  for (int q = 0; q < nv; ++q)                                                                      \
+    out[q] = tree_eval_dual(cand + (size_t)q * N * 4, N, lib, in, nv, q == pt ? pi : -1);
+#define OR_DP_MSE(kk, val)                                                                          \
+  {                                                                                                 \
+    ODual sq = od(0.0f, 0.0f);                                                                      \
+    for (int dd = 0; dd < nv; ++dd) {                                                               \
+      const float e = (val)[dd].v - ro->ys_true[((size_t)r * S + (kk)) * nv + dd];                  \
+      const float de = (val)[dd].d * (2.0f * e);                                                    \
+      sq = dd == 0 ? od(e * e, de) : od(sq.v + e * e, sq.d + de);                                   \
+    }                                                                                               \
+    tot = od(tot.v + sq.v, tot.d + sq.d);                                                           \
+  }
+  for (int i = 0; i < nv; ++i) y[i] = od(ro->x0[(size_t)r * nv + i], 0.0f);
+  OR_DP_MSE(0, y)
+  int k = 1, steps = 0;
+  float t = ts[0];
+  float tnext = t + m->h;
+  if (tnext > t_end) tnext = t_end;
+  for (int i = 0; i < nv; ++i) sv[i] = y[i].v;
+  float prev = cond_fn(m, sv);
+  OR_DP_RHS(y, f[0])
+  const MtgpDpPid def_pid = MTGP_DP_PID_DEFAULT;
+  MtgpDpPid pid = def_pid;
+  if (m->pid_custom) {
+    pid.c1 = m->pid_c1; pid.c2 = m->pid_c2; pid.c3 = m->pid_c3;
+    pid.safety = m->pid_safety; pid.factormin = m->pid_factormin; pid.factormax = m->pid_factormax;
+  }
+  MtgpDpCtl ctl = {1.0f, 1.0f, 0};
+  while (t < t_end && steps < m->max_steps) {
+    const float h = tnext - t;
+    for (int st = 1; st <= 6; ++st) {
+      for (int i = 0; i < nv; ++i) {
+        float acc = 0.0f, dacc = 0.0f;
+        for (int j = 0; j < st; ++j) {
+          acc = mtgp_dp_term(acc, A[st][j], f[j][i].v, j == 0);
+          dacc = mtgp_dp_term(dacc, A[st][j], f[j][i].d, j == 0);
+        }
+        yi[i] = od(MTGP_FMAF(h, acc, y[i].v), MTGP_FMAF(h, dacc, y[i].d));
+        if (st == 6) y1[i] = yi[i];
+      }
+      OR_DP_RHS(yi, f[st])
+    }
+    float msum = 0.0f;
+    for (int i = 0; i < nv; ++i) {
+      float acc = 0.0f;
+      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i].v, j == 0);
+      const float sc = mtgp_dp_scaled(h * acc, y[i].v, y1[i].v, m->rtol, m->atol);
+      msum = (i == 0) ? sc * sc : msum + sc * sc;
+    }
+    const float ms = msum / (float)nv;
+    int keep, fail;
+    const float dt = mtgp_dp_control(ms, h, m->dtmin, m->dtmax, !m->no_force_dtmin, &pid, &ctl, &keep, &fail);
+    ++steps;
+    int done = fail;
+    if (keep) {
+      const float t1 = tnext;
+      while (k < S && ts[k] <= t1) {
+        const float th = (ts[k] - t) / h;
+        ODual sk[OR_MAX_S];
+        for (int i = 0; i < nv; ++i) {
+          float acc = 0.0f, dacc = 0.0f;
+          for (int j = 0; j < 7; ++j) {
+            acc = mtgp_dp_term(acc, CM[j], f[j][i].v, j == 0);
+            dacc = mtgp_dp_term(dacc, CM[j], f[j][i].d, j == 0);
+          }
+          const float ymid = MTGP_FMAF(h, acc, y[i].v), dymid = MTGP_FMAF(h, dacc, y[i].d);
+          sk[i] = od(mtgp_dp_interp(y[i].v, y1[i].v, ymid, h * f[0][i].v, h * f[6][i].v, th),
+                     mtgp_dp_interp(y[i].d, y1[i].d, dymid, h * f[0][i].d, h * f[6][i].d, th));
+        }
+        OR_DP_MSE(k, sk)
+        ++k;
+      }
+      t = t1;
+      for (int i = 0; i < nv; ++i) {
+        y[i] = y1[i];
+        f[0][i] = f[6][i];
+        sv[i] = y[i].v;
+      }
+      const float cur = cond_fn(m, sv);
+      if (prev > 0.0f && cur < 0.0f) done = 1;
+      prev = cur;
+    }
+    if (done) break;
+    tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+  }
+#undef OR_DP_RHS
+#undef OR_DP_MSE
+  /* unsaved points are +inf: the squared error is +inf (NaN stays NaN) */
+  if (k < S && mtgp_isfinite(tot.v)) tot.v = mtgp_u2f(0x7f800000u);
+  return od(tot.v / (float)S, tot.d / (float)S);
+}
+
 /* loss[P] (the evaluator's fitness, no parsimony) and grad[P, K]: prow[P, K] = t * N + i of the
- * k-th coefficient row (-1 = unused).  SR, fixed-step RK4 / Euler. */
+ * k-th coefficient row (-1 = unused).  SR: fixed-step RK4 / Euler, or Dopri5 + PID
+ * (sr_rollout_dual_dp: step sizes held at their primal values). */
 int oracle_sr_grad(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
                    const int8_t* fn, const OrRollouts* ro, const int32_t* prow, int K, float* loss, float* grad) {
-  if (m->model != 3 || m->solver == 1 || N > OR_MAX_N || m->n_var > OR_MAX_S || ro->R > 64 || K < 1) return -1;
+  if (m->model != 3 || N > OR_MAX_N || m->n_var > OR_MAX_S || ro->R > 64 || K < 1) return -1;
   const int R = ro->R;
 #pragma omp parallel for schedule(dynamic, 1)
   for (long pk = 0; pk < (long)P * K; ++pk) {
@@ -852,7 +964,9 @@ int oracle_sr_grad(const OrModel* m, const float* pop, int P, int T, int N, int 
     const float* cand = pop + (size_t)p * T * N * 4;
     float v[64], dv[64];
     for (int r = 0; r < R; ++r) {
-      ODual F = sr_rollout_dual(m, cand, N, &lib, ro, r, row < 0 ? -1 : row / N, row < 0 ? -1 : row % N);
+      const int pt = row < 0 ? -1 : row / N, pi = row < 0 ? -1 : row % N;
+      ODual F = m->solver == 1 ? sr_rollout_dual_dp(m, cand, N, &lib, ro, r, pt, pi)
+                               : sr_rollout_dual(m, cand, N, &lib, ro, r, pt, pi);
       if (!mtgp_isfinite(F.v)) F = od(m->max_fitness, 0.0f); /* sr.py:42-43, derivative of where */
       v[r] = F.v;
       dv[r] = F.d;

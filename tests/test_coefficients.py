@@ -227,9 +227,9 @@ def test_coefficient_optimisation_config_checks():
     with pytest.raises(AssertionError):
         mt.GeneticProgramming(20, 20, ff, lib_ops, vl, [2], coefficient_optimisation=True, gradient_steps=0,
                               verbose=False)
+    # SR with the adaptive solve: mtgp_sr_grad's Dopri5 kernel (step sizes held at their primal values)
     ffd = mt.SREvaluator(solver=mt.Dopri5(), dt0=0.05, stepsize_controller=mt.PIDController(1e-4, 1e-4))
-    with pytest.raises(NotImplementedError):
-        mt.GeneticProgramming(20, 20, ffd, lib_ops, vl, [2], coefficient_optimisation=True, verbose=False)
+    mt.GeneticProgramming(20, 20, ffd, lib_ops, vl, [2], coefficient_optimisation=True, verbose=False)
     # the control evaluators with a fixed-step solver are differentiated too (mtgp_ctl_grad)
     from helpers import CONTROL_OPS
     env = mt.Acrobot(0.0, 0.0)
@@ -273,7 +273,88 @@ def test_optimiser_state_per_candidate():
         assert fit[b] == f1[0] and np.array_equal(out[b], o1[0])
 
 
+# ------------------------------------------------------------------- SR with Dopri5 + PID
+def _setup_dp(P=12, R=4, seed=3, n_var=2, tol=1e-6):
+    env, lib, ff, data, pop = sr_setup(P=P, R=R, n_save=9, save_every=2, h=0.05, depth=4, N=20, seed=seed,
+                                       n_var=n_var, solver=(tol, tol, 0.001, 500))
+    return lib, ff, data, ff.prepare(data), pop
+
+
+def test_oracle_dopri5_loss_is_the_fitness():
+    lib, ff, data, d, pop = _setup_dp()
+    loss, grad, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
+    assert bits_equal(loss, ref), mismatch_report(loss, ref, "loss")
+    assert sum(len(r) for r in rows) > 10
+
+
+def test_oracle_dopri5_gradient_matches_central_differences():
+    """The Dopri5 sensitivities hold the step sizes at their primal values (oracle
+    sr_rollout_dual_dp); a central difference of the oracle's own float32 loss also moves the
+    controller's step sizes, by terms of the order of the tolerance.  Well-conditioned candidates
+    (finite, unclipped loss; forward and backward differences within 2 % of each other) agree to a
+    few 1e-3."""
+    lib, ff, data, d, pop = _setup_dp(P=24, seed=3)
+    m, ro = oracle_model(ff, d), oracle_rollouts(d)
+    loss, grad, rows = orc.sr_grad(m, pop, lib, ro)
+    rel = []
+    for p in range(pop.shape[0]):
+        if not (0 < loss[p] < 1e4):
+            continue
+        for k, (t, i) in enumerate(rows[p][:4]):
+            c = pop[p: p + 1].copy()
+            e = np.float32(1e-3 * max(1.0, abs(float(c[0, t, i, 3]))))
+            base = c[0, t, i, 3]
+            c[0, t, i, 3] = base + e
+            up = orc.evaluate(m, c, lib, ro)["fitness"][0]
+            c[0, t, i, 3] = base - e
+            dn = orc.evaluate(m, c, lib, ro)["fitness"][0]
+            fwd, bwd = (up - loss[p]) / e, (loss[p] - dn) / e
+            if not abs(fwd - bwd) <= 0.02 * (abs(fwd) + abs(bwd)) + 1e-4:
+                continue  # the step sequence (or the float32 loss) is not smooth here
+            fd = (up - dn) / (2 * e)
+            rel.append(abs(grad[p, k] - fd) / (abs(fd) + 1e-3 * (1 + abs(loss[p]))))
+    rel = np.array(rel)
+    assert rel.size >= 20 and np.median(rel) < 5e-3 and np.mean(rel < 3e-2) >= 0.85, np.sort(rel)
+
+
+def test_oracle_dopri5_gradient_of_a_known_fit():
+    """dx0 = x1, dx1 = c*x0 on the Van der Pol data with Dopri5: sign and size of the gradient in
+    c against a central difference of the oracle's loss."""
+    env, lib, ff, data, _ = sr_setup(P=2, R=4, n_save=11, save_every=2, h=0.05, N=20, solver=(1e-6, 1e-6, 0.001, 500))
+    d = ff.prepare(data)
+
+    def cand(c):
+        return np.stack([tree_from_expr("x1", lib, 20), tree_from_expr(("*", c, "x0"), lib, 20)])[None]
+
+    loss, grad, _ = orc.sr_grad(oracle_model(ff, d), cand(-0.8), lib, oracle_rollouts(d))
+    e = 1e-2
+    up = orc.evaluate(oracle_model(ff, d), cand(-0.8 + e), lib, oracle_rollouts(d))["fitness"][0]
+    dn = orc.evaluate(oracle_model(ff, d), cand(-0.8 - e), lib, oracle_rollouts(d))["fitness"][0]
+    fd = (up - dn) / (2 * e)
+    assert np.sign(grad[0, 0]) == np.sign(fd) and abs(grad[0, 0] - fd) < 0.05 * abs(fd), (grad[0, 0], fd)
+
+
 # ------------------------------------------------------------------------------ GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_var,R", [(2, 8), (3, 5), (6, 4)])
+def test_gpu_sr_grad_dopri5_bitexact(n_var, R):
+    """mtgp_sr_grad with Dopri5 + PID (k_sr_grad_dp, 2 / 4 / 16-slot templates) vs the oracle:
+    loss and every coefficient's gradient bit for bit, loss = the evaluator's fitness."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    lib, ff, data, d, pop = _setup_dp(P=24, R=R, seed=21 + n_var, n_var=n_var)
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    opt = co.CoefficientOptimiser(eng)
+    loss, grads = opt.loss_and_grad(pop, data)
+    rl, rg, rows = orc.sr_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    assert sum(len(r) for r in rows) > 5
+    assert bits_equal(loss, rl), mismatch_report(loss, rl, "loss")
+    for p, g in enumerate(grads):
+        assert bits_equal(g, rg[p, : len(g)]), (p, g, rg[p, : len(g)])
+    fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
+    assert bits_equal(loss, fit), mismatch_report(loss, fit, "fitness")
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("euler", [False, True])
 def test_gpu_sr_grad_bitexact(euler):
