@@ -417,7 +417,8 @@ int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, 
 
 /* ABI v16: the same for the dynamic and static control models (dynamic_evaluate.py:37-118,
  * feedforward_evaluate.py:36-110; value_and_grad of gp.py:253 / 435-452): every MTGP_ENV_*,
- * MTGP_SOLVER_RK4 or MTGP_SOLVER_EULER, observation noise included, state_size <= 3, R <= 64.
+ * MTGP_SOLVER_RK4, MTGP_SOLVER_EULER or (ABI v17) MTGP_SOLVER_DOPRI5 (step sizes held at their
+ * primal values, as mtgp_sr_grad), observation noise included, state_size <= 3, R <= 64.
  * The programs read the reference's data vector [y(n_obs), a, u, targets] (MtgpProgramSpec gap 0)
  * followed by the K parameter slots.  Tangent rules: include/mtgp_dual.h (the environment drift,
  * f_obs, clip); the argmax step of the Acrobot fitness (acrobot.py:79) is piecewise constant. */

@@ -139,9 +139,6 @@ class CoefficientOptimiser:
         kind = getattr(ff, "solver_kind", "")
         if kind not in ("rk4", "euler", "dopri5"):
             raise NotImplementedError(f"coefficient optimisation: solver {kind!r}")
-        if kind == "dopri5" and ff.model_id != nat.MODEL_SR:
-            raise NotImplementedError("coefficient optimisation with the adaptive Dopri5 solve: the SR evaluator "
-                                      "(the control evaluators differentiate the fixed-step solves, RK4 or Euler)")
         if ff.model_id != nat.MODEL_SR and getattr(ff, "state_size", 0) > 3:
             raise NotImplementedError("coefficient optimisation of the dynamic evaluator: state_size <= 3")
 

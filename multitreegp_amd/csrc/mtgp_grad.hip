@@ -660,6 +660,82 @@ __global__ void __launch_bounds__(256) k_ctl_grad(GradArgs A) {
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ts[0];
   const bool euler = A.m.solver == MTGP_SOLVER_EULER;
   int q_saved = 0;
+  if (A.m.solver == MTGP_SOLVER_DOPRI5) {
+    // k_ctl_dopri5's solve in duals (oracle ctl_dopri5_dual): the step sizes, accept / reject
+    // decisions and the event held at their primal values; save points by the dense output
+    constexpr float TA[7][6] = MTGP_DP_TABLE_A;
+    constexpr float E[7] = MTGP_DP_TABLE_E;
+    constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+    const float t_end = ts[S - 1];
+    Dual f[7][ND], y1[ND], yi[ND], sk[ND];
+    int ks = 1, steps = 0;
+    float t = ts[0];
+    float tnext = t + h;
+    tnext = tnext > t_end ? t_end : tnext;
+    rhs(t, s, f[0]);
+    const MtgpDpPid pid = A.m.pid_custom ? MtgpDpPid{A.m.pid_c1, A.m.pid_c2, A.m.pid_c3, A.m.pid_safety,
+                                                     A.m.pid_factormin, A.m.pid_factormax}
+                                         : MtgpDpPid MTGP_DP_PID_DEFAULT;
+    MtgpDpCtl ctl{1.0f, 1.0f, 0};
+    const int force_dtmin = !A.m.no_force_dtmin;
+    while (t < t_end && steps < A.m.max_steps) {
+      const float hs = tnext - t;
+      for (int st = 1; st <= 6; ++st) {
+        for (int i = 0; i < ND; ++i) {
+          float a = 0.0f, da = 0.0f;
+          for (int j = 0; j < st; ++j) {
+            a = mtgp_dp_term(a, TA[st][j], f[j][i].v, j == 0);
+            da = mtgp_dp_term(da, TA[st][j], f[j][i].d, j == 0);
+          }
+          yi[i] = {MTGP_FMAF(hs, a, s[i].v), MTGP_FMAF(hs, da, s[i].d)};
+          if (st == 6) y1[i] = yi[i];
+        }
+        rhs(t + mtgp_dp_c(st) * hs, yi, f[st]);
+      }
+      float msum = 0.0f;
+      for (int i = 0; i < ND; ++i) {
+        float a = 0.0f;
+        for (int j = 0; j < 7; ++j) a = mtgp_dp_term(a, E[j], f[j][i].v, j == 0);
+        const float sc = mtgp_dp_scaled(hs * a, s[i].v, y1[i].v, A.m.rtol, A.m.atol);
+        msum = (i == 0) ? sc * sc : msum + sc * sc;
+      }
+      const float ms = msum / (float)ND;
+      int keep, fail;
+      const float dt = mtgp_dp_control(ms, hs, A.m.dtmin, A.m.dtmax, force_dtmin, &pid, &ctl, &keep, &fail);
+      ++steps;
+      bool stop = fail != 0;
+      if (keep) {
+        const float t1 = tnext;
+        while (ks < S && ts[ks] <= t1) {
+          const float th = (ts[ks] - t) / hs;
+          for (int i = 0; i < ND; ++i) {
+            float a = 0.0f, da = 0.0f;
+            for (int j = 0; j < 7; ++j) {
+              a = mtgp_dp_term(a, CM[j], f[j][i].v, j == 0);
+              da = mtgp_dp_term(da, CM[j], f[j][i].d, j == 0);
+            }
+            const float ymid = MTGP_FMAF(hs, a, s[i].v), dymid = MTGP_FMAF(hs, da, s[i].d);
+            sk[i] = {mtgp_dp_interp(s[i].v, y1[i].v, ymid, hs * f[0][i].v, hs * f[6][i].v, th),
+                     mtgp_dp_interp(s[i].d, y1[i].d, dymid, hs * f[0][i].d, hs * f[6][i].d, th)};
+          }
+          save_point(ks, sk);
+          ++ks;
+        }
+        t = t1;
+        for (int i = 0; i < ND; ++i) {
+          s[i] = y1[i];
+          f[0][i] = f[6][i];  // FSAL
+        }
+        const bool ok = !bad(s);
+        if (prev_ok && !ok) stop = true;  // Event(cond_fn_nan), dyn.py:94
+        prev_ok = ok;
+      }
+      if (stop) break;
+      tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+    }
+    q_saved = ks - 1;
+    done = true;
+  }
   for (int step = 1; step <= A.m.n_steps && !done; ++step) {
     const float t = t0 + (float)(step - 1) * h;
     rhs(t, s, kx);
@@ -744,7 +820,9 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
     return MTGP_ERR_ARG;
   const bool dyn = model->model == MTGP_MODEL_DYNAMIC;
   if (!dyn && model->model != MTGP_MODEL_STATIC) return MTGP_ERR_ARG;
-  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER) return MTGP_ERR_ARG;
+  const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
+  if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;
+  if (dopri5 && (model->max_steps <= 0 || !(model->h > 0.0f))) return MTGP_ERR_ARG;
   const int nv = model->env == MTGP_ENV_ACROBOT ? 4 : (model->env == MTGP_ENV_HARMONIC_OSCILLATOR ? 2 : 3);
   if (model->env < 0 || model->env > 2 || model->n_var != nv || model->n_obs < 1 || model->n_obs > nv ||
       model->n_control != 1 || model->n_targets < 0 || model->n_targets > 8 || !ro->params || !ro->x0 || !ro->ts ||

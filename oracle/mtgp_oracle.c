@@ -1061,6 +1061,93 @@ static void ctl_rhs_dual(const OrCtx* c, float t, const ODual* s, ODual* ds, int
   }
 }
 
+/* solve_dopri5 of the control models in dual numbers (the coupled [x, a] state, ctl_rhs_dual at
+ * the stage times t + c_i h), the step sizes, accept / reject decisions and the event held at
+ * their primal values (as sr_rollout_dual_dp): saved[0..k) the dense-output save points; returns
+ * k, the first unsaved index. */
+static int ctl_dopri5_dual(const OrCtx* c, const OrRollouts* ro, const ODual* s0, ODual* saved, int pt, int pi) {
+  static const float A[7][6] = MTGP_DP_TABLE_A;
+  static const float E[7] = MTGP_DP_TABLE_E;
+  static const float CM[7] = MTGP_DP_TABLE_CMID;
+  const OrModel* m = c->m;
+  const int n = state_dim(m), S = m->n_save;
+  const float* ts = ro->ts;
+  const float t_end = ts[S - 1];
+  ODual y[OR_MAX_S], f[7][OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  float sv[OR_MAX_S];
+  for (int i = 0; i < n; ++i) { y[i] = s0[i]; saved[i] = y[i]; sv[i] = y[i].v; }
+  int k = 1, steps = 0;
+  float t = ts[0];
+  float tnext = t + m->h;
+  if (tnext > t_end) tnext = t_end;
+  float prev = cond_fn(m, sv);
+  ctl_rhs_dual(c, t, y, f[0], pt, pi);
+  const MtgpDpPid def_pid = MTGP_DP_PID_DEFAULT;
+  MtgpDpPid pid = def_pid;
+  if (m->pid_custom) {
+    pid.c1 = m->pid_c1; pid.c2 = m->pid_c2; pid.c3 = m->pid_c3;
+    pid.safety = m->pid_safety; pid.factormin = m->pid_factormin; pid.factormax = m->pid_factormax;
+  }
+  MtgpDpCtl ctl = {1.0f, 1.0f, 0};
+  while (t < t_end && steps < m->max_steps) {
+    const float h = tnext - t;
+    for (int st = 1; st <= 6; ++st) {
+      for (int i = 0; i < n; ++i) {
+        float acc = 0.0f, dacc = 0.0f;
+        for (int j = 0; j < st; ++j) {
+          acc = mtgp_dp_term(acc, A[st][j], f[j][i].v, j == 0);
+          dacc = mtgp_dp_term(dacc, A[st][j], f[j][i].d, j == 0);
+        }
+        yi[i] = od(MTGP_FMAF(h, acc, y[i].v), MTGP_FMAF(h, dacc, y[i].d));
+        if (st == 6) y1[i] = yi[i];
+      }
+      ctl_rhs_dual(c, t + mtgp_dp_c(st) * h, yi, f[st], pt, pi);
+    }
+    float msum = 0.0f;
+    for (int i = 0; i < n; ++i) {
+      float acc = 0.0f;
+      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i].v, j == 0);
+      const float sc = mtgp_dp_scaled(h * acc, y[i].v, y1[i].v, m->rtol, m->atol);
+      msum = (i == 0) ? sc * sc : msum + sc * sc;
+    }
+    const float ms = msum / (float)n;
+    int keep, fail;
+    const float dt = mtgp_dp_control(ms, h, m->dtmin, m->dtmax, !m->no_force_dtmin, &pid, &ctl, &keep, &fail);
+    ++steps;
+    int done = fail;
+    if (keep) {
+      const float t1 = tnext;
+      while (k < S && ts[k] <= t1) {
+        const float th = (ts[k] - t) / h;
+        for (int i = 0; i < n; ++i) {
+          float acc = 0.0f, dacc = 0.0f;
+          for (int j = 0; j < 7; ++j) {
+            acc = mtgp_dp_term(acc, CM[j], f[j][i].v, j == 0);
+            dacc = mtgp_dp_term(dacc, CM[j], f[j][i].d, j == 0);
+          }
+          const float ymid = MTGP_FMAF(h, acc, y[i].v), dymid = MTGP_FMAF(h, dacc, y[i].d);
+          saved[(size_t)k * n + i] =
+              od(mtgp_dp_interp(y[i].v, y1[i].v, ymid, h * f[0][i].v, h * f[6][i].v, th),
+                 mtgp_dp_interp(y[i].d, y1[i].d, dymid, h * f[0][i].d, h * f[6][i].d, th));
+        }
+        ++k;
+      }
+      t = t1;
+      for (int i = 0; i < n; ++i) {
+        y[i] = y1[i];
+        f[0][i] = f[6][i];
+        sv[i] = y[i].v;
+      }
+      const float cur = cond_fn(m, sv);
+      if (prev > 0.0f && cur < 0.0f) done = 1;
+      prev = cur;
+    }
+    if (done) break;
+    tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
+  }
+  return k;
+}
+
 /* one rollout: F and dF / d theta (the evaluator's rollout fitness, before NaN/inf replacement) */
 static ODual ctl_rollout_dual(const OrCtx* c, const OrRollouts* ro, int r, int pt, int pi) {
   const OrModel* m = c->m;
@@ -1074,7 +1161,8 @@ static ODual ctl_rollout_dual(const OrCtx* c, const OrRollouts* ro, int r, int p
   float prev = cond_fn(m, sv);
   const float h = m->h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ro->ts[0];
   int k_saved = 0, done = 0;
-  for (int step = 1; step <= m->n_steps && !done; ++step) {
+  if (m->solver == 1) k_saved = ctl_dopri5_dual(c, ro, s, saved, pt, pi) - 1;
+  for (int step = 1; m->solver != 1 && step <= m->n_steps && !done; ++step) {
     const float t = t0 + (float)(step - 1) * h;
     if (m->solver == 2) {
       ctl_rhs_dual(c, t, s, k, pt, pi);
@@ -1174,7 +1262,7 @@ static ODual ctl_rollout_dual(const OrCtx* c, const OrRollouts* ro, int r, int p
 
 int oracle_ctl_grad(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
                     const int8_t* fn, const OrRollouts* ro, const int32_t* prow, int K, float* loss, float* grad) {
-  if ((m->model != 1 && m->model != 2) || m->solver == 1 || N > OR_MAX_N || state_dim(m) > OR_MAX_S ||
+  if ((m->model != 1 && m->model != 2) || N > OR_MAX_N || state_dim(m) > OR_MAX_S ||
       ro->R > 64 || K < 1)
     return -1;
   const int R = ro->R;

@@ -239,10 +239,10 @@ def test_coefficient_optimisation_config_checks():
     st = mt.FeedforwardEvaluator(mt.HarmonicOscillator(0.0, 0.0), 0.05, solver=mt.Euler())
     mt.GeneticProgramming(20, 20, st, CONTROL_OPS, [["y1", "y2", "tar1"]], [1], coefficient_optimisation=True,
                           verbose=False)
+    # ... and with Dopri5 + PID (step sizes held at their primal values)
     dynd = mt.DynamicEvaluator(env, 2, 0.05, solver=mt.Dopri5(), stepsize_controller=mt.PIDController(1e-4, 1e-4))
-    with pytest.raises(NotImplementedError):
-        mt.GeneticProgramming(20, 20, dynd, CONTROL_OPS, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]],
-                              [2, 1], coefficient_optimisation=True, verbose=False)
+    mt.GeneticProgramming(20, 20, dynd, CONTROL_OPS, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]],
+                          [2, 1], coefficient_optimisation=True, verbose=False)
 
 
 class _GlobalNormOptimiser:
@@ -574,11 +574,13 @@ def _ctl_loss_c(cand, lib, ff, d, prow_t, prow_i, eps=1e-30):
     return m if 0 < m.real < 1e4 else complex(np.clip(m.real, 0, 1e4))
 
 
-def _ctl_setup(kind, env="acrobot", euler=False, P=10, R=3, n_steps=16, seed=5, obs_noise=0.0):
+def _ctl_setup(kind, env="acrobot", euler=False, P=10, R=3, n_steps=16, seed=5, obs_noise=0.0, dopri5=False):
     from helpers import dynamic_setup, static_setup
     solver = None
     setup = dynamic_setup if kind == "dynamic" else static_setup
     kw = dict(P=P, R=R, n_steps=n_steps, seed=seed, env=env, obs_noise=obs_noise)
+    if dopri5:
+        kw["solver"] = (1e-5, 1e-5, 0.002, 600)
     if kind == "dynamic":
         kw["depth"], kw["N"] = 4, 24
     e, lib, ff, data, pop = setup(**kw)
@@ -593,6 +595,44 @@ def _ctl_setup(kind, env="acrobot", euler=False, P=10, R=3, n_steps=16, seed=5, 
 CTL_CASES = [("dynamic", "acrobot", False, 0.0), ("dynamic", "acrobot", True, 0.0), ("static", "acrobot", False, 0.0),
              ("dynamic", "harmonic", False, 0.0), ("static", "reactor", False, 0.0),
              ("dynamic", "acrobot", False, 0.1), ("static", "reactor", True, 0.1)]
+
+
+@pytest.mark.parametrize("kind,env,noise", [("dynamic", "acrobot", 0.0), ("static", "harmonic", 0.1),
+                                             ("dynamic", "reactor", 0.0)])
+def test_ctl_oracle_dopri5_loss_is_the_fitness(kind, env, noise):
+    lib, ff, data, d, pop = _ctl_setup(kind, env, obs_noise=noise, n_steps=30, dopri5=True)
+    loss, grad, rows = orc.ctl_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
+    assert bits_equal(loss, ref), mismatch_report(loss, ref, "loss")
+
+
+def test_ctl_oracle_dopri5_gradient_matches_central_differences():
+    """Control evaluators with Dopri5 (HarmonicOscillator, dynamic and static, with observation
+    noise): the primal-step-size sensitivities vs central differences of the oracle's float32 loss
+    on smooth, unclipped candidates (see the SR Dopri5 test)."""
+    rel = []
+    for kind in ("dynamic", "static"):
+        lib, ff, data, d, pop = _ctl_setup(kind, "harmonic", P=24, obs_noise=0.1, n_steps=30, dopri5=True)
+        m, ro = oracle_model(ff, d), oracle_rollouts(d)
+        loss, grad, rows = orc.ctl_grad(m, pop, lib, ro)
+        for p in range(pop.shape[0]):
+            if not (0 < loss[p] < 1e3):
+                continue
+            for k, (t, i) in enumerate(rows[p][:4]):
+                c = pop[p: p + 1].copy()
+                e = np.float32(1e-3 * max(1.0, abs(float(c[0, t, i, 3]))))
+                base = c[0, t, i, 3]
+                c[0, t, i, 3] = base + e
+                up = orc.evaluate(m, c, lib, ro)["fitness"][0]
+                c[0, t, i, 3] = base - e
+                dn = orc.evaluate(m, c, lib, ro)["fitness"][0]
+                fwd, bwd = (up - loss[p]) / e, (loss[p] - dn) / e
+                if not abs(fwd - bwd) <= 0.02 * (abs(fwd) + abs(bwd)) + 1e-4:
+                    continue
+                fd = (up - dn) / (2 * e)
+                rel.append(abs(grad[p, k] - fd) / (abs(fd) + 1e-3 * (1 + abs(loss[p]))))
+    rel = np.array(rel)
+    assert rel.size >= 10 and np.median(rel) < 5e-3 and np.mean(rel < 3e-2) >= 0.85, np.sort(rel)
 
 
 @pytest.mark.parametrize("kind,env,euler,noise", CTL_CASES)
@@ -637,7 +677,10 @@ def test_ctl_oracle_gradient_matches_complex_step(kind, env, euler):
 # ------------------------------------------------------------ GPU: control evaluators
 GPU_CTL_CASES = [("dynamic", "acrobot", False, 0.0, 4), ("dynamic", "acrobot", True, 0.0, 4),
                  ("static", "acrobot", False, 0.1, 4), ("dynamic", "harmonic", False, 0.0, 2),
-                 ("static", "reactor", True, 0.1, 3), ("dynamic", "acrobot", False, 0.1, 2)]
+                 ("static", "reactor", True, 0.1, 3), ("dynamic", "acrobot", False, 0.1, 2),
+                 # Dopri5 + PID (k_ctl_grad's adaptive solve, step sizes held at their primal values)
+                 ("dynamic", "acrobot", "dopri5", 0.0, 4), ("dynamic", "harmonic", "dopri5", 0.1, 2),
+                 ("static", "reactor", "dopri5", 0.0, 3), ("static", "acrobot", "dopri5", 0.1, 4)]
 
 
 @pytest.mark.gpu
@@ -653,7 +696,8 @@ def test_gpu_ctl_grad_bitexact(kind, env, euler, noise, n_obs):
     e = cls(0.0, noise, n_obs=n_obs)
     ys = [f"y{i + 1}" for i in range(e.n_obs)]
     tg = [f"tar{i + 1}" for i in range(e.n_targets)]
-    solver = dict(solver=mt.Euler()) if euler else _ctl_solver(None)
+    solver = (_ctl_solver((1e-5, 1e-5, 0.002, 600)) if euler == "dopri5"
+              else dict(solver=mt.Euler()) if euler else _ctl_solver(None))
     if kind == "dynamic":
         lib = mt.NodeLibrary(CONTROL_OPS, [ys + ["a1", "a2", "u"] + tg, ["a1", "a2"] + tg], [2, 1])
         ff = mt.DynamicEvaluator(e, 2, 0.05, **solver)
