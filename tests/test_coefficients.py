@@ -413,11 +413,12 @@ def test_gpu_sr_grad_chunks():
 
 
 @pytest.mark.gpu
-def test_gpu_evaluate_population_optimises_coefficients():
+@pytest.mark.parametrize("dopri5", [False, True])
+def test_gpu_evaluate_population_optimises_coefficients(dopri5):
     """Generation 14 of a coefficient-optimising run (gp.py:418): the 50 best candidates get
     gradient_steps Adam steps; fitness, population and best tracking equal a CPU restatement of
-    the same loop driven by the oracle's loss and gradients."""
-    lib, ff, data, d, pop = _setup(P=60, R=4, seed=9)
+    the same loop driven by the oracle's loss and gradients (RK4, and Dopri5 + PID)."""
+    lib, ff, data, d, pop = _setup_dp(P=60, R=4, seed=9) if dopri5 else _setup(P=60, R=4, seed=9)
     strategy = mt.GeneticProgramming(20, 60, ff, SR_OPS, [["x0", "x1"]], [2], max_nodes=20, size_parsinomy=0.01,
                                      coefficient_optimisation=True, gradient_steps=4, verbose=False)
     strategy.current_generation = 14
