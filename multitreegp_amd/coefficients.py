@@ -62,10 +62,10 @@ class Adam:
     def update(self, updates, state: AdamState, params=None):
         f = np.float32
         g = np.asarray(updates, np.float32)
-        mu = f(1 - self.b1) * g + f(self.b1) * state.mu
-        nu = f(1 - self.b2) * (g * g) + f(self.b2) * state.nu
         count = state.count + 1
-        with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
+        with np.errstate(over="ignore", invalid="ignore", divide="ignore"):  # float32 as jnp: inf / NaN, silently
+            mu = f(1 - self.b1) * g + f(self.b1) * state.mu
+            nu = f(1 - self.b2) * (g * g) + f(self.b2) * state.nu
             mu_hat = mu / (f(1) - f(self.b1) ** f(count))
             nu_hat = nu / (f(1) - f(self.b2) ** f(count))
             u = mu_hat / (np.sqrt(nu_hat + f(self.eps_root)) + f(self.eps))
