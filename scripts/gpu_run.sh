@@ -44,6 +44,7 @@ for step in "$@"; do
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmask) run pytest_mask 600 python -u -m pytest tests/test_gpu_acrobot_mask.py tests/test_gpu_parity.py tests/test_dopri5.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testcoef) run pytest_coef 600 python -u -m pytest tests/test_coefficients.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    gradtime) run gradtime 300 python scripts/grad_time.py || exit 1 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_c3) run bench_c3 600 python bench.py || exit 1 ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 || exit 1 ;;
