@@ -264,3 +264,155 @@ def test_gpu_dynamic_notebook_config_bitexact():
     d = ff.prepare(data)
     ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
     assert bits_equal(fit[0], ref)
+
+
+# -------------------------------------------------------------------- DynamicPolicy.ipynb
+def dynamic_notebook(max_steps=1000):
+    """DynamicPolicy.ipynb cells 0-4: key = PRNGKey(1); init_key, data_key = split(key);
+    get_data(data_key, Acrobot(0.05, 0.1), 16, 0.2, 50, "Constant"); state_size 2; the notebook's
+    evaluator Dopri5 + PIDController(1e-4, 1e-4, dtmin=0.001), dt0 0.05, max_steps 1000
+    (DynamicPolicy.ipynb:105); size_parsinomy 0 (the gp.py:72 default)."""
+    env = mt.Acrobot(0.05, 0.1)
+    _init_key, data_key = prng.split(prng.PRNGKey(1))
+    data = mt.environments.jax_control_data(data_key, env, 16, 0.2, 50.0)
+    variables = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
+    lib = mt.NodeLibrary(CONTROL_OPS, variables, [2, 1])
+    ff = mt.DynamicEvaluator(env, 2, 0.05, solver=mt.Dopri5(), max_steps=max_steps,
+                             stepsize_controller=mt.PIDController(atol=1e-4, rtol=1e-4, dtmin=0.001))
+    return env, lib, ff, data, variables
+
+
+# The printed bests (DynamicPolicy.ipynb:118, 123, 127) as trees.  to_string prints every
+# coefficient with 2 decimals and sympy then multiplies them out (gp.py:318-319, 344), so the long
+# decimals are sympy's values of coefficient expressions: 0.913088940312308 = cos(0.42),
+# 0.134250724017567 = 0.16*(cos(0.16*0.27) - 0.16), 0.128749603586318 = 0.16*(cos(0.27*cos(0.16))
+# - 0.16) (found by exhaustive search over the 2-decimal coefficients the runs print), -0.285 =
+# -0.30*0.95, 2*a1 = a1 + a1, 2*a2**2 = (a2 + a2)*a2.  The exact tree shapes are not recoverable
+# from the sympy form; other shapes differ in the last bits only, which the ulp ensemble covers.
+def _dyn_gen5(c):  # [-0.285*y1, 0.913088940312308*u + 0.913088940312308*y3], [-0.95*a1 - 4.15*a2]
+    return [("*", ("*", c[0], c[1]), "y1"), ("*", ("+", "u", "y3"), ("cos", c[2])),
+            ("-", ("*", c[3], "a1"), ("*", c[4], "a2"))]
+
+
+def _dyn_gen30(c):  # [(-a1 - sin(y4)*sin(y1 + 1.24) + 1.24)*sin(y4), (u + y3)*cos(0.134250724017567*y3)],
+    #                  [a1*a2 + 2*a1 - 3.15*a2 - cos(2.15*a2) - 2.46]
+    return [("*", ("-", ("-", c[0], "a1"), ("*", ("sin", "y4"), ("sin", ("+", "y1", c[1])))), ("sin", "y4")),
+            ("*", ("+", "u", "y3"), ("cos", ("*", ("*", c[2], ("-", ("cos", ("*", c[3], c[4])), c[5])), "y3"))),
+            ("-", ("-", ("+", ("*", "a1", "a2"), ("+", "a1", "a1")), ("*", c[6], "a2")),
+             ("+", ("cos", ("*", c[7], "a2")), c[8]))]
+
+
+def _dyn_gen50(c):  # [(-a1 - sin(y1)*sin(sin(y1 + 1.24)) - sin(y4)*sin(-a1 + y1 + 1.24) + 1.24)*sin(y4),
+    #                   (u + y3)*cos(0.128749603586318*y3)], [2*a1 + 2*a2**2 - a2 - cos(cos(2.15*a2)) - 1.73]
+    return [("*", ("-", ("-", ("-", c[0], "a1"), ("*", ("sin", "y1"), ("sin", ("sin", ("+", "y1", c[1]))))),
+                   ("*", ("sin", "y4"), ("sin", ("+", ("-", "y1", "a1"), c[2])))), ("sin", "y4")),
+            ("*", ("+", "u", "y3"), ("cos", ("*", ("*", c[3], ("-", ("cos", ("*", c[4], ("cos", c[5]))), c[6])), "y3"))),
+            ("-", ("-", ("+", ("+", "a1", "a1"), ("*", ("+", "a2", "a2"), "a2")), "a2"),
+             ("+", ("cos", ("cos", ("*", c[7], "a2"))), c[8]))]
+
+
+DYNAMIC_PINS = {  # generation: (tree factory, printed 2-decimal coefficients, printed best fitness)
+    "gen5": (_dyn_gen5, [-0.30, 0.95, 0.42, -0.95, 4.15], 171.8213),
+    "gen30": (_dyn_gen30, [1.24, 1.24, 0.16, 0.16, 0.27, 0.16, 3.15, 2.15, 2.46], 133.5592),
+    "gen50": (_dyn_gen50, [1.24, 1.24, 1.24, 0.16, 0.27, 0.16, 0.16, 2.15, 1.73], 129.2088),
+}
+
+
+def _dyn_candidate(lib, make, c):
+    return np.stack([tree_from_expr(e, lib, 30) for e in make([float(v) for v in c])])
+
+
+def _dyn_box(lib, make, c, n, seed=7):
+    """n candidates with every printed coefficient drawn uniformly from its rounding box +-0.005"""
+    rng = np.random.default_rng(seed)
+    return np.stack([_dyn_candidate(lib, make, [v + rng.uniform(-0.005, 0.005) for v in c]) for _ in range(n)])
+
+
+def _dyn_ensemble(name, max_steps, n_ulp=16, n_box=32):
+    """fitness of the pinned candidate over a one-ulp x0 ensemble (central coefficients) and over
+    its coefficient rounding box (notebook data)"""
+    make, c, _ = DYNAMIC_PINS[name]
+    env, lib, ff, data, _ = dynamic_notebook(max_steps)
+    d = ff.prepare(data)
+    model = oracle_model(ff, d)
+    pop = _dyn_candidate(lib, make, c)[None]
+    ulp = [orc.evaluate(model, pop, lib, oracle_rollouts(_perturbed(d, 100 + s)))["fitness"][0] for s in range(n_ulp)]
+    box = orc.evaluate(model, _dyn_box(lib, make, c, n_box), lib, oracle_rollouts(d))["fitness"]
+    return np.concatenate([np.float32(ulp), box])
+
+
+def test_dynamic_notebook_trees_print_like_the_notebook():
+    """The reconstructed trees render (through the reference's own printer, restated in
+    GeneticProgramming.to_string) to the notebook's strings up to sympy's term order."""
+    import sympy
+    env, lib, ff, data, variables = dynamic_notebook()
+    strategy = _gp(CONTROL_OPS, variables, [2, 1], ff, 2)
+    printed = {"gen5": "[-0.285*y1, 0.913088940312308*u + 0.913088940312308*y3], [-0.95*a1 - 4.15*a2]",
+               "gen30": "[(-a1 - sin(y4)*sin(y1 + 1.24) + 1.24)*sin(y4), (u + y3)*cos(0.134250724017567*y3)], "
+                        "[a1*a2 + 2*a1 - 3.15*a2 - cos(2.15*a2) - 2.46]",
+               "gen50": "[(-a1 - sin(y1)*sin(sin(y1 + 1.24)) - sin(y4)*sin(-a1 + y1 + 1.24) + 1.24)*sin(y4), "
+                        "(u + y3)*cos(0.128749603586318*y3)], [2*a1 + 2*a2**2 - a2 - cos(cos(2.15*a2)) - 1.73]"}
+    for name, (make, c, _) in DYNAMIC_PINS.items():
+        ours = strategy.to_string(_dyn_candidate(lib, make, c))
+        split = lambda s: [e.strip() for e in s.replace("[", "").replace("]", "").split(", ")]
+        for a, b in zip(split(ours), split(printed[name])):
+            diff = sympy.simplify(sympy.parse_expr(a) - sympy.parse_expr(b))
+            assert abs(float(diff.subs({s: 0.3 for s in diff.free_symbols}))) < 1e-9, (name, a, b)
+
+
+def test_dynamic_notebook_solves_sit_on_the_max_steps_edge():
+    """Why DynamicPolicy's printed values cannot be matched closely: every rollout of the printed
+    bests needs about max_steps = 1000 Dopri5 attempts (obs noise resampled in every stage keeps
+    the PID controller near the noise floor), and a solve cut at max_steps scores 250 + cost_0
+    (the +inf fill is masked out of acrobot.py:82's cost and never reaches the threshold) -- so
+    the fitness hinges on how many of 16 attempt counts fall below 1000.  At max_steps 800 every
+    rollout of the gen-5 best is cut; at 4000 none is, and the fitness drops by > 30."""
+    make, c, _ = DYNAMIC_PINS["gen5"]
+    out = {}
+    for ms in (800, 1000, 4000):
+        env, lib, ff, data, _ = dynamic_notebook(ms)
+        d = ff.prepare(data)
+        out[ms] = orc.evaluate(oracle_model(ff, d), _dyn_candidate(lib, make, c)[None], lib, oracle_rollouts(d))
+    assert np.all(out[800]["rollout_fitness"] >= 250.0)
+    assert np.all(np.isfinite(out[4000]["rollout_fitness"]))
+    assert out[1000]["fitness"][0] - out[4000]["fitness"][0] > 30.0
+    assert (out[4000]["rollout_fitness"] < 250.0).sum() == 16
+
+
+@pytest.mark.parametrize("name", list(DYNAMIC_PINS))
+def test_dynamic_notebook_printed_best_in_ensemble_tail(name):
+    """Each printed best (gen 5 / 30 / 50) against the oracle's ensemble: one-ulp x0 moves (16) and
+    the printed coefficients' rounding boxes (32 draws).  The ensemble is wide (the noisy solves
+    are chaotic at the last bit: sd 3-10 units), and the printed value is the minimum over 500
+    evolving candidates, so it must sit in the ensemble's lower tail.  With the attempt limit
+    relaxed (max_steps 4000, no solve cut) it does for all three: min <= printed <= mean.  At the
+    notebook's max_steps 1000 the gen-5 and gen-30 values lie below our whole ensemble: our solves
+    are cut more often than the reference's were (DESIGN.md "Parity pins": a few % more Dopri5
+    attempts than diffrax took would do it; not resolvable without diffrax).  The test asserts
+    what holds and pins the measured gap so that a change in either direction is noticed."""
+    printed = DYNAMIC_PINS[name][2]
+    relaxed = _dyn_ensemble(name, 4000)
+    assert np.all(np.isfinite(relaxed))
+    assert relaxed.min() <= printed + 1.0 and printed <= relaxed.mean(), (name, relaxed.min(), relaxed.mean())
+    assert relaxed.mean() - printed < 4.0 * relaxed.std() + 1.0, (name, relaxed.mean(), relaxed.std())
+    notebook = _dyn_ensemble(name, 1000)
+    assert printed <= notebook.max()
+    gap = {"gen5": (25.0, 35.0), "gen30": (3.0, 9.0), "gen50": (-1.0, 2.0)}[name]  # measured: 28.3 / 5.4 / -0.6
+    assert gap[0] <= notebook.min() - printed <= gap[1], (name, notebook.min(), printed)
+
+
+@pytest.mark.gpu
+def test_gpu_dynamic_notebook_pins_bitexact():
+    """The pinned DynamicPolicy candidates (central + rounding-box draws) through
+    GeneticProgramming.evaluate_population on the GPU at the notebook's max_steps and at 4000:
+    bit-exact with the oracle, so the ensemble statements above hold for the HIP path."""
+    for ms in (1000, 4000):
+        env, lib, ff, data, variables = dynamic_notebook(ms)
+        d = ff.prepare(data)
+        pop = np.concatenate([np.stack([_dyn_candidate(lib, make, c) for make, c, _ in DYNAMIC_PINS.values()]),
+                              *[_dyn_box(lib, make, c, 7) for make, c, _ in DYNAMIC_PINS.values()]])
+        pop = pop[:pop.shape[0] // 2 * 2]
+        strategy = _gp(CONTROL_OPS, variables, [2, 1], ff, pop.shape[0])
+        fit, _ = strategy.evaluate_population(pop[None], data)
+        ref = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
+        assert bits_equal(fit[0], ref), ms
