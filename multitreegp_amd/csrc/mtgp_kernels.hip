@@ -26,6 +26,7 @@
 #include <mutex>
 #include <type_traits>
 #include "mtgp.h"
+#include "mtgp_ab.h"
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_dopri5.h"
@@ -144,6 +145,13 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
                                            float dx[4]) {
   const float control = mtgp_clip1(u_raw);
   const float th1 = x[0], th2 = x[1], thd1 = x[2], thd2 = x[3];
+#if MTGP_AB_NODRIFT  // diagnostic (mtgp_ab.h): no drift arithmetic at all
+  dx[0] = thd1; dx[1] = thd2; dx[2] = control; dx[3] = -control;
+  return;
+#endif
+#if MTGP_AB_NOTRIG  // diagnostic: one multiply per trig value
+  const float s2 = th2 * 0.5f, c2 = th2 * 0.25f, s1 = th1 * 0.5f, ca = (th1 + th2) * 0.5f, cb = th1 * 0.25f;
+#else
   // the five trig values of the drift (mtgp_sinf / mtgp_cosf bit for bit), with ONE wave-uniform
   // test for lanes that need the slow reduction (|arg| >= 2^17)
   const float ea = (th1 + th2) - MTGP_HALF_PI_F, eb = th1 - MTGP_HALF_PI_F;
@@ -158,15 +166,22 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
     ca = mtgp_cosf(ea);
     cb = mtgp_cosf(eb);
   }
+#endif
+#if MTGP_AB_NODIV  // diagnostic: the four divisions as products
+#define MTGP_ACRO_DIV(a, b) ((a) * (b))
+#else
+#define MTGP_ACRO_DIV(a, b) ((a) / (b))
+#endif
   const float d1 = ((k.d1a + k.m2 * (k.l1sq_lc2sq + k.two_l1lc2 * c2)) + 1.0f) + 1.0f;
   const float d2 = k.m2 * (k.lc2sq + k.l1lc2 * c2) + 1.0f;
   const float phi2 = k.m2lc2g * ca;
   const float phi1 = (((k.A0 * (thd2 * thd2)) * s2 - ((k.B0 * thd1) * thd2) * s1) +
                       k.C0 * cb) + phi2;
-  const float num = ((control + (d2 / d1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
-  const float den = k.den0 - (d2 * d2) / d1;
-  const float a2 = num / den;
-  const float a1 = (-((d2 * a2) + phi1)) / d1;
+  const float num = ((control + MTGP_ACRO_DIV(d2, d1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
+  const float den = k.den0 - MTGP_ACRO_DIV(d2 * d2, d1);
+  const float a2 = MTGP_ACRO_DIV(num, den);
+  const float a1 = MTGP_ACRO_DIV(-((d2 * a2) + phi1), d1);
+#undef MTGP_ACRO_DIV
   dx[0] = thd1;
   dx[1] = thd2;
   dx[2] = a1;
@@ -251,9 +266,6 @@ __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, fl
   }
 }
 
-#ifndef MTGP_V_OBSFAST
-#define MTGP_V_OBSFAST 1
-#endif
 // y = C@x + nz with C = eye(n_var)[:n_obs]: all NV components are formed, the programs read only
 // the first n_obs (the flattener places the data slots after the observations behind all NV,
 // MtgpProgramSpec.gap) and only those are stored as ys.  (C@x)_i + nz_i
@@ -263,20 +275,23 @@ __device__ __forceinline__ void obs_noise_vec(const ObsNoise<NO>& z, float t, fl
 template <class Env>
 __device__ __forceinline__ void ctl_obs_apply(const float x[Env::NV], const float nz[Env::NV], float y[Env::NV]) {
   constexpr int NV = Env::NV;
+#if MTGP_AB_NOOBS  // diagnostic: observation = state
+#pragma unroll
+  for (int i = 0; i < NV; ++i) y[i] = x[i] + nz[i];
+  return;
+#endif
   bool fin[NV], all = true;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     fin[j] = mtgp_isfinite(x[j]);
     all = all && fin[j];
   }
-#if MTGP_V_OBSFAST
   if (__builtin_expect(__all(all), 1)) {  // every lane's state finite (the common case): no NaN masking
 #pragma unroll
     for (int i = 0; i < NV; ++i) y[i] = x[i] + nz[i];
     Env::obs_transform(y);
     return;
   }
-#endif
   const float qn = mtgp_qnan();
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
@@ -582,18 +597,13 @@ struct EnvReactor {
 // The adaptive kernels' save points are divergent (each round writes one dword per lane into
 // different rows), so their partial lines are left to L2 to merge: plain stores there
 // (DP = true; non-temporal partial writes made the C3 Dopri5 kernel 44 % slower).
-#ifndef MTGP_V_NTSTORE
-#define MTGP_V_NTSTORE 1
-#endif
 template <bool DP = false>
 __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
   float* p = arr + row;
-#if MTGP_V_NTSTORE
   if (!DP) {
     __builtin_nontemporal_store(v, p + off);
     return;
   }
-#endif
   p[off] = v;
 }
 
@@ -617,10 +627,6 @@ struct Lane {
   uint32_t jtab;  // lane j < n_prog: JIT code offset of this wave's program-j unit
   bool jok;       // the JIT code of this launch is complete (plan status 0, fits the buffer)
 };
-
-#ifndef MTGP_V_PTAB
-#define MTGP_V_PTAB 1
-#endif
 
 // program-block offsets of the wave's groups, one per lane (read back with v_readlane)
 __device__ __forceinline__ uint32_t prog_table(const KArgs& A, const Lane& L) {
@@ -702,13 +708,9 @@ __device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
 
 // The same for a whole state vector, branching on the (wave-uniform) stage once instead of
 // selecting per component: the same operations, so the same bits.
-#ifndef MTGP_V_STAGEBR
-#define MTGP_V_STAGEBR 1
-#endif
 template <int N>
 __device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&k)[N], float h, float h2,
                                            float (&out)[N]) {
-#if MTGP_V_STAGEBR
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
@@ -718,14 +720,9 @@ __device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = MTGP_FMAF(c, k[i], s[i]);
   }
-#else
-#pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = stage_in(stage, s[i], k[i], h, h2);
-#endif
 }
 template <int N>
 __device__ __forceinline__ void stage_acc_n(int stage, float (&acc)[N], const float (&k)[N]) {
-#if MTGP_V_STAGEBR
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
@@ -737,10 +734,6 @@ __device__ __forceinline__ void stage_acc_n(int stage, float (&acc)[N], const fl
 #pragma unroll
     for (int i = 0; i < N; ++i) acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]);
   }
-#else
-#pragma unroll
-  for (int i = 0; i < N; ++i) acc[i] = stage_acc(stage, acc[i], k[i]);
-#endif
 }
 
 // --------------------------------------------------------------------------------------
@@ -807,47 +800,15 @@ __device__ __forceinline__ ChainOut jit_call_chain(uint64_t addr_, const float d
   return r;
 }
 
-#ifndef MTGP_V_NOPROG
-#define MTGP_V_NOPROG 0
-#endif
-#ifndef MTGP_V_NOFALLBACK
-#define MTGP_V_NOFALLBACK 0  // diagnostic only: ignore the JIT's slow-lane report (A/B), never shipped
-#endif
-#ifndef MTGP_V_UNROLL
-#define MTGP_V_UNROLL 0
-#endif
-#ifndef MTGP_V_TIMING
-#define MTGP_V_TIMING 0  // diagnostic only: per-wave start/end clock + HW_ID (residency study), never shipped
-#endif
-#if MTGP_V_TIMING
-__device__ uint64_t g_wave_probe[65536 * 4];
-__device__ __forceinline__ void probe(const Lane& L, int what) {
-  const int w = uni((int)(blockIdx.x * kWavesPerBlock + L.wave));
-  if (L.lane == 0 && w < 65536) {
-    g_wave_probe[w * 4 + what] = __builtin_amdgcn_s_memrealtime();
-    if (what == 0) g_wave_probe[w * 4 + 2] = (uint64_t)__builtin_amdgcn_s_getreg((4 << 0) | (0 << 6) | (31 << 11));
-  }
-}
-#define MTGP_PROBE(L, w) probe(L, w)
-#else
-#define MTGP_PROBE(L, w)
-#endif
-
 // The interpreter as an out-of-line function for the JIT kernels' fallback sites (lanes that need
 // the slow sin/cos reduction, populations without usable code).  Inlined, its dispatch trees
 // make the C3 kernel 190 KB of code (19 KB out of line), but the call costs more than the
 // instruction fetch it saves: the call ABI spills SGPRs into VGPR lanes and a few VGPRs to
 // scratch inside the stage loop.  A/B in one process (profiles/r03/v5_ab_cold.log): C3 kernel
-// 2.60 ms out of line vs 2.30 inline, C2 1.06 vs 0.91, C5 7.51 vs 7.14.  Kept inline (0).
-#ifndef MTGP_COLD_INTERP
-#define MTGP_COLD_INTERP 0
-#endif
-// The Dopri5 kernels (two waves per SIMD, 183 VGPRs) can take the fallback out of line too
-// (MTGP_DP_COLD=1); measured on C3 Dopri5 (profiles/r03/v8_dptail.log vs v6): full population
-// 21.4 vs 20.2 ms, a lone tail wave 10.6 vs 9.9 us per attempt -- inline kept.
-#ifndef MTGP_DP_COLD
-#define MTGP_DP_COLD 0
-#endif
+// 2.60 ms out of line vs 2.30 inline, C2 1.06 vs 0.91, C5 7.51 vs 7.14.  Kept inline
+// (MTGP_COLD_INTERP = 0, mtgp_ab.h).  The Dopri5 kernels (two waves per SIMD, 183 VGPRs) can take
+// the fallback out of line too (MTGP_DP_COLD); measured on C3 Dopri5 (profiles/r03/v8_dptail.log vs
+// v6): full population 21.4 vs 20.2 ms, a lone tail wave 10.6 vs 9.9 us per attempt -- inline kept.
 typedef __attribute__((address_space(3))) float LdsFloat;
 __device__ __attribute__((noinline)) float run_prog_cold(const MtgpInstr* code, uint32_t dcol_lds, uint32_t st_lds) {
   const float* dcol = (const float*)(LdsFloat*)(uintptr_t)dcol_lds;
@@ -862,14 +823,9 @@ __device__ __forceinline__ uint32_t lds_addr_of(const float* p) {
 template <bool COLD = false>
 __device__ __forceinline__ float run_one_interp(const KArgs& A, const Lane& L, int gi, int slot, const float* dcol,
                                                 float* st) {
-#if MTGP_V_PTAB
   const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.ptab, gi) +
                        (uint32_t)slot * (uint32_t)A.L * (uint32_t)sizeof(MtgpInstr);
   const MtgpInstr* code = (const MtgpInstr*)((const char*)A.prog + off);
-#else
-  const size_t pj = (size_t)group_ind(A, L, gi) * A.n_prog + slot;
-  const MtgpInstr* code = A.prog + pj * A.L;
-#endif
   if (COLD) return run_prog_cold(code, lds_addr_of(dcol), lds_addr_of(st));
   return run_prog(code, dcol, st);
 }
@@ -901,7 +857,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
     if (__builtin_expect(L.jok, 1)) {
       const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first);
       uint64_t fl = 0;
-#if MTGP_V_NOPROG  // diagnostic only (A/B): no program call at all
+#if MTGP_AB_NOPROG  // diagnostic only (A/B): no program call at all
       (void)off;
       const ChainOut r = {{0.0f, 0.0f, 0.0f, 0.0f}, 0.0f};
 #else
@@ -910,7 +866,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = r.v[j < mtgp::kJitChainMax ? j : 0];
       if (save_prog >= 0) *save_v = r.tail;
-      if (!MTGP_V_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // slow sin/cos lanes: re-run the chain's
+      if (!MTGP_AB_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // slow sin/cos lanes: re-run the chain's
         bool spilled = false;                                      // programs for the groups concerned
         for (int gi = 0; gi < ng; ++gi) {
           if (!(fl & __ballot(L.g == gi && L.active))) continue;
@@ -936,13 +892,13 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
       for (int q = 0; q < M; ++q) {
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first + q);
         uint64_t fl = 0;
-#if MTGP_V_NOPROG  // diagnostic only: the environment without any program call (A/B), never shipped
+#if MTGP_AB_NOPROG  // diagnostic only: the environment without any program call (A/B), never shipped
         (void)off;
         float v = 0.0f;
 #else
         float v = jit_call(A.jit_base + off, D.v, fl);
 #endif
-        if (!MTGP_V_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: re-run only
+        if (!MTGP_AB_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: re-run only
           bool spilled = false;               // this program, only for the groups concerned
           for (int gi = 0; gi < ng; ++gi) {
             if (!(fl & __ballot(L.g == gi && L.active))) continue;
@@ -950,12 +906,6 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
             const float t = run_one_interp<JIT && COLD>(A, L, gi, first + q, D.dcol, D.st);
             v = (L.g == gi) ? t : v;
           }
-#if MTGP_V_TIMING
-          if (spilled && L.lane == 0) {
-            const int w = (int)(blockIdx.x * kWavesPerBlock + L.wave);
-            if (w < 65536) g_wave_probe[w * 4 + 3] += 1;
-          }
-#endif
         }
 #pragma unroll
         for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
@@ -979,7 +929,6 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 
 
 __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, float F) {
-  MTGP_PROBE(L, 1);
   const float mx = A.m.max_fitness;
   if (A.out.rollout_fitness && L.active) A.out.rollout_fitness[(size_t)L.p * A.ro.R + L.r] = F;
   if (L.W > 1) return;  // lane set over several waves: k_rollout_mean forms the fitness
@@ -1049,7 +998,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int na = NA <= 3 ? NA : uni(A.m.state_size);
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -1123,11 +1071,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       ++save_k;
     }
     bool stop = last;
-#if MTGP_V_UNROLL
-#pragma unroll
-#else
 #pragma unroll 1
-#endif
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
       stage_in_n<NV>(stage, x, kx, h, h2, xt);
@@ -1180,10 +1124,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
           }
           if constexpr (Env::kMask) {
             if (active) env.fit_save(fit, k, S, A, PR, loff, dead, us, x);
-          } else if (!dead) {
+          } else if (!dead && !MTGP_AB_NOFIT) {
             env.fit_update(fit, k, S, A.ro.ts, us, x);
           }
-          if (TRAJ && active) {
+          if (TRAJ && active && !MTGP_AB_NOSTORE) {
             if (A.out.xs) {
 #pragma unroll
               for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i]);
@@ -1240,7 +1184,6 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -1459,9 +1402,7 @@ struct DpParked {
   }
 };
 
-#ifndef MTGP_DP_WAVES
-#define MTGP_DP_WAVES 2  // register budget of the Dopri5 control kernels (A/B: 2 beats 4, C3 23 vs 28 ms)
-#endif
+// MTGP_DP_WAVES (mtgp_ab.h, 2): register budget of the Dopri5 control kernels (A/B: 2 beats 4, C3 23 vs 28 ms)
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_DP_WAVES))) k_ctl_dopri5(KArgs A) {
   constexpr int NV = Env::NV;
@@ -1686,7 +1627,6 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
-  MTGP_PROBE(Ln, 0);
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
@@ -1964,10 +1904,8 @@ __device__ __forceinline__ uint32_t lds_address(const float* p) {
 
 
 // The per-save MSE (components summed in index order, sr.py:24) is needed by wave 0 only, which
-// writes the fitness; the other waves skip the 64 LDS reads (MTGP_V_MSE0=0: every wave sums).
-#ifndef MTGP_V_MSE0
-#define MTGP_V_MSE0 1
-#endif
+// writes the fitness; the other waves skip the 64 LDS reads (every wave summing measured 0.7 %
+// slower at C5, profiles/r03/v10_ab_noprog_mse.log).
 template <bool TRAJ, bool JIT>
 __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   extern __shared__ float wl[];
@@ -2030,7 +1968,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
         }
       }
       __syncthreads();
-      if (!MTGP_V_MSE0 || w == 0) {  // (only wave 0 reports the fitness: finish_group)
+      if (w == 0) {  // (only wave 0 reports the fitness: finish_group)
         float sq = nxt[0];
         for (int d = 1; d < NV; ++d) sq = sq + nxt[d * kWave];
         tot = tot + sq;
@@ -2058,7 +1996,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       if (JIT && Ln.jok && A.chain_store) {  // one call: this wave's components' units, results into nxt
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c0);
         uint64_t fl = 0;
-#if MTGP_V_NOPROG  // diagnostic only (A/B): the stage glue without the program calls
+#if MTGP_AB_NOPROG  // diagnostic only (A/B): the stage glue without the program calls
         (void)off;
         for (int t = 0; t < kWideComp; ++t)
           if (c0 + t < NV) nxt[(c0 + t) * kWave] = 0.0f;
@@ -2383,9 +2321,6 @@ __global__ void __launch_bounds__(256) k_eval_programs(const MtgpInstr* __restri
 // translation (jit_words: fall-through code words, < 0 if untranslatable; jit_cost: the schedule
 // weight), so the JIT build needs no translation pass of its own before the code is emitted.
 constexpr int32_t kFlatSerial = 0x7fff;  // status of a program left to k_flatten_serial
-#ifndef MTGP_V_LDS_SERIAL_SIZE
-#define MTGP_V_LDS_SERIAL_SIZE 0
-#endif
 
 // JIT sizing of one flattened program (mtgp_flatten_ex jit_words / jit_cost)
 __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n, int32_t* jit_words_out,
@@ -2618,15 +2553,9 @@ __global__ void __launch_bounds__(64) k_flatten_serial(const float* __restrict__
 
 // lanes per block: the flatten is issue-latency bound (one tree per lane, few lanes in total), so
 // several small waves per SIMD beat one full one
-#ifndef MTGP_FLAT_LANES
-#define MTGP_FLAT_LANES 16
-#endif
 
 // The lane-per-program flattener is the round-1 design, kept for A/B runs only: built with
 // -DMTGP_AB_FLAT_LANE=1 (MTGP_FLAT_MODE=lane then selects it); the product launches k_flatten_wave.
-#ifndef MTGP_AB_FLAT_LANE
-#define MTGP_AB_FLAT_LANE 0
-#endif
 template <int NMAX, int TPB>
 __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, int P, int T, int N,
                                                             MtgpNodeLibrary lib,
@@ -3112,16 +3041,13 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       s_prog[n > 0 ? n : 0] = e;
       len_out[pj] = n > 0 ? n : 0;
       status_out[pj] = n > 0 ? 0 : -n;
-#if MTGP_V_LDS_SERIAL_SIZE  // A/B only: the LDS-data sizing by one lane (jit_program), round-2 behaviour
-      if (jit_mode != kJitModeRegs) flat_jit_size(s_prog, L, n, jit_words_out, jit_cost_out, pj, jit_mode);
-#endif
     }
   }
   if (!shared && (jit_words_out || jit_cost_out)) {  // (shared: wave-uniform)
     constexpr int KI = (2 * NMAX + 8 + kWave - 1) / kWave;
     if (jit_mode == kJitModeRegs)
       flat_jit_size_wave<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
-    else if (!MTGP_V_LDS_SERIAL_SIZE)
+    else
       flat_jit_size_wave_lds<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane, s_fpos);
   }
   // node count (gp.py:424 parsimony).  Few trees (T <= kFlatDirectTrees): the individual's first
@@ -3920,11 +3846,6 @@ extern "C" {
 
 int mtgp_abi_version(void) { return MTGP_ABI_VERSION; }
 
-#if MTGP_V_TIMING
-int mtgp_debug_probe(uint64_t* host, size_t n) {  // diagnostic variant only
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_wave_probe), n * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
-}
-#endif
 
 int mtgp_jit_alloc(int32_t device, size_t bytes, void** code) {
   if (!code || bytes == 0) return MTGP_ERR_ARG;

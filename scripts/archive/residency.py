@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Wave residency study (diagnostic variant MTGP_V_TIMING): per-wave start/end real-time
+"""Wave residency study (diagnostic variant MTGP_AB_TIMING (removed in round 4)): per-wave start/end real-time
 stamps and HW_ID of the C3 evaluation, to see whether all waves are co-resident."""
 import argparse, ctypes, json, os, sys
 import numpy as np

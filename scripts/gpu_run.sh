@@ -77,6 +77,16 @@ for step in "$@"; do
     ab_c3_bfm) run ab_c3_bfm 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,shift" --tag c3_bfm || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
+    budget)  # C3 per-section budget: interleaved timing of every lib/abrun variant, then one SQ pass each
+      V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
+      run budget_time 600 python scripts/kvariants.py --config c3 --rounds 4 --variants $V --tag budget || exit 1
+      for v in ${V//,/ }; do
+        L=multitreegp_amd/lib/libmtgp_hip.so; [ $v != prod ] && L=multitreegp_amd/lib/abrun/libmtgp_hip_$v.so
+        run budget_pmc_$v 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY \
+          SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM -d $O/budget_pmc_$v -o pmc --output-format csv -- \
+          python3 scripts/kprof.py --iters 2 --config c3 --lib $L || exit 1
+        python3 scripts/pmc_summary.py $O/budget_pmc_$v k_ctl_dynamic > $O/budget_pmc_$v.json; cat $O/budget_pmc_$v.json
+      done ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;

@@ -48,10 +48,11 @@ def main():
         envs[v] = dict(x.split("=", 1) for x in kv)
         # variants/ is gpurun-ignored (never pushed wholesale): libraries for an A/B run are copied to lib/ab/
         path = nat.LIB_PATH
-        if name != "prod":
-            path = os.path.join(ROOT, "multitreegp_amd", "lib", "ab", f"libmtgp_hip_{name}.so")
-            if not os.path.exists(path):
-                path = os.path.join(ROOT, "multitreegp_amd", "lib", "variants", f"libmtgp_hip_{name}.so")
+        if name != "prod":  # scripts/build_ab.py output (lib/abrun), else an older variant build
+            for sub in ("abrun", "ab", "variants"):
+                path = os.path.join(ROOT, "multitreegp_amd", "lib", sub, f"libmtgp_hip_{name}.so")
+                if os.path.exists(path):
+                    break
         engines[v] = DeviceEngine(ff, lib, 0.0, dev, native=nat.load(path))
         engines[v].native.mtgp_set_timing(1)
     pop_dev = torch.from_numpy(pop).to(dev)
