@@ -185,7 +185,12 @@ def cpu_baseline(args, lib, ff, data, pop, steps=None):
     d = ff.prepare(data)
     model = oracle_model(ff, d)
     ro = oracle_rollouts(d)
-    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    # threads: OpenMP's team size, OMP_NUM_THREADS when set -- the GPU pool sets it to the job's CPU
+    # share (16 per GPU) and asks jobs not to exceed it -- else the process's CPU affinity;
+    # os.cpu_count() is the whole host
+    affinity = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", affinity))
+    threads = omp
     n = 16
     while True:
         t0 = time.perf_counter()
@@ -200,7 +205,11 @@ def cpu_baseline(args, lib, ff, data, pop, steps=None):
     else:
         units = n * d["R"] * d["n_steps"]
         what = f"{d['n_steps']} RK4 steps"
+    why = ("the CPU affinity of this process" if "OMP_NUM_THREADS" not in os.environ else
+           f"OMP_NUM_THREADS={omp}, set by the GPU pool as this job's CPU share (process affinity {affinity} of "
+           f"{os.cpu_count()} host CPUs)")
     return {"value": units / dt, "unit": "ODE-steps/s", "cores": threads, "kind": "port",
+            "cores_affinity": affinity, "cores_host": os.cpu_count(), "cores_why": why,
             "cpu_model": cpu_model(),
             "sample": f"{n} individuals x {d['R']} rollouts x {what} of the "
                       f"{args.config.upper()} workload, "
@@ -274,7 +283,7 @@ def main():
 
     def step():
         res = eng.evaluate(pop_dev, data, trajectories=traj, check=False, step_counts=adaptive)
-        fit = mdist.gather_fitness(res["fitness"], P * ws, P) if ws > 1 else res["fitness"]
+        fit = mdist.gather_fitness(res["fitness"], P * ws, P, check=False) if ws > 1 else res["fitness"]
         return res, fit
 
     res, _ = step()

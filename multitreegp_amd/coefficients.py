@@ -142,6 +142,20 @@ class CoefficientOptimiser:
         if ff.model_id != nat.MODEL_SR and getattr(ff, "state_size", 0) > 3:
             raise NotImplementedError("coefficient optimisation of the dynamic evaluator: state_size <= 3")
 
+    @staticmethod
+    def check_data(d: dict) -> None:
+        """The data-dependent limits of the gradient kernels on a prepared data dict (the
+        evaluator's `prepare`, host only), raised where the data is first seen
+        (GeneticProgramming.evaluate_population at every generation with coefficient_optimisation,
+        ADVICE r3), not at the first optimising generation (gp.py:418: generation 14): at most 64
+        rollouts (one lane set per candidate), and the Acrobot cost mask of ts on the save grid."""
+        if d.get("fit_kof") is not None:
+            raise NotImplementedError("coefficient optimisation of Acrobot with ts off the one-pass mask "
+                                      "(ts / (ts[1] - ts[0]) outside (k - 1, k + 1]): the general mask is not "
+                                      "differentiated")
+        if d["R"] > 64:
+            raise NotImplementedError("coefficient optimisation with more than 64 rollouts")
+
     def _grad_fn(self):
         eng = self.engine
         return eng.native.mtgp_sr_grad if eng.ff.model_id == nat.MODEL_SR else eng.native.mtgp_ctl_grad
@@ -158,10 +172,7 @@ class CoefficientOptimiser:
         B, T, N, _ = cands.shape
         rows = coefficient_rows(cands) if rows is None else rows
         d = eng.prepare_data(data)
-        if d.get("fit_kof") is not None:
-            raise NotImplementedError("coefficient optimisation of Acrobot with ts off the one-pass mask "
-                                      "(ts / (ts[1] - ts[0]) outside (k - 1, k + 1]): the general mask is not "
-                                      "differentiated")
+        self.check_data(d)
         n_data = eng.ff.n_data()
         specs, _ = eng._specs()
         cap = self.param_cap(n_data)
@@ -173,8 +184,6 @@ class CoefficientOptimiser:
         m = eng.model_struct(d)
         ro = eng.rollouts_struct(d)
         R = d["R"]
-        if R > 64:
-            raise NotImplementedError("coefficient optimisation with more than 64 rollouts")
         L = eng.program_stride(N)
         grad_fn = self._grad_fn()
         for lo in range(0, max(n_max, 1), cap):

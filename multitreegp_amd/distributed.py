@@ -39,31 +39,62 @@ def shard_bounds(P: int, world_size: int, rank: int) -> Tuple[int, int, int]:
     return lo, hi, per
 
 
-def gather_fitness(local: torch.Tensor, P: int, per: int, group=None) -> torch.Tensor:
-    """All-gather fixed-size fitness shards (padded to `per`) and trim to [P]."""
+class RankFailed(RuntimeError):
+    """Raised on every rank when another rank's shard failed (that rank raises its own error)."""
+
+
+def _check_status(status, err):
+    """status: per-rank 0 (ok) / 1 (failed) from the gathered buffers.  Every rank raises when any
+    failed: a rank's exception must not leave the others blocked in a later collective."""
+    if err is not None:
+        raise err
+    bad = [r for r, v in enumerate(status) if v != 0]
+    if bad:
+        raise RankFailed(f"rank(s) {bad} failed in their shard (see their own error)")
+
+
+def gather_fitness(local, P: int, per: int, group=None, err=None, check: bool = True) -> torch.Tensor:
+    """All-gather fixed-size fitness shards (padded to `per`) and trim to [P].  Each rank's block
+    carries one status word (local is None / err set when this rank's shard failed), so a failure
+    anywhere raises on every rank after the one collective instead of leaving ranks blocked.
+    check=False skips reading the status words back (no host synchronisation: bench.py's timed
+    loop, whose launches cannot fail between the status checks it makes before timing)."""
     rank, ws = world()
     if ws == 1:
+        if err is not None:
+            raise err
         return local[:P]
-    if dist.get_backend(group) == "gloo":  # CPU path: gloo takes host tensors, no all_gather_into_tensor
-        buf = torch.full((per,), float("inf"), dtype=local.dtype)
-        buf[: local.numel()] = local.cpu()
+    gloo = dist.get_backend(group) == "gloo"
+    dev = torch.device("cpu") if gloo else (local.device if local is not None else local_device())
+    buf = torch.full((per + 1,), float("inf"), dtype=torch.float32, device=dev)
+    if local is not None:
+        buf[: local.numel()] = local.to(dev)
+    buf[per] = 0.0 if err is None else 1.0
+    if gloo:  # CPU path: gloo takes host tensors, no all_gather_into_tensor
         parts = [torch.empty_like(buf) for _ in range(ws)]
         dist.all_gather(parts, buf, group=group)
-        return torch.cat(parts)[:P]
-    buf = torch.full((per,), float("inf"), dtype=local.dtype, device=local.device)
-    buf[: local.numel()] = local
-    out = torch.empty((per * ws,), dtype=local.dtype, device=local.device)
-    dist.all_gather_into_tensor(out, buf, group=group)  # RCCL over xGMI
-    return out[:P]
+        full = torch.stack(parts)
+    else:
+        full = torch.empty((ws * (per + 1),), dtype=torch.float32, device=dev)
+        dist.all_gather_into_tensor(full, buf, group=group)  # RCCL over xGMI
+        full = full.view(ws, per + 1)
+    if check or err is not None:
+        _check_status(full[:, per].tolist(), err)
+    return full[:, :per].reshape(-1)[:P]
 
 
 def sharded_fitness(evaluate_shard: Callable[[int, int], torch.Tensor], P: int, group=None) -> torch.Tensor:
     """evaluate_shard(lo, hi) -> fitness of individuals [lo, hi) on this rank's device;
-    returns the full [P] fitness on every rank."""
+    returns the full [P] fitness on every rank (an exception on any rank raises on all)."""
     rank, ws = world()
     lo, hi, per = shard_bounds(P, ws, rank)
-    local = evaluate_shard(lo, hi)
-    return gather_fitness(local, P, per, group)
+    if ws == 1:
+        return evaluate_shard(lo, hi)[:P]
+    try:
+        local, err = evaluate_shard(lo, hi), None
+    except Exception as e:  # noqa: BLE001 -- re-raised after the collective, on every rank
+        local, err = None, e
+    return gather_fitness(local, P, per, group, err)
 
 
 def sharded_rows(compute: Callable[[int, int], Tuple["np.ndarray", "np.ndarray"]], n: int, row_shape: tuple,
@@ -71,28 +102,37 @@ def sharded_rows(compute: Callable[[int, int], Tuple["np.ndarray", "np.ndarray"]
     """compute(lo, hi) -> (values [hi-lo] f32, rows [hi-lo, *row_shape] f32) of items [lo, hi)
     on this rank; returns the full (values [n], rows [n, ...]) on every rank.  Items are split
     into contiguous blocks like the population (shard_map's P('i'), gp.py:264-267 shard_optimise);
-    one all-gather of the padded blocks (values and rows packed together)."""
+    one all-gather of the padded blocks (values and rows packed together, plus one status row: an
+    exception on any rank -- a rank with an empty block included -- raises on all)."""
     import numpy as np
     rank, ws = world()
     if ws == 1:
         return compute(0, n)
     lo, hi, per = shard_bounds(n, ws, rank)
-    vals, rows = compute(lo, hi)
+    err = None
+    try:
+        vals, rows = compute(lo, hi)
+    except Exception as e:  # noqa: BLE001 -- re-raised after the collective, on every rank
+        vals = rows = None
+        err = e
     width = 1 + int(np.prod(row_shape))
-    buf = np.zeros((per, width), np.float32)
+    buf = np.zeros((per + 1, width), np.float32)
     m = hi - lo
-    if m > 0:
+    if m > 0 and err is None:
         buf[:m, 0] = np.asarray(vals, np.float32)
         buf[:m, 1:] = np.asarray(rows, np.float32).reshape(m, -1)
+    buf[per, 0] = 0.0 if err is None else 1.0
     t = torch.from_numpy(buf)
     if dist.get_backend(group) == "gloo":
         parts = [torch.empty_like(t) for _ in range(ws)]
         dist.all_gather(parts, t, group=group)
-        full = torch.cat(parts)
+        full = torch.stack(parts)
     else:  # RCCL: device buffers
         dev = local_device()
-        full = torch.empty((per * ws, width), dtype=torch.float32, device=dev)
+        full = torch.empty((ws * (per + 1), width), dtype=torch.float32, device=dev)
         dist.all_gather_into_tensor(full, t.to(dev), group=group)
-        full = full.cpu()
-    full = full.numpy()[:n]
+        full = full.cpu().view(ws, per + 1, width)
+    full = full.numpy()
+    _check_status(full[:, per, 0].tolist(), err)
+    full = full[:, :per].reshape(ws * per, width)[:n]
     return full[:, 0].copy(), full[:, 1:].reshape(n, *row_shape).copy()

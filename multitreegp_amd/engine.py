@@ -208,13 +208,11 @@ class DeviceEngine:
         return np.ascontiguousarray(np.asarray(x))
 
     @staticmethod
-    def data_fingerprint(data, sample_over: int = 1 << 16) -> tuple:
-        """Content key of a reference data tuple: shape, dtype and a 128-bit hash of every array
-        (nested tuples such as `params` included; torch tensors, CUDA ones too, read back).
-        Arrays up to `sample_over` bytes (all rollout data but an SR ground truth) are hashed in
-        full; larger ones by their first/last 4 KiB and 1024 evenly spaced elements, so the check
-        costs microseconds per call -- a larger array mutated in place elsewhere is
-        not detected; pass a new array instead."""
+    def data_fingerprint(data) -> tuple:
+        """Content key of a reference data tuple: shape, dtype and a 128-bit blake2b hash of every
+        array in full (nested tuples such as `params` included; torch tensors, CUDA ones too, read
+        back), so an array mutated in place anywhere is re-uploaded.  Hashing runs at
+        about 1 GB/s: ~0.4 ms for the C5 ground truth, microseconds for rollout data."""
         import hashlib
 
         def fp(x):
@@ -222,15 +220,8 @@ class DeviceEngine:
                 return ("seq", tuple(fp(y) for y in x))
             if x is None:
                 return None
-            a = DeviceEngine._host_array(x)
-            if a.nbytes <= sample_over:
-                body = a.tobytes()
-            else:
-                flat = a.reshape(-1)
-                step = max(1, flat.size // 1024)
-                body = b"".join((flat.view(np.uint8)[:4096].tobytes(), flat.view(np.uint8)[-4096:].tobytes(),
-                                 flat[::step].tobytes()))
-            return (a.shape, a.dtype.str, hashlib.blake2b(body, digest_size=16).digest())
+            a = np.ascontiguousarray(DeviceEngine._host_array(x))
+            return (a.shape, a.dtype.str, hashlib.blake2b(a.reshape(-1).view(np.uint8), digest_size=16).digest())
 
         return fp(data)
 

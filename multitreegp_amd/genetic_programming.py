@@ -151,6 +151,8 @@ class GeneticProgramming:
         P = self.num_populations * self.population_size
         flat = pops.reshape(P, *pops.shape[2:])
         g = self.current_generation
+        if self.coefficient_optimisation:  # on every rank, before any collective: all raise together
+            CoefficientOptimiser.check_data(self.fitness_function.prepare(data))
         if self.coefficient_optimisation and g > 10 and (g + 1) % 5 == 0:
             raw = mdist.sharded_fitness(lambda lo, hi: self._evaluate_shard(flat, lo, hi, data, 0.0), P)
             raw = raw.cpu().numpy()

@@ -761,3 +761,25 @@ def test_gpu_evaluate_population_optimises_control_coefficients():
     assert bits_equal(fit.reshape(-1), want)
     assert np.array_equal(newpop.reshape(pop.shape), want_pop)
     assert (L.min(axis=0) < L[0]).any()  # the optimisation improved some candidate
+
+
+def test_data_limits_raise_at_generation_0():
+    """coefficient optimisation's data limits (at most 64 rollouts; Acrobot ts on the
+    one-pass mask) raise at the first evaluate_population, not at generation 14 when the first
+    optimisation runs (gp.py:418).  Host-side check: no GPU needed, every rank raises together."""
+    from helpers import CONTROL_OPS, dynamic_setup
+    e, lib, ff, data, pop = dynamic_setup(P=8, R=100, n_steps=10, depth=3, N=16, seed=2)
+    gp = mt.GeneticProgramming(20, 8, ff, CONTROL_OPS, lib.variable_list, lib.layer_sizes, max_nodes=16,
+                               migration_percentage=0.5, elite_percentage=0.0, coefficient_optimisation=True,
+                               verbose=False)
+    assert gp.current_generation == 0
+    with pytest.raises(NotImplementedError, match="64 rollouts"):
+        gp.evaluate_population(pop[None], data)
+    e, lib, ff, data, pop = dynamic_setup(P=8, R=4, n_steps=10, depth=3, N=16, seed=2)
+    x0, ts, *rest = data
+    data_off = (x0, (ts + np.float32(1.0)).astype(np.float32), *rest)  # ts[0] = 1.0: off the one-pass mask
+    gp = mt.GeneticProgramming(20, 8, ff, CONTROL_OPS, lib.variable_list, lib.layer_sizes, max_nodes=16,
+                               migration_percentage=0.5, elite_percentage=0.0, coefficient_optimisation=True,
+                               verbose=False)
+    with pytest.raises(NotImplementedError, match="one-pass mask"):
+        gp.evaluate_population(pop[None], data_off)

@@ -220,3 +220,49 @@ def test_coefficient_optimisation_sharded():
         fit, back, bf, rsizes = res[r]
         assert fit == want_fit and back == want_pop and bf == want_bf
         assert rsizes == [25]
+
+
+def _fail_worker(rank, ws, port, q, which):
+    """rank 1 raises inside its shard (which = "fitness") or has an empty block and rank 0
+    raises (which = "rows"): every rank must raise, none may block in the collective."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        try:
+            if which == "fitness":
+                def shard(lo, hi):
+                    if rank == 1:
+                        raise ValueError("shard failed on rank 1")
+                    return torch.zeros(hi - lo)
+                mdist.sharded_fitness(shard, 6)
+            else:
+                def rows(lo, hi):  # n = 1 item: rank 1's block is empty
+                    if rank == 0:
+                        raise NotImplementedError("rank 0 cannot optimise")
+                    return np.zeros(hi - lo, np.float32), np.zeros((hi - lo, 2), np.float32)
+                mdist.sharded_rows(rows, 1, (2,))
+            q.put((rank, "returned"))
+        except Exception as e:  # noqa: BLE001
+            q.put((rank, type(e).__name__))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("which", ["fitness", "rows"])
+def test_failure_on_one_rank_raises_on_all(which):
+    """an exception on one rank (a rank with an empty block included) used to leave the
+    others blocked in the all-gather; the gathered blocks now carry a status word."""
+    ws = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fail_worker, args=(r, ws, port, q, which)) for r in range(ws)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in range(ws))
+    for p in procs:
+        p.join(timeout=60)
+    bad = 1 if which == "fitness" else 0
+    assert res[bad] == ("ValueError" if which == "fitness" else "NotImplementedError")
+    assert res[1 - bad] == "RankFailed"

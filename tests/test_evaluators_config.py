@@ -106,6 +106,16 @@ def test_data_fingerprint_follows_content():
     assert DeviceEngine.data_fingerprint((x0.astype(np.float64),)) != DeviceEngine.data_fingerprint((x0,))
 
 
+def test_data_fingerprint_sees_one_middle_element_of_a_large_array():
+    """a large SR ground truth re-noised in place at one save point in the middle
+    changes the key (the whole buffer is hashed, not a sample)."""
+    from multitreegp_amd.engine import DeviceEngine
+    ys = np.random.default_rng(0).standard_normal((16, 2001, 8)).astype(np.float32)  # ~1 MB
+    a = DeviceEngine.data_fingerprint((ys,))
+    ys[7, 1003, 5] = np.nextafter(ys[7, 1003, 5], np.float32(np.inf))
+    assert DeviceEngine.data_fingerprint((ys,)) != a
+
+
 def test_default_solver_is_the_reference_euler():
     """omitting `solver` gives the reference's default diffrax.Euler() (dyn.py:11,
     ff.py:11, sr.py:21), not RK4."""
