@@ -12,6 +12,7 @@
 //
 // References: initialization.py:9-164 (sample_tree), mutation.py:9-579, crossover.py:8-218,
 // reproduction.py:8-176, genetic_programming.py:475-525.
+#include <sched.h>
 #include <stdint.h>
 #include <string.h>
 
@@ -84,11 +85,19 @@ typedef std::vector<Node> Nodes;
 struct Lib {
   const MtgpEvolveConfig* c;
   std::vector<double> op_p;
+  std::vector<char> op_tab;  // op_tab[k]: k is an operator index (is_op as one lookup)
+  void init(const MtgpEvolveConfig* cfg) {
+    c = cfg;
+    op_p.assign(cfg->op_prob, cfg->op_prob + cfg->n_ops);
+    op_tab.assign(cfg->n_funcs > 0 ? cfg->n_funcs : 1, 0);
+    for (int i = 0; i < cfg->n_ops; ++i)
+      if (cfg->op_index[i] >= 0 && cfg->op_index[i] < cfg->n_funcs) op_tab[cfg->op_index[i]] = 1;
+  }
   int arity(int f) const { return (f >= 0 && f < c->n_funcs) ? c->slots[f] : 0; }
-  bool is_op(float f) const {
-    for (int i = 0; i < c->n_ops; ++i)
-      if (f == (float)c->op_index[i]) return true;
-    return false;
+  bool is_op(float f) const {  // f == (float)op_index[i] for some i (op indices are in [0, n_funcs))
+    if (!(f >= 0.0f && f < (float)c->n_funcs)) return false;
+    const int k = (int)f;
+    return (float)k == f && op_tab[k];
   }
   bool is_var(float f) const { return f >= (float)c->var_start && f < (float)(c->var_start + c->n_vars); }
   bool is_leaf(float f) const { return f == 1.0f || is_var(f); }
@@ -391,21 +400,126 @@ struct Ops {
     }
     return e1 < s2 - s1 || e2 < s1 - s2 || equal;
   }
+  // Crossover of one tree pair (the same draws and results as replacing each subtree through
+  // subtree() / replace(), written without heap traffic: both trees go to preorder once, the two
+  // offspring are spliced from the preorder lists in per-thread scratch; C5's 64 trees per
+  // candidate made the per-call vectors the cost of a generation).
   void crossover(const float* t1, const float* t2, Rng& g, float* o1, float* o2) const {
-    const std::vector<double> w1 = cx_w(t1), w2 = cx_w(t2);
-    memcpy(o1, t1, sizeof(float) * 4 * N);
-    memcpy(o2, t2, sizeof(float) * 4 * N);
-    if (!any(w1) || !any(w2)) return;
+    // row weights (0 empty, 2 operator, 1 leaf: cx_w) as prefix sums -- the weights are small
+    // integers, so Rng::choice's running subtraction and a binary search over the prefix sums pick
+    // the same row for every draw -- and the empty-row counts cx_invalid needs, in one pass
+    thread_local std::vector<int> c1, c2;
+    c1.resize(N + 1);
+    c2.resize(N + 1);
+    c1[0] = c2[0] = 0;
+    int e1 = 0, e2 = 0;
+    for (int k = 0; k < N; ++k) {
+      const float f1 = t1[4 * k], f2 = t2[4 * k];
+      e1 += f1 == 0.0f;
+      e2 += f2 == 0.0f;
+      c1[k + 1] = c1[k] + (f1 == 0.0f ? 0 : (L.is_op(f1) ? 2 : 1));
+      c2[k + 1] = c2[k] + (f2 == 0.0f ? 0 : (L.is_op(f2) ? 2 : 1));
+    }
+    auto unchanged = [&]() {
+      memcpy(o1, t1, sizeof(float) * 4 * N);
+      memcpy(o2, t2, sizeof(float) * 4 * N);
+    };
+    if (c1[N] == 0 || c2[N] == 0) return unchanged();
     for (int it = 0; it < kMaxRetries; ++it) {
-      const int i1 = choose_row(g, w1), i2 = choose_row(g, w2);
-      if (cx_invalid(t1, t2, i1, i2)) continue;
-      const Nodes a = subtree(t1, i1), b = subtree(t2, i2);
-      std::vector<float> n1(4 * N), n2(4 * N);
-      if (replace(t1, i1, b, n1.data()) && replace(t2, i2, a, n2.data())) {
-        memcpy(o1, n1.data(), sizeof(float) * 4 * N);
-        memcpy(o2, n2.data(), sizeof(float) * 4 * N);
+      const int i1 = choose_prefix(g, c1), i2 = choose_prefix(g, c2);
+      if (cx_invalid_e(t1, t2, i1, i2, e1, e2)) continue;
+      thread_local Nodes n1, n2, m1, m2;
+      thread_local std::vector<int> sz1, sz2;
+      preorder_into(t1, n1);
+      preorder_into(t2, n2);
+      sizes_into(n1, sz1);
+      sizes_into(n2, sz2);
+      const int p1 = N - 1 - i1, p2 = N - 1 - i2, s1 = sz1[p1], s2 = sz2[p2];
+      splice(n1, p1, s1, n2, p2, s2, m1);  // t1 with its subtree at i1 replaced by t2's at i2
+      splice(n2, p2, s2, n1, p1, s1, m2);
+      if ((int)m1.size() <= N && (int)m2.size() <= N && !m1.empty() && !m2.empty()) {
+        write_preorder(m1, o1);
+        write_preorder(m2, o2);
+      } else {
+        unchanged();
       }
       return;
+    }
+    unchanged();
+  }
+  // Rng::choice over integer weights w[k] = c[k + 1] - c[k] (c non-decreasing, c[N] > 0): the same
+  // uniform draw, and u - w[0] - ... - w[i-1] < w[i]  <=>  u < c[i + 1] exactly (integer sums)
+  int choose_prefix(Rng& g, const std::vector<int>& c) const {
+    const double u = g.uniform() * (double)c[N];
+    int lo = 0, hi = N - 1;  // first i with c[i + 1] > u
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if ((double)c[mid + 1] > u) hi = mid;
+      else lo = mid + 1;
+    }
+    return lo;
+  }
+  // cx_invalid with the empty-row counts of both trees given
+  bool cx_invalid_e(const float* t1, const float* t2, int i1, int i2, int e1, int e2) const {
+    const int s1 = i1 - find_end_idx(t1, i1), s2 = i2 - find_end_idx(t2, i2);
+    bool equal = false;
+    if (s1 == s2 && (N - e1 > 1 || N - e2 > 1)) {
+      equal = true;
+      for (int k = 0; k < s1; ++k) {
+        const float* a = t1 + 4 * (i1 - k);
+        const float* b = t2 + 4 * (i2 - k);
+        const bool same_leaf = a[3] == b[3] && a[0] == 1.0f;
+        if (!((a[0] == b[0] && a[0] > 1.0f) || same_leaf)) {
+          equal = false;
+          break;
+        }
+      }
+    }
+    return e1 < s2 - s1 || e2 < s1 - s2 || equal;
+  }
+  void preorder_into(const float* t, Nodes& out) const {  // to_preorder without the allocation
+    out.clear();
+    for (int k = N - 1; k >= 0; --k) {
+      const int f = (int)t[4 * k];
+      if (f == 0) break;
+      out.push_back({f, t[4 * k + 3]});
+    }
+  }
+  void sizes_into(const Nodes& n, std::vector<int>& sz) const {  // subtree_sizes without the allocations
+    thread_local std::vector<int> st;
+    sz.resize(n.size());
+    st.clear();
+    for (int i = (int)n.size() - 1; i >= 0; --i) {
+      int sum = 1;
+      for (int a = 0; a < L.arity(n[i].f); ++a) {
+        sum += st.back();
+        st.pop_back();
+      }
+      sz[i] = sum;
+      st.push_back(sum);
+    }
+  }
+  static void splice(const Nodes& a, int pa, int sa, const Nodes& b, int pb, int sb, Nodes& out) {
+    out.clear();
+    out.insert(out.end(), a.begin(), a.begin() + pa);
+    out.insert(out.end(), b.begin() + pb, b.begin() + pb + sb);
+    out.insert(out.end(), a.begin() + pa + sa, a.end());
+  }
+  void write_preorder(const Nodes& n, float* t) const {  // from_preorder (n fits) without the allocations
+    thread_local std::vector<int> sz;
+    sizes_into(n, sz);
+    for (int k = 0; k < N - (int)n.size(); ++k) {
+      t[4 * k + 0] = 0.0f;
+      t[4 * k + 1] = -1.0f;
+      t[4 * k + 2] = -1.0f;
+      t[4 * k + 3] = 0.0f;
+    }
+    for (size_t i = 0; i < n.size(); ++i) {
+      const int k = N - 1 - (int)i, ar = L.arity(n[i].f);
+      t[4 * k + 0] = (float)n[i].f;
+      t[4 * k + 1] = ar >= 1 ? (float)(k - 1) : -1.0f;
+      t[4 * k + 2] = ar == 2 ? (float)(k - 1 - sz[i + 1]) : -1.0f;
+      t[4 * k + 3] = n[i].f == 1 ? n[i].v : 0.0f;
     }
   }
 
@@ -422,12 +536,21 @@ std::vector<char> tree_mask(Rng& g, int T, double p) {
   }
 }
 
-// body(k) for k in [0, n) on up to MTGP_HOST_THREADS (default 8) threads in contiguous blocks; a
-// thread only for every `grain` items
+// Threads: MTGP_HOST_THREADS, else OMP_NUM_THREADS (the CPU share a GPU pool grants the job), else
+// the process's CPU affinity, at most 64.
+long host_threads() {
+  if (const char* e = std::getenv("MTGP_HOST_THREADS")) return std::max(1L, std::atol(e));
+  if (const char* e = std::getenv("OMP_NUM_THREADS")) return std::max(1L, std::min(64L, std::atol(e)));
+  cpu_set_t set;
+  if (sched_getaffinity(0, sizeof(set), &set) == 0) return std::max(1L, std::min(64L, (long)CPU_COUNT(&set)));
+  return 8;
+}
+
+// body(k) for k in [0, n) on host_threads() threads in contiguous blocks; a thread only for every
+// `grain` items
 template <class F>
 void parallel_for(long n, long grain, F body) {
-  long want = 8;
-  if (const char* e = std::getenv("MTGP_HOST_THREADS")) want = std::max(1L, std::atol(e));
+  long want = host_threads();
   const long hw = std::max(1L, (long)std::thread::hardware_concurrency());
   const long nt = std::max(1L, std::min({want, hw, n / std::max(1L, grain)}));
   if (nt == 1) {
@@ -454,8 +577,7 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
     return -1;
   const size_t tsz = (size_t)4 * N, csz = tsz * T, psz = csz * pop_size;
   Ops ops;
-  ops.L.c = cfg;
-  ops.L.op_p.assign(cfg->op_prob, cfg->op_prob + cfg->n_ops);
+  ops.L.init(cfg);
   ops.N = N;
   ops.depth = cfg->max_init_depth;
   ops.sd = cfg->coefficient_sd;
@@ -498,7 +620,8 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
     parallel_for(n_pairs, 256, [&](long k) {
       Rng g(seed, (uint64_t)i + 1, (uint64_t)k + 1);
       auto tournament = [&]() {  // reproduction.py:29-49
-        std::vector<int> idx(cfg->tournament_size);
+        thread_local std::vector<int> idx;
+        idx.resize(cfg->tournament_size);
         for (int j = 0; j < cfg->tournament_size; ++j) idx[j] = g.integer(pop_size);
         std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return F[a] < F[b]; });
         return idx[g.choice(tp, cfg->tournament_size)];
@@ -545,8 +668,7 @@ extern "C" int mtgp_sample_population(int32_t num_pop, int32_t pop_size, int32_t
                                       const MtgpEvolveConfig* cfg, uint64_t seed, float* out) {
   if (!cfg || !out || num_pop < 1 || pop_size < 1 || T < 1 || N < 1 || N > 4096) return -1;
   Ops ops;
-  ops.L.c = cfg;
-  ops.L.op_p.assign(cfg->op_prob, cfg->op_prob + cfg->n_ops);
+  ops.L.init(cfg);
   ops.N = N;
   ops.depth = cfg->max_init_depth;
   ops.sd = cfg->coefficient_sd;

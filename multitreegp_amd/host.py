@@ -6,6 +6,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -62,6 +63,7 @@ class HostEvolver:
                  tournament_probabilities=None, reproduction_type_probabilities=None,
                  reproduction_probabilities=None, num_populations: int = 1):
         self.lib = load()
+        self._pool = []  # populations returned by evolve (see _output)
         self.N = int(max_nodes)
         self.num_populations = int(num_populations)
         self._slots = np.ascontiguousarray(library.slots, np.int32)
@@ -102,13 +104,32 @@ class HostEvolver:
             raise ValueError(f"fitness shape {fit.shape} does not match populations {pops.shape[:2]}")
         P, S = pops.shape[:2]
         pairs = (S - self.cfg.elite_size) // 2
-        out = np.empty((P, self.cfg.elite_size + 2 * pairs, self.num_trees, self.N, 4), np.float32)
+        out = self._output((P, self.cfg.elite_size + 2 * pairs, self.num_trees, self.N, 4))
         self.cfg.current_generation = int(current_generation)
         rc = self.lib.mtgp_evolve_populations(_ptr(pops, _f32p), _ptr(fit, _f32p), P, S, self.num_trees, self.N,
                                               ctypes.byref(self.cfg), ctypes.c_uint64(seed & (2**64 - 1)),
                                               _ptr(out, _f32p))
         if rc < 0:
             raise ValueError("mtgp_evolve_populations rejected its arguments")
+        return out
+
+    def _output(self, shape) -> np.ndarray:
+        """The array evolve writes: a population this object returned earlier that nothing else
+        references any more (the user's loop has moved on to a newer generation), else a new one.
+        A fresh 537 MB C5 population costs more in first-touch page faults than the whole
+        evolution step; reusing a dead one keeps the reference's value semantics (no array the
+        caller can still see is ever overwritten)."""
+        for i in range(len(self._pool)):
+            a = self._pool[i]
+            # references: the pool's slot, `a` and getrefcount's argument -- none from the caller
+            # (a view of the array, e.g. a reshape or a torch tensor on it, holds one too)
+            if a.shape == shape and sys.getrefcount(a) == 3:
+                return a
+            del a
+        out = np.empty(shape, np.float32)
+        self._pool.append(out)
+        if len(self._pool) > 3:
+            self._pool.pop(0)
         return out
 
     def sample_population(self, pop_size: int, seed: int) -> np.ndarray:

@@ -182,3 +182,35 @@ def test_strategy_uses_the_native_step():
     with pytest.raises(ValueError):
         mt.GeneticProgramming(2, 32, ff, ops, VARS[:2], [1, 1], max_nodes=30, migration_percentage=0.125, elite_percentage=0.125,
                               verbose=False, evolve_backend="jax")
+
+
+def test_evolve_never_overwrites_a_population_the_caller_holds():
+    """HostEvolver reuses a returned population's buffer only once nothing outside references it:
+    populations (or views of them) the caller keeps are never overwritten by later generations."""
+    from helpers import CONTROL_OPS
+    import multitreegp_amd as mt
+    env = mt.Acrobot(0, 0)
+    lib_vars = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
+    ff = mt.DynamicEvaluator(env, 2, 0.05)
+    gp = mt.GeneticProgramming(10, 20, ff, CONTROL_OPS, lib_vars, [2, 1], migration_percentage=0.5,
+                               elite_percentage=0.0, verbose=False)
+    pop = gp.initialize_population(3)
+    fit = np.random.default_rng(0).random((1, 20)).astype(np.float32)
+    kept, snaps = [], []
+    cur = pop
+    for g in range(6):
+        cur = gp.evolve(cur, fit, 100 + g)
+        if g % 2 == 0:  # keep every other generation (and a view of one)
+            kept.append(cur if g != 2 else cur.reshape(-1))
+            snaps.append(cur.copy())
+    for k, s in zip(kept, snaps):
+        assert np.array_equal(k.reshape(s.shape), s)
+    # a released population is reused (no fresh allocation once the loop has warmed up)
+    ev = gp._evolver
+    ids = set()
+    cur = None
+    for g in range(6):
+        cur = gp.evolve(pop, fit, 200 + g)
+        ids.add(id(cur))
+        cur = None
+    assert len(ids) <= 2
