@@ -52,7 +52,7 @@
 /* wave-uniform "does any lane need the rare path" test: a single scalar branch on the GPU,
  * the per-element condition on the host (same result per element either way) */
 #if defined(__HIP_DEVICE_COMPILE__)
-#define MTGP_ANY(c) __any(c)
+#define MTGP_ANY(c) (__builtin_amdgcn_ballot_w64(c) != 0)
 #else
 #define MTGP_ANY(c) (c)
 #endif

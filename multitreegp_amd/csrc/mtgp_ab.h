@@ -31,6 +31,12 @@
 #ifndef MTGP_AB_NOFALLBACK
 #define MTGP_AB_NOFALLBACK 0  // ignore the JIT's slow-lane report (no interpreter re-run)
 #endif
+#ifndef MTGP_AB_FBCOUNT
+#define MTGP_AB_FBCOUNT 0     // count JIT calls that report slow sin/cos lanes (mtgp_ab_fb_count)
+#endif
+#ifndef MTGP_AB_NOINTERP
+#define MTGP_AB_NOINTERP 0    // JIT kernels without the interpreter (with NOFALLBACK: a readable ISA of the hot loop)
+#endif
 #ifndef MTGP_AB_FLAT_LANE
 #define MTGP_AB_FLAT_LANE 0   // compile the lane-per-program flattener (MTGP_FLAT_MODE=lane selects it)
 #endif
@@ -40,6 +46,9 @@
 #endif
 #ifndef MTGP_AB_NODIV
 #define MTGP_AB_NODIV 0       // the drift's four IEEE divisions replaced by multiplications
+#endif
+#ifndef MTGP_AB_SLOWDIV
+#define MTGP_AB_SLOWDIV 0     // the drift's divisions always by the compiler's `/` sequence (no shared reciprocal)
 #endif
 #ifndef MTGP_AB_NODRIFT
 #define MTGP_AB_NODRIFT 0     // the whole Acrobot drift replaced by dx = (thd1, thd2, u, -u)

@@ -39,7 +39,9 @@
 // schedule kernels; MTGP_TU=1 and 2 hold the HarmonicOscillator and StirredTankReactor RK4
 // control kernels, MTGP_TU=3 / 4 / 5 the Dopri5 control kernels of Acrobot / HarmonicOscillator /
 // StirredTankReactor, MTGP_TU=6 the Acrobot kernels of the general cost mask (EnvAcrobotMask),
-// behind one hidden C++ entry each.  Without MTGP_TU it is one monolithic TU.
+// MTGP_TU=7 the fixed-step Acrobot control kernels (the C3 / C2 hot kernels: an A/B variant of
+// them recompiles this unit only, scripts/build_ab.py), MTGP_TU=8 the SR kernels, behind one hidden
+// C++ entry each.  Without MTGP_TU it is one monolithic TU.
 #ifndef MTGP_TU
 #define MTGP_TU_MAIN 1
 #define MTGP_TU_HARMONIC 1
@@ -48,6 +50,8 @@
 #define MTGP_TU_HARMONIC_DOPRI5 1
 #define MTGP_TU_REACTOR_DOPRI5 1
 #define MTGP_TU_ACRO_MASK 1
+#define MTGP_TU_ACRO 1
+#define MTGP_TU_SR 1
 #else
 #define MTGP_TU_MAIN (MTGP_TU == 0)
 #define MTGP_TU_HARMONIC (MTGP_TU == 1)
@@ -56,6 +60,8 @@
 #define MTGP_TU_HARMONIC_DOPRI5 (MTGP_TU == 4)
 #define MTGP_TU_REACTOR_DOPRI5 (MTGP_TU == 5)
 #define MTGP_TU_ACRO_MASK (MTGP_TU == 6)
+#define MTGP_TU_ACRO (MTGP_TU == 7)
+#define MTGP_TU_SR (MTGP_TU == 8)
 #endif
 
 namespace {
@@ -70,6 +76,10 @@ constexpr int kLdsWaveWords = (kDMax + kSMax) * kWave;  // per wave: data column
 constexpr float kInf = __builtin_huge_valf();
 
 __device__ __forceinline__ int uni(int v) { return __builtin_amdgcn_readfirstlane(v); }
+// wave votes over the active lanes as one ballot compare (the ockl __all / __any round-trip through
+// a VGPR: v_cndmask + v_cmp + s_cmp per vote)
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+__device__ __forceinline__ bool wave_all(bool p) { return __builtin_amdgcn_ballot_w64(!p) == 0; }
 
 // --------------------------------------------------------------------------------------
 // The interpreter.  `dcol` = this lane's column of the wave's LDS data vector (stride 64
@@ -141,8 +151,63 @@ __device__ __forceinline__ AcroConst acro_const(float l1, float l2, float m1, fl
   return k;
 }
 
+// IEEE fp32 division n / d in two parts, for operands in a safe range.  The hardware sequence
+// LLVM emits for `/` is v_div_scale (x2), v_rcp, a Newton step of the reciprocal, q = n r and two
+// fma corrections, v_div_fmas, v_div_fixup.  When |n| and |d| lie in [2^-40, 2^40] (finite, non-zero,
+// not denormal) v_div_scale scales nothing, v_div_fmas is a plain fma and v_div_fixup passes the
+// quotient through, so the remaining steps below give the same correctly rounded bits; a NaN operand
+// gives NaN either way.  The reciprocal part depends on d alone, so the three divisions of the
+// Acrobot drift by d1 share one (two v_rcp instead of four, and no scale/fixup).  Callers test the
+// range with one wave-uniform branch and fall back to `/` otherwise.
+__device__ __forceinline__ float div_rcp(float d) {
+  const float r = __builtin_amdgcn_rcpf(d);
+  return __builtin_fmaf(__builtin_fmaf(-d, r, 1.0f), r, r);
+}
+__device__ __forceinline__ float div_by(float n, float d, float r) {
+  float q = n * r;
+  q = __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+  return __builtin_fmaf(__builtin_fmaf(-d, q, n), r, q);
+}
+// |v| in [2^-40, 2^40] or NaN (NaN propagates identically through both paths)
+__device__ __forceinline__ bool div_safe(float v) {
+  const float a = __builtin_fabsf(v);
+  return !(a < 9.094947e-13f) && !(a >= 1.0995116e12f);
+}
+
+// The drift's denominators d1 and den and the numerators d2, d2*d2 depend on the state only through
+// c2 = cos(theta2) in [-1, 1]: d1 and d2 are monotone in c2 (each operation rounds monotonically),
+// so their values at c2 = +-1.001 bound them, and den = den0 - d2^2 / d1 is bounded by the extreme
+// quotients.  Safe for every theta2 when those bounds lie well inside [2^-40, 2^40] (true for any
+// physical parameters; a NaN c2 makes everything NaN on both paths).  Per rollout, once.
+__device__ __forceinline__ bool acro_div_ok(const AcroConst& k) {
+  float d1b[2], d2b[2];
+  for (int e = 0; e < 2; ++e) {
+    const float c2 = e ? 1.001f : -1.001f;
+    d1b[e] = ((k.d1a + k.m2 * (k.l1sq_lc2sq + k.two_l1lc2 * c2)) + 1.0f) + 1.0f;
+    d2b[e] = k.m2 * (k.lc2sq + k.l1lc2 * c2) + 1.0f;
+  }
+  const float lo = 1e-9f, hi = 1e9f;  // 2^-40 .. 2^40 with ample margin for the rounding
+  bool ok = true;
+  for (int e = 0; e < 2; ++e) ok = ok && d1b[e] > lo && d1b[e] < hi && d2b[e] > lo && d2b[e] < hi;
+  if (!ok) return false;
+  const float d1lo = fminf(d1b[0], d1b[1]), d1hi = fmaxf(d1b[0], d1b[1]);
+  const float d2lo = fminf(d2b[0], d2b[1]), d2hi = fmaxf(d2b[0], d2b[1]);
+  const float denlo = k.den0 - (d2hi * d2hi) / d1lo * 1.001f, denhi = k.den0 - (d2lo * d2lo) / d1hi * 0.999f;
+  return d2lo * d2lo > lo && d2hi * d2hi < hi && denlo > lo && denhi < hi;
+}
+
+// The fast path of mtgp_trig_pi is the spec's result for |arg| < 2^17 and for non-finite args.
+// Every trig argument of the Acrobot drift and fitness is theta1, theta2, their sum or theta1 -
+// pi/2 (+ theta2): when neither angle is a finite value of magnitude >= 2^15, each argument is
+// either below 2^16 + 2 in magnitude or non-finite, so the fast path is exact for all of them --
+// one range test per angle (on the bits: |v| in [2^15, inf) <=> slow possible) instead of a
+// compare pair per trig value.
+__device__ __forceinline__ bool trig_args_small(float v) {
+  return (__float_as_uint(v) & 0x7fffffffu) - 0x47000000u >= 0x38800000u;
+}
+
 __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4], float u_raw,
-                                           float dx[4]) {
+                                           float dx[4], bool fastdiv = false) {
   const float control = mtgp_clip1(u_raw);
   const float th1 = x[0], th2 = x[1], thd1 = x[2], thd2 = x[3];
 #if MTGP_AB_NODRIFT  // diagnostic (mtgp_ab.h): no drift arithmetic at all
@@ -153,13 +218,14 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
   const float s2 = th2 * 0.5f, c2 = th2 * 0.25f, s1 = th1 * 0.5f, ca = (th1 + th2) * 0.5f, cb = th1 * 0.25f;
 #else
   // the five trig values of the drift (mtgp_sinf / mtgp_cosf bit for bit), with ONE wave-uniform
-  // test for lanes that need the slow reduction (|arg| >= 2^17)
+  // test for lanes that may need the slow reduction (trig_args_small)
   const float ea = (th1 + th2) - MTGP_HALF_PI_F, eb = th1 - MTGP_HALF_PI_F;
   int f0, f1, f2, f3, f4;
   float s2 = mtgp_trig_pi_fast(th2, 0, &f0), c2 = mtgp_trig_pi_fast(th2, 1, &f1);
   float s1 = mtgp_trig_pi_fast(th1, 0, &f2);
   float ca = mtgp_trig_pi_fast(ea, 1, &f3), cb = mtgp_trig_pi_fast(eb, 1, &f4);
-  if (__builtin_expect(__any(f0 | f1 | f2 | f3 | f4), 0)) {
+  (void)f0; (void)f1; (void)f2; (void)f3; (void)f4;
+  if (__builtin_expect(!wave_all(trig_args_small(th1) && trig_args_small(th2)), 0)) {
     s2 = mtgp_sinf(th2);
     c2 = mtgp_cosf(th2);
     s1 = mtgp_sinf(th1);
@@ -177,6 +243,24 @@ __device__ __forceinline__ void acro_drift(const AcroConst& k, const float x[4],
   const float phi2 = k.m2lc2g * ca;
   const float phi1 = (((k.A0 * (thd2 * thd2)) * s2 - ((k.B0 * thd1) * thd2) * s1) +
                       k.C0 * cb) + phi2;
+#if !MTGP_AB_NODIV && !MTGP_AB_SLOWDIV
+  if (__builtin_expect(fastdiv, 1)) {  // wave-uniform: the denominators are safe (acro_div_ok)
+    const float r1 = div_rcp(d1);
+    const float num = ((control + div_by(d2, d1, r1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
+    const float den = k.den0 - div_by(d2 * d2, d1, r1);
+    float a2, a1;
+    if (__builtin_expect(wave_all(div_safe(num)), 1)) a2 = div_by(num, den, div_rcp(den));
+    else a2 = num / den;
+    const float n1 = -((d2 * a2) + phi1);
+    if (__builtin_expect(wave_all(div_safe(n1)), 1)) a1 = div_by(n1, d1, r1);
+    else a1 = n1 / d1;
+    dx[0] = thd1;
+    dx[1] = thd2;
+    dx[2] = a1;
+    dx[3] = a2;
+    return;
+  }
+#endif
   const float num = ((control + MTGP_ACRO_DIV(d2, d1) * phi1) - (k.m2l1lc2 * (thd1 * thd1)) * s2) - phi2;
   const float den = k.den0 - MTGP_ACRO_DIV(d2 * d2, d1);
   const float a2 = MTGP_ACRO_DIV(num, den);
@@ -286,7 +370,7 @@ __device__ __forceinline__ void ctl_obs_apply(const float x[Env::NV], const floa
     fin[j] = mtgp_isfinite(x[j]);
     all = all && fin[j];
   }
-  if (__builtin_expect(__all(all), 1)) {  // every lane's state finite (the common case): no NaN masking
+  if (__builtin_expect(wave_all(all), 1)) {  // every lane's state finite (the common case): no NaN masking
 #pragma unroll
     for (int i = 0; i < NV; ++i) y[i] = x[i] + nz[i];
     Env::obs_transform(y);
@@ -352,25 +436,29 @@ struct AcroFit {
   float csum, c0incl, F;
 };
 
-__device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, bool incl, float u,
+__device__ __forceinline__ bool save_incl(const float* ts, int k);
+// incl (acrobot.py:82's mask at save k, save_incl) is needed only at save 0 and at a lane's first
+// success: it is evaluated there (a division and three loads) instead of at every save point
+__device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, const float* ts, float u,
                                                 float x0, float x1) {
   if (f.settled) return;
   int fa, fb;
   const float x01 = x0 + x1;
   float ca = mtgp_trig_pi_fast(x0, 1, &fa), cb = mtgp_trig_pi_fast(x01, 1, &fb);
-  if (__builtin_expect(__any(fa | fb), 0)) {
+  (void)fa; (void)fb;
+  if (__builtin_expect(!wave_all(trig_args_small(x0) && trig_args_small(x1)), 0)) {
     ca = mtgp_cosf(x0);
     cb = mtgp_cosf(x01);
   }
   const bool reached = ((-ca) - cb) > 1.5f;
   const float cost = (u * 0.01f) * u;
   if (k == 0) {
-    f.c0incl = incl ? cost : 0.0f;
+    f.c0incl = save_incl(ts, 0) ? cost : 0.0f;
     f.csum = cost;
     if (reached) { f.settled = true; f.F = (float)S + f.c0incl; }
   } else if (reached) {
     f.settled = true;
-    f.F = (float)k + (f.csum + (incl ? cost : 0.0f));
+    f.F = (float)k + (f.csum + (save_incl(ts, k) ? cost : 0.0f));
   } else {
     f.csum = f.csum + cost;
   }
@@ -442,6 +530,7 @@ struct EnvAcrobot {
   // the 4 rollout parameters stay in registers; the 12 derived products are rebuilt at each drift
   // (same operations, so bit-identical) -- holding them live cost 8 VGPRs next to the JIT call
   float l1, l2, m1, m2;
+  bool fastdiv;  // wave-uniform: every lane's drift denominators are in the safe range (acro_div_ok)
   typedef AcroFit Fit;
   __device__ __forceinline__ void load(const MtgpRollouts& ro, int rr, int nt) {
     (void)nt;
@@ -449,9 +538,10 @@ struct EnvAcrobot {
     l2 = ro.params[4 * rr + 1];
     m1 = ro.params[4 * rr + 2];
     m2 = ro.params[4 * rr + 3];
+    fastdiv = wave_all(acro_div_ok(acro_const(l1, l2, m1, m2)));
   }
   __device__ __forceinline__ void drift(const float x[4], float u, float dx[4]) const {
-    acro_drift(acro_const(l1, l2, m1, m2), x, u, dx);
+    acro_drift(acro_const(l1, l2, m1, m2), x, u, dx, fastdiv);
   }
   __device__ __forceinline__ static void obs_transform(float y[4]) {
     y[0] = mtgp_wrap_angle(y[0]);
@@ -460,7 +550,7 @@ struct EnvAcrobot {
   __device__ __forceinline__ static bool bad(const float* s, int n) { return acro_bad(s, n); }
   __device__ __forceinline__ static Fit fit_init(bool active) { return Fit{!active, 0.0f, 0.0f, 0.0f}; }
   __device__ __forceinline__ void fit_update(Fit& f, int k, int S, const float* ts, float u, const float x[4]) const {
-    acro_fit_update(f, k, S, save_incl(ts, k), u, x[0], x[1]);
+    acro_fit_update(f, k, S, ts, u, x[0], x[1]);
   }
 
   __device__ __forceinline__ static void fit_kill(Fit& f) { (void)f; }  // fs/cost mask ignore the fill
@@ -597,13 +687,19 @@ struct EnvReactor {
 // The adaptive kernels' save points are divergent (each round writes one dword per lane into
 // different rows), so their partial lines are left to L2 to merge: plain stores there
 // (DP = true; non-temporal partial writes made the C3 Dopri5 kernel 44 % slower).
+// Fixed-step kernels: the row is wave-uniform, so the store addresses a buffer resource at the row
+// (SGPRs) plus the lane's byte offset (a VGPR) -- no per-store 64-bit VGPR address arithmetic; the
+// resource's extent is the row (row_len elements), so a lane offset past it is dropped by the
+// hardware instead of writing out of bounds.  off * 4 < 2^31 (checked by the entry point).
 template <bool DP = false>
-__device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v) {
+__device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v, size_t row_len) {
   float* p = arr + row;
   if (!DP) {
-    __builtin_nontemporal_store(v, p + off);
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(row_len * 4u), 0x00020000);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), r, off * 4, 0, 2 /* nt */);
     return;
   }
+  (void)row_len;
   p[off] = v;
 }
 
@@ -847,6 +943,9 @@ __device__ __forceinline__ float run_groups_interp(const KArgs& A, const Lane& L
 // the interpreter runs when there is no usable code or when a lane needs the slow sin/cos path.
 // chained: the role's code is one chain (A.chain_state, mtgp_jit.h jit_unit_end); with save_prog
 // >= 0 the chain's continuation (program save_prog, the save-point readout) runs too -> *save_v.
+#if MTGP_AB_FBCOUNT  // diagnostic: JIT calls with / without slow sin/cos lanes (chain, single)
+__device__ unsigned long long g_ab_fb_count[4];
+#endif
 template <bool JIT, int M, bool COLD = (MTGP_COLD_INTERP != 0)>
 __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, int role, int first, DataVec<JIT>& D,
                                          float (&out)[M], bool chained = false, int save_prog = -1,
@@ -866,6 +965,10 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 #pragma unroll
       for (int j = 0; j < M; ++j) out[j] = r.v[j < mtgp::kJitChainMax ? j : 0];
       if (save_prog >= 0) *save_v = r.tail;
+#if MTGP_AB_FBCOUNT
+      if (fl != 0 && L.lane == 0) atomicAdd(&g_ab_fb_count[0], 1ull);
+      if (L.lane == 0) atomicAdd(&g_ab_fb_count[1], 1ull);
+#endif
       if (!MTGP_AB_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // slow sin/cos lanes: re-run the chain's
         bool spilled = false;                                      // programs for the groups concerned
         for (int gi = 0; gi < ng; ++gi) {
@@ -898,6 +1001,10 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 #else
         float v = jit_call(A.jit_base + off, D.v, fl);
 #endif
+#if MTGP_AB_FBCOUNT
+        if (fl != 0 && L.lane == 0) atomicAdd(&g_ab_fb_count[2], 1ull);
+        if (L.lane == 0) atomicAdd(&g_ab_fb_count[3], 1ull);
+#endif
         if (!MTGP_AB_NOFALLBACK && __builtin_expect(fl != 0, 0)) {  // lanes that need the slow sin/cos: re-run only
           bool spilled = false;               // this program, only for the groups concerned
           for (int gi = 0; gi < ng; ++gi) {
@@ -915,7 +1022,7 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
     }
     if (interp) D.spill();
   }
-  if (interp) {
+  if (interp && !(JIT && MTGP_AB_NOINTERP)) {
 #pragma unroll 1
     for (int q = 0; q < mr; ++q) {  // mr <= M: a runtime role size (state_size > 3, interpreter only)
       const float v = run_groups_interp<JIT && COLD>(A, L, ng, first + q, D.dcol, D.st, 0.0f);
@@ -982,6 +1089,212 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 }
 
 // --------------------------------------------------------------------------------------
+// The JIT-only stage loop of the fixed-step dynamic policy (round 4).  The JIT's sin/cos/division
+// templates compute every lane themselves (the spec's slow reductions included: s[32:33] is never
+// set, gen_jit_templates.py), so once the launch's code is usable (Lane.jok) no lane ever needs the
+// interpreter: this loop carries no interpreter code at all, its RK4 stages are unrolled (stage
+// constants and branches resolved at compile time), and the kernel runs the general loop below only
+// when the code is not usable.  The arithmetic is k_ctl_dynamic's, operation for operation.
+template <int N>
+__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&k)[N], float c, float (&out)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : MTGP_FMAF(c, k[i], s[i]);
+}
+template <int N>
+__device__ __forceinline__ void rk_acc(int st, float (&acc)[N], const float (&k)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) acc[i] = st == 0 ? k[i] : (st == 3 ? acc[i] + k[i] : MTGP_FMAF(2.0f, k[i], acc[i]));
+}
+
+// one JIT unit call, no fallback (the templates never request one)
+__device__ __forceinline__ float jit_call_nf(uint64_t addr_, const float d[kDMax]) {
+  uint64_t fl = 0;
+  return jit_call(addr_, d, fl);
+}
+__device__ __forceinline__ ChainOut jit_call_chain_nf(uint64_t addr_, const float d[kDMax], int cont) {
+  uint64_t fl = 0;
+  return jit_call_chain(addr_, d, fl, cont);
+}
+
+template <class Env, int NA, bool TRAJ, bool NOISE, int NST>
+__device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) {
+  constexpr int NV = Env::NV;
+  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const float t0 = A.ro.ts[0];
+  ObsNoise<NV> nzc;
+  float nzv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+  if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
+  constexpr int uslot = NV + NA;
+  Env env;
+  env.load(A.ro, rr, A.m.n_targets);
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  float dv[kDMax];
+#pragma unroll
+  for (int k = 0; k < kDMax; ++k) dv[k] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < kDMax - NV - 2; ++t)
+    if (t < A.m.n_targets && uslot + 1 + t < kDMax) dv[uslot + 1 + t] = A.ro.targets[rr * A.m.n_targets + t];
+
+  // groups whose save-time readout differs from the drift readout (it reads y): bit per group
+  uint64_t diff_mask = 0;
+  for (int gi = 0; gi < ng; ++gi) {
+    const size_t pj = (size_t)group_ind(A, Ln, gi) * A.n_prog;
+    bool same = A.m.readout_save_same > 0;
+    if (A.m.readout_save_same < 0) {
+      const int la = uni(A.plen[pj + A.m.prog_readout]), lb = uni(A.plen[pj + A.m.prog_readout_save]);
+      same = la == lb;
+      const MtgpInstr* pa = A.prog + (pj + A.m.prog_readout) * A.L;
+      const MtgpInstr* pb = A.prog + (pj + A.m.prog_readout_save) * A.L;
+      for (int i = 0; same && i < la; ++i)
+        same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
+    }
+    if (!same) diff_mask |= 1ull << gi;
+  }
+  const bool save_readout = __builtin_amdgcn_readfirstlane((int)(diff_mask != 0)) != 0;
+  const bool chain_state = A.chain_state != 0, chain_save = A.chain_save != 0;
+  // code addresses of this wave's units (wave-uniform)
+  const uint64_t u_readout = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout);
+  const uint64_t u_state = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state);
+  uint64_t u_state_j[NA];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) u_state_j[j] = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + j);
+  const uint64_t u_save = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout_save);
+
+  float x[NV], a[NA], kx[NV], ka[NA], ax[NV], aa[NA];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+#pragma unroll
+  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = 0.0f;
+
+  typename Env::Fit fit = Env::fit_init(active);
+  bool dead = !active, pending = false, prev_ok;
+  {
+    float s0[NV + NA];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) s0[i] = x[i];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) s0[NV + j] = a[j];
+    prev_ok = !Env::bad(s0, NV + NA);
+  }
+
+  int save_k = 0, save_ctr = 0;
+  for (int step = 0;; ++step) {
+    const bool last = step == n_steps;
+    const bool is_save = save_ctr == 0;
+    const int ksave = save_k;
+    if (++save_ctr == save_every) {
+      save_ctr = 0;
+      ++save_k;
+    }
+    const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
+    bool stop = false;
+    // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
+    auto stage = [&](auto st_c) -> bool {
+      constexpr int ST = decltype(st_c)::value;
+      float xt[NV], at[NA], y[NV];
+      rk_in<NV>(ST, x, kx, ST == 3 ? h : h2, xt);
+      rk_in<NA>(ST, a, ka, ST == 3 ? h : h2, at);
+#pragma unroll
+      for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
+      const float u = jit_call_nf(u_readout, dv);
+      env.drift(xt, u, kx);
+      if (NOISE && ST != 2) obs_noise_vec<NV>(nzc, ST == 0 ? tk : tk + (ST == 3 ? h : h2), nzv);
+      ctl_obs_apply<Env>(xt, nzv, y);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) dv[i] = y[i];
+      dv[uslot] = u;
+      bool redraw = false;
+      if (NOISE && ST == 0 && is_save) redraw = __float_as_uint(A.ro.ts[ksave]) != __float_as_uint(tk);
+      const bool save_chain = ST == 0 && chain_save && is_save && save_readout && !redraw;
+      float us_chain = u;
+      if (chain_state) {
+        const ChainOut c = jit_call_chain_nf(u_state, dv, save_chain ? 1 : 0);
+#pragma unroll
+        for (int j = 0; j < NA; ++j) ka[j] = c.v[j < mtgp::kJitChainMax ? j : 0];
+        if (save_chain) us_chain = c.tail;
+      } else {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) ka[j] = jit_call_nf(u_state_j[j], dv);
+      }
+      if (ST == 0) {
+        if (is_save) {
+          const int k = ksave;
+          float us = u;
+          if (NOISE && redraw) {
+            ctl_obs<Env, true>(nzc, A.ro.ts[k], x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
+#pragma unroll
+            for (int i = 0; i < NV; ++i) dv[i] = y[i];
+          }
+          if (save_chain) us = us_chain;
+          else if (save_readout) us = jit_call_nf(u_save, dv);  // the unit covers every group
+          if (!dead) env.fit_update(fit, k, S, A.ro.ts, us, x);
+          if (TRAJ && active) {
+            if (A.out.xs) {
+#pragma unroll
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
+            }
+            if (A.out.ys) {
+#pragma unroll
+              for (int i = 0; i < NV; ++i)
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
+            }
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
+            if (A.out.acts) {
+#pragma unroll
+              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR, loff, a[j], PR);
+            }
+          }
+        }
+        if (pending) {  // the event state has been saved: freeze at +inf (saveat fill)
+          pending = false;
+          dead = true;
+          if (!last) Env::fit_kill(fit);
+#pragma unroll
+          for (int i = 0; i < NV; ++i) x[i] = kInf;
+#pragma unroll
+          for (int j = 0; j < NA; ++j) a[j] = kInf;
+        }
+        if (last || (!TRAJ && wave_all(fit.settled || dead))) return true;
+      }
+      rk_acc<NV>(NST == 1 ? 0 : ST, ax, kx);
+      rk_acc<NA>(NST == 1 ? 0 : ST, aa, ka);
+      return false;
+    };
+    if constexpr (NST == 1) {
+      stop = stage(std::integral_constant<int, 0>{});
+    } else {
+      stop = stage(std::integral_constant<int, 0>{});
+      if (!stop) {
+        stage(std::integral_constant<int, 1>{});
+        stage(std::integral_constant<int, 2>{});
+        stage(std::integral_constant<int, 3>{});
+      }
+    }
+    if (stop) break;
+    if (!dead) {
+      float sn[NV + NA];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) { x[i] = NST == 1 ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) { a[j] = NST == 1 ? a[j] + aa[j] * h : MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
+      const bool ok = !Env::bad(sn, NV + NA);
+      if (prev_ok && !ok) pending = true;
+      prev_ok = ok;
+    }
+  }
+  finish_group(A, Ln, Env::fit_final(fit, S));
+}
+
+// --------------------------------------------------------------------------------------
 // Dynamic symbolic policy (dynamic_evaluate.py:65-118) on environment Env.  NA = state_size.
 // Data slots: y 0..NV-1 | a NV..NV+NA-1 | u NV+NA | targets.  Per stage the programs run in
 // the order of _drift (dyn.py:107-118): readout (y, u folded to 0) -> drift -> f_obs ->
@@ -998,13 +1311,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   const int na = NA <= 3 ? NA : uni(A.m.state_size);
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
+  if constexpr (JIT && NA <= 3 && !Env::kMask) {
+    if (__builtin_expect(Ln.jok, 1)) {  // usable code: the JIT-only loop
+      if (A.m.solver == MTGP_SOLVER_EULER) ctl_dynamic_jit<Env, NA, TRAJ, NOISE, 1>(A, Ln);
+      else ctl_dynamic_jit<Env, NA, TRAJ, NOISE, 4>(A, Ln);
+      return;
+    }
+  }
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][DM * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
-  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
 
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
@@ -1130,18 +1450,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
           if (TRAJ && active && !MTGP_AB_NOSTORE) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
             }
             if (A.out.ys) {
 #pragma unroll
               for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
             }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us);
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
             if (A.out.acts) {
 #pragma unroll
               for (int j = 0; j < NA; ++j)
-                if (j < na) store_row(A.out.acts, ((size_t)k * na + j) * PR, loff, a[j]);
+                if (j < na) store_row(A.out.acts, ((size_t)k * na + j) * PR, loff, a[j], PR);
             }
           }
         }
@@ -1154,7 +1474,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
           for (int j = 0; j < NA; ++j) a[j] = kInf;
         }
-        if (!TRAJ && __all(fit.settled || dead)) stop = true;
+        if (!TRAJ && wave_all(fit.settled || dead)) stop = true;
         if (stop) break;
       }
       stage_acc_n<NV>(stage, ax, kx);
@@ -1175,6 +1495,124 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   finish_group(A, Ln, Env::fit_final(fit, S));
 }
 
+// The JIT-only stage loop of the static policy (as ctl_dynamic_jit: no interpreter code, RK4 stages
+// unrolled; k_ctl_static's arithmetic operation for operation).
+template <class Env, bool TRAJ, bool NOISE, int NST>
+__device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
+  constexpr int NV = Env::NV;
+  const int r = Ln.r, rr = Ln.rr;
+  const bool active = Ln.active;
+  const int R = A.ro.R;
+  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
+  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const float t0 = A.ro.ts[0];
+  ObsNoise<NV> nzc;
+  float nzv[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+  if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
+  Env env;
+  env.load(A.ro, rr, A.m.n_targets);
+  const size_t PR = (size_t)A.P * R;
+  const int loff = Ln.p * R + r;
+  float dv[kDMax];
+#pragma unroll
+  for (int k = 0; k < kDMax; ++k) dv[k] = 0.0f;
+#pragma unroll
+  for (int t = 0; t < kDMax - NV; ++t)
+    if (t < A.m.n_targets) dv[NV + t] = A.ro.targets[rr * A.m.n_targets + t];
+  const uint64_t u_policy = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout);
+
+  float x[NV], kx[NV], ax[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = 0.0f;
+  typename Env::Fit fit = Env::fit_init(active);
+  bool dead = !active, pending = false;
+  bool prev_ok = !Env::bad(x, NV);
+
+  int save_k = 0, save_ctr = 0;
+  for (int step = 0;; ++step) {
+    const bool last = step == n_steps;
+    const bool is_save = save_ctr == 0;
+    const int ksave = save_k;
+    if (++save_ctr == save_every) {
+      save_ctr = 0;
+      ++save_k;
+    }
+    const float tk = t0 + (float)step * h;
+    auto stage = [&](auto st_c) -> bool {
+      constexpr int ST = decltype(st_c)::value;
+      float xt[NV], y[NV];
+      rk_in<NV>(ST, x, kx, ST == 3 ? h : h2, xt);
+      if (NOISE && ST != 2) obs_noise_vec<NV>(nzc, ST == 0 ? tk : tk + (ST == 3 ? h : h2), nzv);
+      ctl_obs_apply<Env>(xt, nzv, y);
+#pragma unroll
+      for (int i = 0; i < NV; ++i) dv[i] = y[i];
+      float u = jit_call_nf(u_policy, dv);  // ff.py:106-107 (:97 at saves)
+      env.drift(xt, u, kx);
+      if (ST == 0) {
+        if (is_save) {
+          const int k = ksave;
+          if (NOISE) {
+            const float tsk = A.ro.ts[k];
+            if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
+              ctl_obs<Env, true>(nzc, tsk, x, y);
+#pragma unroll
+              for (int i = 0; i < NV; ++i) dv[i] = y[i];
+              u = jit_call_nf(u_policy, dv);
+            }
+          }
+          if (!dead) env.fit_update(fit, k, S, A.ro.ts, u, x);
+          if (TRAJ && active) {
+            if (A.out.xs) {
+#pragma unroll
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
+            }
+            if (A.out.ys) {
+#pragma unroll
+              for (int i = 0; i < NV; ++i)
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
+            }
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u, PR);
+          }
+        }
+        if (pending) {
+          pending = false;
+          dead = true;
+          if (!last) Env::fit_kill(fit);
+#pragma unroll
+          for (int i = 0; i < NV; ++i) x[i] = kInf;
+        }
+        if (last || (!TRAJ && wave_all(fit.settled || dead))) return true;
+      }
+      rk_acc<NV>(NST == 1 ? 0 : ST, ax, kx);
+      return false;
+    };
+    bool stop;
+    if constexpr (NST == 1) {
+      stop = stage(std::integral_constant<int, 0>{});
+    } else {
+      stop = stage(std::integral_constant<int, 0>{});
+      if (!stop) {
+        stage(std::integral_constant<int, 1>{});
+        stage(std::integral_constant<int, 2>{});
+        stage(std::integral_constant<int, 3>{});
+      }
+    }
+    if (stop) break;
+    if (!dead) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[i] = NST == 1 ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
+      const bool ok = !Env::bad(x, NV);
+      if (prev_ok && !ok) pending = true;
+      prev_ok = ok;
+    }
+  }
+  finish_group(A, Ln, Env::fit_final(fit, S));
+}
+
 // --------------------------------------------------------------------------------------
 // Static policy (feedforward_evaluate.py:64-110) on environment Env.  Data slots:
 // y 0..NV-1 | targets.
@@ -1184,13 +1622,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
+  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
+  if constexpr (JIT && !Env::kMask) {
+    if (__builtin_expect(Ln.jok, 1)) {  // usable code: the JIT-only loop
+      if (A.m.solver == MTGP_SOLVER_EULER) ctl_static_jit<Env, TRAJ, NOISE, 1>(A, Ln);
+      else ctl_static_jit<Env, TRAJ, NOISE, 4>(A, Ln);
+      return;
+    }
+  }
   const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
   const bool active = Ln.active;
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
-  if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
   const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
   const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
   const float t0 = A.ro.ts[0];
@@ -1261,14 +1706,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
           if (TRAJ && active) {
             if (A.out.xs) {
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i]);
+              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
             }
             if (A.out.ys) {
 #pragma unroll
               for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
+                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
             }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u);
+            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u, PR);
           }
         }
         if (pending) {
@@ -1278,7 +1723,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
           for (int i = 0; i < NV; ++i) x[i] = kInf;
         }
-        if (!TRAJ && __all(fit.settled || dead)) stop = true;
+        if (!TRAJ && wave_all(fit.settled || dead)) stop = true;
         if (stop) break;
       }
       stage_acc_n<NV>(stage, ax, kx);
@@ -1491,17 +1936,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     if (TRAJ && active) {
       if (A.out.xs) {
 #pragma unroll
-        for (int i = 0; i < NV; ++i) store_row<true>(A.out.xs, ((size_t)k * NV + i) * PR, loff, sk[i]);
+        for (int i = 0; i < NV; ++i) store_row<true>(A.out.xs, ((size_t)k * NV + i) * PR, loff, sk[i], PR);
       }
       if (A.out.ys) {
 #pragma unroll
         for (int i = 0; i < NV; ++i)
-          if (i < A.m.n_obs) store_row<true>(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i]);
+          if (i < A.m.n_obs) store_row<true>(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
       }
-      if (A.out.us) store_row<true>(A.out.us, (size_t)k * PR, loff, ur[0]);
+      if (A.out.us) store_row<true>(A.out.us, (size_t)k * PR, loff, ur[0], PR);
       if (DYN && A.out.acts) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) store_row<true>(A.out.acts, ((size_t)k * NAX + j) * PR, loff, sk[NV + j]);
+        for (int j = 0; j < NA; ++j) store_row<true>(A.out.acts, ((size_t)k * NAX + j) * PR, loff, sk[NV + j], PR);
       }
     }
   };
@@ -1531,7 +1976,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     live = active && t < t_end && steps < max_steps;
   }
   const int budget = A.dp_pass == 1 ? A.dp_budget : 0x7fffffff;
-  for (int iter = 0; __any(live); ++iter) {
+  for (int iter = 0; wave_any(live); ++iter) {
     if (iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
       park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
       if (Ln.lane == 0) A.dp_pending[1 + atomicAdd(A.dp_pending, 1)] = wv;
@@ -1571,7 +2016,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     }
     // SaveAt(ts) through the dense output of the accepted steps, one save point per round
     bool sv = live && keep && k < S && ts[k] <= tnext;
-    while (__any(sv)) {
+    while (wave_any(sv)) {
       float sk[ND];
       const float th = sv ? (ts[k] - t) / h : 0.0f;
 #pragma unroll
@@ -1612,7 +2057,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     float sk[ND];
 #pragma unroll
     for (int i = 0; i < ND; ++i) sk[i] = kInf;
-    while (__any(fl)) {
+    while (wave_any(fl)) {
       save_round(fl, k, sk, true);
       if (fl) fl = ++k < S;
     }
@@ -1663,7 +2108,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       tot = tot + sq;
       if (TRAJ && active && A.out.xs) {
 #pragma unroll
-        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, x[d]);
+        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, x[d], PR);
       }
     }
     if (pending) {
@@ -1673,7 +2118,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       for (int i = 0; i < NV; ++i) x[i] = kInf;
     }
     if (step == n_steps) break;
-    if (!TRAJ && __all(dead)) {  // every remaining save point adds (inf - y)^2
+    if (!TRAJ && wave_all(dead)) {  // every remaining save point adds (inf - y)^2
       if (active && mtgp_isfinite(tot)) tot = kInf;
       break;
     }
@@ -1736,7 +2181,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
     tot = tot + sq;
     if (TRAJ && active && A.out.xs) {
 #pragma unroll
-      for (int d = 0; d < NV; ++d) store_row<true>(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d]);
+      for (int d = 0; d < NV; ++d) store_row<true>(A.out.xs, ((size_t)k * NV + d) * PR, loff, v[d], PR);
     }
   };
   auto bad = [&](const float* v) __attribute__((always_inline)) {
@@ -1764,7 +2209,7 @@ __global__ void __launch_bounds__(256) k_sr_dopri5(KArgs A) {
 #pragma unroll
   for (int i = 0; i < NV; ++i) f[0][i] = kx[i];
   bool live = active && t < t_end && steps < max_steps;
-  while (__any(live)) {
+  while (wave_any(live)) {
     const float h = tnext - t;
 #pragma unroll 1
     for (int s = 1; s <= 6; ++s) {  // stage s input y + h sum_{j<s} a_sj f_j (wave-uniform s)
@@ -1964,7 +2409,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
         if (c < NV) {
           const float e = x[t] - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
           nxt[c * kWave] = e * e;
-          if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, x[t]);
+          if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, x[t], PR);
         }
       }
       __syncthreads();
@@ -1986,7 +2431,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       __syncthreads();
     }
     if (step == n_steps) break;
-    if (!TRAJ && __all(dead)) {  // dead is identical in every wave: a uniform exit
+    if (!TRAJ && wave_all(dead)) {  // dead is identical in every wave: a uniform exit
       if (active && mtgp_isfinite(tot)) tot = kInf;
       break;
     }
@@ -2179,7 +2624,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
       if (c < NV) {
         const float e = v[t] - A.ro.ys_true[((size_t)kk * NV + c) * R + rr];
         red[c * kWave] = e * e;
-        if (TRAJ && pend && active && A.out.xs) store_row<true>(A.out.xs, ((size_t)kk * NV + c) * PR, loff, v[t]);
+        if (TRAJ && pend && active && A.out.xs) store_row<true>(A.out.xs, ((size_t)kk * NV + c) * PR, loff, v[t], PR);
       }
     }
     const float sq = reduce();
@@ -2205,7 +2650,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
 #pragma unroll
   for (int i = 0; i < kWideComp; ++i) f[0][i] = kx[i];
   bool live = active && t < t_end && steps < max_steps;
-  while (__any(live)) {  // identical in every wave of the workgroup
+  while (wave_any(live)) {  // identical in every wave of the workgroup
     const float h = tnext - t;
 #pragma unroll 1
     for (int s = 1; s <= 6; ++s) {
@@ -2240,7 +2685,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
     const bool keep = kp != 0;
     const bool acc_step = live && keep;
     // SaveAt(ts) through the dense output, in rounds over the lanes that pass save points
-    while (__any(acc_step && k < S && ts[k < S ? k : S - 1] <= tnext)) {
+    while (wave_any(acc_step && k < S && ts[k < S ? k : S - 1] <= tnext)) {
       const bool pend = acc_step && k < S && ts[k < S ? k : S - 1] <= tnext;
       const float th = (ts[k < S ? k : S - 1] - t) / h;
       float v[kWideComp];
@@ -2280,7 +2725,7 @@ __global__ void __launch_bounds__(512) k_sr_wide_dopri5(KArgs A) {
   float inf[kWideComp];
 #pragma unroll
   for (int i = 0; i < kWideComp; ++i) inf[i] = kInf;
-  while (__any(active && k < S)) {  // unsaved points are +inf (throw=False)
+  while (wave_any(active && k < S)) {  // unsaved points are +inf (throw=False)
     const bool pend = active && k < S;
     save(k, inf, pend);
     if (pend) ++k;
@@ -2464,7 +2909,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
     }
   }
   __syncthreads();
-  const bool slot_err = __any(far);
+  const bool slot_err = wave_any(far);
   // lane s: is slot s preloaded (fewer than kJitPreSlots slots first occur before it)
   bool pre = false;
   if (lane < MTGP_MAX_DATA) {
@@ -2887,7 +3332,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
     bool any_ready = false;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) any_ready = any_ready || ready[k];
-    if (!__any(any_ready)) break;  // (a DAG: some row is always ready while any is pending)
+    if (!wave_any(any_ready)) break;  // (a DAG: some row is always ready while any is pending)
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       if (!ready[k]) continue;
@@ -2972,7 +3417,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
           go[k] = i < N && !emitted[k] && s_flag[i] != 0u;
           any = any || go[k];
         }
-        if (!__any(any)) break;
+        if (!wave_any(any)) break;
         __syncthreads();  // every row's go decision precedes this round's visits
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
@@ -3027,7 +3472,7 @@ __global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ p
       }
     }
   }
-  shared = __any(shared);
+  shared = wave_any(shared);
   __syncthreads();  // every lane's program words (LDS copy) precede the END and the JIT sizing
   if (lane == 0) {
     if (shared) {  // arbitrary arrays only: the serial walk duplicates the shared subtree
@@ -3801,6 +4246,19 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS);
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot(MTGP_TU_ENTRY_ARGS);
+#if MTGP_TU_ACRO && MTGP_AB_FBCOUNT
+extern "C" int mtgp_ab_fb_count(unsigned long long* host) {  // diagnostic build only; reads and clears
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ab_fb_count), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_ab_fb_count), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
+#if MTGP_TU_ACRO
+int mtgp_tu_launch_acrobot(MTGP_TU_ENTRY_ARGS) {  // fixed-step solvers (Dopri5 goes on to TU 3)
+  return launch_ctl<EnvAcrobot>(*(const KArgs*)A, model, ro, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
 #if MTGP_TU_ACRO_MASK
 int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS) {  // every solver; the trajectory variants (traj unused)
   (void)traj;
@@ -3830,6 +4288,65 @@ int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_ARGS) {
 #if MTGP_TU_REACTOR
 int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS) {
   return launch_ctl<EnvReactor>(*(const KArgs*)A, model, ro, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+
+
+// the SR kernels (MTGP_TU 8): register-resident n_var <= 4 and the wide-state workgroup kernels
+#define MTGP_TU_SR_ARGS \
+  const void* A_, const MtgpModel* model, bool jit, bool traj, bool dopri5, unsigned G, unsigned Wset, unsigned grid_, \
+      unsigned block_, hipStream_t s
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_sr(MTGP_TU_SR_ARGS);
+#if MTGP_TU_SR
+int mtgp_tu_launch_sr(MTGP_TU_SR_ARGS) {
+  const KArgs& A = *(const KArgs*)A_;
+  const dim3 grid(grid_), block(block_);
+  if (model->n_var > 4) {
+    const int nw = (model->n_var + kWideComp - 1) / kWideComp;
+    const dim3 wgrid((unsigned)(((long)A.P + G - 1) / G * Wset)), wblock(kWave * nw);
+    if (dopri5) {  // + a reduction vector (error norm, MSE)
+      const size_t lds_dp = (size_t)(3 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+      return launch_timed([&] {
+        if (jit) {
+          if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, true>), wgrid, wblock, lds_dp, s, A);
+          else hipLaunchKernelGGL((k_sr_wide_dopri5<false, true>), wgrid, wblock, lds_dp, s, A);
+        } else if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, false>), wgrid, wblock, lds_dp, s, A);
+        else hipLaunchKernelGGL((k_sr_wide_dopri5<false, false>), wgrid, wblock, lds_dp, s, A);
+      }, s);
+    }
+    const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+    return launch_timed([&] {
+      if (jit) {
+        if (traj) hipLaunchKernelGGL((k_sr_wide<true, true>), wgrid, wblock, lds, s, A);
+        else hipLaunchKernelGGL((k_sr_wide<false, true>), wgrid, wblock, lds, s, A);
+      } else if (traj) hipLaunchKernelGGL((k_sr_wide<true, false>), wgrid, wblock, lds, s, A);
+      else hipLaunchKernelGGL((k_sr_wide<false, false>), wgrid, wblock, lds, s, A);
+    }, s);
+  }
+#define MTGP_SR(NV)                                                                                       \
+  case NV:                                                                                                \
+  return launch_timed([&] {                                                                             \
+    if (dopri5) {                                                                                       \
+      if (jit) {                                                                                        \
+        if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, true>), grid, block, 0, s, A);              \
+        else hipLaunchKernelGGL((k_sr_dopri5<NV, false, true>), grid, block, 0, s, A);                  \
+      } else if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, false>), grid, block, 0, s, A);        \
+      else hipLaunchKernelGGL((k_sr_dopri5<NV, false, false>), grid, block, 0, s, A);                   \
+    } else if (jit) {                                                                                   \
+      if (traj) hipLaunchKernelGGL((k_sr<NV, true, true>), grid, block, 0, s, A);                       \
+      else hipLaunchKernelGGL((k_sr<NV, false, true>), grid, block, 0, s, A);                           \
+    } else if (traj) hipLaunchKernelGGL((k_sr<NV, true, false>), grid, block, 0, s, A);                 \
+    else hipLaunchKernelGGL((k_sr<NV, false, false>), grid, block, 0, s, A);                            \
+  }, s);
+  switch (model->n_var) {
+    MTGP_SR(1)
+    MTGP_SR(2)
+    MTGP_SR(3)
+    MTGP_SR(4)
+    default: return MTGP_ERR_ARG;
+  }
+#undef MTGP_SR
+  return MTGP_ERR_ARG;
 }
 #endif
 
@@ -4273,6 +4790,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   A.dp_lanes = (uint32_t)(waves * kWave);
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
   const bool traj = out->xs || out->ys || out->us || out->acts;
+  if (traj && (long)P * rollouts->R * 4 > (long)INT32_MAX) return MTGP_ERR_ARG;  // store_row's 31-bit byte offsets
   const bool noise = rollouts->obs_keys != nullptr;
   if (noise && (!rollouts->obs_w || model->model == MTGP_MODEL_SR)) return MTGP_ERR_ARG;
   if (model->prng_impl != MTGP_PRNG_THREEFRY_ORIGINAL && model->prng_impl != MTGP_PRNG_THREEFRY_PARTITIONABLE)
@@ -4283,7 +4801,7 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
       case MTGP_ENV_ACROBOT:
         if (rollouts->fit_kof)  // the general cost mask: its own kernels (EnvAcrobotMask, TU 6)
           return launch_tu([&] { return mtgp_tu_launch_acrobot_mask(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
-        return launch_ctl<EnvAcrobot>(A, model, rollouts, jit, noise, traj, grid, block, s);
+        return launch_tu([&] { return mtgp_tu_launch_acrobot(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
       case MTGP_ENV_HARMONIC_OSCILLATOR:
         return launch_tu([&] { return mtgp_tu_launch_harmonic(&A, model, rollouts, jit, noise, traj, grid.x, block.x, s); }, s);
       case MTGP_ENV_STIRRED_TANK_REACTOR:
@@ -4292,52 +4810,9 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     }
   } else if (model->model == MTGP_MODEL_SR) {
     if (!rollouts->ys_true) return MTGP_ERR_ARG;
-    if (model->n_var > 4) {
-      if (model->n_var > MTGP_MAX_DATA || n_prog < model->prog_state + model->n_var) return MTGP_ERR_ARG;
-      const int nw = (model->n_var + kWideComp - 1) / kWideComp;
-      const dim3 wgrid((unsigned)(((long)P + G - 1) / G * Wset)), wblock(kWave * nw);
-      if (dopri5) {  // + a reduction vector (error norm, MSE)
-        const size_t lds_dp = (size_t)(3 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
-        return launch_timed([&] {
-          if (jit) {
-            if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, true>), wgrid, wblock, lds_dp, s, A);
-            else hipLaunchKernelGGL((k_sr_wide_dopri5<false, true>), wgrid, wblock, lds_dp, s, A);
-          } else if (traj) hipLaunchKernelGGL((k_sr_wide_dopri5<true, false>), wgrid, wblock, lds_dp, s, A);
-          else hipLaunchKernelGGL((k_sr_wide_dopri5<false, false>), wgrid, wblock, lds_dp, s, A);
-        }, s);
-      }
-      const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
-      return launch_timed([&] {
-        if (jit) {
-          if (traj) hipLaunchKernelGGL((k_sr_wide<true, true>), wgrid, wblock, lds, s, A);
-          else hipLaunchKernelGGL((k_sr_wide<false, true>), wgrid, wblock, lds, s, A);
-        } else if (traj) hipLaunchKernelGGL((k_sr_wide<true, false>), wgrid, wblock, lds, s, A);
-        else hipLaunchKernelGGL((k_sr_wide<false, false>), wgrid, wblock, lds, s, A);
-      }, s);
-    }
-#define MTGP_SR(NV)                                                                                       \
-  case NV:                                                                                                \
-    return launch_timed([&] {                                                                             \
-      if (dopri5) {                                                                                       \
-        if (jit) {                                                                                        \
-          if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, true>), grid, block, 0, s, A);              \
-          else hipLaunchKernelGGL((k_sr_dopri5<NV, false, true>), grid, block, 0, s, A);                  \
-        } else if (traj) hipLaunchKernelGGL((k_sr_dopri5<NV, true, false>), grid, block, 0, s, A);        \
-        else hipLaunchKernelGGL((k_sr_dopri5<NV, false, false>), grid, block, 0, s, A);                   \
-      } else if (jit) {                                                                                   \
-        if (traj) hipLaunchKernelGGL((k_sr<NV, true, true>), grid, block, 0, s, A);                       \
-        else hipLaunchKernelGGL((k_sr<NV, false, true>), grid, block, 0, s, A);                           \
-      } else if (traj) hipLaunchKernelGGL((k_sr<NV, true, false>), grid, block, 0, s, A);                 \
-      else hipLaunchKernelGGL((k_sr<NV, false, false>), grid, block, 0, s, A);                            \
-    }, s);
-    switch (model->n_var) {
-      MTGP_SR(1)
-      MTGP_SR(2)
-      MTGP_SR(3)
-      MTGP_SR(4)
-      default: return MTGP_ERR_ARG;
-    }
-#undef MTGP_SR
+    if (model->n_var > 4 && (model->n_var > MTGP_MAX_DATA || n_prog < model->prog_state + model->n_var))
+      return MTGP_ERR_ARG;
+    return launch_tu([&] { return mtgp_tu_launch_sr(&A, model, jit, traj, dopri5, (unsigned)G, (unsigned)Wset, grid.x, block.x, s); }, s);
   }
   return MTGP_ERR_ARG;
   }();

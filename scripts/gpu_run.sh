@@ -43,6 +43,8 @@ for step in "$@"; do
   case $step in
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmask) run pytest_mask 600 python -u -m pytest tests/test_gpu_acrobot_mask.py tests/test_gpu_parity.py tests/test_dopri5.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    testmaskonly) run pytest_maskonly 300 python -u -m pytest tests/test_gpu_acrobot_mask.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
+    testpin) run pytest_pin 600 python -u -m pytest tests/test_gpu_parity.py tests/test_notebook_pin.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testcoef) run pytest_coef 600 python -u -m pytest tests/test_coefficients.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     gradtime) run gradtime 300 python scripts/grad_time.py || exit 1 ;;
     prof_grad) run prof_grad 300 rocprofv3 --kernel-trace --stats -d $O/prof_grad -o prof_grad -- python3 scripts/grad_time.py || exit 1
@@ -77,6 +79,10 @@ for step in "$@"; do
     ab_c3_bfm) run ab_c3_bfm 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,shift" --tag c3_bfm || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
+    fbcount) run fbcount 300 python scripts/fb_count.py || exit 1 ;;
+    ab_c3) V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
+      V=${V/,fbcount/}
+      run ab_c3 600 python scripts/kvariants.py --config c3 --rounds 6 --variants $V --tag ab_c3 || exit 1 ;;
     budget)  # C3 per-section budget: interleaved timing of every lib/abrun variant, then one SQ pass each
       V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
       run budget_time 600 python scripts/kvariants.py --config c3 --rounds 4 --variants $V --tag budget || exit 1
