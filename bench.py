@@ -333,6 +333,10 @@ def main():
                                                            "obs_w")
                    if d.get(k) is not None) + P * 4 * 2  # rollout data + nodes in + fitness out
     alg_bytes = traj_bytes + prog_bytes + io_bytes
+    # SURVEY.md section 8(d)'s accounting: the same without the observations ys (28.3 B per
+    # unit-step at C3 instead of 44.2); evaluate_candidate returns ys too (dyn.py:99, 105), so the
+    # line's frac keeps them and both are reported
+    alg_bytes_s8d = alg_bytes - (res["ys"].numel() * 4 if "ys" in res else 0)
     kmean = float(np.mean(kernel_ms))
     achieved = alg_bytes / (kmean / 1e3) / 1e9
     traffic = valu = None
@@ -384,6 +388,8 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "alg_bytes_per_launch": alg_bytes,
+                     "alg_bytes_s8d": alg_bytes_s8d,
+                     "frac_s8d": alg_bytes_s8d / (kmean / 1e3) / 1e9 / PEAK_HBM_GBS,
                      "valu_frac": valu,
                      "pmc": None if pmc is None else {k: pmc[k] for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
                                                                            "SQ_WAVES", "GRBM_GUI_ACTIVE")
