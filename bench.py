@@ -217,6 +217,16 @@ def cpu_baseline(args, lib, ff, data, pop, steps=None):
                       f"of {os.cpu_count()} on {cpu_model()}, {dt:.2f} s"}
 
 
+def host_evolve_threads() -> str:
+    """The thread count libmtgp_host.so's evolve uses (mtgp_evolve.cpp host_threads): MTGP_HOST_THREADS,
+    else OMP_NUM_THREADS (the pool's CPU share), else the affinity size, at most 64."""
+    for var in ("MTGP_HOST_THREADS", "OMP_NUM_THREADS"):
+        if os.environ.get(var):
+            n = max(1, int(os.environ[var]))
+            return f"{n if var == 'MTGP_HOST_THREADS' else min(n, 64)} ({var})"
+    return f"{min(len(os.sched_getaffinity(0)), 64)} (affinity)"
+
+
 def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
     """SURVEY §8(d) end-to-end rate: GeneticProgramming.evaluate_population (gp.py:403-433) on a
     host numpy population of P*ws individuals, as the user's loop calls it -- H2D copy of this
@@ -415,7 +425,7 @@ def main():
             "h2d_bytes_per_rank": int(pop.nbytes),
             "host_evolve_ms": evolve_ms,
             "host_evolve_what": f"GeneticProgramming.evolve of the {P * ws}-candidate population (native host "
-                                f"library, MTGP_HOST_THREADS={os.environ.get('MTGP_HOST_THREADS', '8')}), median of 3"}
+                                f"library on {host_evolve_threads()} threads), median of 3"}
     if rank == 0 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:

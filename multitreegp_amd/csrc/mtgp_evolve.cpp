@@ -15,6 +15,7 @@
 #include <sched.h>
 #include <stdint.h>
 #include <string.h>
+#include <xmmintrin.h>
 
 #include <algorithm>
 #include <cmath>
@@ -80,6 +81,19 @@ struct Node {
   float v;
 };
 typedef std::vector<Node> Nodes;
+
+// Copy n floats of tree rows; non-temporal stores when the destination is 16-B aligned (the
+// offspring array is written once and read by the next H2D copy: no read-for-ownership traffic,
+// which at C5's 537 MB per generation is a third of the step's memory traffic).
+inline void copy_rows(float* dst, const float* src, size_t n) {
+  if (((uintptr_t)dst & 15u) != 0) {
+    memcpy(dst, src, sizeof(float) * n);
+    return;
+  }
+  size_t k = 0;
+  for (; k + 4 <= n; k += 4) _mm_stream_ps(dst + k, _mm_loadu_ps(src + k));
+  for (; k < n; ++k) dst[k] = src[k];
+}
 
 // ------------------------------------------------------------------ the library
 struct Lib {
@@ -369,83 +383,117 @@ struct Ops {
       case 5: ok = insert_operator(t, g, vm, out); break;
       default: ok = replace_tree(t, g, vm, out); break;
     }
-    if (!ok) memcpy(out, t, sizeof(float) * 4 * N);
+    if (!ok) copy_rows(out, t, 4 * (size_t)N);
   }
 
   // -- crossover (crossover.py:60-192)
-  std::vector<double> cx_w(const float* t) const {
-    std::vector<double> w(N);
-    for (int k = 0; k < N; ++k) w[k] = t[4 * k] == 0.0f ? 0.0 : (L.is_op(t[4 * k]) ? 2.0 : 1.0);
-    return w;
-  }
-  bool cx_invalid(const float* t1, const float* t2, int i1, int i2) const {
-    const int s1 = i1 - find_end_idx(t1, i1), s2 = i2 - find_end_idx(t2, i2);
-    int e1 = 0, e2 = 0;
-    for (int k = 0; k < N; ++k) {
-      e1 += t1[4 * k] == 0.0f;
-      e2 += t2[4 * k] == 0.0f;
-    }
-    bool equal = false;
-    if (s1 == s2 && (N - e1 > 1 || N - e2 > 1)) {
-      equal = true;
-      for (int k = 0; k < s1; ++k) {
-        const float* a = t1 + 4 * (i1 - k);
-        const float* b = t2 + 4 * (i2 - k);
-        const bool same_leaf = a[3] == b[3] && a[0] == 1.0f;
-        if (!((a[0] == b[0] && a[0] > 1.0f) || same_leaf)) {
-          equal = false;
-          break;
-        }
-      }
-    }
-    return e1 < s2 - s1 || e2 < s1 - s2 || equal;
-  }
-  // Crossover of one tree pair (the same draws and results as replacing each subtree through
-  // subtree() / replace(), written without heap traffic: both trees go to preorder once, the two
-  // offspring are spliced from the preorder lists in per-thread scratch; C5's 64 trees per
-  // candidate made the per-call vectors the cost of a generation).
+  // Crossover of one tree pair (the same draws and results as splicing the preorder lists through
+  // subtree() / replace(), written without them: one scan per parent, then the two offspring rows
+  // are written straight from the parents' rows; C5's 64 trees per candidate made the per-call
+  // work the cost of a generation).
   void crossover(const float* t1, const float* t2, Rng& g, float* o1, float* o2) const {
-    // row weights (0 empty, 2 operator, 1 leaf: cx_w) as prefix sums -- the weights are small
-    // integers, so Rng::choice's running subtraction and a binary search over the prefix sums pick
-    // the same row for every draw -- and the empty-row counts cx_invalid needs, in one pass
-    thread_local std::vector<int> c1, c2;
-    c1.resize(N + 1);
-    c2.resize(N + 1);
-    c1[0] = c2[0] = 0;
-    int e1 = 0, e2 = 0;
-    for (int k = 0; k < N; ++k) {
-      const float f1 = t1[4 * k], f2 = t2[4 * k];
-      e1 += f1 == 0.0f;
-      e2 += f2 == 0.0f;
-      c1[k + 1] = c1[k] + (f1 == 0.0f ? 0 : (L.is_op(f1) ? 2 : 1));
-      c2[k + 1] = c2[k] + (f2 == 0.0f ? 0 : (L.is_op(f2) ? 2 : 1));
-    }
+    thread_local Scan x1, x2;
+    scan(t1, x1);
+    scan(t2, x2);
     auto unchanged = [&]() {
-      memcpy(o1, t1, sizeof(float) * 4 * N);
-      memcpy(o2, t2, sizeof(float) * 4 * N);
+      copy_rows(o1, t1, 4 * (size_t)N);
+      copy_rows(o2, t2, 4 * (size_t)N);
     };
-    if (c1[N] == 0 || c2[N] == 0) return unchanged();
+    if (x1.c[N] == 0 || x2.c[N] == 0) return unchanged();
     for (int it = 0; it < kMaxRetries; ++it) {
-      const int i1 = choose_prefix(g, c1), i2 = choose_prefix(g, c2);
-      if (cx_invalid_e(t1, t2, i1, i2, e1, e2)) continue;
-      thread_local Nodes n1, n2, m1, m2;
-      thread_local std::vector<int> sz1, sz2;
-      preorder_into(t1, n1);
-      preorder_into(t2, n2);
-      sizes_into(n1, sz1);
-      sizes_into(n2, sz2);
-      const int p1 = N - 1 - i1, p2 = N - 1 - i2, s1 = sz1[p1], s2 = sz2[p2];
-      splice(n1, p1, s1, n2, p2, s2, m1);  // t1 with its subtree at i1 replaced by t2's at i2
-      splice(n2, p2, s2, n1, p1, s1, m2);
-      if ((int)m1.size() <= N && (int)m2.size() <= N && !m1.empty() && !m2.empty()) {
-        write_preorder(m1, o1);
-        write_preorder(m2, o2);
+      const int i1 = choose_prefix(g, x1.c), i2 = choose_prefix(g, x2.c);
+      if (cx_invalid_e(t1, t2, i1, i2, x1.e, x2.e)) continue;
+      const int n1 = N - x1.lo, n2 = N - x2.lo, s1 = x1.sz[i1], s2 = x2.sz[i2];
+      // t1 with its subtree at i1 replaced by t2's at i2 (and the converse): n1 - s1 + s2 nodes
+      if (n1 - s1 + s2 <= N && n2 - s2 + s1 <= N && n1 - s1 + s2 > 0 && n2 - s2 + s1 > 0) {
+        splice_rows(t1, x1, i1, s1, t2, x2, i2, s2, o1);
+        splice_rows(t2, x2, i2, s2, t1, x1, i1, s1, o2);
       } else {
         unchanged();
       }
       return;
     }
     unchanged();
+  }
+  // One pass over a parent's rows, low to high: the crossover row weights (crossover.py: 0 empty,
+  // 2 operator, 1 leaf) as prefix sums c -- the weights are small integers, so Rng::choice's
+  // running subtraction and a binary search over the prefix sums pick the same row for every draw
+  // -- the empty-row count e cx_invalid_e needs, the lowest row lo of the preorder (rows N-1 .. lo,
+  // as to_preorder reads them) and every row's subtree size from the arities (subtree_sizes on the
+  // array itself: the operands of row k are the subtrees rooted at k-1 and just below it).
+  struct Scan {
+    std::vector<int> c, sz;
+    int e, lo;
+  };
+  void scan(const float* t, Scan& x) const {
+    x.c.resize(N + 1);
+    x.sz.resize(N);
+    int* c = x.c.data();
+    int* sz = x.sz.data();
+    const char* op = L.op_tab.data();
+    const int* slots = L.c->slots;
+    const int nf = L.c->n_funcs;
+    int e = 0, lo = 0, acc = 0;
+    c[0] = 0;
+    for (int k = 0; k < N; ++k) {
+      const float f = t[4 * k];
+      const int fi = (int)f;
+      const bool in = fi >= 0 && fi < nf;
+      // Lib::is_op and Lib::arity with one range test
+      const bool isop = in && f >= 0.0f && (float)fi == f && op[fi];
+      const int ar = in ? slots[fi] : 0;
+      e += f == 0.0f;
+      lo = fi == 0 ? k + 1 : lo;
+      acc += f == 0.0f ? 0 : (isop ? 2 : 1);
+      c[k + 1] = acc;
+      int s = 1;
+      if (ar >= 1 && k >= 1) {
+        const int sa = sz[k - 1], kb = k - 1 - sa;
+        s += sa;
+        if (ar >= 2 && kb >= 0) s += sz[kb];
+      }
+      sz[k] = s;
+    }
+    x.e = e;
+    x.lo = lo;
+  }
+  // Write one crossover offspring straight from the parents' rows: `a`'s rows above ia, then `b`'s
+  // subtree at ib (sb rows), then `a`'s rows below its subtree at ia (sa rows), each row
+  // [f, k-1 | -1, k-1-|subtree(k-1)| | -1, value if coefficient] exactly as from_preorder
+  // writes the spliced preorder list.  The subtree sizes of `a`'s rows above ia are a's own plus
+  // (sb - sa) for the ancestors of ia (the rows whose subtree contains it).  `a` and `b` may be
+  // the same tree (both tournaments picked one candidate).
+  void splice_rows(const float* a, const Scan& xa, int ia, int sa, const float* b, const Scan& xb, int ib,
+                   int sb, float* o) const {
+    const int d = sb - sa, n = N - xa.lo + d;  // offspring nodes
+    const int* za = xa.sz.data();
+    const int* zb = xb.sz.data();
+    const int kb = ia - sb, lo = N - n;  // the inserted subtree is rows ia .. kb+1
+    auto size_at = [&](int k) {  // subtree size of output row k (any segment)
+      if (k > ia) {
+        const int s = za[k];
+        return k - s + 1 <= ia ? s + d : s;  // an ancestor of the splice point
+      }
+      if (k > kb) return zb[ib - (ia - k)];
+      return za[k + d];
+    };
+    const bool nt = ((uintptr_t)o & 15u) == 0;
+    auto put = [&](int k, float f, float x, float y, float v) {
+      if (nt) _mm_stream_ps(o + 4 * k, _mm_set_ps(v, y, x, f));
+      else { o[4 * k] = f; o[4 * k + 1] = x; o[4 * k + 2] = y; o[4 * k + 3] = v; }
+    };
+    auto row = [&](int k, const float* src, int bsize) {  // bsize: |subtree(k-1)| in the offspring
+      const int f = (int)src[0], ar = L.arity(f);
+      put(k, (float)f, ar >= 1 ? (float)(k - 1) : -1.0f, ar == 2 ? (float)(k - 1 - bsize) : -1.0f,
+          f == 1 ? src[3] : 0.0f);
+    };
+    for (int k = 0; k < lo; ++k) put(k, 0.0f, -1.0f, -1.0f, 0.0f);
+    for (int k = lo; k <= kb; ++k) row(k, a + 4 * (k + d), k >= 1 ? za[k - 1 + d] : 0);
+    for (int k = kb + 1; k <= ia; ++k) {
+      const int r = ib - (ia - k);
+      row(k, b + 4 * r, k - 1 > kb ? zb[r - 1] : size_at(k - 1));
+    }
+    for (int k = ia + 1; k < N; ++k) row(k, a + 4 * k, size_at(k - 1));
   }
   // Rng::choice over integer weights w[k] = c[k + 1] - c[k] (c non-decreasing, c[N] > 0): the same
   // uniform draw, and u - w[0] - ... - w[i-1] < w[i]  <=>  u < c[i + 1] exactly (integer sums)
@@ -476,51 +524,6 @@ struct Ops {
       }
     }
     return e1 < s2 - s1 || e2 < s1 - s2 || equal;
-  }
-  void preorder_into(const float* t, Nodes& out) const {  // to_preorder without the allocation
-    out.clear();
-    for (int k = N - 1; k >= 0; --k) {
-      const int f = (int)t[4 * k];
-      if (f == 0) break;
-      out.push_back({f, t[4 * k + 3]});
-    }
-  }
-  void sizes_into(const Nodes& n, std::vector<int>& sz) const {  // subtree_sizes without the allocations
-    thread_local std::vector<int> st;
-    sz.resize(n.size());
-    st.clear();
-    for (int i = (int)n.size() - 1; i >= 0; --i) {
-      int sum = 1;
-      for (int a = 0; a < L.arity(n[i].f); ++a) {
-        sum += st.back();
-        st.pop_back();
-      }
-      sz[i] = sum;
-      st.push_back(sum);
-    }
-  }
-  static void splice(const Nodes& a, int pa, int sa, const Nodes& b, int pb, int sb, Nodes& out) {
-    out.clear();
-    out.insert(out.end(), a.begin(), a.begin() + pa);
-    out.insert(out.end(), b.begin() + pb, b.begin() + pb + sb);
-    out.insert(out.end(), a.begin() + pa + sa, a.end());
-  }
-  void write_preorder(const Nodes& n, float* t) const {  // from_preorder (n fits) without the allocations
-    thread_local std::vector<int> sz;
-    sizes_into(n, sz);
-    for (int k = 0; k < N - (int)n.size(); ++k) {
-      t[4 * k + 0] = 0.0f;
-      t[4 * k + 1] = -1.0f;
-      t[4 * k + 2] = -1.0f;
-      t[4 * k + 3] = 0.0f;
-    }
-    for (size_t i = 0; i < n.size(); ++i) {
-      const int k = N - 1 - (int)i, ar = L.arity(n[i].f);
-      t[4 * k + 0] = (float)n[i].f;
-      t[4 * k + 1] = ar >= 1 ? (float)(k - 1) : -1.0f;
-      t[4 * k + 2] = ar == 2 ? (float)(k - 1 - sz[i + 1]) : -1.0f;
-      t[4 * k + 3] = n[i].f == 1 ? n[i].v : 0.0f;
-    }
   }
 
   static constexpr int kMaxRetries = 1000;
@@ -617,7 +620,8 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
     const double* tp = cfg->tournament_prob + (size_t)i * cfg->tournament_size;
     const double* rp = cfg->reproduction_type_prob + (size_t)i * 3;
     const double repro = cfg->reproduction_prob[i];
-    parallel_for(n_pairs, 256, [&](long k) {
+    // a thread per >= 64K tree rows of offspring (C5: 8 pairs, C3: 342 pairs)
+    parallel_for(n_pairs, std::max(1L, 65536L / ((long)T * N)), [&](long k) {
       Rng g(seed, (uint64_t)i + 1, (uint64_t)k + 1);
       auto tournament = [&]() {  // reproduction.py:29-49
         thread_local std::vector<int> idx;
@@ -636,8 +640,8 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
         for (int t = 0; t < T; ++t) {
           if (m[t]) ops.crossover(p1 + t * tsz, p2 + t * tsz, g, c1 + t * tsz, c2 + t * tsz);
           else {
-            memcpy(c1 + t * tsz, p1 + t * tsz, sizeof(float) * tsz);
-            memcpy(c2 + t * tsz, p2 + t * tsz, sizeof(float) * tsz);
+            copy_rows(c1 + t * tsz, p1 + t * tsz, tsz);
+            copy_rows(c2 + t * tsz, p2 + t * tsz, tsz);
           }
         }
       } else if (type == 1) {  // mutate_pair (gp.py:499-511, mutation.py:555-577)
@@ -647,7 +651,7 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
           const std::vector<char> m = tree_mask(g, T, repro);
           for (int t = 0; t < T; ++t) {
             if (m[t]) ops.mutate_tree(par + t * tsz, g, cfg->var_mask + (size_t)t * cfg->n_vars, ch + t * tsz);
-            else memcpy(ch + t * tsz, par + t * tsz, sizeof(float) * tsz);
+            else copy_rows(ch + t * tsz, par + t * tsz, tsz);
           }
         }
       } else {  // sample_pair (gp.py:513-525): two fresh candidates
@@ -658,6 +662,7 @@ extern "C" int mtgp_evolve_populations(const float* pops, const float* fitness, 
                           ch + t * tsz);
         }
       }
+      _mm_sfence();  // the non-temporal row stores are visible before the threads join
     });
   }
   return out_size;
