@@ -46,6 +46,9 @@ def parse():
                          "(DynamicPolicy.ipynb:105 / StaticPolicy.ipynb:102); c2/c3 only")
     ap.add_argument("--obs-noise", type=float, default=0.0,
                     help="Acrobot observation noise (the notebooks use 0.1): in-kernel threefry normals per stage")
+    ap.add_argument("--ext-ops", action="store_true",
+                    help="C2/C3 node library + exp, log, sqrt, tanh, abs (p 0.1 each, like sin / cos): the JIT's "
+                         "extended-operator templates under the headline workload (A/B line, not the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-pmc", action="store_true",
@@ -103,6 +106,10 @@ def setup_workload(args, rank):
     env = mt.Acrobot(0.0, getattr(args, "obs_noise", 0.0))
     ops = [("+", None, 2, 0.5), ("-", None, 2, 0.1), ("*", None, 2, 0.5), ("sin", None, 1, 0.1),
            ("cos", None, 1, 0.1)]
+    ext = getattr(args, "ext_ops", False)
+    if ext:
+        ops = ops + [(name, None, 1, 0.1) for name in ("exp", "log", "sqrt", "tanh", "abs")]
+    tag = "_ext" if ext else ""
     if args.solver == "dopri5":
         solver = dict(solver=mt.Dopri5(), stepsize_controller=mt.PIDController(rtol=1e-4, atol=1e-4, dtmin=0.001))
     else:
@@ -111,14 +118,14 @@ def setup_workload(args, rank):
         lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4"]], [1])
         ff = mt.FeedforwardEvaluator(env, 0.05, max_steps=1000, **solver)
         data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
-        pop = _cached_population(f"c2_{args.pop}_r{rank}",
+        pop = _cached_population(f"c2{tag}_{args.pop}_r{rank}",
                                  lambda: sample_population(3000 + rank, lib, args.pop, 1, max_init_depth=4,
                                                            max_nodes=30)[0])
         return env, lib, ff, data, pop
     lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
     ff = mt.DynamicEvaluator(env, 2, 0.05, max_steps=1000, **solver)
     data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
-    pop = _cached_population(f"c3_{args.pop}_r{rank}",
+    pop = _cached_population(f"c3{tag}_{args.pop}_r{rank}",
                              lambda: sample_population(1000 + rank, lib, args.pop, 1, max_init_depth=10,
                                                        max_nodes=64)[0])
     return env, lib, ff, data, pop
@@ -391,7 +398,8 @@ def main():
         "dtype": "f32",
         "data": data_desc[args.config],
         "config": {"workload": workloads[args.config] + (", trajectories on" if traj else ", fitness only")
-                   + (f", obs_noise {args.obs_noise} (threefry in-kernel)" if args.obs_noise else ""),
+                   + (f", obs_noise {args.obs_noise} (threefry in-kernel)" if args.obs_noise else "")
+                   + (", node library + exp log sqrt tanh abs (JIT subroutines)" if args.ext_ops else ""),
                    "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps, "trajectories": traj,
                    "parallelism": f"population-sharded dp{ws}"},
         "kernel_ms": kmean,

@@ -8,9 +8,10 @@
 // vector and the operand stack live in VGPRs, the stack depth is resolved at translation
 // time), sin/cos/division copy the templates of mtgp_jit_blobs.h.  Results are
 // bit-identical to the interpreter: every IEEE operation has the same operands in the same
-// order; the templates follow include/mtgp_f32math.h op for op; lanes that would need the
-// spec's slow sin/cos reduction (finite |x| >= 2^17) are reported in s[32:33] and the
-// evaluator re-runs that program with the interpreter.
+// order; the templates (sin, cos, exp, log, tanh, sqrt as shared subroutines, abs and the
+// division inline) follow include/mtgp_f32math.h op for op, special cases included, so every
+// opcode of the node library translates.  s[32:33] (fallback lanes for the evaluator's
+// interpreter re-run) stays part of the ABI but no template sets it.
 //
 // Register ABI of a generated program (the evaluator's call site pins these):
 //   v0-v7    data slots 0-7 (read only)          v8      accumulator = result
@@ -49,16 +50,24 @@ constexpr uint32_t kJitSrcLiteral = 255u;
 // VOP2 opcodes (gfx9 encoding)
 constexpr uint32_t kVop2Add = 1u, kVop2Sub = 2u, kVop2Subrev = 3u, kVop2Mul = 5u;
 constexpr uint32_t kSetpcS30 = 0xbe801d1eu;  // s_setpc_b64 s[30:31]
-// largest translation of one program instruction (push + two moves + the sin template)
+// largest translation of one program instruction (an upper bound: push + two moves + the sin template)
 constexpr int kJitMaxWordsPerInstr = 1 + 4 + (MTGP_JIT_COS_WORDS > MTGP_JIT_SIN_WORDS ? MTGP_JIT_COS_WORDS : MTGP_JIT_SIN_WORDS);
 
-// The sin/cos templates are shared subroutines at the start of the code buffer (one copy,
-// hot in the instruction cache); generated code calls them with a PC-relative address.
-constexpr uint32_t kJitAlignBytes = 64u;
-constexpr uint32_t kJitSinOffset = 0u;
-constexpr uint32_t kJitCosOffset = (MTGP_JIT_SIN_WORDS * 4u + kJitAlignBytes - 1u) & ~(kJitAlignBytes - 1u);
-constexpr uint32_t kJitTemplateBytes =
-    (kJitCosOffset + MTGP_JIT_COS_WORDS * 4u + kJitAlignBytes - 1u) & ~(kJitAlignBytes - 1u);
+// The sin / cos / exp / log / tanh / sqrt templates are shared subroutines at the start of the
+// code buffer (mtgp_jit_sub_blob: one copy each, hot in the instruction cache); generated code
+// calls them with a PC-relative address.
+constexpr uint32_t kJitSinOffset = MTGP_JIT_SIN_OFFSET, kJitCosOffset = MTGP_JIT_COS_OFFSET;
+constexpr uint32_t kJitTemplateBytes = MTGP_JIT_SUB_WORDS * 4u;
+// executed words of one call of each subroutine (the schedule's cost model: the hot path up to
+// the first return; the out-of-line slow paths -- sin/cos |x| >= 2^17, exp |x| > 88.72 or NaN,
+// log of anything but a positive normal, tanh |x| >= 0.625, sqrt x < 2^-96 / 0 / inf / NaN --
+// run only when some lane needs them)
+constexpr int kJitSinExec = MTGP_JIT_SIN_WORDS - MTGP_JIT_SIN_SKIPPABLE_WORDS;
+constexpr int kJitCosExec = MTGP_JIT_COS_WORDS - MTGP_JIT_COS_SKIPPABLE_WORDS;
+constexpr int kJitExpExec = MTGP_JIT_EXP_WORDS - MTGP_JIT_EXP_SKIPPABLE_WORDS;
+constexpr int kJitLogExec = MTGP_JIT_LOG_WORDS - MTGP_JIT_LOG_SKIPPABLE_WORDS;
+constexpr int kJitTanhExec = MTGP_JIT_TANH_WORDS - MTGP_JIT_TANH_SKIPPABLE_WORDS;
+constexpr int kJitSqrtExec = MTGP_JIT_SQRT_WORDS - MTGP_JIT_SQRT_SKIPPABLE_WORDS;
 constexpr uint32_t kGetpcS44 = 0xbeac1c00u;     // s_getpc_b64 s[44:45]
 constexpr uint32_t kAddS44 = 0x802cff2cu;       // s_add_u32 s44, s44, literal
 constexpr uint32_t kAddcS45M1 = 0x822dc12du;    // s_addc_u32 s45, s45, -1
@@ -68,7 +77,7 @@ constexpr uint32_t kSwappcS40 = 0xbea81e2cu;    // s_swappc_b64 s[40:41], s[44:4
 struct JitOut {
   uint32_t* out;  // nullptr: count only
   int n;
-  int trig = 0;       // sin/cos subroutine calls emitted
+  int sub = 0;        // executed words of the subroutine calls emitted (cost model)
   uint32_t base = 0;  // byte offset of out[0] in the code buffer (for PC-relative calls)
   MTGP_JIT_HD void w(uint32_t v) {
     if (out) out[n] = v;
@@ -125,18 +134,21 @@ MTGP_JIT_HD inline void jit_binop(JitOut& o, int fn, JitSrc x, JitSrc y) {
   else o.vop2(opc, kJitAcc, 256u + (uint32_t)x.reg, y.reg);
 }
 
-MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
-  ++o.trig;
+// v8 = SUB(x): x into v17, then a PC-relative s_swappc_b64 into the subroutine at byte `target`
+MTGP_JIT_HD inline void jit_call(JitOut& o, uint32_t target, int exec_words, JitSrc x) {
+  o.sub += exec_words;
   if (x.lit) o.movc(kJitT0, x.bits); else o.movv(kJitT0, x.reg);
   // s_getpc_b64 yields the address of the next instruction: target = that + rel
   const uint32_t pc_next = o.base + (uint32_t)(o.n + 1) * 4u;
-  const uint32_t target = is_sin ? kJitSinOffset : kJitCosOffset;
   const int64_t rel = (int64_t)target - (int64_t)pc_next;
   o.w(kGetpcS44);
   o.w(kAddS44);
   o.w((uint32_t)(int32_t)rel);
   o.w(rel < 0 ? kAddcS45M1 : kAddcS45Z);
   o.w(kSwappcS40);
+}
+MTGP_JIT_HD inline void jit_trig(JitOut& o, bool is_sin, JitSrc x) {
+  jit_call(o, is_sin ? kJitSinOffset : kJitCosOffset, is_sin ? kJitSinExec : kJitCosExec, x);
 }
 
 enum { kJitOk = 0, kJitErrOpcode = -1, kJitErrSlot = -2, kJitErrStack = -3, kJitErrNoEnd = -4 };
@@ -235,6 +247,11 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
       case MTGP_OP_LDVP: if (sib >= max_slot) return kJitErrSlot; ok = push(); o.movv(kJitAcc, vslot(sib, kJitLoadTmp)); break;
       case MTGP_OP_SIN: jit_trig(o, true, acc); continue;
       case MTGP_OP_COS: jit_trig(o, false, acc); continue;
+      case MTGP_OP_EXP: jit_call(o, MTGP_JIT_EXP_OFFSET, kJitExpExec, acc); continue;
+      case MTGP_OP_LOG: jit_call(o, MTGP_JIT_LOG_OFFSET, kJitLogExec, acc); continue;
+      case MTGP_OP_TANH: jit_call(o, MTGP_JIT_TANH_OFFSET, kJitTanhExec, acc); continue;
+      case MTGP_OP_SQRT: jit_call(o, MTGP_JIT_SQRT_OFFSET, kJitSqrtExec, acc); continue;
+      case MTGP_OP_ABS: o.blob(mtgp_jit_abs_blob, MTGP_JIT_ABS_WORDS); continue;
       case MTGP_OP_SINV: case MTGP_OP_COSV: case MTGP_OP_SINVP: case MTGP_OP_COSVP:
         if (sib >= max_slot) return kJitErrSlot;
         if (code == MTGP_OP_SINVP || code == MTGP_OP_COSVP) ok = push();
@@ -328,13 +345,12 @@ MTGP_JIT_HD inline int jit_translate(const MtgpInstr* prog, int L, uint32_t* out
 }
 
 // Estimated issue cost of one program (schedule weight): code words actually executed, i.e.
-// without the slow-reduction blocks of the sin/cos templates (skipped unless |x| >= 2^17).
-constexpr int kJitTrigExecuted = MTGP_JIT_SIN_WORDS - MTGP_JIT_SIN_SKIPPABLE_WORDS;
+// the program's own words plus the subroutines' executed words (JitOut::sub).
 MTGP_JIT_HD inline int jit_cost(const MtgpInstr* prog, int L) {
   JitOut o{nullptr, 0};
   const int rc = jit_program(o, prog, L, true);
   if (rc < 0) return rc;
-  const int w = o.n + kJitTrigExecuted * o.trig;
+  const int w = o.n + o.sub;
   return w > 1 ? w : 1;
 }
 

@@ -2775,7 +2775,7 @@ __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n
   const int rc = mtgp::jit_program(o, out, L, false, jit_mode);
   if (jit_words_out) jit_words_out[pj] = rc < 0 ? rc : o.n;
   if (jit_cost_out) {  // = k_jit_cost: executed words of the callable translation / 4
-    const int c = rc < 0 ? rc : (o.n + 1 + mtgp::kJitTrigExecuted * o.trig);
+    const int c = rc < 0 ? rc : (o.n + 1 + o.sub);
     jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
   }
 }
@@ -2790,9 +2790,10 @@ __device__ __forceinline__ void flat_jit_size(const MtgpInstr* out, int L, int n
 // flat_jit_size (tests/test_gpu_build.py compares them with the host translation).
 struct JitOpTable {
   uint8_t words[64];  // code words of the opcode's translation
-  uint8_t flags[64];  // kOpValid | kOpTrig | kOpIbSlot | kOpAxSlot | kOpPush | kOpPop
+  uint8_t flags[64];  // kOpValid | kOpIbSlot | kOpAxSlot | kOpPush | kOpPop
+  uint8_t sub[64];    // executed words of the subroutine it calls (JitOut::sub; 0: none)
 };
-enum : uint8_t { kOpValid = 1, kOpTrig = 2, kOpIbSlot = 4, kOpAxSlot = 8, kOpPush = 16, kOpPop = 32 };
+enum : uint8_t { kOpValid = 1, kOpIbSlot = 4, kOpAxSlot = 8, kOpPush = 16, kOpPop = 32 };
 static_assert(MTGP_OP_COUNT <= 64, "JitOpTable holds 64 opcodes");
 
 JitOpTable jit_op_table() {
@@ -2810,13 +2811,14 @@ JitOpTable jit_op_table() {
     };
     mtgp::JitOut o{nullptr, 0};
     if (probe(0u, 0u, o) != mtgp::kJitOk) continue;  // not an opcode
-    uint8_t f = kOpValid | (o.trig ? kOpTrig : 0) | (d > 0 ? kOpPush : 0) | (d < 0 ? kOpPop : 0);
+    uint8_t f = kOpValid | (d > 0 ? kOpPush : 0) | (d < 0 ? kOpPop : 0);
     const uint32_t far = (uint32_t)mtgp::kJitMaxData * MTGP_SLOT_BYTES;
     mtgp::JitOut o1{nullptr, 0}, o2{nullptr, 0};
     if (probe(0u, far, o1) == mtgp::kJitErrSlot) f |= kOpIbSlot;
     if (probe(far, 0u, o2) == mtgp::kJitErrSlot) f |= kOpAxSlot;
     t.words[code] = (uint8_t)o.n;
     t.flags[code] = f;
+    t.sub[code] = (uint8_t)o.sub;
   }
   return t;
 }
@@ -2824,7 +2826,7 @@ JitOpTable jit_op_table() {
 template <int KI>
 __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n, const JitOpTable& T,
                                                    int32_t* jit_words_out, int32_t* jit_cost_out, size_t pj, int lane) {
-  int words = 0, trig = 0, carry = 0, rc = 0;
+  int words = 0, sub = 0, carry = 0, rc = 0;
   bool failed = false;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
@@ -2843,7 +2845,7 @@ __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n,
         e = mtgp::kJitErrSlot;
       d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
       words += code < 64u ? T.words[code] : 0;
-      trig += (f & kOpTrig) ? 1 : 0;
+      sub += code < 64u ? T.sub[code] : 0;
     }
     int incl = d;  // inclusive prefix sum of the stack effects over this chunk
 #pragma unroll
@@ -2863,12 +2865,12 @@ __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n,
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) {
     words += __shfl_xor(words, off);
-    trig += __shfl_xor(trig, off);
+    sub += __shfl_xor(sub, off);
   }
   if (lane == 0) {
     if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
     if (jit_cost_out) {  // = flat_jit_size
-      const int c = failed ? rc : (words + 1 + mtgp::kJitTrigExecuted * trig);
+      const int c = failed ? rc : (words + 1 + sub);
       jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
     }
   }
@@ -2921,7 +2923,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
   }
   const uint64_t pre_mask = __ballot(pre);
   const int npre = __popcll(pre_mask);
-  int words = 0, trig = 0, carry = 0, rc = 0;
+  int words = 0, sub = 0, carry = 0, rc = 0;
   bool failed = false;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
@@ -2936,7 +2938,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
       words += code < 64u ? T.words[code] : 0;
       if (sa[k] >= 0 && sa[k] < MTGP_MAX_DATA && !((pre_mask >> sa[k]) & 1ull)) words += 3;
       if (sb[k] >= 0 && sb[k] < MTGP_MAX_DATA && !((pre_mask >> sb[k]) & 1ull)) words += 3;
-      trig += (f & kOpTrig) ? 1 : 0;
+      sub += code < 64u ? T.sub[code] : 0;
     }
     int incl = d;
 #pragma unroll
@@ -2956,7 +2958,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
 #pragma unroll
   for (int off = kWave / 2; off > 0; off >>= 1) {
     words += __shfl_xor(words, off);
-    trig += __shfl_xor(trig, off);
+    sub += __shfl_xor(sub, off);
   }
   if (slot_err) {
     failed = true;
@@ -2966,7 +2968,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
   if (lane == 0) {
     if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
     if (jit_cost_out) {  // = flat_jit_size
-      const int c = failed ? rc : (words + 1 + mtgp::kJitTrigExecuted * trig);
+      const int c = failed ? rc : (words + 1 + sub);
       jit_cost_out[pj] = c > 0 ? (c + 3) / 4 : (n > 0 ? n : 0);
     }
   }
@@ -3685,7 +3687,7 @@ __global__ void __launch_bounds__(1024) k_jit_scan(uint32_t* __restrict__ offs, 
     part[t] += v;
     __syncthreads();
   }
-  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
+  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared subroutines come first
   for (int i = b; i < e; ++i) {
     const uint64_t w = offs[i];
     offs[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
@@ -3776,7 +3778,7 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes(uint32_t* __restrict__ 
     err[t] = m < err[t] ? m : err[t];
     __syncthreads();
   }
-  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
+  uint64_t run = part[t] - sum + mtgp::kJitTemplateBytes;  // the shared subroutines come first
   for (int k0 = b; k0 < e; k0 += 8) {
     uint32_t v[8];
 #pragma unroll
@@ -3837,7 +3839,7 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restric
     if (q < w) wbase += wsum[q];
     err = werr[q] < err ? werr[q] : err;
   }
-  uint64_t run = wbase + inc - sum + mtgp::kJitTemplateBytes;  // the shared sin/cos subroutines come first
+  uint64_t run = wbase + inc - sum + mtgp::kJitTemplateBytes;  // the shared subroutines come first
 #pragma unroll
   for (int k = 0; k < PER; ++k) {
     if (b + k < total) {
@@ -3858,9 +3860,8 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restric
 __global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
                                                         uint64_t code_bytes) {
-  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared sin/cos subroutines
-    for (int k = threadIdx.x; k < MTGP_JIT_SIN_WORDS; k += blockDim.x) code[mtgp::kJitSinOffset / 4 + k] = mtgp_jit_sin_blob[k];
-    for (int k = threadIdx.x; k < MTGP_JIT_COS_WORDS; k += blockDim.x) code[mtgp::kJitCosOffset / 4 + k] = mtgp_jit_cos_blob[k];
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SUB_WORDS; k += blockDim.x) code[k] = mtgp_jit_sub_blob[k];
   }
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= (long)U.n_units * U.G) return;
@@ -3897,9 +3898,8 @@ template <int KI>
 __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
                                                         uint64_t code_bytes, JitOpTable optab) {
-  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared sin/cos subroutines
-    for (int k = threadIdx.x; k < MTGP_JIT_SIN_WORDS; k += blockDim.x) code[mtgp::kJitSinOffset / 4 + k] = mtgp_jit_sin_blob[k];
-    for (int k = threadIdx.x; k < MTGP_JIT_COS_WORDS; k += blockDim.x) code[mtgp::kJitCosOffset / 4 + k] = mtgp_jit_cos_blob[k];
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SUB_WORDS; k += blockDim.x) code[k] = mtgp_jit_sub_blob[k];
   }
   const int lane = threadIdx.x & (kWave - 1);
   const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave;  // (wave-uniform)
@@ -3964,11 +3964,10 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   }
 }
 
-// the shared sin/cos subroutines at the start of the code buffer
+// the shared subroutines (sin, cos, exp, log, tanh, sqrt) at the start of the code buffer
 __global__ void __launch_bounds__(256) k_jit_templates(uint32_t* __restrict__ code, uint64_t code_bytes) {
   if (code_bytes < mtgp::kJitTemplateBytes) return;
-  for (int i = threadIdx.x; i < MTGP_JIT_SIN_WORDS; i += blockDim.x) code[mtgp::kJitSinOffset / 4 + i] = mtgp_jit_sin_blob[i];
-  for (int i = threadIdx.x; i < MTGP_JIT_COS_WORDS; i += blockDim.x) code[mtgp::kJitCosOffset / 4 + i] = mtgp_jit_cos_blob[i];
+  for (int i = threadIdx.x; i < MTGP_JIT_SUB_WORDS; i += blockDim.x) code[i] = mtgp_jit_sub_blob[i];
 }
 
 bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,

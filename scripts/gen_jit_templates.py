@@ -3,8 +3,8 @@
 multitreegp_amd/csrc/mtgp_jit_blobs.h.
 
 The JIT (csrc/mtgp_jit.h) translates each flattened program into straight-line gfx950 code;
-simple operations are encoded directly (VOP1/VOP2 words), while sin, cos and the IEEE fp32
-division are copied from the templates below.  Register ABI of the generated code
+simple operations are encoded directly (VOP1/VOP2 words), while sin, cos, exp, log, tanh, sqrt,
+abs and the IEEE fp32 division come from the templates below.  Register ABI of the generated code
 (csrc/mtgp_jit.h): v0-v7 data slots (read only), v8 accumulator, v9-v16 operand stack,
 v17-v24 template temporaries, s[30:31] return address, s[32:33] fallback lane mask
 (OR-accumulated), s[34:39] template temporaries, vcc clobbered, exec never written.
@@ -17,8 +17,14 @@ v17-v24 template temporaries, s[30:31] return address, s[32:33] fallback lane ma
                taken in the common case) to out-of-line exec-masked blocks -- the spec's double
                Cody-Waite below 2^28, its Payne-Hanek reduction beyond -- and come back.  exec
                is restored; s[32:33] is never set (the evaluator's fallback stays for safety).
+  EXP / LOG /: subroutines like SIN / COS (x in v17 -> v8), straight-line: include/mtgp_f32math.h
+  TANH / SQRT  mtgp_expf / mtgp_logf / mtgp_tanhf op for op on every lane, their special cases
+               (NaN, infinities, zeros, range limits) by selects at the end; sqrt is the
+               compiler's correctly rounded gfx950 sequence (= HIP's sqrtf, the spec's).  Temps
+               v18-v24 and v8; v17 (x) is kept until the final selects.
   DIV        : v17 / v18 -> v8, the compiler's own IEEE-exact sequence for gfx950
                (v_div_scale / v_rcp / fma refinement / v_div_fmas / v_div_fixup).
+  ABS        : v8 = |v8| inline (v_and_b32 with 0x7fffffff).
 Hazards: VALU-written SGPR/VCC read by a VALU mask operand gets `s_nop 1` in between; the
 division keeps the compiler's instruction order (v_div_fmas >= 4 wait states after VCC); the
 local branch of the sin/cos double block is a relative SOPP offset resolved by llvm-mc.
@@ -229,6 +235,249 @@ def _sin_coefficients():
     return out
 
 
+def _f32(v):
+    """the f32 bit pattern of a decimal constant (rounded as the C compiler rounds `v f`)"""
+    import struct
+    return "0x%08x" % struct.unpack("<I", struct.pack("<f", float(v)))[0]
+
+
+def _spec_consts(fn, count):
+    """the float literals of one spec function of include/mtgp_f32math.h, in source order"""
+    text = open(os.path.join(ROOT, "include", "mtgp_f32math.h")).read()
+    a = text.index("MTGP_INLINE MTGP_HD float %s(" % fn)
+    b = text.index("\n}\n", a)
+    vals = re.findall(r"(?<![\w.])(-?[0-9]+\.[0-9]+(?:e[-+]?[0-9]+)?)f", text[a:b])
+    assert len(vals) == count, (fn, vals)
+    return vals
+
+
+def _exp_body(x, out, tmp_inf, select=True):
+    """mtgp_expf of v{x} into v{out} op for op (fma Cody-Waite, degree-6 polynomial, two
+    power-of-two scalings; n1 = ni / 2 truncated), then (select) x > 88.7228394 -> +inf.  Temps
+    v18-v21 (and v{tmp_inf}); v{x} is kept.  (The x < -103.972084 -> 0 and NaN cases are the
+    caller's.)  Returns (code, the lower limit's literal)."""
+    v = _spec_consts("mtgp_expf", 13)
+    lim_hi, lim_lo, zero, log2e, ln2hi, ln2lo, c6, c5, c4, c3, c2, c1, one = v
+    assert _f32(c1) == _f32(0.5) and _f32(zero) == _f32(0.0) and _f32(one) == _f32(1.0), v  # inline constants
+    code = f"""v_mul_f32 v18, {_f32(log2e)}, v{x}
+v_rndne_f32 v18, v18
+v_fmamk_f32 v19, v18, {_f32(-float(ln2hi))}, v{x}
+v_fmamk_f32 v19, v18, {_f32(-float(ln2lo))}, v19
+v_mov_b32 v20, {_f32(c5)}
+v_fmac_f32 v20, {_f32(c6)}, v19
+v_fmaak_f32 v20, v20, v19, {_f32(c4)}
+v_fmaak_f32 v20, v20, v19, {_f32(c3)}
+v_fmaak_f32 v20, v20, v19, {_f32(c2)}
+v_fma_f32 v20, v20, v19, 0.5
+v_mul_f32 v21, v19, v19
+v_fmac_f32 v19, v20, v21
+v_add_f32 v19, 1.0, v19
+v_cvt_i32_f32 v18, v18
+v_lshrrev_b32 v20, 31, v18
+v_add_u32 v20, v18, v20
+v_ashrrev_i32 v20, 1, v20
+v_sub_u32 v18, v18, v20
+v_lshl_add_u32 v20, v20, 23, 1.0
+v_mul_f32 v19, v19, v20
+v_lshl_add_u32 v18, v18, 23, 1.0
+v_mul_f32 v{out}, v19, v18
+"""
+    if select:
+        code += f"""v_cmp_lt_f32 vcc, {_f32(lim_hi)}, v{x}
+v_mov_b32 v{tmp_inf}, 0x7f800000
+s_nop 1
+v_cndmask_b32 v{out}, v{out}, v{tmp_inf}, vcc
+"""
+    return code, lim_lo
+
+
+# The subroutines are straight-line: every lane runs the spec's main path and the special cases
+# are selects at the end.  (Hot paths with an out-of-line slow path for the special ranges
+# measured slower at C3 -- 2.48-2.50 vs 2.37 ms with the extended library, profiles/r04/v8, v9:
+# negative log / sqrt arguments, |x| >= 0.625 for tanh and the inf / NaN states of diverged
+# rollouts occur in some lane of most waves, and a unit's other groups' lanes run every program
+# too, so the branch was usually taken and only added work.)
+_RET = "s_setpc_b64 s[40:41]\n"
+
+
+def _div_body(q, n, d, t):
+    """the IEEE division n / d into v{q}, the compiler's own gfx950 sequence (as DIV), temps
+    v{t[0..4]}; n may be an inline constant"""
+    a, r, s_, e, f = t
+    return f"""v_div_scale_f32 v{a}, s[34:35], v{d}, v{d}, {n}
+v_rcp_f32 v{r}, v{a}
+v_div_scale_f32 v{s_}, vcc, {n}, v{d}, {n}
+v_fma_f32 v{e}, -v{a}, v{r}, 1.0
+v_fmac_f32 v{r}, v{e}, v{r}
+v_mul_f32 v{e}, v{s_}, v{r}
+v_fma_f32 v{f}, -v{a}, v{e}, v{s_}
+v_fmac_f32 v{e}, v{f}, v{r}
+v_fma_f32 v{a}, -v{a}, v{e}, v{s_}
+v_div_fmas_f32 v{a}, v{a}, v{r}, v{e}
+v_div_fixup_f32 v{q}, v{a}, v{d}, {n}
+"""
+
+
+def _exp():
+    """EXP subroutine: mtgp_expf(v17) -> v8, straight-line on every lane: the spec's hot path, then
+    NaN -> x, x > 88.72 -> +inf, x < -103.97 -> +0 by selects.  (An out-of-line slow path for
+    |x| > 88.72 or NaN measured slower: diverged rollouts carry inf / NaN states, so some lane of
+    most waves needs it.)"""
+    full, lim_lo = _exp_body(17, 8, 18)
+    return full + f"""v_cmp_gt_f32 vcc, {_f32(lim_lo)}, v17
+s_nop 1
+v_cndmask_b32_e64 v8, v8, 0, vcc
+v_cmp_u_f32 vcc, v17, v17
+s_nop 1
+v_cndmask_b32 v8, v8, v17, vcc
+""" + _RET
+
+
+def _log():
+    """LOG subroutine: mtgp_logf(v17) -> v8: mtgp_logf_pos op for op on every lane (subnormal
+    scaling by a select, s = f / (2 + f) by the IEEE division), then the special cases by
+    class selects: -inf/-normal/-subnormal -> NaN, +-0 -> -inf, NaN/+inf -> x."""
+    v = _spec_consts("mtgp_logf_pos", 10)
+    scale, m1, two, c3, c4, c5, c6, half, ln2hi, ln2lo = v
+    assert _f32(scale) == "0x4c000000" and _f32(m1) == _f32(1.0) and _f32(two) == _f32(2.0), v
+    assert _f32(half) == _f32(0.5), v
+    return _log_text(scale, c3, c4, c5, c6, ln2hi, ln2lo)
+
+
+def _log_text(scale, c3, c4, c5, c6, ln2hi, ln2lo):
+    """Straight-line on every lane.  s = f / (2 + f) by the division's fast path -- rcp,
+    one Newton step, two fma corrections: the compiler's IEEE sequence with v_div_scale and
+    v_div_fixup identities, as they are on EVERY lane, special ones included: m is built with a
+    fixed exponent, so f = m - 1 is +0 or in [2^-24, 0.42] in magnitude and 2 + f in [1.7, 2.42]
+    (the scale flag could only be set by the zero numerator, whose quotient is +0 either way)."""
+    def tail(dst):
+        return f"""v_mul_f32 v22, v21, v21
+v_mul_f32 v23, v22, v22
+v_mul_f32 v24, {_f32(c4)}, v23
+v_add_f32 v24, {_f32(c3)}, v24
+v_mul_f32 v24, v23, v24
+v_mul_f32 v23, {_f32(c6)}, v23
+v_add_f32 v23, {_f32(c5)}, v23
+v_mul_f32 v23, v22, v23
+v_add_f32 v23, v23, v24
+v_mul_f32 v22, 0.5, v18
+v_mul_f32 v22, v22, v18
+v_add_f32 v23, v22, v23
+v_mul_f32 v23, v21, v23
+v_cvt_f32_i32 v24, v19
+v_mul_f32 v21, {_f32(ln2lo)}, v24
+v_add_f32 v23, v23, v21
+v_sub_f32 v23, v22, v23
+v_sub_f32 v23, v23, v18
+v_mul_f32 v24, {_f32(ln2hi)}, v24
+v_sub_f32 v{dst}, v24, v23
+"""
+    mant = """v_and_b32 v18, 0x7fffff, v18
+v_add_u32 v20, 0x4afb20, v18
+v_and_b32 v20, 0x800000, v20
+v_xor_b32 v21, 0x3f800000, v20
+v_or_b32 v18, v18, v21
+v_lshrrev_b32 v20, 23, v20
+v_add_u32 v19, v19, v20
+v_add_f32 v18, -1.0, v18
+v_add_f32 v20, 2.0, v18
+"""
+    fast_div = """v_rcp_f32 v22, v20
+s_nop 0
+v_fma_f32 v24, -v20, v22, 1.0
+v_fmac_f32 v22, v24, v22
+v_mul_f32 v24, v18, v22
+v_fma_f32 v8, -v20, v24, v18
+v_fmac_f32 v24, v8, v22
+v_fma_f32 v8, -v20, v24, v18
+v_fma_f32 v21, v8, v22, v24
+"""
+    return f"""v_cmp_gt_u32 vcc, 0x800000, v17
+v_mul_f32 v18, {_f32(scale)}, v17
+v_mov_b32 v19, 0xffffff81
+v_mov_b32 v20, 0xffffff68
+v_cndmask_b32 v18, v17, v18, vcc
+v_cndmask_b32 v19, v19, v20, vcc
+v_lshrrev_b32 v20, 23, v18
+v_add_u32 v19, v19, v20
+""" + mant + fast_div + tail(23) + """v_mov_b32 v21, 0x1c
+v_cmp_class_f32 vcc, v17, v21
+v_mov_b32 v22, 0x7fc00000
+s_nop 1
+v_cndmask_b32 v23, v23, v22, vcc
+v_mov_b32 v21, 0x60
+v_cmp_class_f32 vcc, v17, v21
+v_mov_b32 v22, 0xff800000
+s_nop 1
+v_cndmask_b32 v23, v23, v22, vcc
+v_mov_b32 v21, 0x203
+v_cmp_class_f32 vcc, v17, v21
+s_nop 1
+v_cndmask_b32 v8, v23, v17, vcc
+""" + _RET
+
+
+def _tanh():
+    """TANH subroutine: mtgp_tanhf(v17) -> v8, straight-line on every lane: the odd polynomial
+    x + x^3 P(x^2) (|x| < 0.625) into v23, then sign(x) (1 - 2 / (exp(2|x|) + 1)) with the EXP
+    body (2|x| > 88.72 -> +inf) and the IEEE division; |x| >= 0.625 selects the second;
+    NaN and +-0 -> x."""
+    v = _spec_consts("mtgp_tanhf", 11)
+    cut, one, two, one2, z1, z2, p0, p1, p2, p3, p4 = v
+    assert _f32(one) == _f32(one2) == _f32(1.0) and _f32(two) == _f32(2.0) and _f32(z1) == _f32(z2) == _f32(0.0), v
+    body, _ = _exp_body(24, 19, 18)
+    return f"""v_mul_f32 v18, v17, v17
+v_mov_b32 v19, {_f32(p1)}
+v_fmac_f32 v19, {_f32(p0)}, v18
+v_fmaak_f32 v19, v19, v18, {_f32(p2)}
+v_fmaak_f32 v19, v19, v18, {_f32(p3)}
+v_fmaak_f32 v19, v19, v18, {_f32(p4)}
+v_mul_f32 v19, v19, v18
+v_fma_f32 v23, v19, v17, v17
+v_add_f32_e64 v24, |v17|, |v17|
+""" + body + """v_add_f32 v19, 1.0, v19
+""" + _div_body(18, "2.0", 19, (18, 20, 21, 22, 24)) + f"""v_sub_f32 v18, 1.0, v18
+v_cmp_gt_f32 vcc, 0, v17
+s_nop 1
+v_cndmask_b32_e64 v18, v18, -v18, vcc
+s_mov_b32 s38, {_f32(cut)}
+v_cmp_ge_f32_e64 vcc, |v17|, s38
+s_nop 1
+v_cndmask_b32 v8, v23, v18, vcc
+v_mov_b32 v18, 0x63
+v_cmp_class_f32 vcc, v17, v18
+s_nop 1
+v_cndmask_b32 v8, v8, v17, vcc
+""" + _RET
+
+
+# SQRT subroutine: the compiler's correctly rounded f32 square root for gfx950 (HIP's default
+# sqrtf = include/mtgp_f32math.h mtgp_sqrtf): scale x < 2^-96 by 2^32, v_sqrt_f32, one-ulp
+# correction from the two fma residuals, rescale by 2^-16; +-0 / +inf (class 0x260) pass through.
+_SQRT = """v_mul_f32 v18, 0x4f800000, v17
+v_cmp_gt_f32 vcc, 0xf800000, v17
+s_nop 1
+v_cndmask_b32 v19, v17, v18, vcc
+v_sqrt_f32 v18, v19
+s_nop 0
+v_add_u32 v20, -1, v18
+v_add_u32 v21, 1, v18
+v_fma_f32 v22, -v20, v18, v19
+v_fma_f32 v23, -v21, v18, v19
+v_cmp_ge_f32_e64 s[34:35], 0, v22
+s_nop 1
+v_cndmask_b32_e64 v18, v18, v20, s[34:35]
+v_cmp_lt_f32_e64 s[34:35], 0, v23
+s_nop 1
+v_cndmask_b32_e64 v18, v18, v21, s[34:35]
+v_mul_f32 v20, 0x37800000, v18
+v_cndmask_b32 v18, v18, v20, vcc
+v_mov_b32 v20, 0x260
+v_cmp_class_f32 vcc, v19, v20
+s_nop 1
+v_cndmask_b32 v8, v18, v19, vcc
+""" + _RET
+
 TEMPLATES = {
     "SIN": _trig(0),
     "COS": _trig(1),
@@ -245,7 +494,13 @@ v_fma_f32 v19, -v19, v22, v21
 v_div_fmas_f32 v19, v19, v20, v22
 v_div_fixup_f32 v8, v19, v18, v17
 """,
+    "EXP": _exp(),
+    "LOG": _log(),
+    "TANH": _tanh(),
+    "SQRT": _SQRT,
+    "ABS": "v_and_b32 v8, 0x7fffffff, v8\n",
 }
+
 
 
 def assemble(text):
@@ -272,10 +527,18 @@ def assemble(text):
     return words, lines
 
 
+# The shared subroutines, laid out in this order at the start of every code buffer, each at a
+# 64-byte boundary (padding: s_nop 0); the rest of TEMPLATES (DIV, ABS) are copied inline.
+SUBROUTINES = ("SIN", "COS", "EXP", "LOG", "TANH", "SQRT")
+_ALIGN = 64
+_PAD = 0xBF800000  # s_nop 0
+
+
 def generate():
     out = ["// GENERATED by scripts/gen_jit_templates.py -- do not edit.",
            "// gfx950 machine-code templates of the program JIT (register ABI: csrc/mtgp_jit.h).",
            "#ifndef MTGP_JIT_BLOBS_H", "#define MTGP_JIT_BLOBS_H", "#include <stdint.h>", ""]
+    area, offs = [], {}
     for name, text in TEMPLATES.items():
         words, lines = assemble(text)
         out.append(f"// {name}:")
@@ -288,6 +551,21 @@ def generate():
         out.append(f"#define MTGP_JIT_{name}_SKIPPABLE_WORDS {skip}")
         out.append(f"static const uint32_t mtgp_jit_{name.lower()}_blob[{len(words)}] = {{{body}}};")
         out.append("")
+        if name in SUBROUTINES:
+            assert 0xBE801D28 in words, name  # a subroutine returns with s_setpc_b64 s[40:41]
+            while len(area) * 4 % _ALIGN:
+                area.append(_PAD)
+            offs[name] = len(area) * 4
+            area += words
+    while len(area) * 4 % _ALIGN:
+        area.append(_PAD)
+    out.append("// The subroutine area at the start of every JIT code buffer (byte offsets of each entry).")
+    for name in SUBROUTINES:
+        out.append(f"#define MTGP_JIT_{name}_OFFSET {offs[name]}u")
+    out.append(f"#define MTGP_JIT_SUB_WORDS {len(area)}")
+    rows = [", ".join(f"0x{w:08x}u" for w in area[i:i + 8]) for i in range(0, len(area), 8)]
+    out.append("static const uint32_t mtgp_jit_sub_blob[MTGP_JIT_SUB_WORDS] = {\n    " + ",\n    ".join(rows) + "};")
+    out.append("")
     out.append("#endif")
     return "\n".join(out) + "\n"
 

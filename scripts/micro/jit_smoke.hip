@@ -96,10 +96,8 @@ int main() {
       {IS(MTGP_OP_VV_DIV, 5 * SB, 4 * SB), IS(MTGP_OP_LDVP, 0, 0), I(MTGP_OP_RSUBS, 0, 0), I(MTGP_OP_END, 0, 0)},  // RSUBS: d4/d5 - d0
       {IS(MTGP_OP_COSV, 0, 2 * SB), I(MTGP_OP_END, 0, 0)},                                   // cos d2 (sweep)
   };
-  // shared sin/cos subroutines first (mtgp_jit.h layout), then the programs
-  std::vector<uint32_t> words(mtgp::kJitTemplateBytes / 4, 0xbf800000u), offs;
-  for (int i = 0; i < MTGP_JIT_SIN_WORDS; ++i) words[mtgp::kJitSinOffset / 4 + i] = mtgp_jit_sin_blob[i];
-  for (int i = 0; i < MTGP_JIT_COS_WORDS; ++i) words[mtgp::kJitCosOffset / 4 + i] = mtgp_jit_cos_blob[i];
+  // shared subroutines first (mtgp_jit.h layout), then the programs
+  std::vector<uint32_t> words(mtgp_jit_sub_blob, mtgp_jit_sub_blob + MTGP_JIT_SUB_WORDS), offs;
   for (auto& p : progs) {
     const uint32_t base = (uint32_t)(words.size() * 4);
     offs.push_back(base);

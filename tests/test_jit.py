@@ -5,8 +5,10 @@
   s_setpc_b64 s[30:31] and writes only the registers the call-site ABI allows
   (v8-v24, s[32:39], vcc; never v0-v7, exec or other SGPRs);
 * a word-level emulator of the emitted subset (v_mov / v_add / v_sub / v_subrev / v_mul, the
-  sin / cos / div templates as black boxes) reproduces the row-order oracle bit for bit on
-  random trees and data, which pins operand order and the compile-time operand stack."""
+  templates and subroutine calls as black boxes) reproduces the row-order oracle bit for bit on
+  random trees and data, which pins operand order and the compile-time operand stack;
+* instruction-level emulators of the templates themselves (sin / cos hot path, exp / log / tanh /
+  sqrt) reproduce the include/mtgp_f32math.h specs bit for bit on edge and random inputs."""
 import os
 import ctypes
 import re
@@ -39,10 +41,18 @@ def _blobs():
 
 BLOBS = _blobs()
 SETPC = 0xBE801D1E
-GETPC_S44 = 0xBEAC1C00  # s_getpc_b64 s[44:45] -- starts a call of a shared sin/cos subroutine
-_up = lambda x: (x + 63) // 64 * 64  # noqa: E731
-COS_OFF = _up(len(BLOBS["SIN"]) * 4)
-TEMPLATE_BYTES = _up(COS_OFF + len(BLOBS["COS"]) * 4)  # host translations start right after them
+GETPC_S44 = 0xBEAC1C00  # s_getpc_b64 s[44:45] -- starts a call of a shared subroutine
+
+
+def _defines():
+    text = open(os.path.join(ROOT, "multitreegp_amd", "csrc", "mtgp_jit_blobs.h")).read()
+    return {k: int(v) for k, v in re.findall(r"#define MTGP_JIT_(\w+) (\d+)u?", text)}
+
+
+DEFS = _defines()
+TEMPLATE_BYTES = DEFS["SUB_WORDS"] * 4  # host translations start right after the subroutine area
+FN = {"SIN": 6, "COS": 7, "EXP": 8, "LOG": 9, "SQRT": 10, "TANH": 11}  # include/mtgp.h MTGP_FN_*
+SUB_AT = {DEFS[name + "_OFFSET"]: name for name in FN}  # byte offset -> subroutine
 
 
 def test_templates_up_to_date():
@@ -126,6 +136,12 @@ def _setup(kind):
         lib = mt.NodeLibrary(SR_OPS, [["x0", "x1", "x2", "x3"]], [4])
         pop = sample_population(6, lib, 30, 1, max_init_depth=7, max_nodes=64)[0]
         return lib, pop, 4, [0]
+    if kind == "ext":  # the round-3 unary operators: subroutine calls / inline abs since round 4
+        ext = [("exp", None, 1, 0.2), ("log", None, 1, 0.2), ("sqrt", None, 1, 0.2), ("tanh", None, 1, 0.2),
+               ("abs", None, 1, 0.2)]
+        lib = mt.NodeLibrary(SR_OPS + ext, [["x0", "x1", "x2", "x3"]], [4])
+        pop = sample_population(16, lib, 40, 1, max_init_depth=7, max_nodes=64)[0]
+        return lib, pop, 4, [0]
     lib = mt.NodeLibrary(CONTROL_OPS + [("/", None, 2, 0.1)], [["y1", "y2", "y3", "y4"]], [1])
     pop = sample_population(7, lib, 60, 1, max_init_depth=6, max_nodes=40)[0]
     return lib, pop, 4, [0]
@@ -188,9 +204,8 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
             assert words[i + 1] == 0x802CFF2C and words[i + 4] == 0xBEA81E2C, [hex(x) for x in words[i:i + 5]]
             rel = int(np.array(words[i + 2], np.uint32).view(np.int32))
             target = TEMPLATE_BYTES + 4 * (i + 1) + rel
-            assert target in (0, COS_OFF), target
-            s_, c_ = orc.sincos(v[17])
-            put(8, s_ if target == 0 else c_)
+            assert target in SUB_AT, target
+            put(8, orc.unary(FN[SUB_AT[target]], v[17]))
             i += 5
             continue
         if (w >> 23) == 0x17D:  # SOP1: the exec save / restore / set of per-wave units
@@ -251,6 +266,10 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
             put(8, s if hit == "SIN" else c)
             i += len(BLOBS[hit])
             continue
+        if hit == "ABS":
+            put(8, orc.unary(12, v[8]))
+            i += len(BLOBS[hit])
+            continue
         src0 = w & 0x1FF
         if src0 == 255:
             a = lit(i + 1)
@@ -272,7 +291,7 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
         i += step
 
 
-@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr"])
+@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr", "ext"])
 def test_translation_disassembles_and_respects_abi(kind):
     lib, pop, n_data, masks = _setup(kind)
     progs = _programs(lib, pop[:12], n_data, masks)
@@ -285,7 +304,7 @@ def test_translation_disassembles_and_respects_abi(kind):
     assert len(words_all) >= 12
 
 
-@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr"])
+@pytest.mark.parametrize("kind", ["dynamic", "static_div", "sr", "ext"])
 def test_emulated_code_matches_row_order_oracle(kind):
     lib, pop, n_data, masks = _setup(kind)
     rng = np.random.default_rng(3)
@@ -695,3 +714,267 @@ def test_lds_store_chain_units_emulate_to_oracle(R):
                     got = vals[lane]
                     assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
                         (np.isnan(got) and np.isnan(want)), (wave, lane, j, got, want)
+
+
+# ---- the exp / log / tanh / sqrt subroutines (round 4), instruction by instruction -------------
+class _Tmpl:
+    """Float32 / uint32 lane emulator of the straight-line subroutine templates (every gfx950
+    instruction they use).  IEEE basic operations are numpy float32 (correctly rounded); fma via
+    float64 (exact product, one rounding); the v_div_scale .. v_div_fixup sequence is the IEEE
+    division (its temporaries are poisoned with NaN, so a template that read one after the
+    sequence would fail); v_sqrt_f32 is the correctly rounded root moved by a random -1 / 0 / +1
+    ulp (the hardware's approximation is within one ulp: the template's correction must undo it)."""
+
+    def __init__(self, x, seed=0):
+        self.n = x.size
+        self.v = {17: x.astype(np.float32).view(np.uint32).copy()}
+        self.s = {}
+        self.rng = np.random.default_rng(seed)
+
+    def f(self, o):
+        return self.u(o, float_ctx=True).view(np.float32)
+
+    def u(self, o, float_ctx=False):
+        o = o.strip()
+        neg = absm = False
+        if o.startswith("-") and o[1:2] in ("v", "|", "s"):
+            neg, o = True, o[1:]
+        if o.startswith("|"):
+            absm, o = True, o.strip("|")
+        if o.startswith("v") and o[1:].isdigit():
+            r = self.v[int(o[1:])].copy()
+        elif o.startswith("s") and o[1:].isdigit():
+            r = np.full(self.n, self.s[int(o[1:])], np.uint32)
+        elif o.startswith("0x"):
+            r = np.full(self.n, int(o, 16), np.uint32)
+        elif "." in o:
+            r = np.full(self.n, np.float32(float(o)).view(np.uint32), np.uint32)
+        else:  # integer inline constant (-16 .. 64): in a float operation the integer's value as a float
+            k = int(o)
+            r = np.full(self.n, (np.float32(k).view(np.uint32) if float_ctx else np.uint32(k & 0xFFFFFFFF)), np.uint32)
+        if absm:
+            r = r & np.uint32(0x7FFFFFFF)
+        if neg:
+            r = r ^ np.uint32(0x80000000)
+        return r
+
+    def mask(self, o):
+        o = o.strip()
+        return self.vcc if o == "vcc" else self.s_mask[o]
+
+    def setf(self, d, val):
+        self.v[int(d[1:])] = np.asarray(val, np.float32).view(np.uint32).copy()
+
+    def setu(self, d, val):
+        self.v[int(d[1:])] = np.asarray(val).astype(np.uint32)
+
+    @staticmethod
+    def _class(x, bits):
+        u = x.view(np.uint32)
+        neg = (u >> 31) == 1
+        e, m = (u >> 23) & 0xFF, u & 0x7FFFFF
+        cls = np.select([(e == 255) & (m != 0) & ((m >> 22) == 0), (e == 255) & (m != 0), (e == 255) & neg,
+                         (e == 0) & (m == 0) & neg, (e == 0) & neg, neg,
+                         (e == 255), (e == 0) & (m == 0), (e == 0)],
+                        [0, 1, 2, 5, 4, 3, 9, 6, 7], 8)
+        return ((bits >> cls.astype(np.uint32)) & 1) == 1
+
+    def run(self, text):
+        """-> (v8, whether the out-of-line slow path ran)"""
+        f32, f64 = np.float32, np.float64
+        self.vcc = np.zeros(self.n, bool)
+        self.s_mask = {}
+        in_div = []
+        lines = [ln.strip() for ln in text.strip().splitlines()]
+        labels = {ln[:-1]: k for k, ln in enumerate(lines) if ln.endswith(":")}
+        pc, slow = 0, False
+        while pc < len(lines):
+            ln = lines[pc]
+            pc += 1
+            if ln.endswith(":"):
+                continue
+            op, _, rest = ln.partition(" ")
+            a = [t.strip() for t in rest.split(",")] if rest else []
+            if op == "s_cbranch_vccnz":
+                if self.vcc.any():
+                    pc, slow = labels[a[0]], True
+                continue
+            if op == "s_and_b64" and a == ["vcc", "exec", "vcc"]:
+                continue  # (exec: all lanes)
+            with np.errstate(all="ignore"):
+                if op in ("v_div_scale_f32",) or (in_div and op != "v_div_fixup_f32"):
+                    in_div.append(a[0])
+                    if op == "v_div_scale_f32" and a[1] == "vcc":
+                        self.vcc = np.zeros(self.n, bool)
+                    continue
+                if op == "v_div_fixup_f32":  # = IEEE n / d, temporaries poisoned
+                    for r in in_div:
+                        self.setf(r, np.full(self.n, np.nan, f32))
+                    in_div = []
+                    self.setf(a[0], self.f(a[3]) / self.f(a[2]))
+                elif op == "v_mul_f32":
+                    self.setf(a[0], self.f(a[1]) * self.f(a[2]))
+                elif op in ("v_add_f32", "v_add_f32_e64"):
+                    self.setf(a[0], self.f(a[1]) + self.f(a[2]))
+                elif op == "v_sub_f32":
+                    self.setf(a[0], self.f(a[1]) - self.f(a[2]))
+                elif op == "v_rndne_f32":
+                    self.setf(a[0], np.rint(self.f(a[1])))
+                elif op in ("v_fma_f32", "v_fmamk_f32", "v_fmaak_f32"):
+                    self.setf(a[0], (self.f(a[1]).astype(f64) * self.f(a[2]).astype(f64) +
+                                     self.f(a[3]).astype(f64)).astype(f32))
+                elif op == "v_fmac_f32":
+                    self.setf(a[0], (self.f(a[1]).astype(f64) * self.f(a[2]).astype(f64) +
+                                     self.f(a[0]).astype(f64)).astype(f32))
+                elif op == "v_mov_b32":
+                    self.setu(a[0], self.u(a[1]))
+                elif op == "v_cvt_i32_f32":  # saturating, NaN -> 0
+                    t = self.f(a[1]).astype(f64)
+                    t = np.where(np.isnan(t), 0, np.clip(np.trunc(t), -2.0 ** 31, 2.0 ** 31 - 1))
+                    self.setu(a[0], t.astype(np.int64).astype(np.int32).view(np.uint32))
+                elif op == "v_cvt_f32_i32":
+                    self.setf(a[0], self.u(a[1]).view(np.int32).astype(f32))
+                elif op == "v_lshrrev_b32":
+                    self.setu(a[0], self.u(a[2]) >> (self.u(a[1]) & 31))
+                elif op == "v_ashrrev_i32":
+                    self.setu(a[0], (self.u(a[2]).view(np.int32) >> (self.u(a[1]) & 31).astype(np.int32)).view(np.uint32))
+                elif op == "v_add_u32":
+                    self.setu(a[0], self.u(a[1]).astype(np.uint64) + self.u(a[2]))
+                elif op == "v_subrev_u32":
+                    self.setu(a[0], self.u(a[2]).astype(np.int64) - self.u(a[1]).astype(np.int64))
+                elif op == "v_rcp_f32":  # within one ulp of 1/x: a random -1 / 0 / +1 ulp move of the rounded value
+                    x = self.f(a[1])
+                    r = (np.float64(1.0) / x.astype(f64)).astype(f32)
+                    step = self.rng.integers(-1, 2, self.n).astype(np.int64)
+                    ok = np.isfinite(r) & (r != 0) & (np.abs(r) < f32(3e38))
+                    self.setu(a[0], np.where(ok, (r.view(np.uint32).astype(np.int64) + step).astype(np.uint32),
+                                             r.view(np.uint32)))
+                elif op == "v_sub_u32":
+                    self.setu(a[0], self.u(a[1]).astype(np.int64) - self.u(a[2]).astype(np.int64))
+                elif op == "v_lshl_add_u32":
+                    self.setu(a[0], ((self.u(a[1]).astype(np.uint64) << (self.u(a[2]).astype(np.uint64) & 31))
+                                     + self.u(a[3])) & 0xFFFFFFFF)
+                elif op == "v_and_b32":
+                    self.setu(a[0], self.u(a[1]) & self.u(a[2]))
+                elif op == "v_or_b32":
+                    self.setu(a[0], self.u(a[1]) | self.u(a[2]))
+                elif op == "v_xor_b32":
+                    self.setu(a[0], self.u(a[1]) ^ self.u(a[2]))
+                elif op.startswith("v_cmp_"):
+                    kind = op[6:].replace("_e64", "").replace("_e32", "")
+                    dst = a[0]
+                    if kind == "class_f32":
+                        m = self._class(self.f(a[1]), self.u(a[2]))
+                    elif kind.endswith("_u32"):
+                        x, y = self.u(a[1]), self.u(a[2])
+                        m = {"gt_u32": x > y, "le_u32": x <= y}[kind]
+                    else:
+                        x, y = self.f(a[1]), self.f(a[2])
+                        m = {"lt_f32": x < y, "gt_f32": x > y, "ge_f32": x >= y, "nge_f32": ~(x >= y),
+                             "u_f32": np.isnan(x) | np.isnan(y)}[kind]
+                    if dst == "vcc":
+                        self.vcc = m
+                    else:
+                        self.s_mask[dst] = m
+                elif op in ("v_cndmask_b32", "v_cndmask_b32_e64"):
+                    m = self.mask(a[3]) if len(a) > 3 else self.vcc
+                    self.setu(a[0], np.where(m, self.u(a[2]), self.u(a[1])))
+                elif op == "v_sqrt_f32":
+                    x = self.f(a[1])
+                    r = np.sqrt(x.astype(f64)).astype(f32)
+                    step = self.rng.integers(-1, 2, self.n).astype(np.int64)
+                    moved = (r.view(np.uint32).astype(np.int64) + step).astype(np.uint32)
+                    ok = np.isfinite(r) & (r > 0) & (r.view(np.uint32) < 0x7F7FFFFF)
+                    self.setu(a[0], np.where(ok, moved, r.view(np.uint32)))
+                elif op == "s_mov_b32":
+                    self.s[int(a[0][1:])] = self.u(a[1])[0]
+                elif op == "s_setpc_b64":
+                    return self.v[8].view(np.float32), slow
+                elif op != "s_nop":
+                    raise AssertionError(ln)
+        raise AssertionError("no s_setpc")
+
+
+def _gen_module():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("gen_jit_templates", os.path.join(ROOT, "scripts",
+                                                                                     "gen_jit_templates.py"))
+    g = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(g)
+    return g
+
+
+def _edge_inputs(rng):
+    f32 = np.float32
+    special = [np.nan, -np.nan, np.inf, -np.inf, 0.0, -0.0, 1e-45, -1e-45, 1e-40, -1e-40, 1.1754942e-38, 1.17549435e-38,
+               2.3509886e-38, 1e-30, 1e-7, 0.5, 0.625, -0.625, 0.62499994, 0.62500006, 1.0, -1.0, 2.0, 44.361416,
+               44.36142, 88.7228394, 88.72284, 88.72283, -103.972084, -103.97209, -87.33655, -88.0, 3.4e38, -3.4e38,
+               1e10, -1e10, 2.0 ** 24, 0.70710677, 1.4142135, 1.4142137]
+    parts = [np.array(special, f32), rng.uniform(-120, 100, 60000).astype(f32),
+             rng.uniform(-3, 3, 60000).astype(f32), (np.exp(rng.uniform(-100, 88, 60000))).astype(f32),
+             np.exp(rng.uniform(-103, 0, 20000)).astype(f32) * rng.choice([-1, 1], 20000).astype(f32),
+             rng.integers(0, 2 ** 32, 60000, dtype=np.uint64).astype(np.uint32).view(f32)]
+    x = np.concatenate(parts)
+    with np.errstate(invalid="ignore"):
+        return np.concatenate([x, np.nextafter(x, np.float32(np.inf)), np.nextafter(x, np.float32(-np.inf))])
+
+
+# the hot range of subroutines with an out-of-line slow path (lanes that never take it); none since
+# the straight-line versions measured faster (the machinery stays for a future branchy template)
+HOT = {}
+
+
+@pytest.mark.parametrize("name", ["EXP", "LOG", "TANH", "SQRT"])
+def test_unary_templates_emulate_to_spec(name):
+    """The exp / log / tanh / sqrt subroutines equal the include/mtgp_f32math.h specs (the oracle)
+    bit for bit on every lane: NaN, infinities, signed zeros, subnormals, the range limits and
+    branch points and their neighbours, random bit patterns."""
+    g = _gen_module()
+    x = _edge_inputs(np.random.default_rng(7))
+    batches = [(x, name in HOT)]
+    if name in HOT:
+        batches.append((x[HOT[name](x)], False))
+    for batch, want_slow in batches:
+        got, slow = _Tmpl(batch, seed=1).run(g.TEMPLATES[name])
+        ref = orc.unary(FN[name], batch)
+        same = got.view(np.uint32) == ref.view(np.uint32)
+        assert same.all(), (name, want_slow, batch[~same][:6], got[~same][:6], ref[~same][:6])
+        assert slow == want_slow, (name, want_slow)
+    if name in HOT:
+        for i in np.nonzero(~HOT[name](x))[0][:50]:  # one outside lane is enough
+            assert _Tmpl(np.array([1.25, x[i]], np.float32)).run(g.TEMPLATES[name])[1], (name, x[i])
+
+
+def test_unary_subroutines_abi_clean():
+    """Straight-line (a branchy template: one s_cbranch_vccnz to its slow path, which has its own
+    return and no branch).  Nothing writes exec; only
+    v8 / v18-v24, s[34:35], s38 and vcc are written (v17, the argument, is read to the end: the
+    special-case selects need it)."""
+    for name in ("EXP", "LOG", "TANH", "SQRT"):
+        w = BLOBS[name]
+        ret = w.index(SETPC_S40)
+        hot, cold = _disassemble(w[:ret + 1]), _disassemble(w[ret + 1:]) if ret + 1 < len(w) else []
+        assert hot[-1] == "s_setpc_b64 s[40:41]", name
+        branches = [ln.split()[0] for ln in hot if ln.startswith(("s_cbranch", "s_branch"))]
+        if name in HOT:
+            assert branches == ["s_cbranch_vccnz"] and cold[-1] == "s_setpc_b64 s[40:41]", name
+        else:
+            assert branches == [] and cold == [], name
+        assert not any(ln.startswith(("s_cbranch", "s_branch")) for ln in cold), name
+        for ln in hot[:-1] + cold[:-1]:
+            op, _, rest = ln.partition(" ")
+            assert "exec" not in ln or ln == "s_and_b64 vcc, exec, vcc", (name, ln)
+            if op.startswith(("s_nop", "s_cbranch")) or ln == "s_and_b64 vcc, exec, vcc":
+                continue
+            dst = rest.split(",")[0].strip()
+            if op.startswith("v_cmp") and op.endswith("_e32"):
+                assert dst == "vcc", ln
+                continue
+            m = re.fullmatch(r"v(\d+)", dst)
+            if m:
+                assert int(m.group(1)) in {8} | set(range(18, 25)), (name, ln)
+                if op.startswith("v_div_scale"):
+                    assert rest.split(",")[1].strip() in ("vcc", "s[34:35]"), ln
+                continue
+            assert dst in ("vcc", "s[34:35]", "s38"), (name, ln)
+    assert _disassemble(BLOBS["ABS"]) == ["v_and_b32_e32 v8, 0x7fffffff, v8"]
