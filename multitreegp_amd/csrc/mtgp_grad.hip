@@ -69,6 +69,27 @@ struct GradArgs {
   float* grad;            // [P, K]
 };
 
+// Lane (individual p, parameter k, rollout r).  Each individual owns K * R lanes rounded up to
+// whole waves, so every wave belongs to ONE individual: its programs and coefficients are
+// wave-uniform (p is read from the first lane), the dual interpreter fetches instructions with
+// scalar loads and branches on them with scalar branches (round 4: with p per lane both were
+// vector operations, 22 us per RK4 stage); the padding lanes (k >= K) return at once.
+__host__ __device__ __forceinline__ long grad_lanes_per(int K, int R) { return ((long)K * R + 63) / 64 * 64; }
+__device__ __forceinline__ bool grad_lane(const GradArgs& A, int& p, int& k, int& r, size_t& slot) {
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int R = A.ro.R;
+  const long LP = grad_lanes_per(A.K, R);
+  const long pl = gid / LP;
+  if (pl >= A.P) return false;
+  const int t = (int)(gid - pl * LP);
+  k = t / R;
+  r = t - k * R;
+  if (k >= A.K) return false;
+  p = __builtin_amdgcn_readfirstlane((int)pl);  // (wave-uniform by construction)
+  slot = ((size_t)p * A.K + k) * R + r;
+  return true;
+}
+
 // Data slot s (byte offset s * MTGP_SLOT_BYTES in the program words): the stage state for
 // s < nv, parameter theta[s - nv] otherwise (tangent 1 for the lane's own parameter).
 template <int NV>
@@ -93,18 +114,36 @@ __device__ __forceinline__ Dual slot_val(uint32_t off, const float* sv, const fl
 
 // One program (mtgp.h format, every opcode incl. the fused forms) in dual numbers; V(off) reads
 // data slot off / MTGP_SLOT_BYTES as a Dual.
-template <class Src>
-__device__ Dual run_dual_src(const MtgpInstr* code, Src V) {
+// The operand stack of a lane: a private array (kernels with registers to spare: the compiler keeps
+// it in VGPRs) or, in the register-heavy kernels, a column of the block's LDS (a private array
+// would live in scratch memory there: a scratch round trip per push / pop, round 4).
+struct PrivStack {
+  Dual s[MTGP_STACK_MAX];
+  __device__ Dual& at(int i) { return s[i]; }
+};
+constexpr int kGradBlock = 256;  // threads per block of the gradient kernels
+struct LdsStack {
+  Dual* col;  // &lds[0][threadIdx.x] of a [MTGP_STACK_MAX][kGradBlock] array
+  __device__ Dual& at(int i) { return col[i * kGradBlock]; }
+};
+
+template <class Src, class Stk = PrivStack>
+__device__ Dual run_dual_src(const MtgpInstr* code, Src V, Stk stk = Stk()) {
   Dual acc = {0.0f, 0.0f};
-  Dual stk[MTGP_STACK_MAX];
   int sp = 0;
+  // the next instruction's (scalar) load is issued before this one is dispatched: one load
+  // latency per program instead of one per instruction (a read one past the END stays inside the
+  // program slot or the flattener's spare block)
+  MtgpInstr nxt = code[0];
   for (int pc = 0;; ++pc) {
-    const uint32_t w = code[pc].op, op = w >> MTGP_OP_SHIFT, ax = w & 0xffffffu;
-    const float imm = code[pc].imm;
+    const MtgpInstr cur = nxt;
+    nxt = code[pc + 1];
+    const uint32_t w = cur.op, op = w >> MTGP_OP_SHIFT, ax = w & 0xffffffu;
+    const float imm = cur.imm;
     const uint32_t ib = __float_as_uint(imm);
     const Dual C = {imm, 0.0f};
-    auto push = [&]() { stk[sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1] = acc; ++sp; };
-    auto pop = [&]() { --sp; return stk[sp < 0 ? 0 : (sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1)]; };
+    auto push = [&]() { stk.at(sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1) = acc; ++sp; };
+    auto pop = [&]() { --sp; return stk.at(sp < 0 ? 0 : (sp < MTGP_STACK_MAX ? sp : MTGP_STACK_MAX - 1)); };
     switch (op) {
       case MTGP_OP_END: return acc;
       case MTGP_OP_LDC: acc = C; break;
@@ -167,21 +206,20 @@ __device__ Dual run_dual_src(const MtgpInstr* code, Src V) {
   }
 }
 
-template <int NV>
-__device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd, int nv, const float* th, int kk) {
-  return run_dual_src(code, [&](uint32_t off) { return slot_val<NV>(off, sv, sd, nv, th, kk); });
+template <int NV, class Stk = PrivStack>
+__device__ Dual run_dual(const MtgpInstr* code, const float* sv, const float* sd, int nv, const float* th, int kk,
+                         Stk stk = Stk()) {
+  return run_dual_src(code, [&](uint32_t off) { return slot_val<NV>(off, sv, sd, nv, th, kk); }, stk);
 }
 
 // One (individual p, parameter k, rollout r) per lane; k_sr's integration in dual numbers.
 template <int NV>
 __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int R = A.ro.R;
-  if (gid >= (long)A.P * A.K * R) return;
-  const int r = (int)(gid % R);
-  const long pk = gid / R;
-  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
-  float* out = A.part + (size_t)gid * 2;
+  int p, k, r;
+  size_t slot;
+  if (!grad_lane(A, p, k, r, slot)) return;
+  float* out = A.part + slot * 2;
   const int np = A.nparam[p];
   if (k > 0 && k >= np) {  // unused parameter slot of this individual
     out[0] = 0.0f;
@@ -271,14 +309,14 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
 // saved points bit for bit.  Lanes run independently (no wave-uniform program calls: the grad
 // launch is small, one lane per (individual, parameter, rollout)).
 template <int NV>
-__global__ void __launch_bounds__(256) k_sr_grad_dp(GradArgs A) {
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+__global__ void __launch_bounds__(kGradBlock) k_sr_grad_dp(GradArgs A) {
+  __shared__ Dual s_stk[MTGP_STACK_MAX][kGradBlock];
+  const LdsStack stk{&s_stk[0][threadIdx.x]};
   const int R = A.ro.R;
-  if (gid >= (long)A.P * A.K * R) return;
-  const int r = (int)(gid % R);
-  const long pk = gid / R;
-  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
-  float* out = A.part + (size_t)gid * 2;
+  int p, k, r;
+  size_t slot;
+  if (!grad_lane(A, p, k, r, slot)) return;
+  float* out = A.part + slot * 2;
   const int np = A.nparam[p];
   if (k > 0 && k >= np) {  // unused parameter slot of this individual
     out[0] = 0.0f;
@@ -310,7 +348,7 @@ __global__ void __launch_bounds__(256) k_sr_grad_dp(GradArgs A) {
   };
   auto rhs = [&](const float* xv, const float* xd, float* ov, float* od) {
     for (int i = 0; i < nv; ++i) {
-      const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk);
+      const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
       ov[i] = o.v;
       od[i] = o.d;
     }
@@ -471,16 +509,16 @@ struct CtlEnv<2> {  // StirredTankReactor
 constexpr int kCtlData = 8;  // data slots of the control models (mtgp_kernels.hip kDMax)
 
 template <int ENV, int NA>
-__global__ void __launch_bounds__(256) k_ctl_grad(GradArgs A) {
+__global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
+  __shared__ Dual s_stk[MTGP_STACK_MAX][kGradBlock];
+  const LdsStack stk{&s_stk[0][threadIdx.x]};
   constexpr int NV = CtlEnv<ENV>::NV, NP = CtlEnv<ENV>::NP, ND = NV + NA;
   constexpr bool DYN = NA > 0;
-  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
   const int R = A.ro.R;
-  if (gid >= (long)A.P * A.K * R) return;
-  const int r = (int)(gid % R);
-  const long pk = gid / R;
-  const int k = (int)(pk % A.K), p = (int)(pk / A.K);
-  float* out = A.part + (size_t)gid * 2;
+  int p, k, r;
+  size_t slot;
+  if (!grad_lane(A, p, k, r, slot)) return;
+  float* out = A.part + slot * 2;
   const int np = A.nparam[p];
   if (k > 0 && k >= np) {
     out[0] = 0.0f;
@@ -569,20 +607,20 @@ __global__ void __launch_bounds__(256) k_ctl_grad(GradArgs A) {
 #pragma unroll
       for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, st[NV + j]);
       for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
-      const Dual u = run_dual_src(p_read, V);  // [0, a, 0, tg]
+      const Dual u = run_dual_src(p_read, V, stk);  // [0, a, 0, tg]
       drift(st, u, ds);
 #pragma unroll
       for (int i = 0; i < NV; ++i)
         if (i < no) put(i, y[i]);
       put(no + NA, u);
 #pragma unroll
-      for (int j = 0; j < (DYN ? NA : 1); ++j) ds[NV + j] = run_dual_src(p_state + (size_t)j * A.L, V);
+      for (int j = 0; j < (DYN ? NA : 1); ++j) ds[NV + j] = run_dual_src(p_state + (size_t)j * A.L, V, stk);
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i)
         if (i < no) put(i, y[i]);
       for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
-      const Dual u = run_dual_src(p_read, V);
+      const Dual u = run_dual_src(p_read, V, stk);
       drift(st, u, ds);
     }
   };
@@ -606,10 +644,10 @@ __global__ void __launch_bounds__(256) k_ctl_grad(GradArgs A) {
 #pragma unroll
       for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, xq[NV + j]);
       for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
-      u = run_dual_src(p_save, V);  // dyn.py:101 [y, a, 0, tg]
+      u = run_dual_src(p_save, V, stk);  // dyn.py:101 [y, a, 0, tg]
     } else {
       for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
-      u = run_dual_src(p_read, V);  // ff.py:97
+      u = run_dual_src(p_read, V, stk);  // ff.py:97
     }
     if constexpr (ENV == 0) {
       const MtgpDual ud = tod(u);
@@ -840,7 +878,7 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
   GradArgs A;
   grad_args(A, model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out);
   hipStream_t s = (hipStream_t)stream;
-  const long lanes = (long)P * K * ro->R;
+  const long lanes = (long)P * grad_lanes_per(K, ro->R);  // whole waves per individual (grad_lane)
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
 #define MTGP_CG(E)                                                                  \
   switch (na) {                                                                     \
@@ -887,7 +925,7 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
   A.loss = loss_out;
   A.grad = grad_out;
   hipStream_t s = (hipStream_t)stream;
-  const long lanes = (long)P * K * ro->R;
+  const long lanes = (long)P * grad_lanes_per(K, ro->R);  // whole waves per individual (grad_lane)
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
   const int nv = model->n_var;
   if (dopri5) {

@@ -164,13 +164,18 @@ MTGP_JIT_HD inline uint32_t jit_wait_lgkm(int n) { return kWaitLgkm0 | (uint32_t
 
 // sp_init: operand-stack depth before prog[0] (the per-instruction sizing of k_flatten_wave
 // translates a pop on its own with one element on the stack).
+// Part 3 (the wave-parallel emitter, k_jit_emit_waves_lds): the body of a piece of a program only
+// -- no preloads, no wait -- with the whole program's preload table given (pre_ext[0..npre_ext)).
 MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs,
                                    int part = 0, int pre_base = kJitPre, int wait_n = 0, int* npre_out = nullptr,
-                                   int sp_init = 0) {
+                                   int sp_init = 0, const int* pre_ext = nullptr, int npre_ext = 0) {
   int sp = sp_init;
   int pre[kJitPreSlots];
   int npre = 0;
-  if (mode == kJitModeLds) {  // preload the first kJitPreSlots distinct data slots the program reads
+  if (mode == kJitModeLds && pre_ext) {
+    npre = npre_ext < kJitPreSlots ? npre_ext : kJitPreSlots;
+    for (int q = 0; q < npre; ++q) pre[q] = pre_ext[q];
+  } else if (mode == kJitModeLds) {  // preload the first kJitPreSlots distinct data slots the program reads
     for (int i = 0; i < L; ++i) {
       const uint32_t w = prog[i].op, code = w >> MTGP_OP_SHIFT;
       if (code == MTGP_OP_END) break;
@@ -199,15 +204,17 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
         if (!have && npre < kJitPreSlots) pre[npre++] = cand[k];
       }
     }
+  }
+  if (mode == kJitModeLds) {
     if (npre_out) *npre_out = npre;
-    if (part != 2) {
+    if (part != 2 && part != 3) {
       for (int q = 0; q < npre; ++q) {
         o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
         o.w((uint32_t)(pre_base + q) << 24 | (uint32_t)kJitLdsAddr);
       }
     }
     if (part == 1) return kJitOk;
-    if (npre > 0) o.w(part == 2 ? jit_wait_lgkm(wait_n) : kWaitLgkm0);
+    if (npre > 0 && part != 3) o.w(part == 2 ? jit_wait_lgkm(wait_n) : kWaitLgkm0);
   }
   // register holding data slot s: v0-v7 (register mode) or its preload / a load at the use
   auto vslot = [&](int s_, int tmp) -> int {

@@ -3228,8 +3228,11 @@ constexpr int kFlatDirectTrees = 8;
 //     counter; only in arbitrary arrays) leaves the program to k_flatten_serial.
 // The tables are per wave in LDS (24 B per row), so the occupancy no longer falls with N (the
 // lane-per-tree kernel needs 16 B x N per LANE).  Output = k_flatten's word for word.
+// (8 waves per SIMD: the kernel is latency-bound -- one wave walks a tree level by level through
+// LDS -- so occupancy is its throughput; 64 VGPRs fit without spills for NMAX <= 128)
 template <int NMAX>
-__global__ void __launch_bounds__(64) k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NMAX <= 128 ? 8 : 4)))
+k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
                                                      MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
                                                      int n_prog, int L, MtgpInstr* prog_out, int32_t* len_out,
                                                      int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
@@ -3964,6 +3967,170 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   }
 }
 
+// LDS-data emit with one WAVE per (unit, group) (the wide-state SR kernel's pipelined units,
+// mtgp_jit.h jit_lds_region): the lanes first find the preload tables of the group's program and
+// of the next group's (the first kJitPreSlots distinct data slots in order of first use: per slot
+// its first operand position by an LDS atomicMin, its rank = the slots first used before it, as
+// flat_jit_size_wave_lds sizes them), write the preloads (a lane per slot), then translate the body
+// instructions l, l + 64, ... in isolation (jit_program part 3 with the table, the stack depth and
+// byte address from prefix sums: table words + 3 per operand loaded at its use).  Lane 0 writes
+// the frame (the v25 keep, the wait for the group's own preloads, the select, the unit end).
+// The same words as k_jit_emit_groups' serial jit_unit_group (tests/test_gpu_build.py).
+constexpr int kEmitLdsWaves = 4;  // waves per block
+template <int KI>
+__global__ void __launch_bounds__(kEmitLdsWaves * kWave) k_jit_emit_waves_lds(JitUnitArgs U, const int32_t* __restrict__ jw,
+                                                                             const uint32_t* __restrict__ offs,
+                                                                             uint32_t* __restrict__ code,
+                                                                             uint64_t code_bytes, JitOpTable optab) {
+  static_assert(MTGP_MAX_DATA <= kWave, "one lane per data slot");
+  __shared__ int s_first[kEmitLdsWaves][MTGP_MAX_DATA];
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SUB_WORDS; k += blockDim.x) code[k] = mtgp_jit_sub_blob[k];
+  }
+  const int lane = threadIdx.x & (kWave - 1), wib = threadIdx.x >> 6;
+  int* fpos = s_first[wib];
+  const long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave;  // (wave-uniform)
+  if (i >= (long)U.n_units * U.G) return;
+  const int u = (int)(i / U.G), g = (int)(i - (long)u * U.G);
+  const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  const int q = wave * U.G + g;
+  if (q >= U.P) return;
+  const uint32_t b = offs[u], e = offs[u + 1];
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable unit or short buffer (checked on use)
+  const bool last = (g == U.G - 1) || (q + 1 >= U.P);
+  MtgpInstr end;
+  end.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+  end.imm = 0.0f;
+  // the preload table of program p: pre_slot(r) = the slot of rank r (r < npre), via the lanes
+  // (lane s: slot s's rank, or -1 when it is not preloaded)
+  auto table = [&](const MtgpInstr* p, int& npre) -> int {
+    fpos[lane] = 0x7fffffff;  // (lane < MTGP_MAX_DATA == kWave)
+    __builtin_amdgcn_wave_barrier();
+    bool ended = false;
+#pragma unroll
+    for (int k = 0; k < KI; ++k) {
+      if (ended) break;  // (wave-uniform)
+      const int ii = k * kWave + lane;
+      const MtgpInstr x = ii < U.L ? p[ii] : end;
+      const uint32_t c = x.op >> MTGP_OP_SHIFT;
+      const uint64_t ends = __ballot(c == (uint32_t)MTGP_OP_END);
+      const int first_end = ends ? __ffsll((unsigned long long)ends) - 1 : kWave;
+      if (lane < first_end) {
+        const uint32_t f = c < 64u ? optab.flags[c] : 0u;
+        uint32_t ib;
+        __builtin_memcpy(&ib, &x.imm, 4);
+        const int sa = (f & kOpIbSlot) ? (int)(ib / MTGP_SLOT_BYTES) : -1;
+        const int sb = (f & kOpAxSlot) ? (int)((x.op & 0xffffffu) / MTGP_SLOT_BYTES) : -1;
+        if (sa >= 0 && sa < MTGP_MAX_DATA) atomicMin(&fpos[sa], 2 * ii);
+        if (sb >= 0 && sb < MTGP_MAX_DATA) atomicMin(&fpos[sb], 2 * ii + 1);
+      }
+      ended = ends != 0ull;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const int mine = fpos[lane];
+    int before = 0;
+#pragma unroll 8
+    for (int t = 0; t < MTGP_MAX_DATA; ++t) before += fpos[t] < mine ? 1 : 0;
+    const bool pre = mine != 0x7fffffff && before < mtgp::kJitPreSlots;
+    npre = __popcll(__ballot(pre));
+    __builtin_amdgcn_wave_barrier();
+    return pre ? before : -1;
+  };
+  const int ind = U.order ? U.order[q] : q;
+  const MtgpInstr* prog = U.prog + ((size_t)ind * U.n_prog + j) * U.L;
+  const MtgpInstr* nprog = nullptr;
+  if (!last) nprog = U.prog + ((size_t)(U.order ? U.order[q + 1] : q + 1) * U.n_prog + j) * U.L;
+  int npre = 0, np1 = 0;
+  const int rank = table(prog, npre);
+  // the body's table in every lane: pre_tab[r] = the slot of rank r
+  int pre_tab[mtgp::kJitPreSlots];
+#pragma unroll
+  for (int r = 0; r < mtgp::kJitPreSlots; ++r) {
+    const uint64_t m = __ballot(rank == r);
+    pre_tab[r] = m ? __ffsll((unsigned long long)m) - 1 : 0;
+  }
+  const int nrank = nprog ? table(nprog, np1) : -1;
+  // group g's region (jit_lds_region): [P_0 (g = 0)] [P_(g+1)] [keep (g = 1)] [wait] [body] [select] [end]
+  uint32_t start = 0;  // words before group g inside the unit
+  for (int h = 0; h < g; ++h) {
+    const int ih = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
+    start += (uint32_t)jw[(size_t)ih * U.n_prog + j] + (uint32_t)mtgp::jit_merge_words(h);
+  }
+  if (g > 0) start += 2u * (uint32_t)npre;  // its preloads sit in group g-1's region
+  const uint32_t at = b + start * 4u;
+  uint32_t* out = code + at / 4;
+  const int set = mtgp::jit_pre_set(g), nset = mtgp::jit_pre_set(g + 1);
+  int w0 = 0;  // words written before the body
+  if (g == 0) {
+    if (rank >= 0) {
+      out[2 * rank] = mtgp::kDsReadB32 | (uint32_t)(lane * (int)MTGP_SLOT_BYTES);
+      out[2 * rank + 1] = (uint32_t)(set + rank) << 24 | (uint32_t)mtgp::kJitLdsAddr;
+    }
+    w0 += 2 * npre;
+  }
+  if (nrank >= 0) {
+    out[w0 + 2 * nrank] = mtgp::kDsReadB32 | (uint32_t)(lane * (int)MTGP_SLOT_BYTES);
+    out[w0 + 2 * nrank + 1] = (uint32_t)(nset + nrank) << 24 | (uint32_t)mtgp::kJitLdsAddr;
+  }
+  w0 += 2 * np1;
+  const int keep = mtgp::jit_merge_keep(g) ? 1 : 0;
+  const int wait = npre > 0 ? 1 : 0;
+  const int body0 = w0 + keep + wait;
+  int woff = 0, sp = 0;  // words and stack depth before this chunk
+  bool ended = false;
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    if (ended) break;  // (wave-uniform)
+    const int ii = k * kWave + lane;
+    const MtgpInstr x = ii < U.L ? prog[ii] : end;
+    const uint32_t c = x.op >> MTGP_OP_SHIFT;
+    const uint64_t ends = __ballot(c == (uint32_t)MTGP_OP_END);
+    const int first_end = ends ? __ffsll((unsigned long long)ends) - 1 : kWave;
+    const bool in = lane < first_end;
+    const uint32_t f = (in && c < 64u) ? optab.flags[c] : 0u;
+    int w = (in && c < 64u) ? optab.words[c] : 0;
+    if (in) {  // + a ds_read / s_waitcnt (3 words) per data operand that is not preloaded
+      uint32_t ib;
+      __builtin_memcpy(&ib, &x.imm, 4);
+      const int sa = (f & kOpIbSlot) ? (int)(ib / MTGP_SLOT_BYTES) : -1;
+      const int sb = (f & kOpAxSlot) ? (int)((x.op & 0xffffffu) / MTGP_SLOT_BYTES) : -1;
+      bool pa = false, pb = false;
+#pragma unroll
+      for (int r = 0; r < mtgp::kJitPreSlots; ++r) {
+        pa = pa || (r < npre && pre_tab[r] == sa);
+        pb = pb || (r < npre && pre_tab[r] == sb);
+      }
+      w += (sa >= 0 && !pa ? 3 : 0) + (sb >= 0 && !pb ? 3 : 0);
+    }
+    const int d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
+    int wi = w, di = d;  // inclusive prefix sums over the chunk
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) {
+      const int vw = __shfl_up(wi, off), vd = __shfl_up(di, off);
+      if (lane >= off) { wi += vw; di += vd; }
+    }
+    if (in) {
+      const MtgpInstr t[2] = {x, end};
+      mtgp::JitOut o{out + body0 + woff + (wi - w), 0};
+      o.base = at + (uint32_t)(body0 + woff + (wi - w)) * 4u;
+      (void)mtgp::jit_program(o, t, 2, false, mtgp::kJitModeLds, 3, set, 0, nullptr, sp + di - d, pre_tab, npre);
+    }
+    woff += __shfl(wi, kWave - 1);
+    sp += __shfl(di, kWave - 1);
+    ended = ends != 0ull;
+  }
+  if (lane == 0) {
+    mtgp::JitOut o{out, 0};
+    o.base = at;
+    o.n = w0;
+    if (keep) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
+    if (wait) o.w(mtgp::jit_wait_lgkm(np1));
+    o.n = body0 + woff;
+    if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp, last);
+    if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);
+  }
+}
+
 // the shared subroutines (sin, cos, exp, log, tanh, sqrt) at the start of the code buffer
 __global__ void __launch_bounds__(256) k_jit_templates(uint32_t* __restrict__ code, uint64_t code_bytes) {
   if (code_bytes < mtgp::kJitTemplateBytes) return;
@@ -4473,7 +4640,7 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
   const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
-  static const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread (one thread per group)
+  const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread / wave (read per call: tests switch it)
   if (U.mode == mtgp::kJitModeRegs && !(ew && strcmp(ew, "thread") == 0) && U.L <= 5 * kWave) {
     static const JitOpTable optab = jit_op_table();
     const long wthreads = threads * kWave;
@@ -4483,6 +4650,20 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
     else
       hipLaunchKernelGGL(k_jit_emit_waves<5>, dim3((unsigned)((wthreads + 255) / 256)), dim3(256), 0, s, U, jit_words,
                          offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  }
+  // LDS-data units: one thread per group (k_jit_emit_groups) by default; MTGP_JIT_EMIT=wave selects the
+  // wave-per-group emitter, which measured 3.5x slower at C5 (1.17 vs 0.33 ms, profiles/r04/v11_*:
+  // 262k short programs, most lanes of a wave idle, two slot-rank tables per wave)
+  if (U.mode == mtgp::kJitModeLds && U.pipe && ew && strcmp(ew, "wave") == 0 && U.L <= 5 * kWave) {
+    static const JitOpTable optab = jit_op_table();
+    const long blocks = (threads + kEmitLdsWaves - 1) / kEmitLdsWaves;
+    if (U.L <= 3 * kWave)
+      hipLaunchKernelGGL(k_jit_emit_waves_lds<3>, dim3((unsigned)blocks), dim3(kEmitLdsWaves * kWave), 0, s, U,
+                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    else
+      hipLaunchKernelGGL(k_jit_emit_waves_lds<5>, dim3((unsigned)blocks), dim3(kEmitLdsWaves * kWave), 0, s, U,
+                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
     return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
   }
   hipLaunchKernelGGL(k_jit_emit_groups, dim3((unsigned)((threads + 63) / 64)), dim3(64), 0, s, U, jit_words, offsets,

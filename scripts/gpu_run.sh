@@ -49,6 +49,7 @@ for step in "$@"; do
     gradtime) run gradtime 300 python scripts/grad_time.py || exit 1 ;;
     prof_grad) run prof_grad 300 rocprofv3 --kernel-trace --stats -d $O/prof_grad -o prof_grad -- python3 scripts/grad_time.py || exit 1
                python3 scripts/kstats_db.py $(find $O/prof_grad -name "*.db" | head -1) $O/prof_grad_kernel_stats.csv; head -8 $O/prof_grad_kernel_stats.csv ;;
+    testbuild) run pytest_build 300 python -u -m pytest tests/test_gpu_build.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench_c3q) run bench_c3q 300 python bench.py --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     bench_c3ext) run bench_c3ext 300 python bench.py --ext-ops --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
@@ -67,6 +68,7 @@ for step in "$@"; do
     dpab_legacy) run dpab_legacy 900 python scripts/dp_budget_ab.py --legacy-pop --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab2) run dpab2 900 python scripts/dp_budget_ab.py --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab_noise2) run dpab_noise2 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,384,512,640,768 --rounds 3 || exit 1 ;;
+    dpab_n500) run dpab_n500 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab_noise) run dpab_noise 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,128,256,512 --rounds 3 || exit 1 ;;
     dptail) run dptail 600 python scripts/dp_tail.py || exit 1 ;;
     dptail_noise) run dptail_noise 600 python scripts/dp_tail.py --obs-noise 0.1 --tail 990 || exit 1 ;;

@@ -148,14 +148,20 @@ def test_word_based_jit_plan_and_emit_match_translation(kind, R):
     assert int((bufs[1] != 0).sum()) > size // 16
 
 
+@pytest.mark.parametrize("emit", ["groups", "wave"])
+@pytest.mark.parametrize("kind", ["sr12", "sr40"])
 @pytest.mark.parametrize("store", [0, 8])
 @pytest.mark.parametrize("R", [8, 64])
-def test_lds_mode_units_match_host_units(R, store):
+def test_lds_mode_units_match_host_units(R, store, kind, emit, monkeypatch):
     """LDS-data mode (wide-state SR): the device-built units equal the host-built ones word for word,
     plain or as LDS store chains (ABI v14: groups of 8 units packed back to back, each group ending
-    on a 64-byte line)."""
+    on a 64-byte line), from the default thread-per-group emitter and from the wave-per-group one
+    (MTGP_JIT_EMIT=wave, round 4); sr40's programs read more than kJitPreSlots distinct slots (loads
+    at the use) and run 264 rows."""
     import torch
-    lib, pop, specs = _population("sr12", 129, seed=R)
+    if emit == "wave":
+        monkeypatch.setenv("MTGP_JIT_EMIT", "wave")
+    lib, pop, specs = _population(kind, 129, seed=R)
     P, T, N, _ = pop.shape
     n_prog = len(specs)
     L = (2 * N + 8 + 3) // 4 * 4
