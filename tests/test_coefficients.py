@@ -318,6 +318,37 @@ def test_oracle_dopri5_gradient_matches_central_differences():
     assert rel.size >= 20 and np.median(rel) < 5e-3 and np.mean(rel < 3e-2) >= 0.85, np.sort(rel)
 
 
+def test_oracle_dopri5_gradient_unfiltered_central_difference_error():
+    """the same comparison WITHOUT the forward / backward agreement filter, over every
+    finite, unclipped candidate and coefficient, so the size of the dropped controller (dt) term is
+    measured rather than filtered away.  The numbers are reported (-s) and bounded loosely: the
+    float32 central difference itself is noisy where the accept / reject sequence changes inside
+    +-e, so the bound is on the bulk, not on every coefficient."""
+    lib, ff, data, d, pop = _setup_dp(P=24, seed=3)
+    m, ro = oracle_model(ff, d), oracle_rollouts(d)
+    loss, grad, rows = orc.sr_grad(m, pop, lib, ro)
+    rel = []
+    for p in range(pop.shape[0]):
+        if not (0 < loss[p] < 1e4):
+            continue
+        for k, (t, i) in enumerate(rows[p][:4]):
+            c = pop[p: p + 1].copy()
+            e = np.float32(1e-3 * max(1.0, abs(float(c[0, t, i, 3]))))
+            base = c[0, t, i, 3]
+            c[0, t, i, 3] = base + e
+            up = orc.evaluate(m, c, lib, ro)["fitness"][0]
+            c[0, t, i, 3] = base - e
+            dn = orc.evaluate(m, c, lib, ro)["fitness"][0]
+            if not (0 < up < 1e4 and 0 < dn < 1e4 and np.isfinite(grad[p, k])):
+                continue  # the perturbed solve diverged or hit the fitness clip: no derivative to compare
+            fd = (up - dn) / (2 * e)
+            rel.append(abs(grad[p, k] - fd) / (abs(fd) + 1e-3 * (1 + abs(loss[p]))))
+    rel = np.sort(np.array(rel))
+    q = {f"p{int(x * 100)}": float(np.quantile(rel, x)) for x in (0.5, 0.75, 0.9, 1.0)}
+    print("unfiltered Dopri5 gradient vs central difference, relative error over", rel.size, "coefficients:", q)
+    assert rel.size >= 30 and q["p50"] < 1e-2 and q["p75"] < 0.1, q
+
+
 def test_oracle_dopri5_gradient_of_a_known_fit():
     """dx0 = x1, dx1 = c*x0 on the Van der Pol data with Dopri5: sign and size of the gradient in
     c against a central difference of the oracle's loss."""
@@ -337,9 +368,9 @@ def test_oracle_dopri5_gradient_of_a_known_fit():
 
 # ------------------------------------------------------------------------------ GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("n_var,R", [(2, 8), (3, 5), (6, 4)])
+@pytest.mark.parametrize("n_var,R", [(2, 8), (3, 5), (6, 4), (20, 3)])
 def test_gpu_sr_grad_dopri5_bitexact(n_var, R):
-    """mtgp_sr_grad with Dopri5 + PID (k_sr_grad_dp, 2 / 4 / 16-slot templates) vs the oracle:
+    """mtgp_sr_grad with Dopri5 + PID (k_sr_grad_dp, 2 / 4 / 16 / 64-slot templates) vs the oracle:
     loss and every coefficient's gradient bit for bit, loss = the evaluator's fitness."""
     import torch
     from multitreegp_amd.engine import DeviceEngine
