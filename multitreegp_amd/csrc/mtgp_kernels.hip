@@ -4480,7 +4480,11 @@ int mtgp_tu_launch_sr(MTGP_TU_SR_ARGS) {
         else hipLaunchKernelGGL((k_sr_wide_dopri5<false, false>), wgrid, wblock, lds_dp, s, A);
       }, s);
     }
-    const size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+    size_t lds = (size_t)(2 * model->n_var + nw * kSMax + nw) * kWave * sizeof(float);
+    if (const char* e = getenv("MTGP_WIDE_LDS_MIN")) {  // diagnostic: fewer workgroups per CU (code working set)
+      const long v = atol(e);
+      if (v > 0 && (size_t)v > lds && v <= 160 * 1024) lds = (size_t)v;
+    }
     return launch_timed([&] {
       if (jit) {
         if (traj) hipLaunchKernelGGL((k_sr_wide<true, true>), wgrid, wblock, lds, s, A);

@@ -49,6 +49,9 @@ for step in "$@"; do
     gradtime) run gradtime 300 python scripts/grad_time.py || exit 1 ;;
     prof_grad) run prof_grad 300 rocprofv3 --kernel-trace --stats -d $O/prof_grad -o prof_grad -- python3 scripts/grad_time.py || exit 1
                python3 scripts/kstats_db.py $(find $O/prof_grad -name "*.db" | head -1) $O/prof_grad_kernel_stats.csv; head -8 $O/prof_grad_kernel_stats.csv ;;
+    c5occ) run c5occ_2 300 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1
+           run c5occ_1 300 env MTGP_WIDE_LDS_MIN=90000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1
+           run c5occ_2b 300 env MTGP_WIDE_LDS_MIN=60000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     testbuild) run pytest_build 300 python -u -m pytest tests/test_gpu_build.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench_c3q) run bench_c3q 300 python bench.py --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
