@@ -45,6 +45,12 @@ constexpr int kJitMaxData = 8;
 enum { kJitModeRegs = 0, kJitModeLds = 1 };
 constexpr int kJitLdsAddr = 0, kJitPre = 26, kJitPreSlots = 16, kJitLoadTmp = 42;
 constexpr uint32_t kDsReadB32 = 0xd86c0000u;   // ds_read_b32 (word 0; | offset)
+// ds_read2st64_b32 (word 0; | offset1 << 8 | offset0, in units of 64 dwords = one data slot):
+// two preloads into an even-aligned register pair with one instruction (round 4: the preloads were
+// a quarter of the wide-state SR code, whose working set outgrew the L2)
+constexpr uint32_t kDsRead2St64B32 = 0xd8700000u;
+// preload instructions (= words / 2) of n preloaded slots: pairs, the odd one alone
+MTGP_JIT_HD inline int jit_preload_instrs(int n) { return (n + 1) / 2; }
 constexpr uint32_t kWaitLgkm0 = 0xbf8cc07fu;   // s_waitcnt lgkmcnt(0)
 constexpr uint32_t kJitSrcLiteral = 255u;
 // VOP2 opcodes (gfx9 encoding)
@@ -208,13 +214,15 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
   if (mode == kJitModeLds) {
     if (npre_out) *npre_out = npre;
     if (part != 2 && part != 3) {
-      for (int q = 0; q < npre; ++q) {
-        o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
+      for (int q = 0; q < npre; q += 2) {  // rank pairs (q, q + 1) into v[pre_base + q : + 1]
+        if (q + 1 < npre) o.w(kDsRead2St64B32 | (uint32_t)pre[q + 1] << 8 | (uint32_t)pre[q]);
+        else o.w(kDsReadB32 | (uint32_t)(pre[q] * (int)MTGP_SLOT_BYTES));
         o.w((uint32_t)(pre_base + q) << 24 | (uint32_t)kJitLdsAddr);
       }
     }
     if (part == 1) return kJitOk;
-    if (npre > 0 && part != 3) o.w(part == 2 ? jit_wait_lgkm(wait_n) : kWaitLgkm0);
+    // part 2: wait_n = the slots the NEXT program preloads after these (its instructions may stay in flight)
+    if (npre > 0 && part != 3) o.w(part == 2 ? jit_wait_lgkm(jit_preload_instrs(wait_n)) : kWaitLgkm0);
   }
   // register holding data slot s: v0-v7 (register mode) or its preload / a load at the use
   auto vslot = [&](int s_, int tmp) -> int {
@@ -473,7 +481,7 @@ MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j, uint32_t store = 0
 // program hides behind the previous one's arithmetic.  Layout: [P_0] then per group g
 // [P_(g+1)] [v_mov v25, v8 (g > 0)] [wait for P_g + body_g] [select (g > 0)]; per group the same
 // words as the plain layout (preload, wait, body), only reordered, so group g (> 0) starts
-// 2 * npre(g) words after its plain position.  Register set of group g's preloads:
+// jit_preload_words(prog_g) words after its plain position.  Register set of group g's preloads:
 MTGP_JIT_HD inline int jit_pre_set(int g) { return (g & 1) ? kJitPreB : kJitPre; }
 
 // words of the preloads of one LDS-mode program (< 0: untranslatable)
@@ -538,7 +546,7 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
   const int ind = order ? order[q] : q;
   const MtgpInstr* cur = prog + ((size_t)ind * n_prog + j) * L;
   int rc;
-  if (mode == kJitModeLds && pipe) {  // (the caller placed this region 2 * npre(g) words after the plain start)
+  if (mode == kJitModeLds && pipe) {  // (the caller placed this region jit_preload_words(g) words after the plain start)
     const MtgpInstr* nxt = nullptr;
     if (!last) nxt = prog + ((size_t)(order ? order[q + 1] : q + 1) * n_prog + j) * L;
     rc = jit_lds_region(o, cur, nxt, L, g);

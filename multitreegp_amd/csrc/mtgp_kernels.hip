@@ -2964,7 +2964,7 @@ __device__ __forceinline__ void flat_jit_size_wave_lds(const MtgpInstr* prog, in
     failed = true;
     rc = mtgp::kJitErrSlot;
   }
-  words += npre > 0 ? 2 * npre + 1 : 0;
+  words += npre > 0 ? 2 * mtgp::jit_preload_instrs(npre) + 1 : 0;  // paired preloads + the wait
   if (lane == 0) {
     if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
     if (jit_cost_out) {  // = flat_jit_size
@@ -4050,29 +4050,36 @@ __global__ void __launch_bounds__(kEmitLdsWaves * kWave) k_jit_emit_waves_lds(Ji
     pre_tab[r] = m ? __ffsll((unsigned long long)m) - 1 : 0;
   }
   const int nrank = nprog ? table(nprog, np1) : -1;
+  int nxt_tab[mtgp::kJitPreSlots];  // the next program's table (its preload pairs)
+#pragma unroll
+  for (int r = 0; r < mtgp::kJitPreSlots; ++r) {
+    const uint64_t m = __ballot(nrank == r);
+    nxt_tab[r] = m ? __ffsll((unsigned long long)m) - 1 : 0;
+  }
+  // preload instruction of rank r (even): a pair with rank r + 1, or the odd last one alone
+  auto preload = [&](uint32_t* at, int r, int n, const int* tab, int base_reg) {
+    if (r & 1) return;
+    at[r] = r + 1 < n ? (mtgp::kDsRead2St64B32 | (uint32_t)tab[r + 1] << 8 | (uint32_t)tab[r])
+                      : (mtgp::kDsReadB32 | (uint32_t)(tab[r] * (int)MTGP_SLOT_BYTES));
+    at[r + 1] = (uint32_t)(base_reg + r) << 24 | (uint32_t)mtgp::kJitLdsAddr;
+  };
   // group g's region (jit_lds_region): [P_0 (g = 0)] [P_(g+1)] [keep (g = 1)] [wait] [body] [select] [end]
   uint32_t start = 0;  // words before group g inside the unit
   for (int h = 0; h < g; ++h) {
     const int ih = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
     start += (uint32_t)jw[(size_t)ih * U.n_prog + j] + (uint32_t)mtgp::jit_merge_words(h);
   }
-  if (g > 0) start += 2u * (uint32_t)npre;  // its preloads sit in group g-1's region
+  if (g > 0) start += 2u * (uint32_t)mtgp::jit_preload_instrs(npre);  // its preloads sit in group g-1's region
   const uint32_t at = b + start * 4u;
   uint32_t* out = code + at / 4;
   const int set = mtgp::jit_pre_set(g), nset = mtgp::jit_pre_set(g + 1);
   int w0 = 0;  // words written before the body
   if (g == 0) {
-    if (rank >= 0) {
-      out[2 * rank] = mtgp::kDsReadB32 | (uint32_t)(lane * (int)MTGP_SLOT_BYTES);
-      out[2 * rank + 1] = (uint32_t)(set + rank) << 24 | (uint32_t)mtgp::kJitLdsAddr;
-    }
-    w0 += 2 * npre;
+    if (lane < npre) preload(out, lane, npre, pre_tab, set);
+    w0 += 2 * mtgp::jit_preload_instrs(npre);
   }
-  if (nrank >= 0) {
-    out[w0 + 2 * nrank] = mtgp::kDsReadB32 | (uint32_t)(lane * (int)MTGP_SLOT_BYTES);
-    out[w0 + 2 * nrank + 1] = (uint32_t)(nset + nrank) << 24 | (uint32_t)mtgp::kJitLdsAddr;
-  }
-  w0 += 2 * np1;
+  if (lane < np1) preload(out + w0, lane, np1, nxt_tab, nset);
+  w0 += 2 * mtgp::jit_preload_instrs(np1);
   const int keep = mtgp::jit_merge_keep(g) ? 1 : 0;
   const int wait = npre > 0 ? 1 : 0;
   const int body0 = w0 + keep + wait;
@@ -4124,7 +4131,7 @@ __global__ void __launch_bounds__(kEmitLdsWaves * kWave) k_jit_emit_waves_lds(Ji
     o.base = at;
     o.n = w0;
     if (keep) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
-    if (wait) o.w(mtgp::jit_wait_lgkm(np1));
+    if (wait) o.w(mtgp::jit_wait_lgkm(mtgp::jit_preload_instrs(np1)));
     o.n = body0 + woff;
     if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp, last);
     if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);

@@ -188,6 +188,12 @@ def _emulate(words, data, full=False, lds=False, regs=None, s46=0, lds_out=None)
                 return v if full else v[8]
             i += 3
             continue
+        if (w & 0xFFFF0000) == 0xD8700000:  # ds_read2st64_b32 v[d:d+1], v0 offset0:s0 offset1:s1 (slots)
+            assert lds and (words[i + 1] & 0xFF) == 0 and (words[i + 1] >> 24) % 2 == 0, hex(words[i + 1])
+            put(words[i + 1] >> 24, data[w & 0xFF])
+            put((words[i + 1] >> 24) + 1, data[(w >> 8) & 0xFF])
+            i += 2
+            continue
         if (w & 0xFFFF0000) == 0xD86C0000:  # ds_read_b32 vdst, v0 offset:slot*256
             assert lds and (words[i + 1] & 0xFF) == 0, hex(words[i + 1])
             put(words[i + 1] >> 24, data[(w & 0xFFFF) // 256])
@@ -520,7 +526,8 @@ def _lds_setup():
 
 def test_lds_mode_translation_disassembles_and_emulates_to_oracle():
     """LDS-data mode (the wide-state SR kernel): every program preloads its first 16 distinct data
-    slots with ds_read_b32 from v0 + slot * 256 (one s_waitcnt), loads the rest at their use, and
+    slots from v0 + slot * 256 (pairs with ds_read2st64_b32, an odd last one with ds_read_b32; one
+    s_waitcnt), loads the rest at their use, and
     computes the row-order oracle's value bit for bit; registers stay within v8-v43 / the ABI."""
     import ctypes
     lib, pop, n_data = _lds_setup()
@@ -544,6 +551,10 @@ def test_lds_mode_translation_disassembles_and_emulates_to_oracle():
                     dst = int(re.match(r"ds_read_b32 v(\d+), v0", ln).group(1))
                     assert dst in allowed, ln
                     beyond += dst >= 42
+                    continue
+                if ln.startswith("ds_read2st64_b32"):  # a preload pair (round 4): even-aligned, v26..v41
+                    lo, hi = (int(x) for x in re.match(r"ds_read2st64_b32 v\[(\d+):(\d+)\], v0", ln).groups())
+                    assert lo % 2 == 0 and hi == lo + 1 and 26 <= lo and hi <= 41, ln
                     continue
                 if ln.startswith("s_waitcnt"):
                     continue
