@@ -3860,7 +3860,9 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restric
 
 // Emit with one thread per (unit, group): group g's code starts after groups 0..g-1 (sizes from
 // jit_words), so the G programs of a unit are translated in parallel.
-__global__ void __launch_bounds__(64) k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
+// (4 waves per SIMD: a C5 build is 4,096 waves, one round at 4 per SIMD instead of two at 3)
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4)))
+k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
                                                         uint64_t code_bytes) {
   if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
