@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 17
+#define MTGP_ABI_VERSION 18
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -63,8 +63,8 @@ enum {
   MTGP_FN_COS = 7,  /* "cos"                                                       */
   /* round 3: further unary operators a reference operator_list may name (gp.py:143-162
    * accepts any lambda; these follow jnp.exp / log / sqrt / tanh / abs in f32, specs in
-   * mtgp_f32math.h).  The program JIT does not translate them: a population that uses one is
-   * evaluated by the interpreter (bit-identical, slower). */
+   * mtgp_f32math.h).  Since round 4 the program JIT translates them too (shared machine-code
+   * subroutines for exp / log / tanh / sqrt, abs inline), bit-identical to the interpreter. */
   MTGP_FN_EXP = 8,  /* "exp"  mtgp_expf                                            */
   MTGP_FN_LOG = 9,  /* "log"  mtgp_logf  (x < 0: NaN, 0: -inf)                     */
   MTGP_FN_SQRT = 10, /* "sqrt" IEEE sqrt (correctly rounded; x < 0: NaN)           */
@@ -140,8 +140,8 @@ typedef struct {
   int32_t n_obs;      /* Acrobot: 4                                              */
   int32_t n_control;  /* Acrobot: 1                                              */
   int32_t n_targets;  /* Acrobot: 0                                              */
-  int32_t n_steps;    /* fixed RK4 steps from ts[0] to ts[-1]                    */
-  int32_t save_every; /* steps between save points; n_save = n_steps/save_every+1 */
+  int32_t n_steps;    /* informational (ABI v18): steps of the fixed-step grid    */
+  int32_t save_every; /* ignored since ABI v18 (kept for the struct layout)       */
   int32_t n_save;     /* len(ts)                                                 */
   float h;            /* dt0                                                      */
   float max_fitness;  /* 1e4 control (dyn.py:27, ff.py:27), 1e5 SR (sr.py:22)    */
@@ -155,16 +155,20 @@ typedef struct {
                              /* 0 threefry original (JAX <= 0.4.x default),        */
                              /* 1 threefry partitionable (JAX >= 0.5 default)      */
   int32_t env;               /* control models: MTGP_ENV_* (0 = Acrobot)            */
-  /* Solver.  MTGP_SOLVER_RK4: fixed step h, n_steps / save_every as above (BASELINE).
-   * MTGP_SOLVER_EULER (ABI v10): diffrax.Euler + ConstantStepSize, the reference evaluators'
-   * default (dyn.py:11, ff.py:11, sr.py:21): y1 = y0 + f(t0, y0) * h, same step grid as RK4.
+  /* Solver.  MTGP_SOLVER_RK4 (BASELINE) and MTGP_SOLVER_EULER (ABI v10; diffrax.Euler, the
+   * reference evaluators' default, dyn.py:11, ff.py:11, sr.py:21) run diffrax.ConstantStepSize
+   * from dt0 = h over [ts[0], ts[-1]] (ABI v18, include/mtgp_cstep.h): f32 step ends accumulated
+   * t += dt0 with diffrax's end clip, each step over dt = tn - t, SaveAt(ts) for ANY non-decreasing
+   * ts through the solver's dense output (RK4: cubic Hermite, Euler: linear), at most max_steps
+   * steps (0: no limit) -- the unsaved points are then +inf (throw=False).
    * MTGP_SOLVER_DOPRI5: diffrax.Dopri5 + PIDController(rtol, atol, dtmin, dtmax) from dt0 = h
    * with SaveAt(ts) and at most max_steps step attempts (include/mtgp_dopri5.h, the notebooks'
    * setting, e.g. SymbolicRegression.ipynb:136); n_steps / save_every are ignored.  Implemented
    * for the dynamic and static control models (every MTGP_ENV_*) and for MTGP_MODEL_SR at every
    * n_var (register-resident for n_var <= 4, the wide-state workgroup kernel up to 64). */
   int32_t solver;
-  int32_t max_steps; /* Dopri5: accepted + rejected steps before the solve gives up      */
+  int32_t max_steps; /* steps before the solve gives up (Dopri5: accepted + rejected; 0 = no limit
+                        for the fixed-step solvers)                                        */
   float rtol, atol;  /* PIDController tolerances                                         */
   float dtmin;       /* <= 0: None; else force_dtmin: steps at dtmin are always accepted */
   float dtmax;       /* <= 0: None                                                       */
@@ -197,7 +201,7 @@ typedef struct {
                         /* bit-identical and stay indexed by individual.        */
   /* Observation noise (control models, control_environment_base.py:43-48):      */
   /*   y = C@x + normal(fold_in(obs_keys[r], bitcast(t)), (n_obs,)) @ obs_w       */
-  /* at every RK4 stage time t = ts[0] + n*h + c_i*h and at every save time ts[k]. */
+  /* at every stage time t + c_i*dt of the solve and at every save time ts[k].     */
   const uint32_t* obs_keys; /* [R, 2] obs_noise_keys (dyn.py:65) or NULL = noise-free */
   const float* obs_w;       /* [n_obs, n_obs] W (acrobot.py:49: obs_noise * I;          */
                             /*  reactor.py:43: obs_noise * I * [15, 15, 0.1])          */

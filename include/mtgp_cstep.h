@@ -1,0 +1,97 @@
+/*
+ * mtgp_cstep.h -- fp32 arithmetic spec of the fixed-step solve: diffrax.ConstantStepSize with the
+ * Euler or classical RK4 solver, SaveAt(ts) through the solver's dense output (ABI v18).
+ *
+ * The reference evaluators integrate with
+ *     diffeqsolve(ODETerm(_drift), solver, ts[0], ts[-1], dt0, y0, saveat=SaveAt(ts),
+ *                 stepsize_controller=ConstantStepSize(), max_steps, event=Event(cond_fn), throw=False)
+ *     (dynamic_evaluate.py:11, 88-96; feedforward_evaluate.py:11, 86-93; SR_evaluator.py:21, 70-79)
+ * diffrax is a third-party dependency absent from this image and unpinned by the reference (no lock
+ * file; diffrax.Event implies >= 0.6).  This header restates its published algorithm; like
+ * mtgp_dopri5.h it is the shared arithmetic spec that the GPU kernels and the CPU oracle
+ * (oracle/mtgp_oracle.c) both follow, the stepping loop itself being written on each side.
+ *
+ * Time grid (wave-uniform: ts is shared by every rollout, dyn.py:63 in_axes None):
+ *   t_0 = ts[0];  tn_0 = min(t_0 + dt0, t1)          ConstantStepSize.init + diffeqsolve's minimum
+ *   step n integrates [t_n, tn_n] with dt_n = tn_n - t_n (ODETerm.contr)
+ *   t_{n+1} = tn_n;  tn_{n+1} = t_{n+1} + dt0, and t1 when > t1 - 1e-6   adapt_step_size + _clip_to_end
+ *   the loop runs while t_n < t1 and fewer than max_steps steps were taken (max_steps reached:
+ *   the unsaved points stay +inf, throw=False).  The step ends are ACCUMULATED in f32, so they
+ *   drift off n * dt0 (C3: 189 of 200 step ends differ) and the step count can exceed the
+ *   nominal one (t1 = 2, dt0 = 0.01: 201 steps, the last 1.5e-6 long).
+ * Stages (ODETerm: is_vf_expensive False, so diffrax keeps the vector-field values f_i and forms each
+ * increment as (sum_j a_ij f_j) * dt; zero tableau entries skipped, products and sums rounded
+ * separately, ascending j):
+ *   Euler   f0 = f(t, y);  y1 = y + f0 * dt
+ *   RK4     f0 = f(t, y)
+ *           f1 = f(t + 0.5 dt, y + (0.5 f0) dt)
+ *           f2 = f(t + 0.5 dt, y + (0.5 f1) dt)
+ *           f3 = f(t + 1.0 dt, y + (1.0 f2) dt)
+ *           y1 = y + (((b0 f0 + b1 f1) + b2 f2) + b3 f3) dt,  b = f32(1/6, 1/3, 1/3, 1/6)
+ * SaveAt(ts): after each step every pending ts[k] <= tn (k ascending, ts[0] included at step 0) is
+ *   evaluated through the step's dense output at theta = linear_rescale(t, ts[k], tn):
+ *   Euler   LocalLinearInterpolation: y + theta (y1 - y)
+ *   RK4     ThirdOrderHermitePolynomialInterpolation.from_k (k0 = f0 dt, k1 = f3 dt, the first and
+ *           last stage increments): a = ((k0 + k1) + 2 y) - 2 y1, b = (((-2 k0) - k1) - 3 y) + 3 y1,
+ *           value = jnp.polyval([a, b, k0, y], theta) (Horner from 0: v = v * theta + c)
+ *   so a save on a step end is the interpolant at theta = 1, not the step's y1 bit for bit.
+ * Event: after a step whose y1 turns the condition negative the solve ends; that step's saves are
+ *   written first, the later ones are +inf.
+ */
+#ifndef MTGP_CSTEP_H
+#define MTGP_CSTEP_H
+#include "mtgp_f32math.h"
+
+#define MTGP_CS_END_TOL 1e-6f /* diffrax _clip_to_end, float32 */
+#define MTGP_RK4_B0 ((float)(1.0 / 6.0))
+#define MTGP_RK4_B1 ((float)(1.0 / 3.0))
+
+/* end of the first step: jnp.minimum(t0 + dt0, t1) */
+MTGP_INLINE MTGP_HD float mtgp_cs_first_end(float t0, float dt0, float t1) {
+  const float tn = t0 + dt0;
+  return tn < t1 ? tn : t1;
+}
+
+/* end of the step after one that ended at t (a kept step: _clip_to_end's keep_step branch) */
+MTGP_INLINE MTGP_HD float mtgp_cs_next_end(float t, float dt0, float t1) {
+  const float tn = t + dt0;
+  return tn > t1 - MTGP_CS_END_TOL ? t1 : tn;
+}
+
+/* diffrax misc.linear_rescale: (t - t0) / (t1 - t0), 0 when t0 == t1 */
+MTGP_INLINE MTGP_HD float mtgp_cs_rescale(float t0, float t, float t1) {
+  return t0 == t1 ? 0.0f : (t - t0) / (t1 - t0);
+}
+
+/* ThirdOrderHermitePolynomialInterpolation of one component (see the header comment).  Every
+ * product and sum rounds as written (an fma for "s + 2 y" would differ where 2 y overflows), except
+ * jnp.polyval's first step 0 * th + a: th = linear_rescale(...) is finite and >= +0 on every call
+ * (ts[k] >= t, tn > t), so 0 * th = +0 and +0 + a = a + 0.0f exactly (-0 -> +0, NaN stays NaN). */
+MTGP_INLINE MTGP_HD float mtgp_cs_hermite(float y0, float y1, float k0, float k1, float th) {
+  const float a = ((k0 + k1) + 2.0f * y0) - 2.0f * y1;
+  const float b = (((-2.0f * k0) - k1) - 3.0f * y0) + 3.0f * y1;
+  float v = a + 0.0f;
+  v = v * th + b;
+  v = v * th + k0;
+  return v * th + y0;
+}
+
+/* LocalLinearInterpolation of one component */
+MTGP_INLINE MTGP_HD float mtgp_cs_linear(float y0, float y1, float th) { return y0 + th * (y1 - y0); }
+
+/* RK4 stage input y + (a f) dt for stage st = 1, 2, 3 (a = 0.5, 0.5, 1.0) */
+MTGP_INLINE MTGP_HD float mtgp_rk4_in(int st, float y, float f, float dt) {
+  return st == 3 ? y + f * dt : y + (0.5f * f) * dt;
+}
+/* RK4 stage time t + c dt for stage st = 1, 2, 3 (c = 0.5, 0.5, 1.0) */
+MTGP_INLINE MTGP_HD float mtgp_rk4_time(int st, float t, float dt) {
+  return st == 3 ? t + 1.0f * dt : t + 0.5f * dt;
+}
+/* running b-weighted sum: stage 0 starts it, stages 1..3 add (ascending j) */
+MTGP_INLINE MTGP_HD float mtgp_rk4_acc(int st, float acc, float f) {
+  return st == 0 ? MTGP_RK4_B0 * f : acc + (st == 3 ? MTGP_RK4_B0 : MTGP_RK4_B1) * f;
+}
+/* the step's end state from the full sum */
+MTGP_INLINE MTGP_HD float mtgp_rk4_out(float y, float acc, float dt) { return y + acc * dt; }
+
+#endif /* MTGP_CSTEP_H */

@@ -8,7 +8,7 @@
 // variable rows reading data slots n_var .. n_var + K - 1, flattens that population with the
 // ordinary flattener, and every lane of k_sr_grad integrates one (individual, parameter k,
 // rollout) triple with dual numbers (value, d/dtheta_k).  The value half performs exactly the
-// operations of k_sr (same RK4 fma form, same MSE order), so the loss equals the evaluator's
+// operations of k_sr (the fixed-step spec include/mtgp_cstep.h, same MSE order), so the loss equals the evaluator's
 // fitness bit for bit; the tangent half is the chain rule of those same operations.
 // k_grad_reduce then forms the per-individual loss and gradient with the evaluator's NaN/inf ->
 // max_fitness replacement, the pairwise rollout sum of finish_group and jnp.clip's derivative.
@@ -19,6 +19,7 @@
 #include "mtgp_prng.h"
 #include "mtgp_dual.h"
 #include "mtgp_dopri5.h"
+#include "mtgp_cstep.h"
 
 namespace {
 
@@ -230,51 +231,36 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
   const int nv = A.m.n_var;
   const float* th = A.theta + (size_t)p * A.K;
   const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const int S = A.m.n_save;
+  const float* ts = A.ro.ts;
   const bool euler = A.m.solver == MTGP_SOLVER_EULER;
   const int n_stages = euler ? 1 : 4;
-  float x[NV], dx[NV], kx[NV], dkx[NV], ax[NV], dax[NV], sv[NV], sd[NV];
+  float x[NV], dx[NV], kx[NV], dkx[NV], fx0[NV], dfx0[NV], ax[NV], dax[NV], sv[NV], sd[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     x[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
-    dx[i] = kx[i] = dkx[i] = ax[i] = dax[i] = 0.0f;
+    dx[i] = kx[i] = dkx[i] = fx0[i] = dfx0[i] = ax[i] = dax[i] = 0.0f;
   }
-  auto bad = [&]() {
+  auto bad = [&](const float* v) {
     bool b = false;
 #pragma unroll
-    for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(x[i]));
+    for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(v[i]));
     return b;
   };
-  bool pending = false, prev_ok = !bad();
+  bool prev_ok = !bad(x);
   float tot = 0.0f, dtot = 0.0f;
-  for (int step = 0;; ++step) {
-    if ((step % save_every) == 0) {  // MSE term of this save point (SR_evaluator.py:24)
-      const int ks = step / save_every;
-      float sq = 0.0f, dsq = 0.0f;
-#pragma unroll
-      for (int d = 0; d < NV; ++d) {
-        if (d >= nv) continue;
-        const float e = x[d] - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
-        const float de = dx[d] * (2.0f * e);  // jnp.square's JVP: g * (2 x)
-        sq = (d == 0) ? e * e : sq + e * e;
-        dsq = (d == 0) ? de : dsq + de;
-      }
-      tot = tot + sq;
-      dtot = dtot + dsq;
-    }
-    if (pending) {  // the event fired: every later save point is +inf -> non-finite fitness
-      tot = mtgp_isfinite(tot) ? kInf : tot;
-      break;
-    }
-    if (step == n_steps) break;
+  // the fixed-step grid of include/mtgp_cstep.h (uniform: ts is shared), saves by the dense output
+  const float t_end = ts[S - 1], dt0 = A.m.h;
+  float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
+  int steps = 0, ks = 0;
+  while (t < t_end && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
+    const float dt = tn - t;
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
-      const float hh = stage == 3 ? h : h2;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        sv[i] = stage == 0 ? x[i] : MTGP_FMAF(hh, kx[i], x[i]);
-        sd[i] = stage == 0 ? dx[i] : MTGP_FMAF(hh, dkx[i], dx[i]);
+        sv[i] = stage == 0 ? x[i] : mtgp_rk4_in(stage, x[i], kx[i], dt);
+        sd[i] = stage == 0 ? dx[i] : mtgp_rk4_in(stage, dx[i], dkx[i], dt);
       }
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -285,19 +271,51 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
       }
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        ax[i] = stage == 0 ? kx[i] : (stage == 3 ? ax[i] + kx[i] : MTGP_FMAF(2.0f, kx[i], ax[i]));
-        dax[i] = stage == 0 ? dkx[i] : (stage == 3 ? dax[i] + dkx[i] : MTGP_FMAF(2.0f, dkx[i], dax[i]));
+        if (stage == 0) {
+          fx0[i] = kx[i];
+          dfx0[i] = dkx[i];
+        }
+        ax[i] = mtgp_rk4_acc(stage, ax[i], kx[i]);
+        dax[i] = mtgp_rk4_acc(stage, dax[i], dkx[i]);
       }
+    }
+    float x1[NV], dx1[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+      dx1[i] = euler ? dx[i] + dfx0[i] * dt : mtgp_rk4_out(dx[i], dax[i], dt);
+    }
+    while (ks < S && ts[ks] <= tn) {  // MSE term of each save point (SR_evaluator.py:24) by the dense output
+      const float tq = mtgp_cs_rescale(t, ts[ks], tn);
+      float sq = 0.0f, dsq = 0.0f;
+#pragma unroll
+      for (int d = 0; d < NV; ++d) {
+        if (d >= nv) continue;
+        const float xv = euler ? mtgp_cs_linear(x[d], x1[d], tq) : mtgp_cs_hermite(x[d], x1[d], fx0[d] * dt, kx[d] * dt, tq);
+        const float xd = euler ? mtgp_cs_linear(dx[d], dx1[d], tq)
+                               : mtgp_cs_hermite(dx[d], dx1[d], dfx0[d] * dt, dkx[d] * dt, tq);
+        const float e = xv - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
+        const float de = xd * (2.0f * e);  // jnp.square's JVP: g * (2 x)
+        sq = (d == 0) ? e * e : sq + e * e;
+        dsq = (d == 0) ? de : dsq + de;
+      }
+      tot = tot + sq;
+      dtot = dtot + dsq;
+      ++ks;
     }
 #pragma unroll
     for (int i = 0; i < NV; ++i) {
-      x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
-      dx[i] = euler ? dx[i] + dax[i] * h : MTGP_FMAF(h6, dax[i], dx[i]);
+      x[i] = x1[i];
+      dx[i] = dx1[i];
     }
-    const bool ok = !bad();
-    if (prev_ok && !ok) pending = true;
+    ++steps;
+    t = tn;
+    tn = mtgp_cs_next_end(t, dt0, t_end);
+    const bool ok = !bad(x);
+    if (prev_ok && !ok) break;  // the NaN event (sr.py:93-94)
     prev_ok = ok;
   }
+  if (ks < S) tot = mtgp_isfinite(tot) ? kInf : tot;  // later save points are +inf
   out[0] = tot / (float)S;
   out[1] = dtot / (float)S;
 }
@@ -693,12 +711,12 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   Dual s[ND], kx[ND], acc[ND], tmp[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) s[i] = {i < NV ? A.ro.x0[(size_t)r * NV + i] : 0.0f, 0.0f};
-  save_point(0, s);
-  bool prev_ok = !bad(s), done = false;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ts[0];
+  bool prev_ok = !bad(s);
+  const float h = A.m.h;
   const bool euler = A.m.solver == MTGP_SOLVER_EULER;
   int q_saved = 0;
   if (A.m.solver == MTGP_SOLVER_DOPRI5) {
+    save_point(0, s);
     // k_ctl_dopri5's solve in duals (oracle ctl_dopri5_dual): the step sizes, accept / reject
     // decisions and the event held at their primal values; save points by the dense output
     constexpr float TA[7][6] = MTGP_DP_TABLE_A;
@@ -772,43 +790,56 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
       tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
     q_saved = ks - 1;
-    done = true;
-  }
-  for (int step = 1; step <= A.m.n_steps && !done; ++step) {
-    const float t = t0 + (float)(step - 1) * h;
-    rhs(t, s, kx);
-    if (euler) {
+  } else {
+    // the fixed-step solve (include/mtgp_cstep.h, k_ctl_dynamic / k_ctl_static) in duals: the time
+    // grid and the event primal, the stage sums, step update and dense output applied to both halves
+    const float t_end = ts[S - 1];
+    float t = ts[0], tn = mtgp_cs_first_end(t, h, t_end);
+    int steps = 0, ks = 0;
+    Dual f0[ND], y1[ND], sk[ND];
+    while (t < t_end && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
+      const float dt = tn - t;
+      rhs(t, s, f0);
+      if (euler) {
 #pragma unroll
-      for (int i = 0; i < ND; ++i) s[i] = {s[i].v + kx[i].v * h, s[i].d + kx[i].d * h};
-    } else {
+        for (int i = 0; i < ND; ++i) y1[i] = {s[i].v + f0[i].v * dt, s[i].d + f0[i].d * dt};
+      } else {
 #pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        acc[i] = kx[i];
-        tmp[i] = {MTGP_FMAF(h2, kx[i].v, s[i].v), MTGP_FMAF(h2, kx[i].d, s[i].d)};
+        for (int i = 0; i < ND; ++i) {
+          acc[i] = {mtgp_rk4_acc(0, 0.0f, f0[i].v), mtgp_rk4_acc(0, 0.0f, f0[i].d)};
+          kx[i] = f0[i];
+        }
+        for (int st = 1; st <= 3; ++st) {
+#pragma unroll
+          for (int i = 0; i < ND; ++i)
+            tmp[i] = {mtgp_rk4_in(st, s[i].v, kx[i].v, dt), mtgp_rk4_in(st, s[i].d, kx[i].d, dt)};
+          rhs(mtgp_rk4_time(st, t, dt), tmp, kx);
+#pragma unroll
+          for (int i = 0; i < ND; ++i) acc[i] = {mtgp_rk4_acc(st, acc[i].v, kx[i].v), mtgp_rk4_acc(st, acc[i].d, kx[i].d)};
+        }
+#pragma unroll
+        for (int i = 0; i < ND; ++i) y1[i] = {mtgp_rk4_out(s[i].v, acc[i].v, dt), mtgp_rk4_out(s[i].d, acc[i].d, dt)};
       }
-      rhs(t + h2, tmp, kx);
+      while (ks < S && ts[ks] <= tn) {  // SaveAt(ts) by the dense output
+        const float th = mtgp_cs_rescale(t, ts[ks], tn);
 #pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        acc[i] = {MTGP_FMAF(2.0f, kx[i].v, acc[i].v), MTGP_FMAF(2.0f, kx[i].d, acc[i].d)};
-        tmp[i] = {MTGP_FMAF(h2, kx[i].v, s[i].v), MTGP_FMAF(h2, kx[i].d, s[i].d)};
+        for (int i = 0; i < ND; ++i)
+          sk[i] = euler ? Dual{mtgp_cs_linear(s[i].v, y1[i].v, th), mtgp_cs_linear(s[i].d, y1[i].d, th)}
+                        : Dual{mtgp_cs_hermite(s[i].v, y1[i].v, f0[i].v * dt, kx[i].v * dt, th),
+                               mtgp_cs_hermite(s[i].d, y1[i].d, f0[i].d * dt, kx[i].d * dt, th)};
+        save_point(ks, sk);
+        ++ks;
       }
-      rhs(t + h2, tmp, kx);
 #pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        acc[i] = {MTGP_FMAF(2.0f, kx[i].v, acc[i].v), MTGP_FMAF(2.0f, kx[i].d, acc[i].d)};
-        tmp[i] = {MTGP_FMAF(h, kx[i].v, s[i].v), MTGP_FMAF(h, kx[i].d, s[i].d)};
-      }
-      rhs(t + h, tmp, kx);
-#pragma unroll
-      for (int i = 0; i < ND; ++i) {
-        acc[i] = {acc[i].v + kx[i].v, acc[i].d + kx[i].d};
-        s[i] = {MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d)};
-      }
+      for (int i = 0; i < ND; ++i) s[i] = y1[i];
+      ++steps;
+      t = tn;
+      tn = mtgp_cs_next_end(t, h, t_end);
+      const bool ok = !bad(s);
+      if (prev_ok && !ok) break;  // Event(cond_fn_nan), dyn.py:94
+      prev_ok = ok;
     }
-    if (step % A.m.save_every == 0) save_point(++q_saved, s);
-    const bool ok = !bad(s);
-    if (prev_ok && !ok) done = true;
-    prev_ok = ok;
+    q_saved = ks - 1;
   }
   // the +inf fill after the event (constants): Acrobot masks it (zero additions), the quadratic
   // costs become non-finite
@@ -865,7 +896,7 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
   if (model->env < 0 || model->env > 2 || model->n_var != nv || model->n_obs < 1 || model->n_obs > nv ||
       model->n_control != 1 || model->n_targets < 0 || model->n_targets > 8 || !ro->params || !ro->x0 || !ro->ts ||
       (model->n_targets > 0 && !ro->targets) || (ro->obs_keys && !ro->obs_w) || ro->R < 1 || ro->R > 64 ||
-      model->save_every < 1 || model->n_save < 2 || model->n_steps < 0 || model->prog_readout < 0 ||
+      model->n_save < 2 || !(model->h > 0.0f) || model->prog_readout < 0 ||
       model->prog_readout >= n_prog || ro->fit_kof)  // (the general Acrobot mask is not differentiated)
     return MTGP_ERR_ARG;
   const int na = dyn ? model->state_size : 0;
@@ -905,7 +936,8 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
     return MTGP_ERR_ARG;
   if (model->model != MTGP_MODEL_SR || model->n_var < 1 || model->n_var > MTGP_MAX_DATA ||
       model->n_var + K > MTGP_MAX_DATA || ro->R < 1 || ro->R > 64 || !ro->x0 || !ro->ys_true ||
-      model->save_every < 1 || model->n_save < 1 || model->prog_state < 0 || model->prog_state + model->n_var > n_prog)
+      model->n_save < 2 || !(model->h > 0.0f) || !ro->ts || model->prog_state < 0 ||
+      model->prog_state + model->n_var > n_prog)
     return MTGP_ERR_ARG;
   const bool dopri5 = model->solver == MTGP_SOLVER_DOPRI5;
   if (model->solver != MTGP_SOLVER_RK4 && model->solver != MTGP_SOLVER_EULER && !dopri5) return MTGP_ERR_ARG;

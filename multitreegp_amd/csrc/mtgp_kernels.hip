@@ -30,6 +30,7 @@
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_dopri5.h"
+#include "mtgp_cstep.h"
 #include "mtgp_flatten.h"
 #include "mtgp_flatten_uniform.h"
 #include "mtgp_jit.h"
@@ -418,7 +419,7 @@ struct KArgs {
   const int32_t* jit_info;  // mtgp_jit_plan info {status, total bytes} (device) or NULL
   uint64_t jit_cap;         // bytes of the code buffer
   int32_t chain_state;      // the JIT code chains the state role (MtgpJitChain): one call per stage
-  int32_t chain_save;       // ... and continues it into the save-point readout on request (s46)
+  int32_t chain_save;       // ... and continues it into the save-point readout on request (s46; unused since ABI v18)
   int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
   // Dopri5 in two launches (ABI v16, MtgpModel.dp_budget): launch 1 runs every wave for at most
   // dp_budget attempts and parks the lanes of waves that are not done (dp_state, word-major
@@ -793,42 +794,85 @@ __device__ __forceinline__ int group_ind(const KArgs& A, const Lane& L, int gi) 
   return uni(sched_ind(A, L.q0 + gi));
 }
 
-// RK4 stage input: stage 0 -> s, stages 1,2 -> s + h/2 k, stage 3 -> s + h k
-__device__ __forceinline__ float stage_in(int stage, float s, float k, float h, float h2) {
-  return stage == 0 ? s : MTGP_FMAF(stage == 3 ? h : h2, k, s);
+// The fixed-step solve (include/mtgp_cstep.h): diffrax.ConstantStepSize's accumulated step grid,
+// wave-uniform because ts is shared by every rollout (dyn.py:63).  t, tn, dt are computed by every
+// lane from the same uniform inputs; the loop and save tests go through readfirstlane so that the
+// branches stay scalar.
+struct CsClock {
+  float t, tn, t_end, dt0;
+  int steps, max_steps;
+  __device__ __forceinline__ void init(const KArgs& A) {
+    t = A.ro.ts[0];
+    t_end = A.ro.ts[A.m.n_save - 1];
+    dt0 = A.m.h;
+    tn = mtgp_cs_first_end(t, dt0, t_end);
+    steps = 0;
+    max_steps = A.m.max_steps;
+  }
+  __device__ __forceinline__ bool live() const {
+    return uni((int)(t < t_end && (max_steps <= 0 || steps < max_steps))) != 0;
+  }
+  __device__ __forceinline__ float dt() const { return tn - t; }
+  __device__ __forceinline__ void advance() {
+    ++steps;
+    t = tn;
+    tn = mtgp_cs_next_end(t, dt0, t_end);
+  }
+  // save point k is taken in this step (ts[k] <= tn; k < S checked by the caller)
+  __device__ __forceinline__ bool saves(const float* ts, int k) const { return uni((int)(ts[k] <= tn)) != 0; }
+};
+
+// RK4 stage input (stage 0: s itself; stages 1..3: s + (a f) dt, a = 0.5, 0.5, 1) and the running
+// b-weighted sum of the stage derivatives (mtgp_cstep.h)
+__device__ __forceinline__ float stage_in(int stage, float s, float f, float dt) {
+  return stage == 0 ? s : mtgp_rk4_in(stage, s, f, dt);
 }
-// RK4 accumulator: k1 + 2 k2 + 2 k3 + k4 (fma form shared with the oracle)
-__device__ __forceinline__ float stage_acc(int stage, float acc, float k) {
-  return stage == 0 ? k : (stage == 3 ? acc + k : MTGP_FMAF(2.0f, k, acc));
+__device__ __forceinline__ float stage_acc(int stage, float acc, float f) { return mtgp_rk4_acc(stage, acc, f); }
+__device__ __forceinline__ float stage_time(int stage, float t, float dt) {
+  return stage == 0 ? t : mtgp_rk4_time(stage, t, dt);
 }
 
 // The same for a whole state vector, branching on the (wave-uniform) stage once instead of
 // selecting per component: the same operations, so the same bits.
 template <int N>
-__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&k)[N], float h, float h2,
+__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], float dt,
                                            float (&out)[N]) {
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = s[i];
-  } else {
-    const float c = st == 3 ? h : h2;
+  } else if (st == 3) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = MTGP_FMAF(c, k[i], s[i]);
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(3, s[i], f[i], dt);
+  } else {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(1, s[i], f[i], dt);
   }
 }
 template <int N>
-__device__ __forceinline__ void stage_acc_n(int stage, float (&acc)[N], const float (&k)[N]) {
+__device__ __forceinline__ void stage_acc_n(int stage, float (&acc)[N], const float (&f)[N]) {
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = k[i];
+    for (int i = 0; i < N; ++i) acc[i] = mtgp_rk4_acc(0, 0.0f, f[i]);
   } else if (st == 3) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = acc[i] + k[i];
+    for (int i = 0; i < N; ++i) acc[i] = mtgp_rk4_acc(3, acc[i], f[i]);
   } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i) acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]);
+    for (int i = 0; i < N; ++i) acc[i] = mtgp_rk4_acc(1, acc[i], f[i]);
+  }
+}
+// the state at save time th of the step [y, y1] (RK4: the Hermite cubic from the increments f0 dt,
+// f3 dt; Euler: linear), +inf once the solve has ended (dead)
+template <int N>
+__device__ __forceinline__ void cs_dense(bool euler, bool dead, const float (&y)[N], const float (&y1)[N],
+                                         const float (&f0)[N], const float (&f3)[N], float dt, float th,
+                                         float (&out)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const float v = euler ? mtgp_cs_linear(y[i], y1[i], th) : mtgp_cs_hermite(y[i], y1[i], f0[i] * dt, f3[i] * dt, th);
+    out[i] = dead ? kInf : v;
   }
 }
 
@@ -1096,14 +1140,14 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 // constants and branches resolved at compile time), and the kernel runs the general loop below only
 // when the code is not usable.  The arithmetic is k_ctl_dynamic's, operation for operation.
 template <int N>
-__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&k)[N], float c, float (&out)[N]) {
+__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], float dt, float (&out)[N]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : MTGP_FMAF(c, k[i], s[i]);
+  for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : mtgp_rk4_in(st, s[i], f[i], dt);
 }
 template <int N>
-__device__ __forceinline__ void rk_acc(int st, float (&acc)[N], const float (&k)[N]) {
+__device__ __forceinline__ void rk_acc(int st, float (&acc)[N], const float (&f)[N]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) acc[i] = st == 0 ? k[i] : (st == 3 ? acc[i] + k[i] : MTGP_FMAF(2.0f, k[i], acc[i]));
+  for (int i = 0; i < N; ++i) acc[i] = mtgp_rk4_acc(st, acc[i], f[i]);
 }
 
 // one JIT unit call, no fallback (the templates never request one)
@@ -1116,19 +1160,23 @@ __device__ __forceinline__ ChainOut jit_call_chain_nf(uint64_t addr_, const floa
   return jit_call_chain(addr_, d, fl, cont);
 }
 
+// The fixed-step dynamic policy with usable JIT code (see above), diffrax ConstantStepSize semantics
+// (include/mtgp_cstep.h): per step the NST stages at t + c_i dt, then the step's end state, the
+// event test, and every save point ts[k] <= tn of the step through the dense output -- observation
+// at ts[k] (dyn.py:99), the save-point readout on [y, a, 0, tar] (dyn.py:101), fitness, rows.
 template <class Env, int NA, bool TRAJ, bool NOISE, int NST>
 __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) {
   constexpr int NV = Env::NV;
-  const int r = Ln.r, rr = Ln.rr, ng = groups_live(A, Ln);
+  const int r = Ln.r, rr = Ln.rr;
   const bool active = Ln.active;
   const int R = A.ro.R;
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
-  const float t0 = A.ro.ts[0];
+  const int S = A.m.n_save;
+  const float* __restrict__ ts = A.ro.ts;
   ObsNoise<NV> nzc;
   float nzv[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) nzv[i] = 0.0f;
+  uint32_t nzt = 0xffffffffu;  // bits of the time nzv was drawn at (a NaN pattern: none yet)
   if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
   constexpr int uslot = NV + NA;
   Env env;
@@ -1141,24 +1189,7 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
 #pragma unroll
   for (int t = 0; t < kDMax - NV - 2; ++t)
     if (t < A.m.n_targets && uslot + 1 + t < kDMax) dv[uslot + 1 + t] = A.ro.targets[rr * A.m.n_targets + t];
-
-  // groups whose save-time readout differs from the drift readout (it reads y): bit per group
-  uint64_t diff_mask = 0;
-  for (int gi = 0; gi < ng; ++gi) {
-    const size_t pj = (size_t)group_ind(A, Ln, gi) * A.n_prog;
-    bool same = A.m.readout_save_same > 0;
-    if (A.m.readout_save_same < 0) {
-      const int la = uni(A.plen[pj + A.m.prog_readout]), lb = uni(A.plen[pj + A.m.prog_readout_save]);
-      same = la == lb;
-      const MtgpInstr* pa = A.prog + (pj + A.m.prog_readout) * A.L;
-      const MtgpInstr* pb = A.prog + (pj + A.m.prog_readout_save) * A.L;
-      for (int i = 0; same && i < la; ++i)
-        same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
-    }
-    if (!same) diff_mask |= 1ull << gi;
-  }
-  const bool save_readout = __builtin_amdgcn_readfirstlane((int)(diff_mask != 0)) != 0;
-  const bool chain_state = A.chain_state != 0, chain_save = A.chain_save != 0;
+  const bool chain_state = A.chain_state != 0;
   // code addresses of this wave's units (wave-uniform)
   const uint64_t u_readout = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout);
   const uint64_t u_state = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state);
@@ -1167,16 +1198,16 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   for (int j = 0; j < NA; ++j) u_state_j[j] = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + j);
   const uint64_t u_save = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout_save);
 
-  float x[NV], a[NA], kx[NV], ka[NA], ax[NV], aa[NA];
+  float x[NV], a[NA], kx[NV], ka[NA], fx0[NV], fa0[NA], ax[NV], aa[NA];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = 0.0f;
+  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = fa0[j] = 0.0f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = 0.0f;
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = fx0[i] = 0.0f;
 
   typename Env::Fit fit = Env::fit_init(active);
-  bool dead = !active, pending = false, prev_ok;
+  bool dead = !active, prev_ok;
   {
     float s0[NV + NA];
 #pragma unroll
@@ -1185,110 +1216,138 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
     for (int j = 0; j < NA; ++j) s0[NV + j] = a[j];
     prev_ok = !Env::bad(s0, NV + NA);
   }
-
-  int save_k = 0, save_ctr = 0;
-  for (int step = 0;; ++step) {
-    const bool last = step == n_steps;
-    const bool is_save = save_ctr == 0;
-    const int ksave = save_k;
-    if (++save_ctr == save_every) {
-      save_ctr = 0;
-      ++save_k;
+  // one save point: state (xs, as) at ts[k]; fill = a point of the +inf fill after the solve ended
+  auto save_point = [&](int k, const float (&xs)[NV], const float (&as)[NA], bool fill) __attribute__((always_inline)) {
+    float yo[NV];
+    if (NOISE) {
+      const uint32_t tb = __float_as_uint(ts[k]);
+      if (tb != nzt) {  // (the noise of ts[k] is drawn unless the last stage was at that very time)
+        obs_noise_vec<NV>(nzc, ts[k], nzv);
+        nzt = tb;
+      }
     }
-    const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-    bool stop = false;
+    ctl_obs_apply<Env>(xs, nzv, yo);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dv[i] = yo[i];
+#pragma unroll
+    for (int j = 0; j < NA; ++j) dv[NV + j] = as[j];
+    const float us = jit_call_nf(u_save, dv);  // readout([y, a, 0, tar]), dyn.py:101 (u folded to 0)
+    if (!fill && !MTGP_AB_NOFIT) env.fit_update(fit, k, S, ts, us, xs);
+    if (TRAJ && active && !MTGP_AB_NOSTORE) {
+      if (A.out.xs) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, xs[i], PR);
+      }
+      if (A.out.ys) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, yo[i], PR);
+      }
+      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
+      if (A.out.acts) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR, loff, as[j], PR);
+      }
+    }
+  };
+
+  CsClock clk;
+  clk.init(A);
+  int k = 0;  // next save point
+  while (clk.live()) {
+    const float t = clk.t, dt = clk.dt();
     // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
-    auto stage = [&](auto st_c) -> bool {
+    auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], at[NA], y[NV];
-      rk_in<NV>(ST, x, kx, ST == 3 ? h : h2, xt);
-      rk_in<NA>(ST, a, ka, ST == 3 ? h : h2, at);
+      rk_in<NV>(ST, x, kx, dt, xt);
+      rk_in<NA>(ST, a, ka, dt, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
       const float u = jit_call_nf(u_readout, dv);
       env.drift(xt, u, kx);
-      if (NOISE && ST != 2) obs_noise_vec<NV>(nzc, ST == 0 ? tk : tk + (ST == 3 ? h : h2), nzv);
+      if (NOISE && ST != 2) {  // stages 1 and 2 share the time t + dt/2, hence the noise draw
+        const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
+        obs_noise_vec<NV>(nzc, tc, nzv);
+        nzt = __float_as_uint(tc);
+      }
       ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
       for (int i = 0; i < NV; ++i) dv[i] = y[i];
       dv[uslot] = u;
-      bool redraw = false;
-      if (NOISE && ST == 0 && is_save) redraw = __float_as_uint(A.ro.ts[ksave]) != __float_as_uint(tk);
-      const bool save_chain = ST == 0 && chain_save && is_save && save_readout && !redraw;
-      float us_chain = u;
       if (chain_state) {
-        const ChainOut c = jit_call_chain_nf(u_state, dv, save_chain ? 1 : 0);
+        const ChainOut c = jit_call_chain_nf(u_state, dv, 0);
 #pragma unroll
         for (int j = 0; j < NA; ++j) ka[j] = c.v[j < mtgp::kJitChainMax ? j : 0];
-        if (save_chain) us_chain = c.tail;
       } else {
 #pragma unroll
         for (int j = 0; j < NA; ++j) ka[j] = jit_call_nf(u_state_j[j], dv);
       }
       if (ST == 0) {
-        if (is_save) {
-          const int k = ksave;
-          float us = u;
-          if (NOISE && redraw) {
-            ctl_obs<Env, true>(nzc, A.ro.ts[k], x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
 #pragma unroll
-            for (int i = 0; i < NV; ++i) dv[i] = y[i];
-          }
-          if (save_chain) us = us_chain;
-          else if (save_readout) us = jit_call_nf(u_save, dv);  // the unit covers every group
-          if (!dead) env.fit_update(fit, k, S, A.ro.ts, us, x);
-          if (TRAJ && active) {
-            if (A.out.xs) {
+        for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
-            }
-            if (A.out.ys) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
-            }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
-            if (A.out.acts) {
-#pragma unroll
-              for (int j = 0; j < NA; ++j) store_row(A.out.acts, ((size_t)k * NA + j) * PR, loff, a[j], PR);
-            }
-          }
-        }
-        if (pending) {  // the event state has been saved: freeze at +inf (saveat fill)
-          pending = false;
-          dead = true;
-          if (!last) Env::fit_kill(fit);
-#pragma unroll
-          for (int i = 0; i < NV; ++i) x[i] = kInf;
-#pragma unroll
-          for (int j = 0; j < NA; ++j) a[j] = kInf;
-        }
-        if (last || (!TRAJ && wave_all(fit.settled || dead))) return true;
+        for (int j = 0; j < NA; ++j) fa0[j] = ka[j];
       }
-      rk_acc<NV>(NST == 1 ? 0 : ST, ax, kx);
-      rk_acc<NA>(NST == 1 ? 0 : ST, aa, ka);
-      return false;
+      if (NST == 4) {
+        rk_acc<NV>(ST, ax, kx);
+        rk_acc<NA>(ST, aa, ka);
+      }
     };
-    if constexpr (NST == 1) {
-      stop = stage(std::integral_constant<int, 0>{});
-    } else {
-      stop = stage(std::integral_constant<int, 0>{});
-      if (!stop) {
-        stage(std::integral_constant<int, 1>{});
-        stage(std::integral_constant<int, 2>{});
-        stage(std::integral_constant<int, 3>{});
-      }
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (NST == 4) {
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
     }
-    if (stop) break;
+    // the step's end state and the event (Event(cond_fn_nan) after the step, dyn.py:94)
+    float x1[NV], a1[NA];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) a1[j] = NST == 1 ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
+    bool ev = false;
     if (!dead) {
       float sn[NV + NA];
 #pragma unroll
-      for (int i = 0; i < NV; ++i) { x[i] = NST == 1 ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+      for (int i = 0; i < NV; ++i) sn[i] = x1[i];
 #pragma unroll
-      for (int j = 0; j < NA; ++j) { a[j] = NST == 1 ? a[j] + aa[j] * h : MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
+      for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
       const bool ok = !Env::bad(sn, NV + NA);
-      if (prev_ok && !ok) pending = true;
+      ev = prev_ok && !ok;
       prev_ok = ok;
+    }
+    // SaveAt(ts): every pending ts[k] <= tn through this step's dense output
+    while (k < S && clk.saves(ts, k)) {
+      const float th = mtgp_cs_rescale(t, ts[k], clk.tn);
+      float xs[NV], as[NA];
+      cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
+      cs_dense<NA>(NST == 1, dead, a, a1, fa0, ka, dt, th, as);
+      save_point(k, xs, as, dead);
+      ++k;
+    }
+    if (!dead) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[i] = x1[i];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) a[j] = a1[j];
+    }
+    if (ev) {  // the solve ends: later save points are the +inf fill
+      dead = true;
+      if (k < S) Env::fit_kill(fit);
+    }
+    clk.advance();
+    if (!TRAJ && wave_all(fit.settled || dead)) break;
+  }
+  if (k < S) {  // unsaved points (event everywhere / max_steps): +inf (throw=False)
+    if (!fit.settled) Env::fit_kill(fit);
+    if (TRAJ) {
+      float xs[NV], as[NA];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) xs[i] = kInf;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) as[j] = kInf;
+      for (; k < S; ++k) save_point(k, xs, as, true);
     }
   }
   finish_group(A, Ln, Env::fit_final(fit, S));
@@ -1326,9 +1385,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   float* st = &lds[Ln.wave][DM * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
 
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
-  const float t0 = A.ro.ts[0];
+  const int S = A.m.n_save;
   ObsNoise<NV> nzc;
   float nzv[NV];
 #pragma unroll
@@ -1343,32 +1400,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   for (int t = 0; t < DM - NV - 2; ++t)
     if (t < A.m.n_targets && uslot + 1 + t < DM) D.put(uslot + 1 + t, A.ro.targets[rr * A.m.n_targets + t]);
 
-  // groups whose save-time readout differs from the drift readout (it reads y): bit per group
-  uint64_t diff_mask = 0;
-  for (int gi = 0; gi < ng; ++gi) {
-    const size_t pj = (size_t)group_ind(A, Ln, gi) * A.n_prog;
-    bool same = A.m.readout_save_same > 0;
-    if (A.m.readout_save_same < 0) {
-      const int la = uni(A.plen[pj + A.m.prog_readout]), lb = uni(A.plen[pj + A.m.prog_readout_save]);
-      same = la == lb;
-      const MtgpInstr* pa = A.prog + (pj + A.m.prog_readout) * A.L;
-      const MtgpInstr* pb = A.prog + (pj + A.m.prog_readout_save) * A.L;
-      for (int i = 0; same && i < la; ++i)
-        same = (pa[i].op == pb[i].op) && (__float_as_uint(pa[i].imm) == __float_as_uint(pb[i].imm));
-    }
-    if (!same) diff_mask |= 1ull << gi;
-  }
-  diff_mask = __builtin_amdgcn_readfirstlane(diff_mask);
-
-  float x[NV], a[NA], kx[NV], ka[NA], ax[NV], aa[NA];
+  float x[NV], a[NA], kx[NV], ka[NA], fx0[NV], fa0[NA], ax[NV], aa[NA];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
 #pragma unroll
-  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = 0.0f;
+  for (int j = 0; j < NA; ++j) a[j] = ka[j] = aa[j] = fa0[j] = 0.0f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = fx0[i] = 0.0f;
 
   typename Env::Fit fit = Env::fit_init(active);
-  bool dead = !active;  // state frozen at +inf once the event state has been saved
-  bool pending = false; // event fired at the end of the previous step
+  bool dead = !active;  // the solve has ended (event): later save points are the +inf fill
   bool prev_ok;
   {
     float s0[NV + NA];
@@ -1378,24 +1419,56 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
     for (int j = 0; j < NA; ++j) s0[NV + j] = a[j];
     prev_ok = !Env::bad(s0, NV + NA);
   }
-
-  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
-  const int n_stages = euler ? 1 : 4;
-  int save_k = 0, save_ctr = 0;  // save index / steps since the last save (no per-step division)
-  for (int step = 0;; ++step) {
-    const bool last = step == n_steps;
-    const bool is_save = save_ctr == 0;
-    const int ksave = save_k;
-    if (++save_ctr == save_every) {
-      save_ctr = 0;
-      ++save_k;
+  // one save point: the state (xs, as) at ts[k] -> f_obs(key, (ts[k], xs)) (dyn.py:99), the
+  // save-point readout on [y, a, 0, tar] (dyn.py:101), fitness, rows
+  auto save_point = [&](int k, const float (&xs)[NV], const float (&as)[NA], bool fill) __attribute__((always_inline)) {
+    float yo[NV];
+    ctl_obs<Env, NOISE>(nzc, A.ro.ts[k], xs, yo);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) D.put(i, yo[i]);
+#pragma unroll
+    for (int j = 0; j < NA; ++j)
+      if (j < na) D.put(NV + j, as[j]);
+    D.put(uslot, 0.0f);
+    float sr[1];
+    run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
+    const float us = sr[0];
+    if constexpr (Env::kMask) {
+      if (active) env.fit_save(fit, k, S, A, PR, loff, fill, us, xs);
+    } else if (!fill && !MTGP_AB_NOFIT) {
+      env.fit_update(fit, k, S, A.ro.ts, us, xs);
     }
-    bool stop = last;
+    if (TRAJ && active && !MTGP_AB_NOSTORE) {
+      if (A.out.xs) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, xs[i], PR);
+      }
+      if (A.out.ys) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, yo[i], PR);
+      }
+      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
+      if (A.out.acts) {
+#pragma unroll
+        for (int j = 0; j < NA; ++j)
+          if (j < na) store_row(A.out.acts, ((size_t)k * na + j) * PR, loff, as[j], PR);
+      }
+    }
+  };
+
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + f dt
+  const int n_stages = euler ? 1 : 4;
+  CsClock clk;
+  clk.init(A);
+  int k = 0;  // next save point
+  while (clk.live()) {
+    const float t = clk.t, dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
-      stage_in_n<NV>(stage, x, kx, h, h2, xt);
-      stage_in_n<NA>(stage, a, ka, h, h2, at);
+      stage_in_n<NV>(stage, x, kx, dt, xt);
+      stage_in_n<NA>(stage, a, ka, dt, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j)
         if (j < na) D.put(NV + j, at[j]);
@@ -1403,93 +1476,68 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       const float u = ur[0];
       env.drift(xt, u, kx);
-      const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      // stages 1 and 2 share the time t + h/2, hence the noise draw
-      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+      // stages 1 and 2 share the time t + dt/2, hence the noise draw
+      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage_time(stage, t, dt), nzv);
       ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, u);
-      // the save-point readout (dyn.py:101) reads this stage-0 data vector (y = f_obs(ts[k], x),
-      // a; u is folded to 0), so the state chain continues into it -- unless the save-point
-      // observation needs its own noise draw (ts[k] off the step grid)
-      bool redraw = false;
-      if (NOISE && stage == 0 && is_save)
-        redraw = __float_as_uint(A.ro.ts[ksave]) != __float_as_uint(t0 + (float)step * h);
-      const bool save_chain = JIT && A.chain_save && stage == 0 && is_save && diff_mask != 0 && !redraw;
-      float us_chain = u;
-      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0,
-                        save_chain ? A.m.prog_readout_save : -1, &us_chain, na);
+      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0, -1, nullptr, na);
       if (stage == 0) {
-        if (is_save) {
-          const int k = ksave;
-          float us = u;
-          if (NOISE && redraw) {
-            ctl_obs<Env, true>(nzc, A.ro.ts[k], x, y);  // f_obs(key, (ts[k], xs[k])), dyn.py:99
 #pragma unroll
-            for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-          }
-          if (save_chain) {
-            us = us_chain;
-          } else if (JIT && diff_mask != 0) {  // the save-readout unit covers every group (equal programs give u again)
-            float sr[1];
-            run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
-            us = sr[0];
-          } else if (!JIT && diff_mask != 0) {
-            for (int gi = 0; gi < ng; ++gi) {
-              if (!((diff_mask >> gi) & 1ull)) continue;
-              const float t = run_one_interp(A, Ln, gi, A.m.prog_readout_save, D.dcol, D.st);
-              us = (Ln.g == gi) ? t : us;
-            }
-          }
-          if constexpr (Env::kMask) {
-            if (active) env.fit_save(fit, k, S, A, PR, loff, dead, us, x);
-          } else if (!dead && !MTGP_AB_NOFIT) {
-            env.fit_update(fit, k, S, A.ro.ts, us, x);
-          }
-          if (TRAJ && active && !MTGP_AB_NOSTORE) {
-            if (A.out.xs) {
+        for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
 #pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
-            }
-            if (A.out.ys) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
-            }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
-            if (A.out.acts) {
-#pragma unroll
-              for (int j = 0; j < NA; ++j)
-                if (j < na) store_row(A.out.acts, ((size_t)k * na + j) * PR, loff, a[j], PR);
-            }
-          }
-        }
-        if (pending) {  // the event state has been saved: freeze at +inf (saveat fill)
-          pending = false;
-          dead = true;
-          if (!last) Env::fit_kill(fit);  // save points of the +inf fill follow
-#pragma unroll
-          for (int i = 0; i < NV; ++i) x[i] = kInf;
-#pragma unroll
-          for (int j = 0; j < NA; ++j) a[j] = kInf;
-        }
-        if (!TRAJ && wave_all(fit.settled || dead)) stop = true;
-        if (stop) break;
+        for (int j = 0; j < NA; ++j) fa0[j] = ka[j];
       }
       stage_acc_n<NV>(stage, ax, kx);
       stage_acc_n<NA>(stage, aa, ka);
     }
-    if (stop) break;
+    float x1[NV], a1[NA];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) a1[j] = euler ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
+    bool ev = false;
     if (!dead) {
       float sn[NV + NA];
 #pragma unroll
-      for (int i = 0; i < NV; ++i) { x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]); sn[i] = x[i]; }
+      for (int i = 0; i < NV; ++i) sn[i] = x1[i];
 #pragma unroll
-      for (int j = 0; j < NA; ++j) { a[j] = euler ? a[j] + aa[j] * h : MTGP_FMAF(h6, aa[j], a[j]); sn[NV + j] = a[j]; }
+      for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
       const bool ok = !Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
-      if (prev_ok && !ok) pending = true;
+      ev = prev_ok && !ok;
       prev_ok = ok;
+    }
+    while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
+      const float th = mtgp_cs_rescale(t, A.ro.ts[k], clk.tn);
+      float xs[NV], as[NA];
+      cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
+      cs_dense<NA>(euler, dead, a, a1, fa0, ka, dt, th, as);
+      save_point(k, xs, as, dead);
+      ++k;
+    }
+    if (!dead) {
+#pragma unroll
+      for (int i = 0; i < NV; ++i) x[i] = x1[i];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) a[j] = a1[j];
+    }
+    if (ev) {
+      dead = true;
+      if (k < S) Env::fit_kill(fit);  // save points of the +inf fill follow
+    }
+    clk.advance();
+    if (!TRAJ && wave_all(fit.settled || dead)) break;
+  }
+  if (k < S) {  // unsaved points (max_steps, or every lane ended): +inf (throw=False)
+    if (!fit.settled) Env::fit_kill(fit);
+    if (TRAJ) {
+      float xs[NV], as[NA];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) xs[i] = kInf;
+#pragma unroll
+      for (int j = 0; j < NA; ++j) as[j] = kInf;
+      for (; k < S; ++k) save_point(k, xs, as, true);
     }
   }
   finish_group(A, Ln, Env::fit_final(fit, S));
@@ -1503,9 +1551,9 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   const int r = Ln.r, rr = Ln.rr;
   const bool active = Ln.active;
   const int R = A.ro.R;
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
-  const float t0 = A.ro.ts[0];
+  const int S = A.m.n_save;
+  const float* __restrict__ ts = A.ro.ts;
+  uint32_t nzt = 0xffffffffu;  // bits of the time nzv was drawn at
   ObsNoise<NV> nzc;
   float nzv[NV];
 #pragma unroll
@@ -1523,91 +1571,108 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
     if (t < A.m.n_targets) dv[NV + t] = A.ro.targets[rr * A.m.n_targets + t];
   const uint64_t u_policy = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout);
 
-  float x[NV], kx[NV], ax[NV];
+  float x[NV], kx[NV], fx0[NV], ax[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = 0.0f;
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = fx0[i] = 0.0f;
   typename Env::Fit fit = Env::fit_init(active);
-  bool dead = !active, pending = false;
+  bool dead = !active;
   bool prev_ok = !Env::bad(x, NV);
-
-  int save_k = 0, save_ctr = 0;
-  for (int step = 0;; ++step) {
-    const bool last = step == n_steps;
-    const bool is_save = save_ctr == 0;
-    const int ksave = save_k;
-    if (++save_ctr == save_every) {
-      save_ctr = 0;
-      ++save_k;
+  // one save point: ys = f_obs(key, (ts[k], xs)) (ff.py:96), us = policy([ys, tar]) (ff.py:97)
+  auto save_point = [&](int k, const float (&xs)[NV], bool fill) __attribute__((always_inline)) {
+    float yo[NV];
+    if (NOISE) {
+      const uint32_t tb = __float_as_uint(ts[k]);
+      if (tb != nzt) {
+        obs_noise_vec<NV>(nzc, ts[k], nzv);
+        nzt = tb;
+      }
     }
-    const float tk = t0 + (float)step * h;
-    auto stage = [&](auto st_c) -> bool {
+    ctl_obs_apply<Env>(xs, nzv, yo);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) dv[i] = yo[i];
+    const float us = jit_call_nf(u_policy, dv);
+    if (!fill) env.fit_update(fit, k, S, ts, us, xs);
+    if (TRAJ && active) {
+      if (A.out.xs) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, xs[i], PR);
+      }
+      if (A.out.ys) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, yo[i], PR);
+      }
+      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
+    }
+  };
+
+  CsClock clk;
+  clk.init(A);
+  int k = 0;
+  while (clk.live()) {
+    const float t = clk.t, dt = clk.dt();
+    auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], y[NV];
-      rk_in<NV>(ST, x, kx, ST == 3 ? h : h2, xt);
-      if (NOISE && ST != 2) obs_noise_vec<NV>(nzc, ST == 0 ? tk : tk + (ST == 3 ? h : h2), nzv);
+      rk_in<NV>(ST, x, kx, dt, xt);
+      if (NOISE && ST != 2) {
+        const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
+        obs_noise_vec<NV>(nzc, tc, nzv);
+        nzt = __float_as_uint(tc);
+      }
       ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
       for (int i = 0; i < NV; ++i) dv[i] = y[i];
-      float u = jit_call_nf(u_policy, dv);  // ff.py:106-107 (:97 at saves)
+      const float u = jit_call_nf(u_policy, dv);  // ff.py:106-107
       env.drift(xt, u, kx);
       if (ST == 0) {
-        if (is_save) {
-          const int k = ksave;
-          if (NOISE) {
-            const float tsk = A.ro.ts[k];
-            if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
-              ctl_obs<Env, true>(nzc, tsk, x, y);
 #pragma unroll
-              for (int i = 0; i < NV; ++i) dv[i] = y[i];
-              u = jit_call_nf(u_policy, dv);
-            }
-          }
-          if (!dead) env.fit_update(fit, k, S, A.ro.ts, u, x);
-          if (TRAJ && active) {
-            if (A.out.xs) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
-            }
-            if (A.out.ys) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
-            }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u, PR);
-          }
-        }
-        if (pending) {
-          pending = false;
-          dead = true;
-          if (!last) Env::fit_kill(fit);
-#pragma unroll
-          for (int i = 0; i < NV; ++i) x[i] = kInf;
-        }
-        if (last || (!TRAJ && wave_all(fit.settled || dead))) return true;
+        for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
       }
-      rk_acc<NV>(NST == 1 ? 0 : ST, ax, kx);
-      return false;
+      if (NST == 4) rk_acc<NV>(ST, ax, kx);
     };
-    bool stop;
-    if constexpr (NST == 1) {
-      stop = stage(std::integral_constant<int, 0>{});
-    } else {
-      stop = stage(std::integral_constant<int, 0>{});
-      if (!stop) {
-        stage(std::integral_constant<int, 1>{});
-        stage(std::integral_constant<int, 2>{});
-        stage(std::integral_constant<int, 3>{});
-      }
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (NST == 4) {
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
     }
-    if (stop) break;
+    float x1[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+    bool ev = false;
+    if (!dead) {
+      const bool ok = !Env::bad(x1, NV);
+      ev = prev_ok && !ok;
+      prev_ok = ok;
+    }
+    while (k < S && clk.saves(ts, k)) {
+      const float th = mtgp_cs_rescale(t, ts[k], clk.tn);
+      float xs[NV];
+      cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
+      save_point(k, xs, dead);
+      ++k;
+    }
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = NST == 1 ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
-      const bool ok = !Env::bad(x, NV);
-      if (prev_ok && !ok) pending = true;
-      prev_ok = ok;
+      for (int i = 0; i < NV; ++i) x[i] = x1[i];
+    }
+    if (ev) {
+      dead = true;
+      if (k < S) Env::fit_kill(fit);
+    }
+    clk.advance();
+    if (!TRAJ && wave_all(fit.settled || dead)) break;
+  }
+  if (k < S) {
+    if (!fit.settled) Env::fit_kill(fit);
+    if (TRAJ) {
+      float xs[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) xs[i] = kInf;
+      for (; k < S; ++k) save_point(k, xs, true);
     }
   }
   finish_group(A, Ln, Env::fit_final(fit, S));
@@ -1636,9 +1701,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
-  const float t0 = A.ro.ts[0];
+  const int S = A.m.n_save;
   ObsNoise<NV> nzc;
   float nzv[NV];
 #pragma unroll
@@ -1652,89 +1715,101 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   for (int t = 0; t < kDMax - NV; ++t)
     if (t < A.m.n_targets) D.put(NV + t, A.ro.targets[rr * A.m.n_targets + t]);
 
-  float x[NV], kx[NV], ax[NV];
+  float x[NV], kx[NV], fx0[NV], ax[NV];
 #pragma unroll
   for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) kx[i] = ax[i] = fx0[i] = 0.0f;
   typename Env::Fit fit = Env::fit_init(active);
-  bool dead = !active, pending = false;
+  bool dead = !active;
   bool prev_ok = !Env::bad(x, NV);
-
-  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
-  const int n_stages = euler ? 1 : 4;
-  int save_k = 0, save_ctr = 0;  // save index / steps since the last save (no per-step division)
-  for (int step = 0;; ++step) {
-    const bool last = step == n_steps;
-    const bool is_save = save_ctr == 0;
-    const int ksave = save_k;
-    if (++save_ctr == save_every) {
-      save_ctr = 0;
-      ++save_k;
+  // one save point: ys = f_obs(key, (ts[k], xs)) (ff.py:96), us = policy([ys, tar]) (ff.py:97)
+  auto save_point = [&](int k, const float (&xs)[NV], bool fill) __attribute__((always_inline)) {
+    float yo[NV];
+    ctl_obs<Env, NOISE>(nzc, A.ro.ts[k], xs, yo);
+#pragma unroll
+    for (int i = 0; i < NV; ++i) D.put(i, yo[i]);
+    float ur[1];
+    run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+    const float us = ur[0];
+    if constexpr (Env::kMask) {
+      if (active) env.fit_save(fit, k, S, A, PR, loff, fill, us, xs);
+    } else if (!fill) {
+      env.fit_update(fit, k, S, A.ro.ts, us, xs);
     }
-    bool stop = last;
+    if (TRAJ && active) {
+      if (A.out.xs) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, xs[i], PR);
+      }
+      if (A.out.ys) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, yo[i], PR);
+      }
+      if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, us, PR);
+    }
+  };
+
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + f dt
+  const int n_stages = euler ? 1 : 4;
+  CsClock clk;
+  clk.init(A);
+  int k = 0;
+  while (clk.live()) {
+    const float t = clk.t, dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
-      stage_in_n<NV>(stage, x, kx, h, h2, xt);
-      const float tk = t0 + (float)step * h;  // step start; stages at tk + c_i h (oracle rk4_step)
-      // stages 1 and 2 share the time t + h/2, hence the noise draw
-      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage == 0 ? tk : tk + (stage == 3 ? h : h2), nzv);
+      stage_in_n<NV>(stage, x, kx, dt, xt);
+      // stages 1 and 2 share the time t + dt/2, hence the noise draw
+      if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage_time(stage, t, dt), nzv);
       ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       float ur[1];
-      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // ff.py:106-107 (:97 at saves)
-      float u = ur[0];
-      env.drift(xt, u, kx);
+      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // ff.py:106-107
+      env.drift(xt, ur[0], kx);
       if (stage == 0) {
-        if (is_save) {
-          const int k = ksave;
-          if (NOISE) {
-            const float tsk = A.ro.ts[k];
-            if (__float_as_uint(tsk) != __float_as_uint(tk)) {  // ys at ts[k] (ff.py:96), us = policy(ys) (:97)
-              ctl_obs<Env, true>(nzc, tsk, x, y);
 #pragma unroll
-              for (int i = 0; i < NV; ++i) D.put(i, y[i]);
-              run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
-              u = ur[0];
-            }
-          }
-          if constexpr (Env::kMask) {
-            if (active) env.fit_save(fit, k, S, A, PR, loff, dead, u, x);
-          } else if (!dead) {
-            env.fit_update(fit, k, S, A.ro.ts, u, x);
-          }
-          if (TRAJ && active) {
-            if (A.out.xs) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i) store_row(A.out.xs, ((size_t)k * NV + i) * PR, loff, x[i], PR);
-            }
-            if (A.out.ys) {
-#pragma unroll
-              for (int i = 0; i < NV; ++i)
-                if (i < A.m.n_obs) store_row(A.out.ys, ((size_t)k * A.m.n_obs + i) * PR, loff, y[i], PR);
-            }
-            if (A.out.us) store_row(A.out.us, (size_t)k * PR, loff, u, PR);
-          }
-        }
-        if (pending) {
-          pending = false;
-          dead = true;
-          if (!last) Env::fit_kill(fit);
-#pragma unroll
-          for (int i = 0; i < NV; ++i) x[i] = kInf;
-        }
-        if (!TRAJ && wave_all(fit.settled || dead)) stop = true;
-        if (stop) break;
+        for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
       }
       stage_acc_n<NV>(stage, ax, kx);
     }
-    if (stop) break;
+    float x1[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+    bool ev = false;
+    if (!dead) {
+      const bool ok = !Env::bad(x1, NV);
+      ev = prev_ok && !ok;
+      prev_ok = ok;
+    }
+    while (k < S && clk.saves(A.ro.ts, k)) {
+      const float th = mtgp_cs_rescale(t, A.ro.ts[k], clk.tn);
+      float xs[NV];
+      cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
+      save_point(k, xs, dead);
+      ++k;
+    }
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
-      const bool ok = !Env::bad(x, NV);
-      if (prev_ok && !ok) pending = true;
-      prev_ok = ok;
+      for (int i = 0; i < NV; ++i) x[i] = x1[i];
+    }
+    if (ev) {
+      dead = true;
+      if (k < S) Env::fit_kill(fit);
+    }
+    clk.advance();
+    if (!TRAJ && wave_all(fit.settled || dead)) break;
+  }
+  if (k < S) {
+    if (!fit.settled) Env::fit_kill(fit);
+    if (TRAJ) {
+      float xs[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) xs[i] = kInf;
+      for (; k < S; ++k) save_point(k, xs, true);
     }
   }
   finish_group(A, Ln, Env::fit_final(fit, S));
@@ -2079,63 +2154,93 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
   if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const int S = A.m.n_save;
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;
-  float x[NV], kx[NV], ax[NV];
+  float x[NV], kx[NV], fx0[NV], ax[NV];
 #pragma unroll
-  for (int i = 0; i < NV; ++i) x[i] = A.ro.x0[rr * NV + i];
+  for (int i = 0; i < NV; ++i) {
+    x[i] = A.ro.x0[rr * NV + i];
+    kx[i] = fx0[i] = ax[i] = 0.0f;
+  }
   auto bad = [&](const float* s) {
     bool b = false;
 #pragma unroll
     for (int i = 0; i < NV; ++i) b = b || !mtgp_isfinite(s[i]);
     return b;
   };
-  bool dead = !active, pending = false, prev_ok = !bad(x);
+  bool dead = !active, prev_ok = !bad(x);
   float tot = 0.0f;
-  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
-  const int n_stages = euler ? 1 : 4;
-  for (int step = 0;; ++step) {
-    if ((step % save_every) == 0) {
-      const int k = step / save_every;
+  // one save point: the MSE term sum_d (pred - true)^2 (sr.py:24); a point of the +inf fill makes
+  // the sum +inf (NaN stays NaN), as the oracle's MSE of the saved arrays
+  auto save_point = [&](int k, const float (&xs)[NV], bool fill) __attribute__((always_inline)) {
+    if (fill) {
+      if (mtgp_isfinite(tot)) tot = kInf;
+    } else {
       float sq = 0.0f;
 #pragma unroll
       for (int d = 0; d < NV; ++d) {
-        const float e = x[d] - A.ro.ys_true[((size_t)k * NV + d) * R + rr];
+        const float e = xs[d] - A.ro.ys_true[((size_t)k * NV + d) * R + rr];
         sq = (d == 0) ? e * e : sq + e * e;
       }
       tot = tot + sq;
-      if (TRAJ && active && A.out.xs) {
+    }
+    if (TRAJ && active && A.out.xs) {
 #pragma unroll
-        for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, x[d], PR);
-      }
+      for (int d = 0; d < NV; ++d) store_row(A.out.xs, ((size_t)k * NV + d) * PR, loff, xs[d], PR);
     }
-    if (pending) {
-      pending = false;
-      dead = true;
-#pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = kInf;
-    }
-    if (step == n_steps) break;
-    if (!TRAJ && wave_all(dead)) {  // every remaining save point adds (inf - y)^2
-      if (active && mtgp_isfinite(tot)) tot = kInf;
-      break;
-    }
+  };
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + f dt
+  const int n_stages = euler ? 1 : 4;
+  CsClock clk;
+  clk.init(A);
+  int k = 0;
+  while (clk.live()) {
+    const float dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], h, h2));
+      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], dt));
       run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
+      if (stage == 0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
+      }
 #pragma unroll
       for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
+    float x1[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+    bool ev = false;
+    if (!dead) {
+      const bool ok = !bad(x1);
+      ev = prev_ok && !ok;  // the NaN event (sr.py:93-94)
+      prev_ok = ok;
+    }
+    while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
+      const float th = mtgp_cs_rescale(clk.t, A.ro.ts[k], clk.tn);
+      float xs[NV];
+      cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
+      save_point(k, xs, dead);
+      ++k;
+    }
     if (!dead) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) x[i] = euler ? x[i] + ax[i] * h : MTGP_FMAF(h6, ax[i], x[i]);
-      const bool ok = !bad(x);
-      if (prev_ok && !ok) pending = true;
-      prev_ok = ok;
+      for (int i = 0; i < NV; ++i) x[i] = x1[i];
+    }
+    if (ev) dead = true;
+    clk.advance();
+    if (!TRAJ && wave_all(dead)) break;  // every remaining save point adds (inf - y)^2
+  }
+  if (k < S) {  // unsaved points (event / max_steps): +inf
+    float xs[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) xs[i] = kInf;
+    if (TRAJ) {
+      for (; k < S; ++k) save_point(k, xs, true);
+    } else {
+      save_point(k, xs, true);
     }
   }
   const float F = tot / (float)S;
@@ -2366,27 +2471,28 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   float* bufB = wl + (size_t)NV * kWave + lane;
   float* st = wl + (size_t)(2 * NV + w * kSMax) * kWave + lane;
   float* flags = wl + (size_t)(2 * NV + NW * kSMax) * kWave + lane;  // [NW] columns
-  const int S = A.m.n_save, n_steps = A.m.n_steps, save_every = A.m.save_every;
-  const float h = A.m.h, h2 = h * 0.5f, h6 = h / 6.0f;
+  const int S = A.m.n_save;
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;
   const int c0 = w * kWideComp;
 
-  float x[kWideComp], ax[kWideComp];
+  // x: this wave's components of the lane's state; fx0: their stage-0 derivatives (Hermite k0 =
+  // f0 dt); ax: the running b-weighted stage sum (mtgp_cstep.h)
+  float x[kWideComp], ax[kWideComp], fx0[kWideComp];
 #pragma unroll
   for (int t = 0; t < kWideComp; ++t) {
     x[t] = (c0 + t < NV) ? A.ro.x0[rr * NV + c0 + t] : 0.0f;
-    ax[t] = 0.0f;
+    ax[t] = fx0[t] = 0.0f;
   }
-  // workgroup-wide "any component non-finite" of this lane's state
-  auto any_bad = [&]() {
+  // workgroup-wide "any component of v non-finite" for this lane (two barriers)
+  auto any_bad = [&](const float (&v)[kWideComp]) {
     bool b = false;
 #pragma unroll
-    for (int t = 0; t < kWideComp; ++t) b = b || ((c0 + t < NV) && !mtgp_isfinite(x[t]));
+    for (int t = 0; t < kWideComp; ++t) b = b || ((c0 + t < NV) && !mtgp_isfinite(v[t]));
     flags[w * kWave] = b ? 1.0f : 0.0f;
     __syncthreads();
     bool all = false;
-    for (int v = 0; v < NW; ++v) all = all || (flags[v * kWave] != 0.0f);
+    for (int v2 = 0; v2 < NW; ++v2) all = all || (flags[v2 * kWave] != 0.0f);
     __syncthreads();
     return all;
   };
@@ -2395,49 +2501,43 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
 #pragma unroll
   for (int t = 0; t < kWideComp; ++t)
     if (c0 + t < NV) cur[(c0 + t) * kWave] = x[t];
-  bool dead = !active, pending = false;
-  bool prev_ok = !any_bad();  // (its barrier also publishes cur)
+  bool dead = !active;
+  bool prev_ok = !any_bad(x);  // (its barrier also publishes cur)
   float tot = 0.0f;
-  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + k h
+  // one save point (every wave, uniform): the per-component squared errors meet in LDS (scratch
+  // column buffer sq) and wave 0 sums them in index order (sr.py:24); fill: +inf, as k_sr
+  auto save_point = [&](int k, const float (&xs)[kWideComp], bool fill, float* sq) __attribute__((always_inline)) {
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) {
+      const int c = c0 + t;
+      if (c < NV) {
+        const float e = xs[t] - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
+        sq[c * kWave] = e * e;
+        if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, xs[t], PR);
+      }
+    }
+    __syncthreads();  // (uniform: a lane's fill flag is the same in every wave)
+    if (w == 0) {  // (only wave 0 reports the fitness: finish_group)
+      if (fill) {
+        if (mtgp_isfinite(tot)) tot = kInf;
+      } else {
+        float v = sq[0];
+        for (int d = 1; d < NV; ++d) v = v + sq[d * kWave];
+        tot = tot + v;
+      }
+    }
+    __syncthreads();
+  };
+  const bool euler = A.m.solver == MTGP_SOLVER_EULER;  // diffrax.Euler: one stage, y + f dt
   const int n_stages = euler ? 1 : 4;
-  for (int step = 0;; ++step) {
-    if ((step % save_every) == 0) {
-      const int k = step / save_every;
-#pragma unroll
-      for (int t = 0; t < kWideComp; ++t) {
-        const int c = c0 + t;
-        if (c < NV) {
-          const float e = x[t] - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
-          nxt[c * kWave] = e * e;
-          if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, x[t], PR);
-        }
-      }
-      __syncthreads();
-      if (w == 0) {  // (only wave 0 reports the fitness: finish_group)
-        float sq = nxt[0];
-        for (int d = 1; d < NV; ++d) sq = sq + nxt[d * kWave];
-        tot = tot + sq;
-      }
-      __syncthreads();
-    }
-    if (pending) {
-      pending = false;
-      dead = true;
-#pragma unroll
-      for (int t = 0; t < kWideComp; ++t) {
-        x[t] = kInf;
-        if (c0 + t < NV) cur[(c0 + t) * kWave] = kInf;
-      }
-      __syncthreads();
-    }
-    if (step == n_steps) break;
-    if (!TRAJ && wave_all(dead)) {  // dead is identical in every wave: a uniform exit
-      if (active && mtgp_isfinite(tot)) tot = kInf;
-      break;
-    }
+  CsClock clk;
+  clk.init(A);
+  int k = 0;
+  while (clk.live()) {
+    const float dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
-      // trees of this wave's components on the shared stage vector; k parks in nxt
+      // trees of this wave's components on the shared stage vector; f parks in nxt
       if (JIT && Ln.jok && A.chain_store) {  // one call: this wave's components' units, results into nxt
         const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + c0);
         uint64_t fl = 0;
@@ -2483,13 +2583,15 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
           nxt[c * kWave] = run_groups_interp<JIT && MTGP_COLD_INTERP != 0>(A, Ln, ng, A.m.prog_state + c, cur, st, 0.0f);
         }
       }
+      const bool last = stage == n_stages - 1;
 #pragma unroll
       for (int t = 0; t < kWideComp; ++t) {
         const int c = c0 + t;
         if (c < NV) {
           const float kv = nxt[c * kWave];
+          if (stage == 0) fx0[t] = kv;
           ax[t] = stage_acc(stage, ax[t], kv);
-          if (stage < 3) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, h, h2);
+          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, dt);  // the next stage's input
         }
       }
       __syncthreads();
@@ -2497,17 +2599,45 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       cur = nxt;
       nxt = tmp;
     }
+    // cur holds the last stage's derivatives f3 (Euler: f0); the step's end state and the event
+    float x1[kWideComp];
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) x1[t] = euler ? x[t] + fx0[t] * dt : mtgp_rk4_out(x[t], ax[t], dt);
+    const bool bad = any_bad(x1);
+    bool ev = false;
+    if (!dead) {
+      ev = prev_ok && bad;
+      prev_ok = !bad;
+    }
+    while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
+      const float th = mtgp_cs_rescale(clk.t, A.ro.ts[k], clk.tn);
+      float xs[kWideComp], f3[kWideComp];
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t) f3[t] = (c0 + t < NV) ? cur[(c0 + t) * kWave] : 0.0f;
+      cs_dense<kWideComp>(euler, dead, x, x1, fx0, f3, dt, th, xs);
+      save_point(k, xs, dead, nxt);
+      ++k;
+    }
     if (!dead) {
 #pragma unroll
-      for (int t = 0; t < kWideComp; ++t) x[t] = euler ? x[t] + ax[t] * h : MTGP_FMAF(h6, ax[t], x[t]);
+      for (int t = 0; t < kWideComp; ++t) x[t] = x1[t];
     }
+    if (ev) dead = true;
 #pragma unroll
     for (int t = 0; t < kWideComp; ++t)
-      if (c0 + t < NV) cur[(c0 + t) * kWave] = x[t];
-    const bool bad = any_bad();  // (its barrier also publishes cur)
-    if (!dead) {
-      if (prev_ok && bad) pending = true;
-      prev_ok = !bad;
+      if (c0 + t < NV) cur[(c0 + t) * kWave] = dead ? kInf : x[t];
+    __syncthreads();  // publishes cur for the next step's stage 0
+    clk.advance();
+    if (!TRAJ && wave_all(dead)) break;  // dead is identical in every wave: a uniform exit
+  }
+  if (k < S) {  // unsaved points (event / max_steps): +inf
+    float xs[kWideComp];
+#pragma unroll
+    for (int t = 0; t < kWideComp; ++t) xs[t] = kInf;
+    if (TRAJ) {
+      for (; k < S; ++k) save_point(k, xs, true, nxt);
+    } else {
+      save_point(k, xs, true, nxt);
     }
   }
   if (w == 0) finish_group(A, Ln, tot / (float)S);
@@ -4187,7 +4317,7 @@ MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
     M = m.n_var;
   } else if (m.model == MTGP_MODEL_DYNAMIC) {
     M = m.state_size;
-    save = m.solver != MTGP_SOLVER_DOPRI5 && m.readout_save_same != 1 && m.prog_readout_save == first + M;
+    save = false;  // (ABI v18: the save-point readout reads the dense-output state, not a stage's data vector)
   } else {
     return c;
   }
@@ -4932,9 +5062,9 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > MTGP_MAX_DATA)) return MTGP_ERR_ARG;
     if (model->n_save < 2 || model->max_steps <= 0 || !(model->h > 0.0f)) return MTGP_ERR_ARG;
     if (!(model->rtol >= 0.0f) || !(model->atol >= 0.0f)) return MTGP_ERR_ARG;
-  } else {
-    if (model->n_steps < 0 || model->save_every <= 0 || model->n_steps % model->save_every != 0) return MTGP_ERR_ARG;
-    if (model->n_save != model->n_steps / model->save_every + 1 || model->n_save < 2) return MTGP_ERR_ARG;
+  } else {  // fixed step (ABI v18): diffrax ConstantStepSize from dt0 = h, save points from ts (mtgp_cstep.h)
+    if (model->model == MTGP_MODEL_SR && (model->n_var < 1 || model->n_var > MTGP_MAX_DATA)) return MTGP_ERR_ARG;
+    if (model->n_save < 2 || model->max_steps < 0 || !(model->h > 0.0f) || !(model->h < 3.0e38f)) return MTGP_ERR_ARG;
   }
   if (!rollouts->x0 || !rollouts->ts) return MTGP_ERR_ARG;
   if (rollouts->fit_kof && (model->model == MTGP_MODEL_SR || model->env != MTGP_ENV_ACROBOT)) return MTGP_ERR_ARG;

@@ -9,7 +9,8 @@ one launch; these per-candidate calls exist for API parity and trajectory inspec
 
 Solver: BASELINE.json prescribes an explicit fixed-step RK4 (``RK4()`` or "rk4" with
 ``ConstantStepSize()``); omitting ``solver`` gives the reference's default ``Euler()`` (fixed
-step).  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)`` (SURVEY.md
+step).  Both follow diffrax.ConstantStepSize exactly (include/mtgp_cstep.h): accumulated f32 step
+ends, per-step dt, SaveAt(ts) for any non-decreasing ts through the dense output.  The notebooks' adaptive ``Dopri5()`` + ``PIDController(rtol, atol, dtmin)`` (SURVEY.md
 §8f row 2, spec include/mtgp_dopri5.h) runs on the GPU for the dynamic and static control
 evaluators (every environment) and for ``SREvaluator``.
 """
@@ -117,30 +118,58 @@ def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
 
 
 def _solver_fields(kind: str, controller, max_steps: int) -> dict:
-    if kind != "dopri5":
-        return dict(solver=nat.SOLVER_EULER if kind == "euler" else nat.SOLVER_RK4, max_steps=0, rtol=0.0, atol=0.0,
-                    dtmin=0.0, dtmax=0.0)
+    if kind != "dopri5":  # ConstantStepSize: max_steps bounds the fixed-step solve too (ABI v18)
+        return dict(solver=nat.SOLVER_EULER if kind == "euler" else nat.SOLVER_RK4, max_steps=int(max_steps), rtol=0.0,
+                    atol=0.0, dtmin=0.0, dtmax=0.0)
     return dict(solver=nat.SOLVER_DOPRI5, max_steps=int(max_steps), rtol=controller.rtol, atol=controller.atol,
                 dtmin=controller.dtmin or 0.0, dtmax=controller.dtmax or 0.0, **controller.model_fields())
 
 
-def rk4_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
-    """Map (ts, dt0) to (n_steps, save_every, n_save) for save points on step ends."""
+def constant_step_grid(ts: np.ndarray, dt0: float, max_steps: Optional[int] = None) -> np.ndarray:
+    """Step ends of diffrax.ConstantStepSize through diffeqsolve(t0=ts[0], t1=ts[-1], dt0)
+    (include/mtgp_cstep.h): float32, accumulated t += dt0 (the first end min(t0 + dt0, t1), later
+    ends t1 once past t1 - 1e-6), at most max_steps of them.  -> float32 [n_steps + 1] = the step
+    boundaries from ts[0].  The kernels follow the same rules on the device; this host copy sizes
+    the work (bench unit-steps, MtgpModel.n_steps)."""
+    f = np.float32
+    ts = np.asarray(ts, dtype=f)
+    t0, t1, dt0 = f(ts[0]), f(ts[-1]), f(dt0)
+    if not dt0 > 0 or not np.isfinite(dt0):
+        raise ValueError(f"dt0 must be a positive finite number, got {dt0}")
+    if not t0 < t1:
+        return np.array([t0], f)
+    first = min(f(t0 + dt0), t1)
+    cap = int(np.ceil((float(t1) - float(t0)) / float(dt0))) + 4
+    if max_steps is not None and max_steps > 0:
+        cap = min(cap, int(max_steps) + 1)
+    # sequential float32 accumulation (np.add.accumulate adds left to right in the array dtype)
+    ends = np.add.accumulate(np.concatenate([[first], np.full(max(cap - 1, 0), dt0, f)]).astype(f), dtype=f)
+    tol = f(t1 - f(1e-6))
+    over = np.nonzero(ends[1:] > tol)[0]
+    n = (over[0] + 2) if len(over) else len(ends)  # step ends kept, the clipped one included
+    if first >= t1:
+        n = 1
+    ends = ends[:n].copy()
+    if n > 1 and ends[-1] > tol:
+        ends[-1] = t1
+    if max_steps is not None and max_steps > 0:
+        ends = ends[: int(max_steps)]
+    return np.concatenate([[t0], ends]).astype(f)
+
+
+def fixed_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
+    """Euler / RK4 with ConstantStepSize (ABI v18): save points straight from ts, any non-decreasing
+    grid (SaveAt(ts) through the dense output), steps from the accumulated dt0 grid.
+    -> (n_steps of the grid, save_every 1 (unused), n_save)."""
     ts = np.asarray(ts, dtype=np.float32)
     S = int(ts.shape[0])
-    if S < 2:
-        raise ValueError("ts needs at least two save points")
-    dts = float(ts[1]) - float(ts[0])
-    save_every = int(round(dts / float(dt0)))
-    if save_every < 1 or abs(save_every * float(dt0) - dts) > 1e-4 * max(abs(dts), 1e-30):
-        raise ValueError(f"save spacing {dts} is not a multiple of dt0={dt0}")
-    expect = np.float64(ts[0]) + np.arange(S) * dts
-    if np.max(np.abs(ts.astype(np.float64) - expect)) > 1e-4 * max(abs(float(ts[-1])), 1.0):
-        raise ValueError("ts must be uniformly spaced (fixed-step RK4 saves on step ends)")
-    n_steps = (S - 1) * save_every
-    if n_steps > max_steps:
-        raise ValueError(f"{n_steps} RK4 steps exceed max_steps={max_steps}")
-    return n_steps, save_every, S
+    if S < 2 or np.any(np.diff(ts) < 0) or not np.all(np.isfinite(ts)):
+        raise ValueError("ts needs at least two finite non-decreasing save points")
+    n_steps = len(constant_step_grid(ts, dt0, max_steps)) - 1
+    return n_steps, 1, S
+
+
+rk4_schedule = fixed_schedule  # (round-1 name)
 
 
 def adaptive_schedule(ts: np.ndarray) -> Tuple[int, int, int]:
@@ -298,7 +327,7 @@ class _ControlEvaluator(_CandidateAPI):
         if self.solver_kind == "dopri5":
             n_steps, save_every, S = adaptive_schedule(ts)
         else:
-            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+            n_steps, save_every, S = fixed_schedule(ts, self.dt0, self.max_steps)
         mask = acrobot_mask(ts) if self.env_id == nat.ENV_ACROBOT else None
         out = dict(x0=x0, params=_f32(prm), targets=tg, ts=_f32(ts), ys_true=None, R=R, n_var=nv, env=self.env_id,
                    n_steps=n_steps, save_every=save_every, n_save=S, prng_impl=prng.prng_impl_code(),
@@ -397,7 +426,7 @@ class SREvaluator(_CandidateAPI):
         if self.solver_kind == "dopri5":  # save points straight from ts, steps from the controller
             n_steps, save_every, S = adaptive_schedule(ts)
         else:
-            n_steps, save_every, S = rk4_schedule(ts, self.dt0, self.max_steps)
+            n_steps, save_every, S = fixed_schedule(ts, self.dt0, self.max_steps)
         if ys.shape[1] != S:
             raise ValueError("ys must have len(ts) save points")
         ys_tm = np.ascontiguousarray(np.transpose(ys, (1, 2, 0)))  # [S, n_var, R] time-major
@@ -420,4 +449,4 @@ class SREvaluator(_CandidateAPI):
 
 
 __all__ = ["RK4", "Euler", "ConstantStepSize", "Dopri5", "PIDController", "DynamicEvaluator", "FeedforwardEvaluator", "SREvaluator",
-           "rk4_schedule", "adaptive_schedule", "acrobot_mask"]
+           "fixed_schedule", "rk4_schedule", "constant_step_grid", "adaptive_schedule", "acrobot_mask"]

@@ -28,6 +28,7 @@
 #include "mtgp_f32math.h"
 #include "mtgp_prng.h"
 #include "mtgp_dopri5.h"
+#include "mtgp_cstep.h"
 #include "mtgp_dual.h"
 
 #define OR_MAX_N 256
@@ -115,7 +116,22 @@ typedef struct {
   int32_t pid_custom;             /* 0: diffrax's default PID coefficients (mtgp.h ABI v15) */
   float pid_c1, pid_c2, pid_c3, pid_safety, pid_factormin, pid_factormax;
   int32_t no_force_dtmin;         /* 1: force_dtmin=False (dt < dtmin ends the solve) */
+  /* Oracle-only alternative readings of diffrax rules for the Dopri5 solve (scripts/dp_gap_study.py,
+   * DESIGN.md "Parity pins"); 0 = the spec (include/mtgp_dopri5.h) that the product follows.  Bits
+   * OR_DP_ALT_*.  Never part of the product ABI. */
+  int32_t dp_alt;
 } OrModel;
+
+enum {
+  OR_DP_ALT_EO6 = 1,           /* error order 6 (AbstractSolver.error_order = order + 1): exponent 1/6 */
+  OR_DP_ALT_FSAL_T1 = 2,       /* the last (FSAL) stage evaluated at t1 instead of t + 1 * h          */
+  OR_DP_ALT_DTMIN_ATTEMPT = 4, /* at_dtmin from the attempted step (h <= dtmin), not carried         */
+  OR_DP_ALT_SUM_LITERAL = 8,   /* stage sums sum(a f) with separate products / adds, then y + sum * h */
+  OR_DP_ALT_NORM_X = 16,       /* error norm over the environment state only (not the hidden state)  */
+  OR_DP_ALT_MAXSTEPS_ACC = 32, /* max_steps counts accepted steps only                                */
+  OR_DP_ALT_EVENT_ALL = 64,    /* the Event tested on every attempt's candidate, rejected ones too    */
+  OR_DP_ALT_INTERP_T0 = 128    /* ts[0] saved through the first step's dense output (not y0 directly) */
+};
 
 enum { ENV_ACROBOT = 0, ENV_HARMONIC = 1, ENV_REACTOR = 2 };
 
@@ -297,72 +313,103 @@ static float cond_fn(const OrModel* m, const float* s) {
   return bad ? -1.0f : 1.0f;
 }
 
-/* The solver step: classical RK4 (c = 0,1/2,1/2,1; b = 1/6,1/3,1/3,1/6), written with
- * explicit fma so that the GPU kernel can reproduce it bit-for-bit.  Step n starts at
- * t = ts[0] + f32(n) * h; stage i is evaluated at t + c_i * h (t, t + h/2, t + h/2, t + h),
- * which matters only for the time-dependent observation noise (cbase.py:45). */
-static void rk4_step(const OrCtx* c, float t, float* s) {
-  const int n = state_dim(c->m);
-  const float h = c->m->h, h2 = h * 0.5f, h6 = h / 6.0f;
-  float k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
-  rhs(c, t, s, k);
-  for (int i = 0; i < n; ++i) { acc[i] = k[i]; tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
-  rhs(c, t + h2, tmp, k);
-  for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h2, k[i], s[i]); }
-  rhs(c, t + h2, tmp, k);
-  for (int i = 0; i < n; ++i) { acc[i] = MTGP_FMAF(2.0f, k[i], acc[i]); tmp[i] = MTGP_FMAF(h, k[i], s[i]); }
-  rhs(c, t + h, tmp, k);
-  for (int i = 0; i < n; ++i) { acc[i] = acc[i] + k[i]; s[i] = MTGP_FMAF(h6, acc[i], s[i]); }
-}
-
-/* diffrax.Euler (the reference evaluators' default solver, dyn.py:11, ff.py:11, sr.py:21):
- * y1 = y0 + f(t0, y0) * dt, the product and the sum rounded separately (ODETerm.vf_prod, then
- * the add), at the fixed-grid step time like rk4_step. */
-static void euler_step(const OrCtx* c, float t, float* s) {
-  const int n = state_dim(c->m);
-  float k[OR_MAX_S];
-  rhs(c, t, s, k);
-  for (int i = 0; i < n; ++i) s[i] = s[i] + k[i] * c->m->h;
-}
-
-/* Solve one rollout: saved[n_save][dim]; unsaved points after termination = +inf. */
-static void solve(const OrCtx* c, float t0, const float* s0, float* saved) {
+/* diffeqsolve(solver, ts[0], ts[-1], dt0 = h, SaveAt(ts), ConstantStepSize(), max_steps,
+ * Event(cond_fn), throw=False) with solver = Euler (the reference evaluators' default, dyn.py:11,
+ * ff.py:11, sr.py:21) or classical RK4 (BASELINE.json) -- diffrax restated in the fp32 spec of
+ * include/mtgp_cstep.h (see its header comment for every rule used here): accumulated step ends
+ * t += dt0 with the end clip, each step over dt = tn - t, stage times t + c_i dt, stage sums
+ * (sum a_ij f_j) dt, every save point through the step's dense output, Event after the step.
+ * saved[n_save][dim]; unsaved points (after the event or max_steps) = +inf.  Returns the number of
+ * steps taken. */
+static int solve_fixed(const OrCtx* c, const float* ts, const float* s0, float* saved) {
   const OrModel* m = c->m;
-  const int n = state_dim(m);
-  float s[OR_MAX_S];
-  for (int i = 0; i < n; ++i) s[i] = s0[i];
-  for (int i = 0; i < n; ++i) saved[i] = s[i];
-  float prev = cond_fn(m, s);
-  int k_saved = 0, done = 0;
-  for (int step = 1; step <= m->n_steps && !done; ++step) {
-    if (m->solver == 2) euler_step(c, t0 + (float)(step - 1) * m->h, s);
-    else rk4_step(c, t0 + (float)(step - 1) * m->h, s);
-    if (step % m->save_every == 0) {
-      ++k_saved;
-      for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];
+  const int n = state_dim(m), S = m->n_save, euler = m->solver == 2;
+  const float t_end = ts[S - 1], dt0 = m->h;
+  float y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  for (int i = 0; i < n; ++i) y[i] = s0[i];
+  float prev = cond_fn(m, y);
+  int k = 0, steps = 0;
+  float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
+  while (t < t_end && (m->max_steps <= 0 || steps < m->max_steps)) {
+    const float dt = tn - t;
+    rhs(c, t, y, f0);
+    if (euler) {
+      for (int i = 0; i < n; ++i) y1[i] = y[i] + f0[i] * dt;
+    } else {
+      for (int i = 0; i < n; ++i) { acc[i] = mtgp_rk4_acc(0, 0.0f, f0[i]); f[i] = f0[i]; }
+      for (int st = 1; st <= 3; ++st) {
+        for (int i = 0; i < n; ++i) yi[i] = mtgp_rk4_in(st, y[i], f[i], dt);
+        rhs(c, mtgp_rk4_time(st, t, dt), yi, f);
+        for (int i = 0; i < n; ++i) acc[i] = mtgp_rk4_acc(st, acc[i], f[i]);
+      }
+      for (int i = 0; i < n; ++i) y1[i] = mtgp_rk4_out(y[i], acc[i], dt);
     }
-    const float cur = cond_fn(m, s);
-    if (prev > 0.0f && cur < 0.0f) done = 1;
+    ++steps;
+    while (k < S && ts[k] <= tn) { /* SaveAt(ts) by the dense output */
+      const float th = mtgp_cs_rescale(t, ts[k], tn);
+      for (int i = 0; i < n; ++i)
+        saved[(size_t)k * n + i] = euler ? mtgp_cs_linear(y[i], y1[i], th)
+                                         : mtgp_cs_hermite(y[i], y1[i], f0[i] * dt, f[i] * dt, th);
+      ++k;
+    }
+    for (int i = 0; i < n; ++i) y[i] = y1[i];
+    t = tn;
+    const float cur = cond_fn(m, y);
+    if (prev > 0.0f && cur < 0.0f) break;
     prev = cur;
+    tn = mtgp_cs_next_end(t, dt0, t_end);
   }
-  for (int k = k_saved + 1; k < m->n_save; ++k)
+  for (; k < S; ++k)
     for (int i = 0; i < n; ++i) saved[(size_t)k * n + i] = mtgp_u2f(0x7f800000u);
+  return steps;
+}
+
+/* the number of steps of the fixed-step grid (mtgp_cstep.h) from ts[0] to ts[S-1] */
+int oracle_cs_steps(const float* ts, int S, float dt0) {
+  const float t_end = ts[S - 1];
+  float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
+  int steps = 0;
+  while (t < t_end) {
+    ++steps;
+    t = tn;
+    tn = mtgp_cs_next_end(t, dt0, t_end);
+  }
+  return steps;
 }
 
 /* diffeqsolve(Dopri5(), t0=ts[0], t1=ts[-1], dt0=h, SaveAt(ts), PIDController(rtol, atol, dtmin,
  * dtmax), Event(cond_fn), max_steps, throw=False) -- diffrax restated in the fp32 spec of
  * include/mtgp_dopri5.h (see its header comment for every rule used below). */
-static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float* saved) {
+/* one weighted stage sum: the spec's fma chain (mtgp_dp_term) or, OR_DP_ALT_SUM_LITERAL, separate
+ * products and adds */
+static float dp_sum(const float* w, const float (*f)[OR_MAX_S], int n_terms, int i, int literal) {
+  float acc = 0.0f;
+  int first = 1;
+  for (int j = 0; j < n_terms; ++j) {
+    if (!literal) { acc = mtgp_dp_term(acc, w[j], f[j][i], j == 0); continue; }
+    if (w[j] == 0.0f) continue;
+    const float p = w[j] * f[j][i];
+    acc = first ? p : acc + p;
+    first = 0;
+  }
+  return acc;
+}
+static float dp_apply(float y, float h, float acc, int literal) { return literal ? y + acc * h : MTGP_FMAF(h, acc, y); }
+
+static int solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float* saved) {
   static const float A[7][6] = MTGP_DP_TABLE_A;
   static const float E[7] = MTGP_DP_TABLE_E;
   static const float CM[7] = MTGP_DP_TABLE_CMID;
   const OrModel* m = c->m;
+  const int alt = m->dp_alt, lit = (alt & OR_DP_ALT_SUM_LITERAL) != 0;
   const int n = state_dim(m), S = m->n_save;
+  const int n_err = (alt & OR_DP_ALT_NORM_X) && m->model != 3 ? m->n_var : n;
   const float t_end = ts[S - 1];
   float y[OR_MAX_S], f[7][OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
   for (int i = 0; i < n; ++i) y[i] = s0[i];
-  for (int i = 0; i < n; ++i) saved[i] = y[i];
-  int k = 1, steps = 0;
+  int k = 1, steps = 0, accepted = 0;
+  if (alt & OR_DP_ALT_INTERP_T0) k = 0;
+  else for (int i = 0; i < n; ++i) saved[i] = y[i];
   float t = ts[0];
   float tnext = t + m->h;
   if (tnext > t_end) tnext = t_end;
@@ -374,38 +421,39 @@ static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float
     pid.c1 = m->pid_c1; pid.c2 = m->pid_c2; pid.c3 = m->pid_c3;
     pid.safety = m->pid_safety; pid.factormin = m->pid_factormin; pid.factormax = m->pid_factormax;
   }
+  if (alt & OR_DP_ALT_EO6) pid.c1 = (float)(1.0 / 6.0);
   MtgpDpCtl ctl = {1.0f, 1.0f, 0};
-  while (t < t_end && steps < m->max_steps) {
+  while (t < t_end && ((alt & OR_DP_ALT_MAXSTEPS_ACC) ? accepted : steps) < m->max_steps) {
     const float h = tnext - t;
     for (int st = 1; st <= 6; ++st) {
       for (int i = 0; i < n; ++i) {
-        float acc = 0.0f;
-        for (int j = 0; j < st; ++j) acc = mtgp_dp_term(acc, A[st][j], f[j][i], j == 0);
-        yi[i] = MTGP_FMAF(h, acc, y[i]);
+        yi[i] = dp_apply(y[i], h, dp_sum(A[st], (const float (*)[OR_MAX_S])f, st, i, lit), lit);
         if (st == 6) y1[i] = yi[i];
       }
-      rhs(c, t + mtgp_dp_c(st) * h, yi, f[st]);
+      rhs(c, (st == 6 && (alt & OR_DP_ALT_FSAL_T1)) ? tnext : t + mtgp_dp_c(st) * h, yi, f[st]);
     }
     float msum = 0.0f;
-    for (int i = 0; i < n; ++i) {
-      float acc = 0.0f;
-      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
+    for (int i = 0; i < n_err; ++i) {
+      const float acc = dp_sum(E, (const float (*)[OR_MAX_S])f, 7, i, lit);
       const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], m->rtol, m->atol);
       msum = (i == 0) ? sc * sc : msum + sc * sc;
     }
-    const float ms = msum / (float)n;
+    const float ms = msum / (float)n_err;
     int keep, fail;
+    if (alt & OR_DP_ALT_DTMIN_ATTEMPT) ctl.at_dtmin = m->dtmin > 0.0f && h <= m->dtmin;
     const float dt = mtgp_dp_control(ms, h, m->dtmin, m->dtmax, !m->no_force_dtmin, &pid, &ctl, &keep, &fail);
     ++steps;
     int done = fail; /* dt_min_reached: the solve ends after this attempt */
+    if (!keep && (alt & OR_DP_ALT_EVENT_ALL)) {
+      if (prev > 0.0f && cond_fn(m, y1) < 0.0f) done = 1;
+    }
     if (keep) {
+      ++accepted;
       const float t1 = tnext;
       while (k < S && ts[k] <= t1) { /* SaveAt(ts) by the dense output */
         const float th = (ts[k] - t) / h;
         for (int i = 0; i < n; ++i) {
-          float acc = 0.0f;
-          for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, CM[j], f[j][i], j == 0);
-          const float ymid = MTGP_FMAF(h, acc, y[i]);
+          const float ymid = dp_apply(y[i], h, dp_sum(CM, (const float (*)[OR_MAX_S])f, 7, i, lit), lit);
           saved[(size_t)k * n + i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
         }
         ++k;
@@ -424,6 +472,7 @@ static void solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float
   }
   for (; k < S; ++k)
     for (int i = 0; i < n; ++i) saved[(size_t)k * n + i] = mtgp_u2f(0x7f800000u);
+  return steps;
 }
 
 /* Acrobot.fitness_function (acrobot.py:77-84) on full arrays. */
@@ -518,9 +567,19 @@ static float pairwise_sum(const float* v, int R) {
  *   trajectories in the reference's evaluate_candidate layout, each nullable:
  *   xs[P, R, S, n_var], ys[P, R, S, n_obs], us[P, R, S, n_control], acts[P, R, S, state_size].
  */
+int oracle_eval_ex(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
+                   const int8_t* fn, const OrRollouts* ro, float* fitness, float* rollout_fitness, float* xs,
+                   float* ys, float* us, float* acts, int32_t* steps_out);
 int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
                 const int8_t* fn, const OrRollouts* ro, float* fitness, float* rollout_fitness, float* xs,
                 float* ys, float* us, float* acts) {
+  return oracle_eval_ex(m, pop, P, T, N, n_funcs, var_start, fn, ro, fitness, rollout_fitness, xs, ys, us, acts, NULL);
+}
+
+/* oracle_eval plus the solve's step count per rollout (steps_out [P, R] or NULL; Dopri5: attempts) */
+int oracle_eval_ex(const OrModel* m, const float* pop, int P, int T, int N, int n_funcs, int var_start,
+                   const int8_t* fn, const OrRollouts* ro, float* fitness, float* rollout_fitness, float* xs,
+                   float* ys, float* us, float* acts, int32_t* steps_out) {
   if (N > OR_MAX_N || state_dim(m) > OR_MAX_S || ro->R > 65536) return -1;
   const int R = ro->R, S = m->n_save, dim = state_dim(m);
 #pragma omp parallel for schedule(dynamic, 1)
@@ -545,8 +604,8 @@ int oracle_eval(const OrModel* m, const float* pop, int P, int T, int N, int n_f
       for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
       c.key = ro->obs_keys ? ro->obs_keys + 2 * (size_t)r : NULL;
       c.W = ro->obs_w;
-      if (m->solver == 1) solve_dopri5(&c, ro->ts, s0, saved);
-      else solve(&c, ro->ts[0], s0, saved);
+      const int nst = m->solver == 1 ? solve_dopri5(&c, ro->ts, s0, saved) : solve_fixed(&c, ro->ts, s0, saved);
+      if (steps_out) steps_out[(size_t)p * R + r] = nst;
       float f;
       const size_t base = ((size_t)p * R + r) * S;
       if (m->model == 3) {
@@ -767,70 +826,99 @@ static ODual tree_eval_dual(const float* tree, int N, const OrLib* lib, const OD
   return val[N - 1];
 }
 
-/* one rollout of one candidate: F = MSE and dF/dtheta (theta at tree pt, row pi; pt < 0: none) */
+/* solve_fixed in dual numbers: the value half is solve_fixed bit for bit, the tangent half applies
+ * the same linear maps (stage sums, step update, the dense output at the primal theta) to the
+ * tangents; the step grid and the event are primal.  The state has n = state_dim(m) components;
+ * rhs(ctx, t, s, ds) is the model's dual RHS.  saved[k * n + i] for k < the returned count (the
+ * first unsaved save index). */
+typedef void (*OrDualRhs)(const void* ctx, float t, const ODual* s, ODual* ds);
+
+static int fixed_dual(const OrModel* m, const float* ts, const ODual* s0, OrDualRhs rhs, const void* ctx,
+                      ODual* saved) {
+  const int n = state_dim(m), S = m->n_save, euler = m->solver == 2;
+  const float t_end = ts[S - 1], dt0 = m->h;
+  ODual y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  float sv[OR_MAX_S];
+  for (int i = 0; i < n; ++i) { y[i] = s0[i]; sv[i] = y[i].v; }
+  float prev = cond_fn(m, sv);
+  int k = 0, steps = 0;
+  float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
+  while (t < t_end && (m->max_steps <= 0 || steps < m->max_steps)) {
+    const float dt = tn - t;
+    rhs(ctx, t, y, f0);
+    if (euler) {
+      for (int i = 0; i < n; ++i) y1[i] = od(y[i].v + f0[i].v * dt, y[i].d + f0[i].d * dt);
+    } else {
+      for (int i = 0; i < n; ++i) {
+        acc[i] = od(mtgp_rk4_acc(0, 0.0f, f0[i].v), mtgp_rk4_acc(0, 0.0f, f0[i].d));
+        f[i] = f0[i];
+      }
+      for (int st = 1; st <= 3; ++st) {
+        for (int i = 0; i < n; ++i)
+          yi[i] = od(mtgp_rk4_in(st, y[i].v, f[i].v, dt), mtgp_rk4_in(st, y[i].d, f[i].d, dt));
+        rhs(ctx, mtgp_rk4_time(st, t, dt), yi, f);
+        for (int i = 0; i < n; ++i) acc[i] = od(mtgp_rk4_acc(st, acc[i].v, f[i].v), mtgp_rk4_acc(st, acc[i].d, f[i].d));
+      }
+      for (int i = 0; i < n; ++i) y1[i] = od(mtgp_rk4_out(y[i].v, acc[i].v, dt), mtgp_rk4_out(y[i].d, acc[i].d, dt));
+    }
+    ++steps;
+    while (k < S && ts[k] <= tn) {
+      const float th = mtgp_cs_rescale(t, ts[k], tn);
+      for (int i = 0; i < n; ++i)
+        saved[(size_t)k * n + i] =
+            euler ? od(mtgp_cs_linear(y[i].v, y1[i].v, th), mtgp_cs_linear(y[i].d, y1[i].d, th))
+                  : od(mtgp_cs_hermite(y[i].v, y1[i].v, f0[i].v * dt, f[i].v * dt, th),
+                       mtgp_cs_hermite(y[i].d, y1[i].d, f0[i].d * dt, f[i].d * dt, th));
+      ++k;
+    }
+    for (int i = 0; i < n; ++i) { y[i] = y1[i]; sv[i] = y[i].v; }
+    t = tn;
+    const float cur = cond_fn(m, sv);
+    if (prev > 0.0f && cur < 0.0f) break;
+    prev = cur;
+    tn = mtgp_cs_next_end(t, dt0, t_end);
+  }
+  return k;
+}
+
+typedef struct {
+  const float* cand;
+  int N, nv, pt, pi;
+  const OrLib* lib;
+} OrSrDualCtx;
+
+/* sr.py:85-88 in duals */
+static void sr_rhs_dual(const void* ctx, float t, const ODual* s, ODual* ds) {
+  const OrSrDualCtx* c = (const OrSrDualCtx*)ctx;
+  (void)t;
+  for (int q = 0; q < c->nv; ++q)
+    ds[q] = tree_eval_dual(c->cand + (size_t)q * c->N * 4, c->N, c->lib, s, c->nv, q == c->pt ? c->pi : -1);
+}
+
+/* one rollout of one candidate: F = MSE and dF/dtheta (theta at tree pt, row pi; pt < 0: none) --
+ * the fixed-step solve (fixed_dual), the MSE of the saved points (sr.py:24) in duals */
 static ODual sr_rollout_dual(const OrModel* m, const float* cand, int N, const OrLib* lib, const OrRollouts* ro, int r,
                              int pt, int pi) {
   const int nv = m->n_var, S = m->n_save;
-  ODual s[OR_MAX_S], k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
-  for (int i = 0; i < nv; ++i) s[i] = od(ro->x0[(size_t)r * nv + i], 0.0f);
-  const float h = m->h, h2 = h * 0.5f, h6 = h / 6.0f;
+  ODual s0[OR_MAX_S];
+  for (int i = 0; i < nv; ++i) s0[i] = od(ro->x0[(size_t)r * nv + i], 0.0f);
+  const OrSrDualCtx ctx = {cand, N, nv, pt, pi, lib};
+  ODual* saved = (ODual*)malloc(sizeof(ODual) * (size_t)S * nv);
+  const int ks = fixed_dual(m, ro->ts, s0, sr_rhs_dual, &ctx, saved);
   ODual tot = od(0.0f, 0.0f);
-  int bad_prev = 0;
-  for (int i = 0; i < nv; ++i) bad_prev |= !mtgp_isfinite(s[i].v);
-  int k_saved = 0, done = 0;
-#define OR_SR_RHS(in, out)                                                                          \
-  for (int q = 0; q < nv; ++q)                                                                      \
-    out[q] = tree_eval_dual(cand + (size_t)q * N * 4, N, lib, in, nv, q == pt ? pi : -1);
-#define OR_MSE_TERM(kk)                                                                             \
-  {                                                                                                 \
-    ODual sq = od(0.0f, 0.0f);                                                                      \
-    for (int dd = 0; dd < nv; ++dd) {                                                               \
-      const float e = s[dd].v - ro->ys_true[((size_t)r * S + (kk)) * nv + dd];                     \
-      const float de = s[dd].d * (2.0f * e);                                                        \
-      sq = dd == 0 ? od(e * e, de) : od(sq.v + e * e, sq.d + de);                                   \
-    }                                                                                               \
-    tot = od(tot.v + sq.v, tot.d + sq.d);                                                           \
-  }
-  OR_MSE_TERM(0)
-  for (int step = 1; step <= m->n_steps && !done; ++step) {
-    if (m->solver == 2) { /* Euler: y + f h */
-      OR_SR_RHS(s, k)
-      for (int i = 0; i < nv; ++i) s[i] = od(s[i].v + k[i].v * h, s[i].d + k[i].d * h);
-    } else { /* rk4_step's fma form, tangents by the same linear maps */
-      OR_SR_RHS(s, k)
-      for (int i = 0; i < nv; ++i) {
-        acc[i] = k[i];
-        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
-      }
-      OR_SR_RHS(tmp, k)
-      for (int i = 0; i < nv; ++i) {
-        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
-        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
-      }
-      OR_SR_RHS(tmp, k)
-      for (int i = 0; i < nv; ++i) {
-        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
-        tmp[i] = od(MTGP_FMAF(h, k[i].v, s[i].v), MTGP_FMAF(h, k[i].d, s[i].d));
-      }
-      OR_SR_RHS(tmp, k)
-      for (int i = 0; i < nv; ++i) {
-        acc[i] = od(acc[i].v + k[i].v, acc[i].d + k[i].d);
-        s[i] = od(MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d));
-      }
+  for (int kk = 0; kk < ks; ++kk) {
+    ODual sq = od(0.0f, 0.0f);
+    for (int dd = 0; dd < nv; ++dd) {
+      const ODual sv = saved[(size_t)kk * nv + dd];
+      const float e = sv.v - ro->ys_true[((size_t)r * S + kk) * nv + dd];
+      const float de = sv.d * (2.0f * e);
+      sq = dd == 0 ? od(e * e, de) : od(sq.v + e * e, sq.d + de);
     }
-    if (step % m->save_every == 0) {
-      ++k_saved;
-      OR_MSE_TERM(k_saved)
-    }
-    int bad = 0;
-    for (int i = 0; i < nv; ++i) bad |= !mtgp_isfinite(s[i].v);
-    if (!bad_prev && bad) done = 1; /* the NaN event (sr.py:93-94) */
-    bad_prev = bad;
+    tot = od(tot.v + sq.v, tot.d + sq.d);
   }
-#undef OR_SR_RHS
-#undef OR_MSE_TERM
+  free(saved);
   /* points after the event are +inf: the squared error is +inf (NaN stays NaN) */
-  if (k_saved + 1 < S && mtgp_isfinite(tot.v)) tot.v = mtgp_u2f(0x7f800000u);
+  if (ks < S && mtgp_isfinite(tot.v)) tot.v = mtgp_u2f(0x7f800000u);
   return od(tot.v / (float)S, tot.d / (float)S);
 }
 
@@ -1061,6 +1149,15 @@ static void ctl_rhs_dual(const OrCtx* c, float t, const ODual* s, ODual* ds, int
   }
 }
 
+typedef struct {
+  const OrCtx* c;
+  int pt, pi;
+} OrCtlDualCtx;
+static void ctl_rhs_dual_cb(const void* ctx, float t, const ODual* s, ODual* ds) {
+  const OrCtlDualCtx* x = (const OrCtlDualCtx*)ctx;
+  ctl_rhs_dual(x->c, t, s, ds, x->pt, x->pi);
+}
+
 /* solve_dopri5 of the control models in dual numbers (the coupled [x, a] state, ctl_rhs_dual at
  * the stage times t + c_i h), the step sizes, accept / reject decisions and the event held at
  * their primal values (as sr_rollout_dual_dp): saved[0..k) the dense-output save points; returns
@@ -1153,52 +1250,17 @@ static ODual ctl_rollout_dual(const OrCtx* c, const OrRollouts* ro, int r, int p
   const OrModel* m = c->m;
   const int n = state_dim(m), nv = m->n_var, S = m->n_save;
   ODual* saved = (ODual*)malloc(sizeof(ODual) * (size_t)S * n);
-  ODual s[OR_MAX_S], k[OR_MAX_S], acc[OR_MAX_S], tmp[OR_MAX_S];
+  ODual s[OR_MAX_S];
   for (int i = 0; i < n; ++i) s[i] = od(i < nv ? ro->x0[(size_t)r * nv + i] : 0.0f, 0.0f);
-  for (int i = 0; i < n; ++i) saved[i] = s[i];
-  float sv[OR_MAX_S];
-  for (int i = 0; i < n; ++i) sv[i] = s[i].v;
-  float prev = cond_fn(m, sv);
-  const float h = m->h, h2 = h * 0.5f, h6 = h / 6.0f, t0 = ro->ts[0];
-  int k_saved = 0, done = 0;
-  if (m->solver == 1) k_saved = ctl_dopri5_dual(c, ro, s, saved, pt, pi) - 1;
-  for (int step = 1; m->solver != 1 && step <= m->n_steps && !done; ++step) {
-    const float t = t0 + (float)(step - 1) * h;
-    if (m->solver == 2) {
-      ctl_rhs_dual(c, t, s, k, pt, pi);
-      for (int i = 0; i < n; ++i) s[i] = od(s[i].v + k[i].v * h, s[i].d + k[i].d * h);
-    } else {
-      ctl_rhs_dual(c, t, s, k, pt, pi);
-      for (int i = 0; i < n; ++i) {
-        acc[i] = k[i];
-        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
-      }
-      ctl_rhs_dual(c, t + h2, tmp, k, pt, pi);
-      for (int i = 0; i < n; ++i) {
-        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
-        tmp[i] = od(MTGP_FMAF(h2, k[i].v, s[i].v), MTGP_FMAF(h2, k[i].d, s[i].d));
-      }
-      ctl_rhs_dual(c, t + h2, tmp, k, pt, pi);
-      for (int i = 0; i < n; ++i) {
-        acc[i] = od(MTGP_FMAF(2.0f, k[i].v, acc[i].v), MTGP_FMAF(2.0f, k[i].d, acc[i].d));
-        tmp[i] = od(MTGP_FMAF(h, k[i].v, s[i].v), MTGP_FMAF(h, k[i].d, s[i].d));
-      }
-      ctl_rhs_dual(c, t + h, tmp, k, pt, pi);
-      for (int i = 0; i < n; ++i) {
-        acc[i] = od(acc[i].v + k[i].v, acc[i].d + k[i].d);
-        s[i] = od(MTGP_FMAF(h6, acc[i].v, s[i].v), MTGP_FMAF(h6, acc[i].d, s[i].d));
-      }
-    }
-    if (step % m->save_every == 0) {
-      ++k_saved;
-      for (int i = 0; i < n; ++i) saved[(size_t)k_saved * n + i] = s[i];
-    }
-    for (int i = 0; i < n; ++i) sv[i] = s[i].v;
-    const float cur = cond_fn(m, sv);
-    if (prev > 0.0f && cur < 0.0f) done = 1;
-    prev = cur;
+  int ks;
+  if (m->solver == 1) {
+    for (int i = 0; i < n; ++i) saved[i] = s[i];
+    ks = ctl_dopri5_dual(c, ro, s, saved, pt, pi);
+  } else {
+    const OrCtlDualCtx ctx = {c, pt, pi};
+    ks = fixed_dual(m, ro->ts, s, ctl_rhs_dual_cb, &ctx, saved);
   }
-  for (int q = k_saved + 1; q < S; ++q)  /* the +inf fill after the event: constants, no tangent */
+  for (int q = ks; q < S; ++q)  /* the +inf fill after the event: constants, no tangent */
     for (int i = 0; i < n; ++i) saved[(size_t)q * n + i] = od(mtgp_u2f(0x7f800000u), 0.0f);
   /* controls at the save points (dyn.py:99-101 / ff.py:96-97) */
   ODual* us = (ODual*)malloc(sizeof(ODual) * (size_t)S);

@@ -18,7 +18,8 @@ LIB = os.path.join(HERE, "build", "libmtgp_oracle.so")
 def build(force: bool = False) -> str:
     src = [os.path.join(HERE, "mtgp_oracle.c"), os.path.join(HERE, "..", "include", "mtgp_f32math.h"),
            os.path.join(HERE, "..", "include", "mtgp_prng.h"),
-           os.path.join(HERE, "..", "include", "mtgp_dopri5.h"), os.path.join(HERE, "..", "include", "mtgp_dual.h")]
+           os.path.join(HERE, "..", "include", "mtgp_dopri5.h"), os.path.join(HERE, "..", "include", "mtgp_dual.h"),
+           os.path.join(HERE, "..", "include", "mtgp_cstep.h")]
     if force or not os.path.exists(LIB) or any(os.path.getmtime(s) > os.path.getmtime(LIB) for s in src):
         subprocess.run(["make", "-C", HERE, "-B" if force else "all"], check=True,
                        stdout=subprocess.DEVNULL)
@@ -35,11 +36,12 @@ class OrModel(ctypes.Structure):
                 ("atol", ctypes.c_float), ("dtmin", ctypes.c_float), ("dtmax", ctypes.c_float),
                 ("pid_custom", ctypes.c_int32), ("pid_c1", ctypes.c_float), ("pid_c2", ctypes.c_float),
                 ("pid_c3", ctypes.c_float), ("pid_safety", ctypes.c_float), ("pid_factormin", ctypes.c_float),
-                ("pid_factormax", ctypes.c_float), ("no_force_dtmin", ctypes.c_int32)]
+                ("pid_factormax", ctypes.c_float), ("no_force_dtmin", ctypes.c_int32),
+                ("dp_alt", ctypes.c_int32)]  # oracle-only alternative Dopri5 readings (OR_DP_ALT_*)
 
 _MODEL_DEFAULTS = dict(prng_impl=0, env=0, solver=0, max_steps=0, rtol=0.0, atol=0.0, dtmin=0.0, dtmax=0.0,
                        pid_custom=0, pid_c1=0.0, pid_c2=0.0, pid_c3=0.0, pid_safety=0.0, pid_factormin=0.0,
-                       pid_factormax=0.0, no_force_dtmin=0)
+                       pid_factormax=0.0, no_force_dtmin=0, dp_alt=0)
 
 
 class OrRollouts(ctypes.Structure):
@@ -63,6 +65,8 @@ def lib():
                                   ctypes.c_int, ctypes.c_int, vp, ctypes.POINTER(OrRollouts), vp, vp, vp, vp, vp,
                                   vp]
         L.oracle_eval.restype = ctypes.c_int
+        L.oracle_eval_ex.argtypes = L.oracle_eval.argtypes + [vp]
+        L.oracle_eval_ex.restype = ctypes.c_int
         L.oracle_sincos.argtypes = [vp, vp, vp, ctypes.c_long]
         L.oracle_wrap.argtypes = [vp, vp, ctypes.c_long]
         L.oracle_unary.argtypes = [ctypes.c_int, vp, vp, vp, vp, ctypes.c_long]
@@ -87,6 +91,8 @@ def lib():
         L.oracle_sr_grad.restype = ctypes.c_int
         L.oracle_ctl_grad.argtypes = L.oracle_sr_grad.argtypes
         L.oracle_ctl_grad.restype = ctypes.c_int
+        L.oracle_cs_steps.argtypes = [vp, ctypes.c_int, ctypes.c_float]
+        L.oracle_cs_steps.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -134,14 +140,15 @@ def wrap(x: np.ndarray):
     return o
 
 
-def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories: bool = False):
+def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories: bool = False, steps: bool = False):
     """Evaluate a flat population [P, T, N, 4].
 
     model: dict(model, n_var, state_size, n_obs, n_control, n_targets, n_steps, save_every, n_save,
                 h, max_fitness, parsimony[, prng_impl])
     rollouts: dict(x0 [R, n_var], params [R, 4] or None, targets [R, nt] or None, ts [S],
                    ys_true [R, S, n_var] or None[, obs_keys uint32 [R, 2], obs_w [n_obs, n_obs]])
-    Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c])."""
+    Returns dict(fitness [P], rollout_fitness [P, R], xs/ys/us/acts [P, R, S, c][, steps [P, R]: the solve's
+    step count, Dopri5 attempts])."""
     pop = np.ascontiguousarray(pop, np.float32)
     P, T, N, _ = pop.shape
     m = OrModel(**{k: model.get(k, _MODEL_DEFAULTS[k]) if k in _MODEL_DEFAULTS else model[k]
@@ -178,8 +185,11 @@ def evaluate(model: dict, pop: np.ndarray, library, rollouts: dict, trajectories
             if b is not None:
                 out[k] = b
     fn = np.ascontiguousarray(library.fn_codes, np.int8)
-    rc = lib().oracle_eval(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
-                           ctypes.byref(ro), _p(fit), _p(rf), *[_p(b) for b in bufs])
+    st = np.zeros((P, R), np.int32) if steps else None
+    rc = lib().oracle_eval_ex(ctypes.byref(m), _p(pop), P, T, N, library.n_funcs, library.var_start, _p(fn),
+                              ctypes.byref(ro), _p(fit), _p(rf), *[_p(b) for b in bufs], _p(st))
+    if steps:
+        out["steps"] = st
     if rc != 0:
         raise RuntimeError(f"oracle_eval failed {rc}")
     return out
@@ -268,6 +278,12 @@ def log1p(x):
     o = np.empty_like(x)
     lib().oracle_log1p(_p(x), _p(o), x.size)
     return o
+
+
+def cs_steps(ts, dt0) -> int:
+    """Steps of diffrax's ConstantStepSize grid from ts[0] to ts[-1] (include/mtgp_cstep.h)."""
+    ts = np.ascontiguousarray(ts, np.float32)
+    return int(lib().oracle_cs_steps(_p(ts), ts.shape[0], ctypes.c_float(dt0)))
 
 
 def pairwise_sum(v):

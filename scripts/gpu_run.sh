@@ -41,6 +41,7 @@ pmcic() {  # name config: one pass of instruction-cache counters over kprof (2 e
 }
 for step in "$@"; do
   case $step in
+    testall) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread || exit 1 ;;
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmask) run pytest_mask 600 python -u -m pytest tests/test_gpu_acrobot_mask.py tests/test_gpu_parity.py tests/test_dopri5.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmaskonly) run pytest_maskonly 300 python -u -m pytest tests/test_gpu_acrobot_mask.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;

@@ -123,6 +123,75 @@ def rk4_t(rhs, s0, t0, h, n):
     return np.array(out)
 
 
+def cs_grid(ts, dt0, max_steps=None):
+    """diffrax.ConstantStepSize's step grid through diffeqsolve(t0=ts[0], t1=ts[-1], dt0), written
+    from diffrax's published loop: float32 times, t += dt0 accumulated, the first end
+    min(t0 + dt0, t1), later ends clipped to t1 when > t1 - 1e-6 (_clip_to_end).
+    -> list of (t, tn) float32 pairs."""
+    f = np.float32
+    ts = np.asarray(ts, f)
+    t, t1, dt0 = f(ts[0]), f(ts[-1]), f(dt0)
+    tn = min(f(t + dt0), t1)
+    out = []
+    while t < t1 and (max_steps is None or len(out) < max_steps):
+        out.append((t, tn))
+        t = tn
+        tn = f(t + dt0)
+        if tn > f(t1 - f(1e-6)):
+            tn = t1
+    return out
+
+
+def cs_solve(rhs, s0, ts, dt0, solver="rk4", dtype=np.float64, event=None):
+    """diffeqsolve(solver, ConstantStepSize, SaveAt(ts)) restated from diffrax's text (the time grid
+    of cs_grid, stage times t + c dt, increments (sum a f) dt, every ts[k] through the dense output:
+    Euler linear, RK4 the cubic Hermite from the first and last stage increments).  dtype float64
+    (semantics, to a tolerance) or float32 (literal rounding: every product / sum rounded in the
+    order written).  rhs(t, s) -> ds.  event(s) -> True terminates after the step (its saves kept).
+    -> saved [len(ts), n] (+inf after termination)."""
+    d = dtype
+    ts = np.asarray(ts, np.float32)
+    S = ts.shape[0]
+    y = np.array(s0, d)
+    saved = np.full((S, y.shape[0]), np.inf, d)
+    k = 0
+    b0, b1 = d(1.0 / 6.0), d(1.0 / 3.0)
+    with np.errstate(all="ignore"):
+        for t, tn in cs_grid(ts, dt0):
+            dtf = np.float32(tn - t)  # the step (float32 times: the stage times key the noise)
+            dt = d(dtf)
+            f0 = np.asarray(rhs(t, y), d)
+            if solver == "euler":
+                y1 = y + f0 * dt
+            else:
+                f1 = np.asarray(rhs(np.float32(t + np.float32(0.5) * dtf), y + (d(0.5) * f0) * dt), d)
+                f2 = np.asarray(rhs(np.float32(t + np.float32(0.5) * dtf), y + (d(0.5) * f1) * dt), d)
+                f3 = np.asarray(rhs(np.float32(t + dtf), y + f2 * dt), d)
+                y1 = y + (((b0 * f0 + b1 * f1) + b1 * f2) + b0 * f3) * dt
+            while k < S and ts[k] <= tn:
+                if t == tn:
+                    th = d(0.0)
+                elif d is np.float32:
+                    th = np.float32(np.float32(ts[k] - t) / np.float32(tn - t))
+                else:
+                    th = (d(ts[k]) - d(t)) / (d(tn) - d(t))
+                if solver == "euler":
+                    saved[k] = y + th * (y1 - y)
+                else:
+                    k0, k1 = f0 * dt, f3 * dt
+                    a = ((k0 + k1) + d(2) * y) - d(2) * y1
+                    b = (((d(-2) * k0) - k1) - d(3) * y) + d(3) * y1
+                    v = d(0) * th + a
+                    v = v * th + b
+                    v = v * th + k0
+                    saved[k] = v * th + y
+                k += 1
+            y = y1
+            if event is not None and event(y):
+                break
+    return saved
+
+
 def rk4(rhs, s0, h, n):
     s = np.array(s0, np.float64)
     out = [s.copy()]

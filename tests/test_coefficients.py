@@ -14,6 +14,7 @@ import pytest
 
 import multitreegp_amd as mt
 from multitreegp_amd import coefficients as co
+import np_reference as npr
 from oracle import oracle as orc
 
 from helpers import SR_OPS, bits_equal, mismatch_report, oracle_model, oracle_rollouts, sr_setup, tree_from_expr
@@ -54,28 +55,16 @@ def _sr_loss_c(cand, lib, d, prow_t, prow_i, eps=1e-30, euler=False):
     """SR_evaluator.__call__ (sr.py:30-45) over complex numbers: RK4 / Euler, MSE, NaN -> max, mean, clip."""
     x0, ys = d["x0"].astype(np.float64), np.transpose(d["ys_true"], (2, 0, 1)).astype(np.float64)  # [R, S, nv]
     R, nv = x0.shape
-    h, se, n = float(np.float32(d["h"])), d["save_every"], d["n_steps"]
+    h, ts = float(np.float32(d["h"])), d["ts"]
 
-    def rhs(s):
+    def rhs(t, s):
         return np.array([_eval_tree_c(cand[q], lib, s, prow_i if q == prow_t else -1, eps) for q in range(nv)])
 
     fits = []
     with np.errstate(all="ignore"):
-        for r in range(R):
-            s = x0[r].astype(np.complex128)
-            tot = np.sum((s - ys[r, 0]) ** 2)
-            for step in range(1, n + 1):
-                if euler:
-                    s = s + rhs(s) * h
-                else:
-                    k1 = rhs(s)
-                    k2 = rhs(s + 0.5 * h * k1)
-                    k3 = rhs(s + 0.5 * h * k2)
-                    k4 = rhs(s + h * k3)
-                    s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
-                if step % se == 0:
-                    tot = tot + np.sum((s - ys[r, step // se]) ** 2)
-            f = tot / (n // se + 1)
+        for r in range(R):  # diffrax ConstantStepSize + SaveAt(ts) (np_reference.cs_solve) over complex numbers
+            saved = npr.cs_solve(rhs, x0[r].astype(np.complex128), ts, h, "euler" if euler else "rk4", np.complex128)
+            f = np.sum((saved - ys[r]) ** 2) / ts.shape[0]
             fits.append(f if np.isfinite(f.real) else complex(1e5))
     m = np.mean(fits)
     return m if 0 < m.real < 1e5 else complex(np.clip(m.real, 0, 1e5))
@@ -504,7 +493,7 @@ def _ctl_loss_c(cand, lib, ff, d, prow_t, prow_i, eps=1e-30):
     na = ff.state_size if dyn else 0
     no = ff.env.n_obs
     ts = d["ts"].astype(np.float32)
-    h, se, n, S = float(np.float32(ff.dt0)), d["save_every"], d["n_steps"], d["n_save"]
+    h, S = float(np.float32(ff.dt0)), d["n_save"]
     solver = d.get("solver", 0)
 
     def tree(q, data):
@@ -564,26 +553,16 @@ def _ctl_loss_c(cand, lib, ff, d, prow_t, prow_i, eps=1e-30):
     with np.errstate(all="ignore"):
         for r in range(R):
             s = np.concatenate([x0[r], np.zeros(na)]).astype(np.complex128)
-            saved = [s.copy()]
-            prev_ok, done = not bad(s), False
-            for step in range(1, n + 1):
-                if done:
-                    break
-                if solver == 2:
-                    s = s + rhs(s, r) * h
-                else:
-                    k1 = rhs(s, r)
-                    k2 = rhs(s + 0.5 * h * k1, r)
-                    k3 = rhs(s + 0.5 * h * k2, r)
-                    k4 = rhs(s + h * k3, r)
-                    s = s + h / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
-                if step % se == 0:
-                    saved.append(s.copy())
-                ok = not bad(s)
-                done = prev_ok and not ok
-                prev_ok = ok
-            while len(saved) < S:
-                saved.append(np.full(nv + na, np.inf, np.complex128))
+            ev = {"prev_ok": not bad(s)}
+
+            def event(y):  # Event(cond_fn_nan): the condition turns negative after a step
+                ok = not bad(y)
+                fire = ev["prev_ok"] and not ok
+                ev["prev_ok"] = ok
+                return fire
+            # diffrax ConstantStepSize + SaveAt(ts) (np_reference.cs_solve) over complex numbers; +inf fill
+            saved = list(npr.cs_solve(lambda t, y: rhs(y, r), s, ts, h, "euler" if solver == 2 else "rk4",
+                                      np.complex128, event=event))
             us = []
             for sk in saved:
                 y = obs(sk[:nv])

@@ -3,7 +3,7 @@ import numpy as np
 import pytest
 
 import multitreegp_amd as mt
-from multitreegp_amd.evaluators import rk4_schedule
+from multitreegp_amd.evaluators import constant_step_grid, fixed_schedule
 
 
 class Dopri5:  # stand-in with diffrax's class name
@@ -11,8 +11,10 @@ class Dopri5:  # stand-in with diffrax's class name
 
 
 def test_notebook_schedule():
-    ts = np.arange(0, 50, 0.2, dtype=np.float32)  # DynamicPolicy.ipynb get_data
-    assert rk4_schedule(ts, 0.05, 1000) == (996, 4, 250)
+    """The notebook grid with dt0 0.05 (DynamicPolicy.ipynb get_data): diffrax's accumulated
+    ConstantStepSize grid to t1 = 49.8 takes 997 steps (nominally 996), save points straight from ts."""
+    ts = np.arange(0, 50, 0.2, dtype=np.float32)
+    assert fixed_schedule(ts, 0.05, 16 ** 4) == (997, 1, 250)
 
 
 def test_rejects_adaptive_solver():
@@ -43,14 +45,19 @@ def test_obs_noise_data_preparation():
     assert "obs_keys" not in mt.DynamicEvaluator(mt.Acrobot(0.05, 0.0), 2, 0.05).prepare(data)
 
 
-def test_schedule_errors():
+def test_schedule_any_grid():
+    """ABI v18: any non-decreasing ts (SaveAt(ts) through the dense output); max_steps caps the grid
+    (the solve then ends early with +inf saves instead of raising)."""
+    assert fixed_schedule(np.array([0.0, 0.07, 0.14], np.float32), 0.05, 100) == (3, 1, 3)  # off the step grid
+    assert fixed_schedule(np.array([0.0, 0.1, 0.3], np.float32), 0.05, 100) == (6, 1, 3)    # non-uniform
+    assert fixed_schedule(np.arange(0, 10, 0.1, dtype=np.float32), 0.05, 10) == (10, 1, 100)  # max_steps
+    assert fixed_schedule(np.array([5.0, 5.1, 5.2], np.float32), 0.05, 100)[::2] == (4, 3)    # offset start
+    g = constant_step_grid(np.array([5.0, 5.2], np.float32), 0.05)
+    assert g[0] == np.float32(5.0) and g[-1] == np.float32(5.2) and len(g) == 5
     with pytest.raises(ValueError):
-        rk4_schedule(np.array([0.0, 0.07, 0.14], np.float32), 0.05, 100)  # not a multiple of dt0
+        fixed_schedule(np.array([0.0, 0.2, 0.1], np.float32), 0.05, 100)  # decreasing
     with pytest.raises(ValueError):
-        rk4_schedule(np.array([0.0, 0.1, 0.3], np.float32), 0.05, 100)  # non-uniform
-    with pytest.raises(ValueError):
-        rk4_schedule(np.arange(0, 10, 0.1, dtype=np.float32), 0.05, 10)  # max_steps
-    assert rk4_schedule(np.array([5.0, 5.1, 5.2], np.float32), 0.05, 100) == (4, 2, 3)  # offset start
+        fixed_schedule(np.array([0.0], np.float32), 0.05, 100)  # one point
 
 
 @pytest.mark.parametrize("t0,dt,S", [(0.0, 0.2, 250), (5.0, 0.1, 40), (0.05, 0.1, 30), (-0.35, 0.05, 50),
@@ -129,7 +136,7 @@ def test_default_solver_is_the_reference_euler():
 
 
 def test_oracle_euler_known_answer():
-    """dx/dt = -x (tree 0 - x0), Euler: x_{n+1} = x_n + (-x_n) * h in float32, saved every step."""
+    """dx/dt = -x (tree 0 - x0), Euler: x_{n+1} = x_n + (-x_n) * dt in float32 on diffrax's grid."""
     from helpers import SR_OPS, oracle_model, oracle_rollouts
     from oracle import oracle as orc
     lib = mt.NodeLibrary(SR_OPS, [["x0"]], [1])
@@ -145,9 +152,11 @@ def test_oracle_euler_known_answer():
     ff = mt.SREvaluator(dt0=0.05)
     d = ff.prepare((x0, ts, np.zeros((2, 21, 1), np.float32), None))
     out = orc.evaluate(oracle_model(ff, d), cand, lib, oracle_rollouts(d), trajectories=True)
-    want = np.empty((2, 21), np.float32)
-    x = x0[:, 0].copy()
-    for k in range(21):
-        want[:, k] = x
-        x = (x + (np.float32(0.0) - x) * h).astype(np.float32)
-    assert np.array_equal(out["xs"][0, :, :, 0].view(np.uint32), want.view(np.uint32))
+    # diffrax ConstantStepSize (ABI v18): x1 = x + (0 - x) * dt over the accumulated f32 grid, each
+    # ts[k] through LocalLinearInterpolation -- literal float32 (np_reference.cs_solve)
+    import np_reference as npr
+    for r in range(2):
+        want = npr.cs_solve(lambda t, s: np.float32(0.0) - s, x0[r], ts, 0.05, "euler", np.float32)[:, 0]
+        assert np.array_equal(out["xs"][0, r, :, 0].view(np.uint32), want.view(np.uint32))
+    # and the textbook closed form of Euler's recursion within the grid's rounding
+    assert np.allclose(out["xs"][0, 0, :, 0], (1.0 - 0.05) ** np.arange(21), rtol=1e-5)

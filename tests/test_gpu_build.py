@@ -221,7 +221,8 @@ def test_chained_units_match_host_units(R):
     m.model, m.state_size, m.n_var, m.solver = nat.MODEL_ACROBOT_DYNAMIC, 2, 4, nat.SOLVER_RK4
     m.prog_state, m.prog_readout, m.prog_readout_save, m.readout_save_same = 1, 0, 3, -1
     ch = nat.MtgpJitChain()
-    assert L_.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0 and ch.next == 0b110
+    assert L_.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0 and ch.next == 0b010
+    ch.next, ch.cond = 0b110, 0b100  # the ABI v13 form with the conditional save continuation (emitter test)
     order_np = np.random.default_rng(R).permutation(P).astype(np.int32)
     order = torch.from_numpy(order_np).cuda()
     n = L_.mtgp_jit_units(P, n_prog, R)
@@ -260,7 +261,7 @@ def test_chained_units_match_host_units(R):
 def test_chained_and_unchained_evaluations_agree():
     """The same population evaluated with chained JIT code, one-call-per-program JIT code
     (MTGP_JIT_CHAIN=0) and the interpreter: bit-identical fitness and trajectories (RK4 dynamic
-    policy with the save-point continuation, SR n_var 2 chain)."""
+    policy, SR n_var 2 chain)."""
     import os
     import torch
     from multitreegp_amd.engine import DeviceEngine

@@ -192,8 +192,9 @@ def test_static_obs_noise_bitexact():
 
 @pytest.mark.parametrize("kind", ["dynamic", "static"])
 def test_obs_noise_save_time_differs_from_step_time(kind):
-    """dt0 = 0.1, save spacing f32(0.3): several ts[k] differ in their bits from the step start
-    t0 + f32(3k) * h, so the save observation is redrawn at ts[k] (dyn.py:99 / ff.py:96)."""
+    """dt0 = 0.1, save spacing f32(0.3): the save times are not step ends of the accumulated grid, so
+    the save state comes from the dense output and its observation is drawn at ts[k] (dyn.py:99 /
+    ff.py:96)."""
     if kind == "dynamic":
         env = mt.Acrobot(0.0, 0.1)
         from helpers import CONTROL_OPS
@@ -214,7 +215,7 @@ def test_obs_noise_save_time_differs_from_step_time(kind):
     assert (ts.view(np.uint32) != tk.view(np.uint32)).sum() > 5
     pop = sample_population(3, lib, 30, 1, max_init_depth=5, max_nodes=30)[0]
     res, ref, d = _run(ff, lib, data, pop)
-    assert d["save_every"] == 3
+    assert d["n_steps"] == orc.cs_steps(ts, 0.1) > 3 * (len(ts) - 1) - 2
     _check(res, ref, pop.shape[0], 16, names)
 
 

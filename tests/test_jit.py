@@ -582,14 +582,15 @@ def _chain_model(kind):
 
 
 def test_chain_masks():
-    """mtgp_jit_chain: the dynamic policy chains its state programs into the save-point readout
-    (conditional), register-resident SR its n_var trees; Dopri5 drops the save continuation,
-    wide SR and static policies have no chain."""
+    """mtgp_jit_chain: the dynamic policy chains its state programs, register-resident SR its n_var
+    trees; wide SR and static policies have no chain.  (ABI v18: no save-point continuation -- the
+    save readout reads the dense-output state, so no solver asks for one; the emitter keeps the
+    conditional form, tested below with an explicit chain.)"""
     lib_n = nat.load()
     ch = nat.MtgpJitChain()
     m = _chain_model("dynamic")
     assert lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch)) == 0
-    assert (ch.next, ch.cond) == (0b110, 0b100)
+    assert (ch.next, ch.cond) == (0b010, 0)
     m.solver = nat.SOLVER_DOPRI5
     lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch))
     assert (ch.next, ch.cond) == (0b010, 0)
@@ -624,6 +625,8 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
     lib_n = nat.load()
     ch = nat.MtgpJitChain()
     lib_n.mtgp_jit_chain(ctypes.byref(_chain_model(kind)), n_prog, ctypes.byref(ch))
+    if kind == "dynamic":  # the conditional continuation into the save-point readout (ABI v13 form)
+        ch.next, ch.cond = 0b110, 0b100
     first = roles["prog_state"]
     members = [j for j in range(n_prog) if ch.next >> j & 1] + [j for j in range(n_prog) if
                                                                  j > 0 and ch.next >> (j - 1) & 1 and

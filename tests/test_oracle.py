@@ -184,14 +184,15 @@ def test_oracle_vs_float64_short_horizon(setup):
     for p in range(pop.shape[0]):
         for r in range(d["R"]):
             x0 = d["x0"][r].astype(np.float64)
+            ts = d["ts"]
             if setup == "dynamic":
-                traj = npr.rk4(lambda s: npr.dyn_rhs(pop[p], lib, s, 2), np.concatenate([x0, [0, 0]]), 0.05, 20)
+                traj = npr.cs_solve(lambda t, s: npr.dyn_rhs(pop[p], lib, s, 2), np.concatenate([x0, [0, 0]]), ts, 0.05)
                 got = np.concatenate([out["xs"][p, r], out["acts"][p, r]], -1)
             elif setup == "static":
-                traj = npr.rk4(lambda s: npr.ff_rhs(pop[p], lib, s), x0, 0.05, 20)
+                traj = npr.cs_solve(lambda t, s: npr.ff_rhs(pop[p], lib, s), x0, ts, 0.05)
                 got = out["xs"][p, r]
             else:
-                traj = npr.rk4(lambda s: npr.sr_rhs(pop[p], lib, s), x0, 0.05, 20)[::4]
+                traj = npr.cs_solve(lambda t, s: npr.sr_rhs(pop[p], lib, s), x0, ts, 0.05)
                 got = out["xs"][p, r]
             ok = np.all(np.isfinite(traj)) and np.all(np.abs(traj) < 1e3) and np.all(np.isfinite(got))
             if not ok:
@@ -265,11 +266,11 @@ def test_oracle_obs_noise_vs_float64_short_horizon(setup, impl):
                 nz = lambda t: npr.obs_noise(key, t, W, bool(impl))  # noqa: E731
                 x0 = d["x0"][r].astype(np.float64)
                 if setup == "dynamic":
-                    traj = npr.rk4_t(lambda t, s: npr.dyn_rhs(pop[p], lib, s, 2, noise=nz(t)),
-                                     np.concatenate([x0, [0, 0]]), 0.0, 0.05, 20)
+                    traj = npr.cs_solve(lambda t, s: npr.dyn_rhs(pop[p], lib, s, 2, noise=nz(t)),
+                                        np.concatenate([x0, [0, 0]]), d["ts"], 0.05)
                     got = np.concatenate([out["xs"][p, r], out["acts"][p, r]], -1)
                 else:
-                    traj = npr.rk4_t(lambda t, s: npr.ff_rhs(pop[p], lib, s, noise=nz(t)), x0, 0.0, 0.05, 20)
+                    traj = npr.cs_solve(lambda t, s: npr.ff_rhs(pop[p], lib, s, noise=nz(t)), x0, d["ts"], 0.05)
                     got = out["xs"][p, r]
                 ys_want = np.array([npr.acro_f_obs(traj[k, :4], nz(d["ts"][k])) for k in range(traj.shape[0])])
                 ok = np.all(np.isfinite(traj)) and np.all(np.abs(traj) < 1e3) and np.all(np.isfinite(got))
@@ -285,3 +286,96 @@ def test_oracle_obs_noise_vs_float64_short_horizon(setup, impl):
         assert 0.05 < np.std(res) < 0.2
     finally:
         prng.set_threefry_partitionable(False)
+
+
+# ---------------------------------------------------------------- diffrax ConstantStepSize (ABI v18)
+def _linear_sr_candidate():
+    """dx0 = x1, dx1 = 0 - x0: every tree operation is exact in f32, so the solve is pure spec arithmetic."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    N = 4
+    cand = np.zeros((1, 2, N, 4), np.float32)
+    cand[..., 1:3] = -1
+    cand[0, 0, N - 1] = [lib.string_to_node["x1"], -1, -1, 0]
+    cand[0, 1, N - 3] = [lib.string_to_node["x0"], -1, -1, 0]
+    cand[0, 1, N - 2] = [1, -1, -1, 0.0]
+    cand[0, 1, N - 1] = [lib.string_to_node["-"], N - 2, N - 3, 0]
+    return lib, cand
+
+
+CS_GRIDS = {
+    "uniform_c3": ((np.arange(201, dtype=np.float32) * np.float32(0.05)).astype(np.float32), 0.05),
+    "notebook": (np.arange(0, 50, 0.2).astype(np.float32), 0.05),            # DynamicPolicy.ipynb:55 grid
+    "off_multiple": (np.arange(0, 10, 0.03).astype(np.float32), 0.05),       # ts not on the step grid
+    "nonuniform": (np.sort(np.random.default_rng(0).uniform(0, 3, 40)).astype(np.float32), 0.07),
+    "tiny_last": ((np.arange(201, dtype=np.float32) * np.float32(0.01)).astype(np.float32), 0.01),
+    "offset": ((np.float32(1.0) + np.arange(30, dtype=np.float32) * np.float32(0.1)).astype(np.float32), 0.04),
+    "repeats": (np.array([0, 0, 0.5, 0.5, 0.5, 1.3, 2.0, 2.0], np.float32), 0.25),
+}
+
+
+@pytest.mark.parametrize("solver", ["rk4", "euler"])
+@pytest.mark.parametrize("grid", sorted(CS_GRIDS))
+def test_constant_step_solve_bitexact_vs_literal_f32(solver, grid):
+    """diffeqsolve(Euler | RK4, ConstantStepSize, SaveAt(ts)): the oracle equals, bit for bit, a
+    literal float32 numpy restatement of diffrax's loop (tests/np_reference.cs_solve: accumulated
+    step ends with the end clip, per-step dt, stage sums (sum a f) dt, every ts[k] through the
+    dense output) on a system whose trees are exact in f32."""
+    lib, cand = _linear_sr_candidate()
+    ts, dt0 = CS_GRIDS[grid]
+    S = ts.shape[0]
+    x0 = np.array([[1.0, 0.0], [0.3, -0.7], [-2.0, 1.5]], np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                 n_save=S, h=dt0, max_fitness=1e5, parsimony=0.0, solver=2 if solver == "euler" else 0)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((3, S, 2), np.float32)), trajectories=True)
+    f = np.float32
+    for r in range(3):
+        want = npr.cs_solve(lambda t, s: np.array([s[1], f(0) - s[0]], f), x0[r], ts, dt0, solver, np.float32)
+        assert np.array_equal(out["xs"][0, r].view(np.uint32), want.astype(f).view(np.uint32)), (grid, solver, r)
+    assert orc.cs_steps(ts, dt0) == len(npr.cs_grid(ts, dt0))
+
+
+def test_constant_step_grid_accumulates():
+    """The grid really is diffrax's accumulated one, not n * dt0: at C3 (dt0 0.05, 200 steps) most
+    step ends differ from the f32 multiples, t1 = 2 with dt0 0.01 takes 201 steps (the last
+    ~1.5e-6 long), and the notebook grid arange(0, 50, 0.2) (t1 = 49.8) takes 997 steps of dt0 0.05 (nominally 996)."""
+    from multitreegp_amd.evaluators import constant_step_grid
+    g = constant_step_grid(CS_GRIDS["uniform_c3"][0], 0.05)
+    mult = (np.arange(201, dtype=np.float32) * np.float32(0.05)).astype(np.float32)
+    assert len(g) == 201 and np.sum(g != mult) > 150 and g[-1] == np.float32(10.0)
+    g2 = constant_step_grid(CS_GRIDS["tiny_last"][0], 0.01)
+    assert len(g2) == 202 and 0 < g2[-1] - g2[-2] < 1e-5
+    assert len(constant_step_grid(CS_GRIDS["notebook"][0], 0.05)) - 1 == orc.cs_steps(CS_GRIDS["notebook"][0], 0.05) == 997
+    for name, (ts, dt0) in CS_GRIDS.items():
+        ref = npr.cs_grid(ts, dt0)
+        want = np.array([ts[0]] + [b for _, b in ref], np.float32)
+        assert np.array_equal(constant_step_grid(ts, dt0), want), name
+        assert np.array_equal(constant_step_grid(ts, dt0, 7), want[:8]), name
+
+
+def test_constant_step_max_steps_fills_inf():
+    """max_steps ends the fixed-step solve too (throw=False): the unsaved points are +inf."""
+    lib, cand = _linear_sr_candidate()
+    ts, dt0 = CS_GRIDS["uniform_c3"]
+    x0 = np.array([[1.0, 0.0]], np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                 n_save=201, h=dt0, max_fitness=1e5, parsimony=0.0, solver=0, max_steps=50)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((1, 201, 2), np.float32)), trajectories=True)
+    xs = out["xs"][0, 0]
+    # 50 steps end at ~2.5: the points up to there are saved, the rest +inf, so the MSE is +inf
+    assert np.all(np.isfinite(xs[:50])) and np.all(np.isposinf(xs[51:]))
+    assert np.isposinf(out["rollout_fitness"][0, 0])
+
+
+def test_constant_step_save_on_step_end_is_interpolated():
+    """A save on a step end is the dense output at theta = 1 (diffrax never reads y1 directly): the
+    Hermite polynomial's ((a + b) + k0) + y0 differs from the step's y1 in the last bits."""
+    lib, cand = _linear_sr_candidate()
+    ts = np.array([0.0, 0.5], np.float32)
+    x0 = np.array([[1.0, 0.25]], np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                 n_save=2, h=0.5, max_fitness=1e5, parsimony=0.0, solver=0)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((1, 2, 2), np.float32)), trajectories=True)
+    f = np.float32
+    want = npr.cs_solve(lambda t, s: np.array([s[1], f(0) - s[0]], f), x0[0], ts, 0.5, "rk4", np.float32)
+    assert np.array_equal(out["xs"][0, 0], want)
+    assert np.array_equal(out["xs"][0, 0, 0], x0[0])  # theta = 0: y0 exactly
