@@ -274,6 +274,30 @@ def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
     return el * 1e3 / args.e2e_steps, fit, float(np.median(ev[1:]))
 
 
+def build_record() -> dict:
+    """Which kernel library this line measured: the in-tree libmtgp_hip.so, its size / mtime / hash
+    prefix, and whether __graft_entry__.build() would have recompiled it (a source newer than the
+    library) -- i.e. whether the line ran the shipped prebuilt library or a fresh build of the
+    sources."""
+    import hashlib
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import __graft_entry__ as ge
+    from multitreegp_amd import _native as nat
+    path = nat.LIB_PATH
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    st = os.stat(path)
+    newest = max(ge.HIP_SOURCES, key=os.path.getmtime)
+    return {"lib": os.path.relpath(path, os.path.dirname(os.path.abspath(__file__))), "bytes": st.st_size,
+            "mtime": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(st.st_mtime)), "sha256_16": h.hexdigest()[:16],
+            "stale_vs_sources": bool(ge._stale(path, ge.HIP_SOURCES)),
+            "newest_source": os.path.basename(newest),
+            "newest_source_mtime": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(os.path.getmtime(newest))),
+            "note": "stale_vs_sources false: build() reuses this library as shipped (no recompilation)"}
+
+
 def main():
     args = parse()
     import torch
@@ -369,13 +393,16 @@ def main():
         traffic = pmc["FETCH_SIZE"] * 1024 * 2 + pmc["WRITE_SIZE"] * 1024
         kcycles = pmc["GRBM_GUI_ACTIVE"] / 8.0
         valu = pmc["SQ_INSTS_VALU"] / (1024 * 0.5 * kcycles) if kcycles > 0 else None
+    dt0 = {"c3": 0.05, "c2": 0.05, "c5": 0.01}[args.config]
+    solver_txt = ("Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000" if adaptive else
+                  f"RK4 + diffrax ConstantStepSize dt0={dt0} ({n_steps} accumulated f32 steps), SaveAt(ts) by dense output")
     workloads = {
-        "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, 3 trees, max_nodes 64, depth<=10, "
-              "RK4 h=0.05 x %d, S=%d" % (P, R, n_steps, S),
-        "c2": "C2 StaticPolicy Acrobot: pop %d/GPU x %d rollouts, 1 tree, max_nodes 30, depth<=4, "
-              "RK4 h=0.05 x %d, S=%d" % (P, R, n_steps, S),
+        "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, 3 trees, max_nodes 64, depth<=10, %s, S=%d"
+              % (P, R, solver_txt, S),
+        "c2": "C2 StaticPolicy Acrobot: pop %d/GPU x %d rollouts, 1 tree, max_nodes 30, depth<=4, %s, S=%d"
+              % (P, R, solver_txt, S),
         "c5": "C5 64-dim SR (neural-ODE style): pop %d/GPU x %d rollouts, 64 trees, max_nodes 128, depth<=16, "
-              "RK4 h=0.01 x %d, S=%d, MSE vs a stable linear system" % (P, R, n_steps, S),
+              "%s, S=%d, MSE vs a stable linear system" % (P, R, solver_txt, S),
     }
     data_desc = {
         "c3": "synthetic: reference-distribution random trees (numpy PCG64), x0 ~ U(-0.1,0.1)^4",
@@ -385,7 +412,7 @@ def main():
     }
 
     out = {
-        "metric": "population x rollout ODE-steps/sec (fixed-step RK4)",
+        "metric": "population x rollout ODE-steps/sec (fixed-step RK4, diffrax ConstantStepSize)",
         "value": value,
         "unit": "ODE-steps/s",
         "n_gpus": ws,
@@ -413,11 +440,10 @@ def main():
                                                                            "SQ_WAVES", "GRBM_GUI_ACTIVE")
                                                       if k in pmc}},
     }
+    out["build"] = build_record()
     if adaptive:
         out["metric"] = ("population x rollout ODE-steps/sec (adaptive Dopri5 + PIDController; a step = one step "
                          "attempt, rejected ones included)")
-        out["config"]["workload"] = out["config"]["workload"].replace(
-            "RK4 h=0.05 x 0", "Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000")
         out["config"]["ode_steps"] = units_per_step / (P * R * ws)  # mean attempts per rollout
         out["config"]["solver"] = "dopri5"
     if args.e2e_steps > 0:

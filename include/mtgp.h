@@ -329,7 +329,7 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  * callable chain: bit j of `next` makes unit j fall through into unit j + 1 (laid out right
  * behind it) instead of returning; bit j of `cond` makes that continuation optional (taken when
  * the evaluator asks for it: the fixed-step dynamic kernel continues the state chain into the
- * save-point readout at save points).  mtgp_jit_chain gives the chain the evaluator kernels of
+ * save-point readout at save points; unused by the evaluators since ABI v18).  mtgp_jit_chain gives the chain the evaluator kernels of
  * `model` call; code built with another non-zero chain is rejected (MTGP_ERR_ARG), code built
  * without one ({0, 0, 0}) is called one program at a time as before.
  * store (ABI v14): LDS store chains for the wide-state SR kernels (MTGP_JIT_MODE_LDS code): every
@@ -340,6 +340,11 @@ typedef struct {
   uint32_t next;
   uint32_t cond;
   uint32_t store;
+  /* ABI v18: bit j of `put` -- unit j also copies its result into data register v[put_slot]
+   * before falling through, so the next units read it as a data slot.  The fixed-step dynamic
+   * policy chains readout -> (u into its slot) -> state programs: one call per stage. */
+  uint32_t put;
+  int32_t put_slot;
 } MtgpJitChain;
 
 typedef struct {

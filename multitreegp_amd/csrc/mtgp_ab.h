@@ -62,5 +62,11 @@
 #ifndef MTGP_AB_NOFIT
 #define MTGP_AB_NOFIT 0       // no online fitness update at the save points
 #endif
+// Debug build (round 5, never shipped): bounds checks on every trajectory-row store and on the
+// Acrobot mask's fit_hist row index; a violation is counted (mtgp_debug_violations_tuN) and the
+// access skipped instead of trapping, so a bad offset can never fault the GPU or hide silently.
+#ifndef MTGP_DEBUG_CHECKS
+#define MTGP_DEBUG_CHECKS 0
+#endif
 
 #endif  // MTGP_AB_H

@@ -129,7 +129,7 @@ struct LdsStack {
 };
 
 template <class Src, class Stk = PrivStack>
-__device__ Dual run_dual_src(const MtgpInstr* code, Src V, Stk stk = Stk()) {
+__device__ __forceinline__ Dual run_dual_src(const MtgpInstr* code, Src V, Stk stk = Stk()) {
   Dual acc = {0.0f, 0.0f};
   int sp = 0;
   // the next instruction's (scalar) load is issued before this one is dispatched: one load
@@ -320,6 +320,11 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
   out[1] = dtot / (float)S;
 }
 
+// Dopri5 tableau rows read with a run-time stage index (wave-uniform: scalar loads)
+__constant__ float kDpA[7][6] = MTGP_DP_TABLE_A;
+__constant__ float kDpE[7] = MTGP_DP_TABLE_E;
+__constant__ float kDpCM[7] = MTGP_DP_TABLE_CMID;
+
 // k_sr_grad for the adaptive solve (SR_evaluator.py:76-79 with Dopri5 + PIDController): k_sr_dopri5's
 // integration (include/mtgp_dopri5.h) in dual numbers, the step sizes, accept / reject decisions and
 // the event held at their primal values (oracle sr_rollout_dual_dp: the derivative of the discrete
@@ -349,109 +354,255 @@ __global__ void __launch_bounds__(kGradBlock) k_sr_grad_dp(GradArgs A) {
   const float rtol = A.m.rtol, atol = A.m.atol, dtmin = A.m.dtmin, dtmax = A.m.dtmax;
   const float* __restrict__ ts = A.ro.ts;
   const float t_end = ts[S - 1];
-  constexpr float TA[7][6] = MTGP_DP_TABLE_A;
-  constexpr float E[7] = MTGP_DP_TABLE_E;
-  constexpr float CM[7] = MTGP_DP_TABLE_CMID;
-  float yv[NV], yd[NV], y1v[NV], y1d[NV], fv[7][NV], fd[7][NV], sv[NV], sd[NV];
-#pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    yv[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
-    yd[i] = 0.0f;
-  }
-  auto bad = [&]() {
-    bool b = false;
-#pragma unroll
-    for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(yv[i]));
-    return b;
-  };
-  auto rhs = [&](const float* xv, const float* xd, float* ov, float* od) {
-    for (int i = 0; i < nv; ++i) {
-      const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
-      ov[i] = o.v;
-      od[i] = o.d;
-    }
-  };
   float tot = 0.0f, dtot = 0.0f;
-  auto mse = [&](int ks, const float* xv, const float* xd) {  // SR_evaluator.py:24, save point ks
-    float sq = 0.0f, dsq = 0.0f;
-    for (int d = 0; d < nv; ++d) {
-      const float e = xv[d] - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
-      const float de = xd[d] * (2.0f * e);
-      sq = (d == 0) ? e * e : sq + e * e;
-      dsq = (d == 0) ? de : dsq + de;
-    }
-    tot = tot + sq;
-    dtot = dtot + dsq;
-  };
-  mse(0, yv, yd);
-  int ks = 1, steps = 0;
-  float t = ts[0];
-  float tnext = t + A.m.h;
-  tnext = tnext > t_end ? t_end : tnext;
-  bool prev_ok = !bad();
-  rhs(yv, yd, fv[0], fd[0]);
+  int ks = 1;
   const MtgpDpPid pid = A.m.pid_custom ? MtgpDpPid{A.m.pid_c1, A.m.pid_c2, A.m.pid_c3, A.m.pid_safety,
                                                    A.m.pid_factormin, A.m.pid_factormax}
                                        : MtgpDpPid MTGP_DP_PID_DEFAULT;
   MtgpDpCtl ctl{1.0f, 1.0f, 0};
   const int force_dtmin = !A.m.no_force_dtmin;
-  while (t < t_end && steps < max_steps) {
-    const float h = tnext - t;
-    for (int st = 1; st <= 6; ++st) {
+  if constexpr (NV <= 4) {
+    // small states: k_ctl_grad's register form -- compile-time component indices, the tableau sums
+    // accumulated as the stages arrive (each sum's ascending-j order of mtgp_dp_term), one rhs site
+    float yv[NV], yd[NV], sv[NV], sd[NV], f0v[NV], f0d[NV], fcv[NV], fcd[NV];
+    float acv[6][NV], acd[6][NV], aev[NV], amv[NV], amd[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      yv[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
+      yd[i] = 0.0f;
+    }
+    auto bad = [&]() {
+      bool b = false;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(yv[i]));
+      return b;
+    };
+    auto rhs = [&](const float (&xv)[NV], const float (&xd)[NV]) {
+#pragma unroll 1
       for (int i = 0; i < nv; ++i) {
-        float acc = 0.0f, dacc = 0.0f;
-        for (int j = 0; j < st; ++j) {
-          acc = mtgp_dp_term(acc, TA[st][j], fv[j][i], j == 0);
-          dacc = mtgp_dp_term(dacc, TA[st][j], fd[j][i], j == 0);
-        }
-        sv[i] = MTGP_FMAF(h, acc, yv[i]);
-        sd[i] = MTGP_FMAF(h, dacc, yd[i]);
-        if (st == 6) { y1v[i] = sv[i]; y1d[i] = sd[i]; }
+        const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
+#pragma unroll
+        for (int c = 0; c < NV; ++c)
+          if (c == i) {
+            fcv[c] = o.v;
+            fcd[c] = o.d;
+          }
       }
-      rhs(sv, sd, fv[st], fd[st]);
+    };
+    auto mse = [&](int q, const float (&xv)[NV], const float (&xd)[NV]) {  // SR_evaluator.py:24
+      float sq = 0.0f, dsq = 0.0f;
+#pragma unroll
+      for (int d = 0; d < NV; ++d) {
+        if (d >= nv) continue;
+        const float e = xv[d] - A.ro.ys_true[((size_t)q * nv + d) * R + r];
+        const float de = xd[d] * (2.0f * e);
+        sq = (d == 0) ? e * e : sq + e * e;
+        dsq = (d == 0) ? de : dsq + de;
+      }
+      tot = tot + sq;
+      dtot = dtot + dsq;
+    };
+    auto contrib = [&](int j) __attribute__((always_inline)) {  // stage j's f = (fcv, fcd)
+      const bool first = j == 0;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        if (q + 1 <= j) continue;
+        const float w = kDpA[q + 1][j];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          acv[q][i] = mtgp_dp_term(acv[q][i], w, fcv[i], first);
+          acd[q][i] = mtgp_dp_term(acd[q][i], w, fcd[i], first);
+        }
+      }
+      const float we = kDpE[j], wm = kDpCM[j];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        aev[i] = mtgp_dp_term(aev[i], we, fcv[i], first);
+        amv[i] = mtgp_dp_term(amv[i], wm, fcv[i], first);
+        amd[i] = mtgp_dp_term(amd[i], wm, fcd[i], first);
+      }
+    };
+    mse(0, yv, yd);
+    int steps = 0;
+    float t = ts[0];
+    float tnext = t + A.m.h;
+    tnext = tnext > t_end ? t_end : tnext;
+    bool prev_ok = !bad(), have_f0 = false;
+    while (t < t_end && steps < max_steps) {
+      const float h = tnext - t;
+      if (have_f0) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          fcv[i] = f0v[i];
+          fcd[i] = f0d[i];
+        }
+        contrib(0);
+      }
+#pragma unroll 1
+      for (int st = have_f0 ? 1 : 0; st <= 6; ++st) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          float av = acv[0][i], ad = acd[0][i];
+#pragma unroll
+          for (int q = 1; q < 6; ++q) {
+            av = (st == q + 1) ? acv[q][i] : av;
+            ad = (st == q + 1) ? acd[q][i] : ad;
+          }
+          sv[i] = st == 0 ? yv[i] : MTGP_FMAF(h, av, yv[i]);
+          sd[i] = st == 0 ? yd[i] : MTGP_FMAF(h, ad, yd[i]);
+        }
+        rhs(sv, sd);
+        if (st == 0) {
+#pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            f0v[i] = fcv[i];
+            f0d[i] = fcd[i];
+          }
+          have_f0 = true;
+        }
+        contrib(st);
+      }
+      // sv, sd = y1 (stage 6's input); fcv, fcd = f_6
+      float msum = 0.0f;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        if (i >= nv) continue;
+        const float sc = mtgp_dp_scaled(h * aev[i], yv[i], sv[i], rtol, atol);
+        msum = (i == 0) ? sc * sc : msum + sc * sc;
+      }
+      const float ms = msum / (float)nv;
+      int keep, fail;
+      const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &keep, &fail);
+      ++steps;
+      bool done = fail != 0;
+      if (keep) {
+        const float t1 = tnext;
+        while (ks < S && ts[ks] <= t1) {  // SaveAt(ts) by the dense output at the primal theta
+          const float thk = (ts[ks] - t) / h;
+          float qv[NV], qd[NV];
+#pragma unroll
+          for (int i = 0; i < NV; ++i) {
+            const float ymid = MTGP_FMAF(h, amv[i], yv[i]), dymid = MTGP_FMAF(h, amd[i], yd[i]);
+            qv[i] = mtgp_dp_interp(yv[i], sv[i], ymid, h * f0v[i], h * fcv[i], thk);
+            qd[i] = mtgp_dp_interp(yd[i], sd[i], dymid, h * f0d[i], h * fcd[i], thk);
+          }
+          mse(ks, qv, qd);
+          ++ks;
+        }
+        t = t1;
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          yv[i] = sv[i];
+          yd[i] = sd[i];
+          f0v[i] = fcv[i];  // FSAL
+          f0d[i] = fcd[i];
+        }
+        const bool ok = !bad();
+        if (prev_ok && !ok) done = true;  // the NaN event (sr.py:93-94)
+        prev_ok = ok;
+      }
+      if (done) break;
+      tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
-    float msum = 0.0f;
-    for (int i = 0; i < nv; ++i) {
-      float acc = 0.0f;
-      for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], fv[j][i], j == 0);
-      const float sc = mtgp_dp_scaled(h * acc, yv[i], y1v[i], rtol, atol);
-      msum = (i == 0) ? sc * sc : msum + sc * sc;
+  } else {
+    constexpr float TA[7][6] = MTGP_DP_TABLE_A;
+    constexpr float E[7] = MTGP_DP_TABLE_E;
+    constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+    float yv[NV], yd[NV], y1v[NV], y1d[NV], fv[7][NV], fd[7][NV], sv[NV], sd[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) {
+      yv[i] = i < nv ? A.ro.x0[(size_t)r * nv + i] : 0.0f;
+      yd[i] = 0.0f;
     }
-    const float ms = msum / (float)nv;
-    int keep, fail;
-    const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &keep, &fail);
-    ++steps;
-    bool done = fail != 0;
-    if (keep) {
-      const float t1 = tnext;
-      while (ks < S && ts[ks] <= t1) {  // SaveAt(ts) by the dense output at the primal theta
-        const float thk = (ts[ks] - t) / h;
+    auto bad = [&]() {
+      bool b = false;
+#pragma unroll
+      for (int i = 0; i < NV; ++i) b = b || (i < nv && !mtgp_isfinite(yv[i]));
+      return b;
+    };
+    auto rhs = [&](const float* xv, const float* xd, float* ov, float* od) {
+      for (int i = 0; i < nv; ++i) {
+        const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
+        ov[i] = o.v;
+        od[i] = o.d;
+      }
+    };
+    auto mse = [&](int ks, const float* xv, const float* xd) {  // SR_evaluator.py:24, save point ks
+      float sq = 0.0f, dsq = 0.0f;
+      for (int d = 0; d < nv; ++d) {
+        const float e = xv[d] - A.ro.ys_true[((size_t)ks * nv + d) * R + r];
+        const float de = xd[d] * (2.0f * e);
+        sq = (d == 0) ? e * e : sq + e * e;
+        dsq = (d == 0) ? de : dsq + de;
+      }
+      tot = tot + sq;
+      dtot = dtot + dsq;
+    };
+    mse(0, yv, yd);
+    int steps = 0;
+    float t = ts[0];
+    float tnext = t + A.m.h;
+    tnext = tnext > t_end ? t_end : tnext;
+    bool prev_ok = !bad();
+    rhs(yv, yd, fv[0], fd[0]);
+    while (t < t_end && steps < max_steps) {
+      const float h = tnext - t;
+      for (int st = 1; st <= 6; ++st) {
         for (int i = 0; i < nv; ++i) {
           float acc = 0.0f, dacc = 0.0f;
-          for (int j = 0; j < 7; ++j) {
-            acc = mtgp_dp_term(acc, CM[j], fv[j][i], j == 0);
-            dacc = mtgp_dp_term(dacc, CM[j], fd[j][i], j == 0);
+          for (int j = 0; j < st; ++j) {
+            acc = mtgp_dp_term(acc, TA[st][j], fv[j][i], j == 0);
+            dacc = mtgp_dp_term(dacc, TA[st][j], fd[j][i], j == 0);
           }
-          const float ymid = MTGP_FMAF(h, acc, yv[i]), dymid = MTGP_FMAF(h, dacc, yd[i]);
-          sv[i] = mtgp_dp_interp(yv[i], y1v[i], ymid, h * fv[0][i], h * fv[6][i], thk);
-          sd[i] = mtgp_dp_interp(yd[i], y1d[i], dymid, h * fd[0][i], h * fd[6][i], thk);
+          sv[i] = MTGP_FMAF(h, acc, yv[i]);
+          sd[i] = MTGP_FMAF(h, dacc, yd[i]);
+          if (st == 6) { y1v[i] = sv[i]; y1d[i] = sd[i]; }
         }
-        mse(ks, sv, sd);
-        ++ks;
+        rhs(sv, sd, fv[st], fd[st]);
       }
-      t = t1;
+      float msum = 0.0f;
       for (int i = 0; i < nv; ++i) {
-        yv[i] = y1v[i];
-        yd[i] = y1d[i];
-        fv[0][i] = fv[6][i];  // FSAL
-        fd[0][i] = fd[6][i];
+        float acc = 0.0f;
+        for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], fv[j][i], j == 0);
+        const float sc = mtgp_dp_scaled(h * acc, yv[i], y1v[i], rtol, atol);
+        msum = (i == 0) ? sc * sc : msum + sc * sc;
       }
-      const bool ok = !bad();
-      if (prev_ok && !ok) done = true;  // the NaN event (sr.py:93-94)
-      prev_ok = ok;
+      const float ms = msum / (float)nv;
+      int keep, fail;
+      const float dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &keep, &fail);
+      ++steps;
+      bool done = fail != 0;
+      if (keep) {
+        const float t1 = tnext;
+        while (ks < S && ts[ks] <= t1) {  // SaveAt(ts) by the dense output at the primal theta
+          const float thk = (ts[ks] - t) / h;
+          for (int i = 0; i < nv; ++i) {
+            float acc = 0.0f, dacc = 0.0f;
+            for (int j = 0; j < 7; ++j) {
+              acc = mtgp_dp_term(acc, CM[j], fv[j][i], j == 0);
+              dacc = mtgp_dp_term(dacc, CM[j], fd[j][i], j == 0);
+            }
+            const float ymid = MTGP_FMAF(h, acc, yv[i]), dymid = MTGP_FMAF(h, dacc, yd[i]);
+            sv[i] = mtgp_dp_interp(yv[i], y1v[i], ymid, h * fv[0][i], h * fv[6][i], thk);
+            sd[i] = mtgp_dp_interp(yd[i], y1d[i], dymid, h * fd[0][i], h * fd[6][i], thk);
+          }
+          mse(ks, sv, sd);
+          ++ks;
+        }
+        t = t1;
+        for (int i = 0; i < nv; ++i) {
+          yv[i] = y1v[i];
+          yd[i] = y1d[i];
+          fv[0][i] = fv[6][i];  // FSAL
+          fd[0][i] = fd[6][i];
+        }
+        const bool ok = !bad();
+        if (prev_ok && !ok) done = true;  // the NaN event (sr.py:93-94)
+        prev_ok = ok;
+      }
+      if (done) break;
+      tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
     }
-    if (done) break;
-    tnext = mtgp_dp_clip_end(t, dt, t_end, keep);
   }
   // unsaved points are +inf: the squared error is +inf (NaN stays NaN)
   if (ks < S && mtgp_isfinite(tot)) tot = kInf;
@@ -526,7 +677,12 @@ struct CtlEnv<2> {  // StirredTankReactor
 
 constexpr int kCtlData = 8;  // data slots of the control models (mtgp_kernels.hip kDMax)
 
-template <int ENV, int NA>
+// DP: the Dopri5 + PID solve, else the fixed-step one -- separate kernels, so neither pays for
+// the other's arrays.  Every per-component array is indexed at compile time (unrolled loops, a
+// run-time index only selects among registers), so the dual state lives in VGPRs, not scratch
+// (round 4: 450-576 bytes of scratch per lane, a scratch round trip per access on a latency-bound
+// launch).
+template <int ENV, int NA, bool DP>
 __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   __shared__ Dual s_stk[MTGP_STACK_MAX][kGradBlock];
   const LdsStack stk{&s_stk[0][threadIdx.x]};
@@ -554,7 +710,11 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   float prm[NP], tg[kCtlData];
 #pragma unroll
   for (int i = 0; i < NP; ++i) prm[i] = A.ro.params[(size_t)r * NP + i];
-  for (int i = 0; i < nt && i < kCtlData; ++i) tg[i] = A.ro.targets[(size_t)r * nt + i];
+#pragma unroll
+  for (int i = 0; i < kCtlData; ++i) {
+    tg[i] = 0.0f;
+    if (i < nt) tg[i] = A.ro.targets[(size_t)r * nt + i];
+  }
   const uint32_t* key = A.ro.obs_keys ? A.ro.obs_keys + 2 * (size_t)r : nullptr;
   // the data vector of a program call, and its reader
   float dvv[kCtlData], dvd[kCtlData];
@@ -583,12 +743,20 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     float nz[NV];
 #pragma unroll
     for (int j = 0; j < NV; ++j) nz[j] = 0.0f;
-    if (key) {
-      float n[8];
-      mtgp_obs_normals(key[0], key[1], t, no, A.m.prng_impl, n);
-      for (int j = 0; j < no; ++j) {
+    if (key) {  // mtgp_obs_normals word by word (compile-time indices)
+      uint32_t n0, n1;
+      mtgp_fold_in(key[0], key[1], mtgp_f2u(t), &n0, &n1);
+      float n[NV];
+#pragma unroll
+      for (int i = 0; i < NV; ++i)
+        n[i] = i < no ? mtgp_normal_from_bits(mtgp_random_bits_word(n0, n1, i, no, A.m.prng_impl)) : 0.0f;
+#pragma unroll
+      for (int j = 0; j < NV; ++j) {
+        if (j >= no) continue;
         float sacc = n[0] * A.ro.obs_w[0 * no + j];
-        for (int i = 1; i < no; ++i) sacc = sacc + n[i] * A.ro.obs_w[i * no + j];
+#pragma unroll
+        for (int i = 1; i < NV; ++i)
+          if (i < no) sacc = sacc + n[i] * A.ro.obs_w[i * no + j];
         nz[j] = sacc;
       }
     }
@@ -615,7 +783,11 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
 #pragma unroll
     for (int i = 0; i < NV; ++i) dx[i] = frd(d[i]);
   };
-  // _drift (dyn.py:107-118 / ff.py:104-110) in duals
+  // _drift (dyn.py:107-118 / ff.py:104-110) in duals.  The readout and the state programs run
+  // from ONE interpreter site (program q = 0 the readout, q >= 1 state program q - 1), and the
+  // drift after them (it reads only the state and u; no program reads its result): the inlined
+  // interpreter is then one copy per rhs, its data vector registers (a called interpreter would
+  // read the data vector through memory -- scratch, round 4).
   auto rhs = [&](float t, const Dual* st, Dual* ds) {
     Dual y[NV];
     f_obs(t, st, y);
@@ -624,23 +796,30 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     if (DYN) {
 #pragma unroll
       for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, st[NV + j]);
-      for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
-      const Dual u = run_dual_src(p_read, V, stk);  // [0, a, 0, tg]
-      drift(st, u, ds);
-#pragma unroll
-      for (int i = 0; i < NV; ++i)
-        if (i < no) put(i, y[i]);
-      put(no + NA, u);
-#pragma unroll
-      for (int j = 0; j < (DYN ? NA : 1); ++j) ds[NV + j] = run_dual_src(p_state + (size_t)j * A.L, V, stk);
     } else {
 #pragma unroll
       for (int i = 0; i < NV; ++i)
         if (i < no) put(i, y[i]);
-      for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
-      const Dual u = run_dual_src(p_read, V, stk);
-      drift(st, u, ds);
     }
+#pragma unroll
+    for (int j = 0; j < kCtlData; ++j)
+      if (j < nt) put(DYN ? no + NA + 1 + j : no + j, {tg[j], 0.0f});
+    Dual u = {0.0f, 0.0f};
+#pragma unroll 1
+    for (int q = 0; q <= NA; ++q) {
+      if (DYN && q == 1) {  // the state programs read [y, a, u, tg]; the readout read [0, a, 0, tg]
+#pragma unroll
+        for (int i = 0; i < NV; ++i)
+          if (i < no) put(i, y[i]);
+        put(no + NA, u);
+      }
+      const Dual o = run_dual_src(q == 0 ? p_read : p_state + (size_t)(q - 1) * A.L, V, stk);
+      if (q == 0) u = o;
+#pragma unroll
+      for (int j = 0; j < (DYN ? NA : 1); ++j)
+        if (DYN && q == j + 1) ds[NV + j] = o;
+    }
+    drift(st, u, ds);
   };
   // online fitness over the save points (oracle_ctl_grad's full-array loop, addition for addition)
   const int S = A.m.n_save;
@@ -661,10 +840,14 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     if (DYN) {
 #pragma unroll
       for (int j = 0; j < (DYN ? NA : 1); ++j) put(no + j, xq[NV + j]);
-      for (int j = 0; j < nt; ++j) put(no + NA + 1 + j, {tg[j], 0.0f});
+#pragma unroll
+      for (int j = 0; j < kCtlData; ++j)
+        if (j < nt) put(no + NA + 1 + j, {tg[j], 0.0f});
       u = run_dual_src(p_save, V, stk);  // dyn.py:101 [y, a, 0, tg]
     } else {
-      for (int j = 0; j < nt; ++j) put(no + j, {tg[j], 0.0f});
+#pragma unroll
+      for (int j = 0; j < kCtlData; ++j)
+        if (j < nt) put(no + j, {tg[j], 0.0f});
       u = run_dual_src(p_read, V, stk);  // ff.py:97
     }
     if constexpr (ENV == 0) {
@@ -708,27 +891,45 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     }
     return b;
   };
-  Dual s[ND], kx[ND], acc[ND], tmp[ND];
+  Dual s[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) s[i] = {i < NV ? A.ro.x0[(size_t)r * NV + i] : 0.0f, 0.0f};
   bool prev_ok = !bad(s);
   const float h = A.m.h;
-  const bool euler = A.m.solver == MTGP_SOLVER_EULER;
   int q_saved = 0;
-  if (A.m.solver == MTGP_SOLVER_DOPRI5) {
+  if constexpr (DP) {
     save_point(0, s);
     // k_ctl_dopri5's solve in duals (oracle ctl_dopri5_dual): the step sizes, accept / reject
-    // decisions and the event held at their primal values; save points by the dense output
-    constexpr float TA[7][6] = MTGP_DP_TABLE_A;
-    constexpr float E[7] = MTGP_DP_TABLE_E;
-    constexpr float CM[7] = MTGP_DP_TABLE_CMID;
+    // decisions and the event held at their primal values; save points by the dense output.
+    // The tableau sums are accumulated as the stages arrive -- stage j's f adds its a_ij f_j to
+    // the sum of every later stage i, the error sum and the midpoint sum -- which is each sum's
+    // ascending-j order of mtgp_dp_term exactly, with no per-stage f kept (f_0 and f_6 aside).
     const float t_end = ts[S - 1];
-    Dual f[7][ND], y1[ND], yi[ND], sk[ND];
+    Dual f0[ND], fc[ND], yi[ND], sk[ND];
+    Dual ac[6][ND], am[ND];  // ac[i - 1]: stage i's sum; am: the midpoint sum
+    float ae[ND];            // the error sum (values only)
+    auto contrib = [&](int j, const Dual* f) __attribute__((always_inline)) {
+      const bool first = j == 0;
+#pragma unroll
+      for (int q = 0; q < 6; ++q) {
+        if (q + 1 <= j) continue;  // stages up to j are done
+        const float w = kDpA[q + 1][j];
+#pragma unroll
+        for (int i = 0; i < ND; ++i)
+          ac[q][i] = {mtgp_dp_term(ac[q][i].v, w, f[i].v, first), mtgp_dp_term(ac[q][i].d, w, f[i].d, first)};
+      }
+      const float we = kDpE[j], wm = kDpCM[j];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) {
+        ae[i] = mtgp_dp_term(ae[i], we, f[i].v, first);
+        am[i] = {mtgp_dp_term(am[i].v, wm, f[i].v, first), mtgp_dp_term(am[i].d, wm, f[i].d, first)};
+      }
+    };
     int ks = 1, steps = 0;
     float t = ts[0];
     float tnext = t + h;
     tnext = tnext > t_end ? t_end : tnext;
-    rhs(t, s, f[0]);
+    bool have_f0 = false;  // f_0 of the first attempt comes from the stage loop (one rhs site)
     const MtgpDpPid pid = A.m.pid_custom ? MtgpDpPid{A.m.pid_c1, A.m.pid_c2, A.m.pid_c3, A.m.pid_safety,
                                                      A.m.pid_factormin, A.m.pid_factormax}
                                          : MtgpDpPid MTGP_DP_PID_DEFAULT;
@@ -736,23 +937,29 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     const int force_dtmin = !A.m.no_force_dtmin;
     while (t < t_end && steps < A.m.max_steps) {
       const float hs = tnext - t;
-      for (int st = 1; st <= 6; ++st) {
+      if (have_f0) contrib(0, f0);
+#pragma unroll 1
+      for (int st = have_f0 ? 1 : 0; st <= 6; ++st) {
+#pragma unroll
         for (int i = 0; i < ND; ++i) {
-          float a = 0.0f, da = 0.0f;
-          for (int j = 0; j < st; ++j) {
-            a = mtgp_dp_term(a, TA[st][j], f[j][i].v, j == 0);
-            da = mtgp_dp_term(da, TA[st][j], f[j][i].d, j == 0);
-          }
-          yi[i] = {MTGP_FMAF(hs, a, s[i].v), MTGP_FMAF(hs, da, s[i].d)};
-          if (st == 6) y1[i] = yi[i];
+          Dual a = ac[0][i];
+#pragma unroll
+          for (int q = 1; q < 6; ++q) a = (st == q + 1) ? ac[q][i] : a;
+          yi[i] = st == 0 ? s[i] : Dual{MTGP_FMAF(hs, a.v, s[i].v), MTGP_FMAF(hs, a.d, s[i].d)};
         }
-        rhs(t + mtgp_dp_c(st) * hs, yi, f[st]);
+        rhs(st == 0 ? t : t + mtgp_dp_c(st) * hs, yi, fc);
+        if (st == 0) {
+#pragma unroll
+          for (int i = 0; i < ND; ++i) f0[i] = fc[i];
+          have_f0 = true;
+        }
+        contrib(st, fc);
       }
+      // yi = y1 (stage 6's input), fc = f_6
       float msum = 0.0f;
+#pragma unroll
       for (int i = 0; i < ND; ++i) {
-        float a = 0.0f;
-        for (int j = 0; j < 7; ++j) a = mtgp_dp_term(a, E[j], f[j][i].v, j == 0);
-        const float sc = mtgp_dp_scaled(hs * a, s[i].v, y1[i].v, A.m.rtol, A.m.atol);
+        const float sc = mtgp_dp_scaled(hs * ae[i], s[i].v, yi[i].v, A.m.rtol, A.m.atol);
         msum = (i == 0) ? sc * sc : msum + sc * sc;
       }
       const float ms = msum / (float)ND;
@@ -764,23 +971,20 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
         const float t1 = tnext;
         while (ks < S && ts[ks] <= t1) {
           const float th = (ts[ks] - t) / hs;
+#pragma unroll
           for (int i = 0; i < ND; ++i) {
-            float a = 0.0f, da = 0.0f;
-            for (int j = 0; j < 7; ++j) {
-              a = mtgp_dp_term(a, CM[j], f[j][i].v, j == 0);
-              da = mtgp_dp_term(da, CM[j], f[j][i].d, j == 0);
-            }
-            const float ymid = MTGP_FMAF(hs, a, s[i].v), dymid = MTGP_FMAF(hs, da, s[i].d);
-            sk[i] = {mtgp_dp_interp(s[i].v, y1[i].v, ymid, hs * f[0][i].v, hs * f[6][i].v, th),
-                     mtgp_dp_interp(s[i].d, y1[i].d, dymid, hs * f[0][i].d, hs * f[6][i].d, th)};
+            const float ymid = MTGP_FMAF(hs, am[i].v, s[i].v), dymid = MTGP_FMAF(hs, am[i].d, s[i].d);
+            sk[i] = {mtgp_dp_interp(s[i].v, yi[i].v, ymid, hs * f0[i].v, hs * fc[i].v, th),
+                     mtgp_dp_interp(s[i].d, yi[i].d, dymid, hs * f0[i].d, hs * fc[i].d, th)};
           }
           save_point(ks, sk);
           ++ks;
         }
         t = t1;
+#pragma unroll
         for (int i = 0; i < ND; ++i) {
-          s[i] = y1[i];
-          f[0][i] = f[6][i];  // FSAL
+          s[i] = yi[i];
+          f0[i] = fc[i];  // FSAL
         }
         const bool ok = !bad(s);
         if (prev_ok && !ok) stop = true;  // Event(cond_fn_nan), dyn.py:94
@@ -793,33 +997,30 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   } else {
     // the fixed-step solve (include/mtgp_cstep.h, k_ctl_dynamic / k_ctl_static) in duals: the time
     // grid and the event primal, the stage sums, step update and dense output applied to both halves
+    const bool euler = A.m.solver == MTGP_SOLVER_EULER;
     const float t_end = ts[S - 1];
     float t = ts[0], tn = mtgp_cs_first_end(t, h, t_end);
     int steps = 0, ks = 0;
-    Dual f0[ND], y1[ND], sk[ND];
+    Dual f0[ND], y1[ND], sk[ND], kx[ND], acc[ND], tmp[ND];
     while (t < t_end && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
       const float dt = tn - t;
-      rhs(t, s, f0);
-      if (euler) {
+      // the stages from one rhs site (stage 0 included; Euler: stage 0 only)
+#pragma unroll 1
+      for (int st = 0; st <= (euler ? 0 : 3); ++st) {
 #pragma unroll
-        for (int i = 0; i < ND; ++i) y1[i] = {s[i].v + f0[i].v * dt, s[i].d + f0[i].d * dt};
-      } else {
+        for (int i = 0; i < ND; ++i)
+          tmp[i] = st == 0 ? s[i] : Dual{mtgp_rk4_in(st, s[i].v, kx[i].v, dt), mtgp_rk4_in(st, s[i].d, kx[i].d, dt)};
+        rhs(st == 0 ? t : mtgp_rk4_time(st, t, dt), tmp, kx);
 #pragma unroll
         for (int i = 0; i < ND; ++i) {
-          acc[i] = {mtgp_rk4_acc(0, 0.0f, f0[i].v), mtgp_rk4_acc(0, 0.0f, f0[i].d)};
-          kx[i] = f0[i];
+          if (st == 0) f0[i] = kx[i];
+          acc[i] = {mtgp_rk4_acc(st, acc[i].v, kx[i].v), mtgp_rk4_acc(st, acc[i].d, kx[i].d)};
         }
-        for (int st = 1; st <= 3; ++st) {
-#pragma unroll
-          for (int i = 0; i < ND; ++i)
-            tmp[i] = {mtgp_rk4_in(st, s[i].v, kx[i].v, dt), mtgp_rk4_in(st, s[i].d, kx[i].d, dt)};
-          rhs(mtgp_rk4_time(st, t, dt), tmp, kx);
-#pragma unroll
-          for (int i = 0; i < ND; ++i) acc[i] = {mtgp_rk4_acc(st, acc[i].v, kx[i].v), mtgp_rk4_acc(st, acc[i].d, kx[i].d)};
-        }
-#pragma unroll
-        for (int i = 0; i < ND; ++i) y1[i] = {mtgp_rk4_out(s[i].v, acc[i].v, dt), mtgp_rk4_out(s[i].d, acc[i].d, dt)};
       }
+#pragma unroll
+      for (int i = 0; i < ND; ++i)
+        y1[i] = euler ? Dual{s[i].v + f0[i].v * dt, s[i].d + f0[i].d * dt}
+                      : Dual{mtgp_rk4_out(s[i].v, acc[i].v, dt), mtgp_rk4_out(s[i].d, acc[i].d, dt)};
       while (ks < S && ts[ks] <= tn) {  // SaveAt(ts) by the dense output
         const float th = mtgp_cs_rescale(t, ts[ks], tn);
 #pragma unroll
@@ -911,17 +1112,21 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
   hipStream_t s = (hipStream_t)stream;
   const long lanes = (long)P * grad_lanes_per(K, ro->R);  // whole waves per individual (grad_lane)
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
-#define MTGP_CG(E)                                                                  \
-  switch (na) {                                                                     \
-    case 0: hipLaunchKernelGGL((k_ctl_grad<E, 0>), grid, block, 0, s, A); break;    \
-    case 1: hipLaunchKernelGGL((k_ctl_grad<E, 1>), grid, block, 0, s, A); break;    \
-    case 2: hipLaunchKernelGGL((k_ctl_grad<E, 2>), grid, block, 0, s, A); break;    \
-    default: hipLaunchKernelGGL((k_ctl_grad<E, 3>), grid, block, 0, s, A); break;   \
+#define MTGP_CG2(E, DPV)                                                                  \
+  switch (na) {                                                                           \
+    case 0: hipLaunchKernelGGL((k_ctl_grad<E, 0, DPV>), grid, block, 0, s, A); break;     \
+    case 1: hipLaunchKernelGGL((k_ctl_grad<E, 1, DPV>), grid, block, 0, s, A); break;     \
+    case 2: hipLaunchKernelGGL((k_ctl_grad<E, 2, DPV>), grid, block, 0, s, A); break;     \
+    default: hipLaunchKernelGGL((k_ctl_grad<E, 3, DPV>), grid, block, 0, s, A); break;    \
   }
+#define MTGP_CG(E)              \
+  if (dopri5) MTGP_CG2(E, true) \
+  else MTGP_CG2(E, false)
   if (model->env == MTGP_ENV_ACROBOT) { MTGP_CG(0) }
   else if (model->env == MTGP_ENV_HARMONIC_OSCILLATOR) { MTGP_CG(1) }
   else { MTGP_CG(2) }
 #undef MTGP_CG
+#undef MTGP_CG2
   if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
   hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(((long)P * K + 255) / 256)), dim3(256), 0, s, A);
   if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;

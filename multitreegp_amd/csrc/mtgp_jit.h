@@ -65,9 +65,11 @@ constexpr int kJitMaxWordsPerInstr = 1 + 4 + (MTGP_JIT_COS_WORDS > MTGP_JIT_SIN_
 constexpr uint32_t kJitSinOffset = MTGP_JIT_SIN_OFFSET, kJitCosOffset = MTGP_JIT_COS_OFFSET;
 constexpr uint32_t kJitTemplateBytes = MTGP_JIT_SUB_WORDS * 4u;
 // executed words of one call of each subroutine (the schedule's cost model: the hot path up to
-// the first return; the out-of-line slow paths -- sin/cos |x| >= 2^17, exp |x| > 88.72 or NaN,
-// log of anything but a positive normal, tanh |x| >= 0.625, sqrt x < 2^-96 / 0 / inf / NaN --
-// run only when some lane needs them)
+// the return).  Only sin / cos have out-of-line words after the return (the |x| >= 2^17 Payne-
+// Hanek reduction, run only when some lane needs it); exp / log / tanh / sqrt are branch-free,
+// their special ranges (exp |x| > 88.72 or NaN, log of anything but a positive normal, tanh
+// |x| >= 0.625, sqrt x < 2^-96 / 0 / inf / NaN) handled by selects inside the counted words, so
+// their SKIPPABLE counts are 0 (tests/test_jit.py checks these counts against the blobs)
 constexpr int kJitSinExec = MTGP_JIT_SIN_WORDS - MTGP_JIT_SIN_SKIPPABLE_WORDS;
 constexpr int kJitCosExec = MTGP_JIT_COS_WORDS - MTGP_JIT_COS_SKIPPABLE_WORDS;
 constexpr int kJitExpExec = MTGP_JIT_EXP_WORDS - MTGP_JIT_EXP_SKIPPABLE_WORDS;
@@ -174,7 +176,8 @@ MTGP_JIT_HD inline uint32_t jit_wait_lgkm(int n) { return kWaitLgkm0 | (uint32_t
 // -- no preloads, no wait -- with the whole program's preload table given (pre_ext[0..npre_ext)).
 MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool ret, int mode = kJitModeRegs,
                                    int part = 0, int pre_base = kJitPre, int wait_n = 0, int* npre_out = nullptr,
-                                   int sp_init = 0, const int* pre_ext = nullptr, int npre_ext = 0) {
+                                   int sp_init = 0, const int* pre_ext = nullptr, int npre_ext = 0,
+                                   int remap_slot = -1, int remap_reg = 0) {
   int sp = sp_init;
   int pre[kJitPreSlots];
   int npre = 0;
@@ -226,7 +229,7 @@ MTGP_JIT_HD inline int jit_program(JitOut& o, const MtgpInstr* prog, int L, bool
   }
   // register holding data slot s: v0-v7 (register mode) or its preload / a load at the use
   auto vslot = [&](int s_, int tmp) -> int {
-    if (mode != kJitModeLds) return kJitData + s_;
+    if (mode != kJitModeLds) return s_ == remap_slot ? remap_reg : kJitData + s_;  // (remap: jit_put_remap)
     for (int q = 0; q < npre; ++q)
       if (pre[q] == s_) return pre_base + q;
     o.w(kDsReadB32 | (uint32_t)(s_ * (int)MTGP_SLOT_BYTES));
@@ -476,6 +479,18 @@ MTGP_JIT_HD inline bool jit_unit_packed(uint32_t next, int j, uint32_t store = 0
   return j < 32 && ((next >> j) & 1u) != 0u;
 }
 
+// Put chains (ABI v18, MtgpJitChain.put): a unit p with bit p of `put` passes its result on AS a
+// data slot -- the units it falls through into (within its chain) read data slot put_slot from
+// v(26 + position of p), where the chain epilogue of p leaves it, instead of from v[put_slot].
+// (The fixed-step dynamic policy: readout -> the state programs read u = the readout's result.)
+// -> the register, or -1 when unit j reads its data slots plainly.
+MTGP_JIT_HD inline int jit_put_remap(uint32_t next, uint32_t put, int j) {
+  if (put == 0u || j <= 0 || j >= 32) return -1;
+  for (int p = j - 1; p >= 0 && ((next >> p) & 1u); --p)
+    if ((put >> p) & 1u) return kJitChainOut + jit_chain_pos(next, p);
+  return -1;
+}
+
 // LDS-data units are software-pipelined: the preloads of group g + 1's program are issued before
 // group g's body runs (alternating register sets v26.. / v44..), so the LDS latency of one
 // program hides behind the previous one's arithmetic.  Layout: [P_0] then per group g
@@ -509,7 +524,8 @@ MTGP_JIT_HD inline int jit_lds_region(JitOut& o, const MtgpInstr* cur, const Mtg
 // Code of unit (wave, program j): individuals order[wave*G + g] (identity without a schedule).
 MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P, const int32_t* order, int G, int Rp,
                                 int wave, int j, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
-                                uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u, bool pipe = true) {
+                                uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u, bool pipe = true,
+                                uint32_t put = 0u, int put_slot = 0) {
   JitOut o{out, 0};
   o.base = base;
   for (int g = 0; g < G; ++g) {
@@ -524,7 +540,8 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
       rc = jit_lds_region(o, cur, nxt, L, g);
     } else {
       if (jit_merge_keep(g)) o.movv(kJitKeep, kJitAcc);
-      rc = jit_program(o, cur, L, false, mode);
+      const int rr = jit_put_remap(next, put, j);
+      rc = jit_program(o, cur, L, false, mode, 0, kJitPre, 0, nullptr, 0, nullptr, 0, rr < 0 ? -1 : put_slot, rr);
     }
     if (rc < 0) return rc;
     if (g > 0) jit_merge_tail(o, g, Rp, g == G - 1 || q + 1 >= P);
@@ -539,7 +556,7 @@ MTGP_JIT_HD inline int jit_unit(const MtgpInstr* prog, int n_prog, int L, int P,
 MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, const int32_t* order, int Rp, int q0,
                                       int g, int j, bool last, uint32_t* out, uint32_t base, int mode = kJitModeRegs,
                                       uint32_t next = 0u, uint32_t cond = 0u, uint32_t store = 0u,
-                                      bool pipe = true) {
+                                      bool pipe = true, uint32_t put = 0u, int put_slot = 0) {
   JitOut o{out, 0};
   o.base = base;
   const int q = q0 + g;
@@ -552,7 +569,8 @@ MTGP_JIT_HD inline int jit_unit_group(const MtgpInstr* prog, int n_prog, int L, 
     rc = jit_lds_region(o, cur, nxt, L, g);
   } else {
     if (jit_merge_keep(g)) o.movv(kJitKeep, kJitAcc);
-    rc = jit_program(o, cur, L, false, mode);
+    const int rr = jit_put_remap(next, put, j);
+    rc = jit_program(o, cur, L, false, mode, 0, kJitPre, 0, nullptr, 0, nullptr, 0, rr < 0 ? -1 : put_slot, rr);
   }
   if (rc < 0) return rc;
   if (g > 0) jit_merge_tail(o, g, Rp, last);

@@ -421,6 +421,7 @@ struct KArgs {
   int32_t chain_state;      // the JIT code chains the state role (MtgpJitChain): one call per stage
   int32_t chain_save;       // ... and continues it into the save-point readout on request (s46; unused since ABI v18)
   int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
+  int32_t chain_merge;      // (ABI v18) the dynamic policy's readout chains into its state programs, u put in its slot
   // Dopri5 in two launches (ABI v16, MtgpModel.dp_budget): launch 1 runs every wave for at most
   // dp_budget attempts and parks the lanes of waves that are not done (dp_state, word-major
   // [kDpStateWords][waves * 64]) in the list dp_pending ([0] = count, then wave ids); launch 2
@@ -473,12 +474,22 @@ __device__ __forceinline__ void acro_fit_update(AcroFit& f, int k, int S, const 
 // reached, or reached at save 0), F = first success + 1 as int bits until settled (0 = none yet).
 // The +inf fill after a termination never reaches (cos(inf) is NaN) but its costs (the policy on
 // the fill) still count when the prefix runs past it; the last save point settles every lane.
+#if MTGP_DEBUG_CHECKS
+// violation counters of the debug build: [0] store_row lane offset outside its row, [1] a store
+// row past the end of its array (row >= n_rows * row_len is checked by the callers' indices),
+// [2] fit_hist write index outside [0, S * PR), [3] fit_hist read index outside it
+static __device__ unsigned long long g_dbg_viol[4];  // one per TU (static: no host-symbol clash at link)
+__device__ __forceinline__ void dbg_count(int i) { atomicAdd(&g_dbg_viol[i], 1ull); }
+#endif
 __device__ __forceinline__ void acro_fit_general(AcroFit& f, int k, int S, const int32_t* __restrict__ kof,
                                                  float* hist, size_t PR, int loff, bool dead, float u,
                                                  float x0, float x1) {
   if (f.settled) return;
   const float P = f.csum + (u * 0.01f) * u;  // save 0: 0 + cost = cost
   f.csum = P;
+#if MTGP_DEBUG_CHECKS
+  if (hist && (k < 0 || k >= S || loff < 0 || (size_t)loff >= PR)) { dbg_count(2); hist = nullptr; }
+#endif
   if (hist) hist[(size_t)k * PR + loff] = P;  // read back by this lane only (below)
   if (k + 1 == kof[0]) f.c0incl = P;
   int fs1 = __float_as_int(f.F);
@@ -500,7 +511,17 @@ __device__ __forceinline__ void acro_fit_general(AcroFit& f, int k, int S, const
   if (K > 0) {
     if (fs == 0) v = f.c0incl;
     else if (K == k + 1) v = P;
-    else v = __hip_atomic_load(hist + (size_t)(K - 1) * PR + loff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else {
+#if MTGP_DEBUG_CHECKS
+      if (!hist || K - 1 < 0 || K - 1 >= S || loff < 0 || (size_t)loff >= PR) {
+        dbg_count(3);
+        f.settled = true;
+        f.F = mtgp_qnan();
+        return;
+      }
+#endif
+      v = __hip_atomic_load(hist + (size_t)(K - 1) * PR + loff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   f.settled = true;
   f.F = (float)(fs + (fs == 0) * S) + v;
@@ -692,8 +713,15 @@ struct EnvReactor {
 // (SGPRs) plus the lane's byte offset (a VGPR) -- no per-store 64-bit VGPR address arithmetic; the
 // resource's extent is the row (row_len elements), so a lane offset past it is dropped by the
 // hardware instead of writing out of bounds.  off * 4 < 2^31 (checked by the entry point).
+
 template <bool DP = false>
 __device__ __forceinline__ void store_row(float* __restrict__ arr, size_t row, int off, float v, size_t row_len) {
+#if MTGP_DEBUG_CHECKS
+  if (off < 0 || (size_t)off >= row_len || row % row_len != 0) {
+    dbg_count(0);
+    return;
+  }
+#endif
   float* p = arr + row;
   if (!DP) {
     const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc(p, (short)0, (int)(row_len * 4u), 0x00020000);
@@ -1189,13 +1217,8 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
 #pragma unroll
   for (int t = 0; t < kDMax - NV - 2; ++t)
     if (t < A.m.n_targets && uslot + 1 + t < kDMax) dv[uslot + 1 + t] = A.ro.targets[rr * A.m.n_targets + t];
-  const bool chain_state = A.chain_state != 0;
-  // code addresses of this wave's units (wave-uniform)
+  // code addresses of this wave's units (wave-uniform): the readout -> state put chain, the save readout
   const uint64_t u_readout = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout);
-  const uint64_t u_state = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state);
-  uint64_t u_state_j[NA];
-#pragma unroll
-  for (int j = 0; j < NA; ++j) u_state_j[j] = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_state + j);
   const uint64_t u_save = A.jit_base + (uint32_t)__builtin_amdgcn_readlane((int)Ln.jtab, A.m.prog_readout_save);
 
   float x[NV], a[NA], kx[NV], ka[NA], fx0[NV], fa0[NA], ax[NV], aa[NA];
@@ -1232,7 +1255,11 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
 #pragma unroll
     for (int j = 0; j < NA; ++j) dv[NV + j] = as[j];
     const float us = jit_call_nf(u_save, dv);  // readout([y, a, 0, tar]), dyn.py:101 (u folded to 0)
-    if (!fill && !MTGP_AB_NOFIT) env.fit_update(fit, k, S, ts, us, xs);
+    if constexpr (Env::kMask) {
+      if (active) env.fit_save(fit, k, S, A, PR, loff, fill, us, xs);
+    } else if (!fill && !MTGP_AB_NOFIT) {
+      env.fit_update(fit, k, S, ts, us, xs);
+    }
     if (TRAJ && active && !MTGP_AB_NOSTORE) {
       if (A.out.xs) {
 #pragma unroll
@@ -1264,25 +1291,20 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
       rk_in<NA>(ST, a, ka, dt, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
-      const float u = jit_call_nf(u_readout, dv);
-      env.drift(xt, u, kx);
       if (NOISE && ST != 2) {  // stages 1 and 2 share the time t + dt/2, hence the noise draw
         const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
         obs_noise_vec<NV>(nzc, tc, nzv);
         nzt = __float_as_uint(tc);
       }
+      // one call: the readout (y, u folded: reads [0, a, 0, tar]) returns u in v26, and the state
+      // programs it falls into read their u slot from there ([y, a, u, tar]) -- MtgpJitChain.put
       ctl_obs_apply<Env>(xt, nzv, y);
 #pragma unroll
       for (int i = 0; i < NV; ++i) dv[i] = y[i];
-      dv[uslot] = u;
-      if (chain_state) {
-        const ChainOut c = jit_call_chain_nf(u_state, dv, 0);
+      const ChainOut c = jit_call_chain_nf(u_readout, dv, 0);
 #pragma unroll
-        for (int j = 0; j < NA; ++j) ka[j] = c.v[j < mtgp::kJitChainMax ? j : 0];
-      } else {
-#pragma unroll
-        for (int j = 0; j < NA; ++j) ka[j] = jit_call_nf(u_state_j[j], dv);
-      }
+      for (int j = 0; j < NA; ++j) ka[j] = c.v[1 + j < mtgp::kJitChainMax ? 1 + j : 0];
+      env.drift(xt, c.v[0], kx);
       if (ST == 0) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
@@ -1371,8 +1393,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   Lane Ln;
   if (!lane_setup(A, Ln)) return;
   if (JIT) asm volatile("s_icache_inv");  // the JIT code was written by an earlier kernel
-  if constexpr (JIT && NA <= 3 && !Env::kMask) {
-    if (__builtin_expect(Ln.jok, 1)) {  // usable code: the JIT-only loop
+  if constexpr (JIT && NA <= 3) {
+    if (__builtin_expect(Ln.jok && A.chain_merge, 1)) {  // usable put-chain code: the JIT-only loop
       if (A.m.solver == MTGP_SOLVER_EULER) ctl_dynamic_jit<Env, NA, TRAJ, NOISE, 1>(A, Ln);
       else ctl_dynamic_jit<Env, NA, TRAJ, NOISE, 4>(A, Ln);
       return;
@@ -3765,12 +3787,14 @@ struct JitUnitArgs {
   int mode;  // mtgp_jit.h kJitModeRegs / kJitModeLds
   uint32_t next, cond, store;  // role / LDS store chains (MtgpJitChain, mtgp_jit.h jit_unit_end)
   int pipe;                    // LDS-data units software-pipelined (mtgp_jit.h jit_lds_region)
+  uint32_t put;                // MtgpJitChain.put / put_slot (ABI v18)
+  int put_slot;
 };
 
 __device__ __forceinline__ int jit_unit_words(const JitUnitArgs& U, int u, uint32_t* out, uint32_t base) {
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
   return mtgp::jit_unit(U.prog, U.n_prog, U.L, U.P, U.order, U.G, U.Rp, wave, j, out, base, mtgp::kJitModeRegs,
-                        U.next, U.cond, U.store);
+                        U.next, U.cond, U.store, true, U.put, U.put_slot);
 }
 
 // byte span of unit u in the layout: a unit that falls through into the next one (a chain member)
@@ -4020,7 +4044,7 @@ k_jit_emit_groups(JitUnitArgs U, const int32_t* __restrict__ jw,
   }
   const uint32_t at = b + start * 4u;
   mtgp::jit_unit_group(U.prog, U.n_prog, U.L, U.order, U.Rp, wave * U.G, g, j, last, code + at / 4, at, U.mode,
-                       U.next, U.cond, U.store, U.pipe != 0);
+                       U.next, U.cond, U.store, U.pipe != 0, U.put, U.put_slot);
 }
 
 // Register-data emit with one WAVE per (unit, group): as in k_flatten_wave's sizing, an
@@ -4041,6 +4065,7 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   if (i >= (long)U.n_units * U.G) return;
   const int u = (int)(i / U.G), g = (int)(i - (long)u * U.G);
   const int wave = u / U.n_prog, j = u - wave * U.n_prog;
+  const int remap = mtgp::jit_put_remap(U.next, U.put, j);  // (put chains: slot put_slot read from v26 + pos)
   const int q = wave * U.G + g;
   if (q >= U.P) return;
   const uint32_t b = offs[u], e = offs[u + 1];
@@ -4083,7 +4108,8 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
       const MtgpInstr t[2] = {x, end};
       mtgp::JitOut o{out + pre + woff + (wi - w), 0};
       o.base = at + (uint32_t)(pre + woff + (wi - w)) * 4u;
-      (void)mtgp::jit_program(o, t, 2, false, mtgp::kJitModeRegs, 0, mtgp::kJitPre, 0, nullptr, sp + di - d);
+      (void)mtgp::jit_program(o, t, 2, false, mtgp::kJitModeRegs, 0, mtgp::kJitPre, 0, nullptr, sp + di - d,
+                              nullptr, 0, remap < 0 ? -1 : U.put_slot, remap);
     }
     woff += __shfl(wi, kWave - 1);
     sp += __shfl(di, kWave - 1);
@@ -4293,7 +4319,8 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
   U.G = kWave / Rp;
   U.order = order;
   U.mode = mtgp::kJitModeRegs;
-  U.next = U.cond = U.store = 0u;
+  U.next = U.cond = U.store = U.put = 0u;
+  U.put_slot = 0;
   U.pipe = 1;
   const long waves = ((long)P + U.G - 1) / U.G;
   if (waves * n_prog > INT32_MAX - 1) return false;
@@ -4306,9 +4333,9 @@ bool jit_unit_args(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, 
 // register-resident SR) as one chain when M >= 2, continued into the save-point readout when the
 // fixed-step dynamic kernel can use it (the readout_save program right after the state programs).
 MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
-  MtgpJitChain c{0u, 0u, 0u};
+  MtgpJitChain c{0u, 0u, 0u, 0u, 0};
   int first = m.prog_state, M = 0;
-  bool save = false;
+  const int lim = n_prog < 32 ? n_prog : 32;
   if (m.model == MTGP_MODEL_SR) {
     if (m.n_var > 4) {  // the wide-state kernels: one LDS store chain per wave (its kWideComp components)
       if (m.prog_state == 0 && n_prog >= m.n_var) c.store = (uint32_t)kWideComp;
@@ -4317,20 +4344,26 @@ MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
     M = m.n_var;
   } else if (m.model == MTGP_MODEL_DYNAMIC) {
     M = m.state_size;
-    save = false;  // (ABI v18: the save-point readout reads the dense-output state, not a stage's data vector)
+    // fixed step (ABI v18): readout -> u into its data slot -> state programs, one call per stage
+    // (the readout reads [0, a, 0, tar] with y and u folded, so y may already sit in its slots)
+    const int uslot = m.n_var + m.state_size;
+    if (m.solver != MTGP_SOLVER_DOPRI5 && m.state_size >= 1 && m.prog_readout >= 0 && m.prog_readout + 1 == first &&
+        1 + M <= mtgp::kJitChainMax && first + M <= lim && uslot < kDMax) {
+      for (int k = 0; k < M; ++k) c.next |= 1u << (m.prog_readout + k);
+      c.put = 1u << m.prog_readout;
+      c.put_slot = uslot;
+      return c;
+    }
   } else {
     return c;
   }
-  const int lim = n_prog < 32 ? n_prog : 32;
-  if (M < 1 || M > mtgp::kJitChainMax || first < 0 || first + M + (save ? 1 : 0) > lim) return c;
-  if (M == 1 && !save) return c;
+  if (M < 2 || M > mtgp::kJitChainMax || first < 0 || first + M > lim) return c;
   for (int k = 0; k + 1 < M; ++k) c.next |= 1u << (first + k);
-  if (save) {
-    c.next |= 1u << (first + M - 1);
-    c.cond |= 1u << (first + M - 1);
-  }
   return c;
 }
+
+// a chain's put is a data register of the register-data ABI (v0-v7)
+static bool jit_chain_put_ok(const MtgpJitChain& c) { return c.put == 0u || (c.put_slot >= 0 && c.put_slot < kDMax); }
 
 // Executable device memory for the JIT (HSA pool allocation with the executable flag on the
 // coarse-grained pool of the agent that backs HIP device `dev`, matched by PCI location).
@@ -4552,6 +4585,16 @@ __attribute__((visibility("hidden"))) int mtgp_tu_launch_harmonic(MTGP_TU_ENTRY_
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_reactor(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS);
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_acrobot(MTGP_TU_ENTRY_ARGS);
+#if MTGP_DEBUG_CHECKS && defined(MTGP_TU)
+#define MTGP_DBG_CAT2(a, b) a##b
+#define MTGP_DBG_CAT(a, b) MTGP_DBG_CAT2(a, b)
+// debug build only: this translation unit's violation counters (read and cleared)
+extern "C" int MTGP_DBG_CAT(mtgp_debug_violations_tu, MTGP_TU)(unsigned long long* host) {
+  if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_dbg_viol), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  const unsigned long long z[4] = {0, 0, 0, 0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_viol), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif
 #if MTGP_TU_ACRO && MTGP_AB_FBCOUNT
 extern "C" int mtgp_ab_fb_count(unsigned long long* host) {  // diagnostic build only; reads and clears
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ab_fb_count), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
@@ -4738,7 +4781,10 @@ int mtgp_jit_plan_words_chain(const int32_t* jit_words, int32_t P, int32_t n_pro
   JitUnitArgs U;
   static const MtgpInstr dummy = {0u, 0.0f};
   if (!jit_words || !offsets_out || !info_out || !jit_unit_args(&dummy, P, n_prog, 1, R, order, U)) return MTGP_ERR_ARG;
-  if (chain) { U.next = chain->next; U.cond = chain->cond; U.store = chain->store; }
+  if (chain) {
+    if (!jit_chain_put_ok(*chain)) return MTGP_ERR_ARG;
+    U.next = chain->next; U.cond = chain->cond; U.store = chain->store; U.put = chain->put; U.put_slot = chain->put_slot;
+  }
   hipStream_t s = (hipStream_t)stream;
   if (U.n_units == 0) {
     if (hipMemsetAsync(info_out, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
@@ -4776,9 +4822,12 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   if (chain) {
     if (jit_mode != mtgp::kJitModeRegs && (chain->next | chain->cond) != 0u) return MTGP_ERR_ARG;  // v26.. are preloads
     if (jit_mode != mtgp::kJitModeLds && chain->store != 0u) return MTGP_ERR_ARG;  // store chains: LDS-data code
+    if (!jit_chain_put_ok(*chain) || (jit_mode != mtgp::kJitModeRegs && chain->put != 0u)) return MTGP_ERR_ARG;
     U.next = chain->next;
     U.cond = chain->cond;
     U.store = chain->store;
+    U.put = chain->put;
+    U.put_slot = chain->put_slot;
   }
   if (U.n_units == 0) return MTGP_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -4838,18 +4887,18 @@ int mtgp_jit_cost(const MtgpInstr* prog, const int32_t* plen, int32_t P, int32_t
 
 static int jit_unit_host_impl(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R,
                               const int32_t* order, int32_t unit, uint32_t* out, int32_t max_words, int32_t jit_mode,
-                              uint32_t next, uint32_t cond, uint32_t store) {
+                              uint32_t next, uint32_t cond, uint32_t store, uint32_t put = 0u, int put_slot = 0) {
   JitUnitArgs U;
   if (!jit_unit_args(prog, P, n_prog, L, R, order, U) || unit < 0 || unit >= U.n_units) return MTGP_ERR_ARG;
   if (jit_mode != mtgp::kJitModeRegs && jit_mode != mtgp::kJitModeLds) return MTGP_ERR_ARG;
   const int wave = unit / n_prog, j = unit - wave * n_prog;
   const int n = mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, nullptr, mtgp::kJitTemplateBytes, jit_mode,
-                               next, cond, store);
+                               next, cond, store, true, put, put_slot);
   if (n <= 0) return n < 0 ? n - 100 : MTGP_ERR_ARG;
   if (out) {
     if (n > max_words) return MTGP_ERR_ARG;
     mtgp::jit_unit(prog, n_prog, L, P, order, U.G, U.Rp, wave, j, out, mtgp::kJitTemplateBytes, jit_mode, next, cond,
-                   store);
+                   store, true, put, put_slot);
   }
   return n;
 }
@@ -4863,7 +4912,8 @@ int mtgp_jit_unit_host_chain(const MtgpInstr* prog, int32_t P, int32_t n_prog, i
                              const int32_t* order, const MtgpJitChain* chain, int32_t unit, uint32_t* out,
                              int32_t max_words, int32_t jit_mode) {
   return jit_unit_host_impl(prog, P, n_prog, L, R, order, unit, out, max_words, jit_mode, chain ? chain->next : 0u,
-                            chain ? chain->cond : 0u, chain ? chain->store : 0u);
+                            chain ? chain->cond : 0u, chain ? chain->store : 0u, chain ? chain->put : 0u,
+                            chain ? chain->put_slot : 0);
 }
 
 int mtgp_jit_unit_host(const MtgpInstr* prog, int32_t P, int32_t n_prog, int32_t L, int32_t R, const int32_t* order,
@@ -5096,13 +5146,16 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     A.dp_state = out->dp_state;
     A.dp_pending = out->dp_pending;
   }
-  if (jit && (jitc->chain.next | jitc->chain.cond | jitc->chain.store) != 0u) {  // must be the chain this model calls
-    const MtgpJitChain want = jit_chain_for(*model, n_prog);
-    if (want.next != jitc->chain.next || want.cond != jitc->chain.cond || want.store != jitc->chain.store)
+  A.chain_merge = 0;
+  if (jit && (jitc->chain.next | jitc->chain.cond | jitc->chain.store | jitc->chain.put) != 0u) {
+    const MtgpJitChain want = jit_chain_for(*model, n_prog);  // must be the chain this model calls
+    if (want.next != jitc->chain.next || want.cond != jitc->chain.cond || want.store != jitc->chain.store ||
+        want.put != jitc->chain.put || (want.put != 0u && want.put_slot != jitc->chain.put_slot))
       return MTGP_ERR_ARG;
     A.chain_state = (want.next | want.cond) != 0u;
     A.chain_save = want.cond != 0u;
     A.chain_store = want.store != 0u;
+    A.chain_merge = want.put != 0u;
   }
   // (the wide-state SR kernel keeps its data vector in LDS: its code is built in kJitModeLds)
   hipStream_t s = (hipStream_t)stream;

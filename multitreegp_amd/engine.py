@@ -125,7 +125,8 @@ class DeviceEngine:
         earlier builds (read back asynchronously), and the evaluator checks the plan's status and
         size on the device, interpreting when the code is unusable.  Returns None when disabled."""
         chain = self.jit_chain(m, fl.n_prog) if fl.jit_words is not None else nat.MtgpJitChain(0, 0, 0)
-        key = (R, None if order is None else order.data_ptr(), id(self), (chain.next, chain.cond, chain.store))
+        key = (R, None if order is None else order.data_ptr(), id(self),
+               (chain.next, chain.cond, chain.store, chain.put, chain.put_slot))
         if fl.jit_key is not None and fl.jit_key[:4] == key:
             slot, gen = fl.jit_key[4:]
             if slot is None or self._arena_gen[slot] == gen:  # code still in place (or none was built)

@@ -6,7 +6,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-import sys
+import weakref
 
 import numpy as np
 
@@ -52,6 +52,17 @@ def load():
 
 def _ptr(a, t):
     return a.ctypes.data_as(t)
+
+
+class _Lease:
+    """Exports a pooled block (HostEvolver._output) as a fresh array; holds the block alive for as
+    long as any array on it exists."""
+    __slots__ = ("_block", "__array_interface__", "__weakref__")
+
+    def __init__(self, block: np.ndarray):
+        self._block = block
+        self.__array_interface__ = {"data": (block.ctypes.data, False), "shape": block.shape, "typestr": "<f4",
+                                    "version": 3}
 
 
 class HostEvolver:
@@ -114,22 +125,33 @@ class HostEvolver:
         return out
 
     def _output(self, shape) -> np.ndarray:
-        """The array evolve writes: a population this object returned earlier that nothing else
-        references any more (the user's loop has moved on to a newer generation), else a new one.
-        A fresh 537 MB C5 population costs more in first-touch page faults than the whole
-        evolution step; reusing a dead one keeps the reference's value semantics (no array the
-        caller can still see is ever overwritten)."""
-        for i in range(len(self._pool)):
-            a = self._pool[i]
-            # references: the pool's slot, `a` and getrefcount's argument -- none from the caller
-            # (a view of the array, e.g. a reshape or a torch tensor on it, holds one too)
-            if a.shape == shape and sys.getrefcount(a) == 3:
-                return a
-            del a
-        out = np.empty(shape, np.float32)
-        self._pool.append(out)
+        """The array evolve writes: the memory of a population this object returned earlier that
+        nothing references any more (the user's loop has moved on to a newer generation), else new
+        memory.  A fresh 537 MB C5 population costs more in first-touch page faults than the whole
+        evolution step; reusing dead memory keeps the reference's value semantics (no array the
+        caller can still see is ever overwritten).
+
+        Ownership, not reference counting: each returned array is built on a _Lease, a non-array
+        object exporting the pooled block through __array_interface__.  numpy stops base collapsing
+        at a non-array base, so every view, slice, reshape, memoryview or torch.from_numpy of the
+        returned array keeps the array -- and through it the lease -- alive; the pool holds the
+        block strongly and the lease only through a weakref, and reuses a block once its lease is
+        gone."""
+        for i, (block, lease) in enumerate(self._pool):
+            if block.shape == shape and lease() is None:
+                return self._lend(i, block)
+        block = np.empty(shape, np.float32)
+        self._pool.append((block, None))
+        out = self._lend(len(self._pool) - 1, block)
         if len(self._pool) > 3:
-            self._pool.pop(0)
+            self._pool.pop(0)  # an outstanding lease keeps its block alive by itself
+        return out
+
+    def _lend(self, i: int, block: np.ndarray) -> np.ndarray:
+        lease = _Lease(block)
+        self._pool[i] = (block, weakref.ref(lease))
+        out = np.asarray(lease)
+        assert out.base is lease and out.ctypes.data == block.ctypes.data
         return out
 
     def sample_population(self, pop_size: int, seed: int) -> np.ndarray:

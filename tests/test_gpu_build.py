@@ -201,8 +201,9 @@ def test_lds_mode_units_match_host_units(R, store, kind, emit, monkeypatch):
         assert np.array_equal(code[o[u] // 4: o[u] // 4 + w], host[:w]), u
 
 
+@pytest.mark.parametrize("form", ["merged", "cond"])
 @pytest.mark.parametrize("R", [4, 32])
-def test_chained_units_match_host_units(R):
+def test_chained_units_match_host_units(R, form):
     """Role chains (ABI v13): the device plan packs a chain member's successor right behind it
     (no alignment padding), every other unit starts on a 64-byte line, and the emitted code equals
     the host-built chained units word for word (the PC-relative literal of each sin/cos call
@@ -221,8 +222,10 @@ def test_chained_units_match_host_units(R):
     m.model, m.state_size, m.n_var, m.solver = nat.MODEL_ACROBOT_DYNAMIC, 2, 4, nat.SOLVER_RK4
     m.prog_state, m.prog_readout, m.prog_readout_save, m.readout_save_same = 1, 0, 3, -1
     ch = nat.MtgpJitChain()
-    assert L_.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0 and ch.next == 0b010
-    ch.next, ch.cond = 0b110, 0b100  # the ABI v13 form with the conditional save continuation (emitter test)
+    assert L_.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch)) == 0
+    assert (ch.next, ch.put, ch.put_slot) == (0b011, 0b001, 6)  # ABI v18: readout -> u slot -> state chain
+    if form == "cond":  # the ABI v13 form with the conditional save continuation (emitter test)
+        ch.next, ch.cond, ch.put, ch.put_slot = 0b110, 0b100, 0, 0
     order_np = np.random.default_rng(R).permutation(P).astype(np.int32)
     order = torch.from_numpy(order_np).cuda()
     n = L_.mtgp_jit_units(P, n_prog, R)

@@ -196,21 +196,42 @@ def test_evolve_never_overwrites_a_population_the_caller_holds():
                                elite_percentage=0.0, verbose=False)
     pop = gp.initialize_population(3)
     fit = np.random.default_rng(0).random((1, 20)).astype(np.float32)
+    import torch
     kept, snaps = [], []
     cur = pop
-    for g in range(6):
+    for g in range(10):
         cur = gp.evolve(cur, fit, 100 + g)
-        if g % 2 == 0:  # keep every other generation (and a view of one)
-            kept.append(cur if g != 2 else cur.reshape(-1))
+        if g % 2 == 0:  # keep every other generation, through the kinds of view a caller makes
+            hold = {0: lambda a: a, 2: lambda a: a.reshape(-1), 4: lambda a: np.asarray(a)[:, 1:][0],
+                    6: lambda a: torch.from_numpy(a), 8: lambda a: memoryview(a)}[g](cur)
+            kept.append(hold)
             snaps.append(cur.copy())
     for k, s in zip(kept, snaps):
-        assert np.array_equal(k.reshape(s.shape), s)
+        a = k.numpy() if isinstance(k, torch.Tensor) else np.asarray(k)
+        assert np.array_equal(a.reshape(-1), (s[:, 1:][0] if a.size != s.size else s).reshape(-1))
     # a released population is reused (no fresh allocation once the loop has warmed up)
-    ev = gp._evolver
-    ids = set()
+    blocks = set()
     cur = None
     for g in range(6):
         cur = gp.evolve(pop, fit, 200 + g)
-        ids.add(id(cur))
+        blocks.add(cur.ctypes.data)
         cur = None
-    assert len(ids) <= 2
+    assert len(blocks) <= 2
+
+
+@pytest.mark.parametrize("rtp,digests", [
+    ((1.0, 0.0, 0.0), ("cf77ed59b80e2aff", "e2e8ed97af983120", "35a8bb31cd0a003c")),
+    ((0.9, 0.1, 0.0), ("f02b338a65b441b4", "993f7c2cb0397115", "4fbf6b2af620dfbe")),
+])
+def test_evolve_golden_digest(rtp, digests):
+    """Pins the native evolution step bit for bit (the crossover's scan / splice_rows /
+    choose_prefix path): sha256 prefixes of three generations from fixed seeds -- all crossover,
+    and crossover + mutation, with ring migration every generation.  Recorded from the round-4
+    library (the crossover rewrite), so any later change to the draws or the splice shows here."""
+    import hashlib
+    ev = _evolver(_lib(), rtp=rtp, num_pop=2, migration_size=2, period=1)
+    pop = ev.sample_population(64, 7)
+    fit = np.random.default_rng(3).random((2, 64)).astype(np.float32)
+    for g in range(3):
+        pop = ev.evolve(pop, fit, 11 + g, g)
+        assert hashlib.sha256(np.ascontiguousarray(pop).tobytes()).hexdigest()[:16] == digests[g], g

@@ -590,10 +590,11 @@ def test_chain_masks():
     ch = nat.MtgpJitChain()
     m = _chain_model("dynamic")
     assert lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch)) == 0
-    assert (ch.next, ch.cond) == (0b010, 0)
+    # fixed step (ABI v18): readout -> u into data slot n_var + state_size -> the state programs
+    assert (ch.next, ch.cond, ch.put, ch.put_slot) == (0b011, 0, 0b001, 6)
     m.solver = nat.SOLVER_DOPRI5
     lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch))
-    assert (ch.next, ch.cond) == (0b010, 0)
+    assert (ch.next, ch.cond, ch.put) == (0b010, 0, 0)
     m = _chain_model("sr")
     lib_n.mtgp_jit_chain(ctypes.byref(m), 4, ctypes.byref(ch))
     assert (ch.next, ch.cond) == (0b0111, 0)
@@ -626,7 +627,7 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
     ch = nat.MtgpJitChain()
     lib_n.mtgp_jit_chain(ctypes.byref(_chain_model(kind)), n_prog, ctypes.byref(ch))
     if kind == "dynamic":  # the conditional continuation into the save-point readout (ABI v13 form)
-        ch.next, ch.cond = 0b110, 0b100
+        ch.next, ch.cond, ch.put, ch.put_slot = 0b110, 0b100, 0, 0
     first = roles["prog_state"]
     members = [j for j in range(n_prog) if ch.next >> j & 1] + [j for j in range(n_prog) if
                                                                  j > 0 and ch.next >> (j - 1) & 1 and
@@ -677,6 +678,68 @@ def test_role_chain_units_emulate_to_oracle(kind, R):
                     got = regs[reg, lane]
                     assert np.float32(got).view(np.uint32) == np.float32(want).view(np.uint32) or \
                         (np.isnan(got) and np.isnan(want)), (wave, lane, reg, got, want)
+
+
+@pytest.mark.parametrize("R", [32, 4, 64])
+def test_merged_readout_chain_emulates_to_oracle(R):
+    """The fixed-step dynamic policy's put chain (ABI v18, MtgpJitChain.put): the readout unit
+    computes u on [y, a, u, tar] with y and u folded to 0 and leaves it in v26 (its chain slot);
+    the state units it falls into read their data slot 6 (u) from v26 instead of v6 and return in
+    v27 / v28.  Emulated per wave against the oracle: u = readout([0, a, 0]), state_j =
+    tree_j([y, a, u]); v6 itself is never written (the call site's data registers are inputs)."""
+    lib, pop, n_data, _ = _setup("dynamic")
+    ff = mt.DynamicEvaluator(mt.Acrobot(0, 0), 2, 0.05, solver=mt.RK4())
+    prog, specs, roles, L = _host_flatten(ff, lib, pop[:24])
+    P, n_prog = prog.shape[:2]
+    order = np.random.default_rng(7).permutation(P).astype(np.int32)
+    lib_n = nat.load()
+    ch = nat.MtgpJitChain()
+    lib_n.mtgp_jit_chain(ctypes.byref(_chain_model("dynamic")), n_prog, ctypes.byref(ch))
+    assert ch.put == 1 and ch.put_slot == 6 and roles["prog_readout"] == 0 and roles["prog_state"] == 1
+    Rp = 1 << max(R - 1, 0).bit_length()
+    G = 64 // Rp
+    rng = np.random.default_rng(8)
+    out = np.zeros(1 << 16, np.uint32)
+    for wave in range(-(-P // G)):
+        data = (rng.standard_normal((8, 64)) * 2).astype(np.float32)
+        codes = []
+        for j in (0, 1, 2):
+            n = lib_n.mtgp_jit_unit_host_chain(prog.ctypes.data, P, n_prog, L, R, order.ctypes.data,
+                                               ctypes.byref(ch), wave * n_prog + j, out.ctypes.data, out.size, 0)
+            assert n > 0, n
+            codes.append([int(x) for x in out[:n]])
+            for ln in _disassemble(codes[-1]):
+                assert "invalid" not in ln.lower() and "exec" not in ln, ln
+                mm = re.fullmatch(r"v_\w+ v(\d+),.*", ln)
+                if mm:
+                    assert 8 <= int(mm.group(1)) <= 29, ln
+        regs = None
+        for c in codes:
+            try:
+                regs = _emulate(c, data, full=True, regs=regs)
+                break
+            except FellThrough as e:
+                regs = e.regs
+        else:
+            raise AssertionError("the chain never returned")
+        for lane in range(64):
+            q = wave * G + lane // Rp
+            if q >= P:
+                continue
+            d = data[:n_data, lane].copy()
+            t, nd, zm = specs[0][:3]
+            dz = d.copy()
+            for b in range(nd):
+                if zm >> b & 1:
+                    dz[b] = 0.0
+            u = orc.eval_tree(pop[order[q], t], lib.fn_codes, lib.n_funcs, lib.var_start, dz)
+            d[6] = u
+            got = [regs[26, lane], regs[27, lane], regs[28, lane]]
+            want = [u] + [orc.eval_tree(pop[order[q], specs[1 + k][0]], lib.fn_codes, lib.n_funcs, lib.var_start, d)
+                             for k in range(2)]
+            for g_, w_ in zip(got, want):
+                assert np.float32(g_).view(np.uint32) == np.float32(w_).view(np.uint32) or \
+                    (np.isnan(g_) and np.isnan(w_)), (wave, lane, got, want)
 
 
 @pytest.mark.parametrize("R", [8, 64])
@@ -992,3 +1055,23 @@ def test_unary_subroutines_abi_clean():
                 continue
             assert dst in ("vcc", "s[34:35]", "s38"), (name, ln)
     assert _disassemble(BLOBS["ABS"]) == ["v_and_b32_e32 v8, 0x7fffffff, v8"]
+
+
+def test_subroutine_cost_counts_match_blobs():
+    """The schedule's per-call cost (mtgp_jit.h kJit*Exec = WORDS - SKIPPABLE_WORDS) counts exactly
+    the words up to each subroutine's return: sin / cos keep their Payne-Hanek reduction after the
+    return (skippable), exp / log / tanh / sqrt are branch-free (no s_cbranch; 0 skippable)."""
+    text = open(os.path.join(ROOT, "multitreegp_amd", "csrc", "mtgp_jit_blobs.h")).read()
+    for name in ("SIN", "COS", "EXP", "LOG", "TANH", "SQRT"):
+        words = int(re.search(rf"#define MTGP_JIT_{name}_WORDS (\d+)", text).group(1))
+        skip = int(re.search(rf"#define MTGP_JIT_{name}_SKIPPABLE_WORDS (\d+)", text).group(1))
+        blob = re.search(rf"mtgp_jit_{name.lower()}_blob\[\d+\] = \{{(.*?)\}};", text).group(1)
+        ws = [int(w.strip().rstrip("u"), 16) for w in blob.split(",")]
+        assert len(ws) == words
+        ret = ws.index(0xBE801D28)  # s_setpc_b64 s[40:41]
+        assert skip == words - ret - 1
+        listing = text[text.index(f"// {name}:"):text.index(f"#define MTGP_JIT_{name}_WORDS")]
+        if name in ("SIN", "COS"):
+            assert skip > 100 and "s_cbranch" in listing
+        else:
+            assert skip == 0 and "s_cbranch" not in listing

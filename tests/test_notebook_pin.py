@@ -328,13 +328,14 @@ def _dyn_box(lib, make, c, n, seed=7):
     return np.stack([_dyn_candidate(lib, make, [v + rng.uniform(-0.005, 0.005) for v in c]) for _ in range(n)])
 
 
-def _dyn_ensemble(name, max_steps, n_ulp=16, n_box=32):
+def _dyn_ensemble(name, max_steps, n_ulp=16, n_box=32, dp_alt=0):
     """fitness of the pinned candidate over a one-ulp x0 ensemble (central coefficients) and over
-    its coefficient rounding box (notebook data)"""
+    its coefficient rounding box (notebook data); dp_alt: an oracle-only alternative reading of a
+    diffrax rule (OR_DP_ALT_*, scripts/dp_gap_study.py)"""
     make, c, _ = DYNAMIC_PINS[name]
     env, lib, ff, data, _ = dynamic_notebook(max_steps)
     d = ff.prepare(data)
-    model = oracle_model(ff, d)
+    model = dict(oracle_model(ff, d), dp_alt=dp_alt)
     pop = _dyn_candidate(lib, make, c)[None]
     ulp = [orc.evaluate(model, pop, lib, oracle_rollouts(_perturbed(d, 100 + s)))["fitness"][0] for s in range(n_ulp)]
     box = orc.evaluate(model, _dyn_box(lib, make, c, n_box), lib, oracle_rollouts(d))["fitness"]
@@ -397,8 +398,31 @@ def test_dynamic_notebook_printed_best_in_ensemble_tail(name):
     assert relaxed.mean() - printed < 4.0 * relaxed.std() + 1.0, (name, relaxed.mean(), relaxed.std())
     notebook = _dyn_ensemble(name, 1000)
     assert printed <= notebook.max()
+    # the recorded, unexplained gap at the notebook's max_steps (DESIGN.md "Parity pins": every
+    # published-behaviour reading of diffrax leaves it; test_dynamic_notebook_gap_readings)
     gap = {"gen5": (25.0, 35.0), "gen30": (3.0, 9.0), "gen50": (-1.0, 2.0)}[name]  # measured: 28.3 / 5.4 / -0.6
     assert gap[0] <= notebook.min() - printed <= gap[1], (name, notebook.min(), printed)
+
+
+# oracle-only alternative readings (oracle/mtgp_oracle.c OR_DP_ALT_*)
+DP_ALT = {"eo6": 1, "fsal_t1": 2, "dtmin_attempt": 4, "sum_literal": 8, "norm_x": 16, "maxsteps_acc": 32,
+          "event_all": 64, "interp_t0": 128}
+
+
+@pytest.mark.parametrize("name", ["gen5", "gen30"])
+def test_dynamic_notebook_gap_readings(name):
+    """The gap study (scripts/dp_gap_study.py) in test form, at max_steps 1000:
+    under the spec and under the readings diffrax demonstrably follows (or that only move the last
+    bits) the printed value stays below the whole ensemble; only the two readings that contradict
+    diffrax's published loop -- the error norm without the hidden state, max_steps counting accepted
+    steps only -- put it inside the ensemble's lower tail.  The cause of the gap is unresolved."""
+    printed = DYNAMIC_PINS[name][2]
+    for alt in ("eo6", "fsal_t1", "dtmin_attempt", "interp_t0"):
+        ens = _dyn_ensemble(name, 1000, n_ulp=8, n_box=16, dp_alt=DP_ALT[alt])
+        assert printed < ens.min(), (name, alt, ens.min())
+    for alt in ("norm_x", "maxsteps_acc"):
+        ens = _dyn_ensemble(name, 1000, n_ulp=16, n_box=32, dp_alt=DP_ALT[alt])
+        assert ens.min() <= printed + 0.5 and printed <= ens.mean(), (name, alt, ens.min(), ens.mean())
 
 
 @pytest.mark.gpu
