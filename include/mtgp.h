@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 18
+#define MTGP_ABI_VERSION 19
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -434,6 +434,38 @@ int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, 
 int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
                   const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
                   float* scratch, float* loss_out, float* grad_out, void* stream);
+
+/* ABI v19: the gradient programs as dual-number machine code (multitreegp_amd/csrc/mtgp_jit_dual.h):
+ * value and tangent of every program instruction in registers, operation for operation the dual
+ * interpreter (results bit-identical), the coefficients theta baked in as literals -- the code is
+ * emitted on the stream by the call itself (count, scan, emit: a few microseconds), no host
+ * round trip.  code: executable device memory from mtgp_jit_alloc; code_bytes: its size, at
+ * least MTGP_GRAD_JIT_BYTES(P, n_prog, L) suffices for any program; offsets: device uint32
+ * [P * n_prog + 1]; info: device int32 [2], written by the call ([0] < 0: some program does not
+ * translate, [1]: bytes the code needs).  When the code does not fit or a program does not
+ * translate, the kernel interprets (same results, slower).  jit == NULL or jit->code == NULL:
+ * exactly mtgp_ctl_grad. */
+typedef struct {
+  void* code;
+  size_t code_bytes;
+  uint32_t* offsets;
+  int32_t* info;
+} MtgpGradJit;
+#define MTGP_GRAD_JIT_WORDS_PER_INSTR 64
+#define MTGP_GRAD_JIT_BYTES(P, n_prog, L) \
+  (65536u + (size_t)(P) * (size_t)(n_prog) * ((size_t)(L) * 4u * MTGP_GRAD_JIT_WORDS_PER_INSTR + 64u))
+int mtgp_ctl_grad_jit(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                      const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
+                      float* scratch, float* loss_out, float* grad_out, const MtgpGradJit* jit, void* stream);
+/* the same for the SR gradient (mtgp_sr_grad): code for n_var <= 4 (the register-state kernels;
+ * wider states interpret) */
+int mtgp_sr_grad_jit(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                     const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
+                     float* scratch, float* loss_out, float* grad_out, const MtgpGradJit* jit, void* stream);
+/* host translation of one program in dual numbers (D data slots <= 8, K coefficients theta):
+ * words written (out == NULL: counted), or < 0 (untranslatable / out too short) */
+int mtgp_jit_dual_translate_host(const MtgpInstr* prog, int32_t L, int32_t D, const float* theta, int32_t K,
+                                 uint32_t base, uint32_t* out, int32_t max_words);
 
 /* Wall time of the calling thread's last timed mtgp_eval_rk4 kernel (ms), measured with
  * hipEvents recorded on its stream around the launch; -1 if none.  Synchronises that event.

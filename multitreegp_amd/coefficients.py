@@ -37,8 +37,9 @@ filter, tests/test_coefficients.py): median relative error 7e-4, 75th percentile
 from __future__ import annotations
 
 import ctypes
+import os
 from dataclasses import dataclass
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -139,9 +140,13 @@ class CoefficientOptimiser:
     """GeneticProgramming.optimise on the GPU for one evaluator config (a DeviceEngine with
     size_parsinomy 0: the loss is the evaluator's fitness, gp.py:447)."""
 
-    def __init__(self, engine):
+    def __init__(self, engine, jit: Optional[bool] = None):
         self.check_evaluator(engine.ff)
         self.engine = engine
+        # the control evaluators' programs as dual-number machine code (mtgp_ctl_grad_jit, ABI v19):
+        # on with the engine's program JIT unless disabled here or by MTGP_GRAD_JIT=0
+        self.use_jit = (engine.use_jit and os.environ.get("MTGP_GRAD_JIT", "1") != "0") if jit is None else bool(jit)
+        self.last_jit_info = None  # device int32 [2] of the last call: [0] < 0 untranslatable, [1] bytes used
 
     @staticmethod
     def check_evaluator(ff):
@@ -220,8 +225,19 @@ class CoefficientOptimiser:
             scratch = torch.empty((B * K * R * 2,), dtype=torch.float32, device=dev)
             lo_d = torch.empty((B,), dtype=torch.float32, device=dev)
             gr_d = torch.empty((B, K), dtype=torch.float32, device=dev)
-            rc = grad_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
-                         ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), stream)
+            if self.use_jit and (eng.ff.model_id != nat.MODEL_SR or n_data <= 4):
+                code, nbytes = eng.grad_code_buffer(nat.grad_jit_bytes(B, n_prog, L))
+                offs = torch.empty((B * n_prog + 1,), dtype=torch.int32, device=dev)
+                info = torch.empty((2,), dtype=torch.int32, device=dev)
+                gj = nat.MtgpGradJit(code, nbytes, offs.data_ptr(), info.data_ptr())
+                jit_fn = eng.native.mtgp_sr_grad_jit if eng.ff.model_id == nat.MODEL_SR else eng.native.mtgp_ctl_grad_jit
+                rc = jit_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
+                            ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), ctypes.byref(gj),
+                            stream)
+                self.last_jit_info = info
+            else:
+                rc = grad_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
+                             ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), stream)
             if rc != nat.OK:
                 raise RuntimeError(f"{grad_fn.__name__} rejected the configuration (code {rc})")
             g = gr_d.cpu().numpy()

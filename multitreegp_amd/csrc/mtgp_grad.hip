@@ -20,6 +20,7 @@
 #include "mtgp_dual.h"
 #include "mtgp_dopri5.h"
 #include "mtgp_cstep.h"
+#include "mtgp_jit_dual.h"
 
 namespace {
 
@@ -68,7 +69,42 @@ struct GradArgs {
   float* part;            // [P, K, R, 2] per-rollout (F, dF/dtheta_k)
   float* loss;            // [P]
   float* grad;            // [P, K]
+  // dual-number program code (mtgp_jit_dual.h; mtgp_ctl_grad_jit), or null: interpret
+  const uint8_t* jit_code;
+  const uint32_t* jit_offs;  // [P * n_prog + 1] byte offsets of the units
+  const int32_t* jit_info;   // [2]: [0] < 0 some program untranslatable, [1] bytes the code needs
+  uint64_t jit_bytes;
 };
+
+// The code of this launch is usable: every program translated and the buffer large enough
+// (device-side check, no host round trip; otherwise the interpreter runs)
+__device__ __forceinline__ bool dual_jit_ok(const GradArgs& A) {
+  if (!A.jit_code) return false;
+  const int32_t e = __builtin_amdgcn_readfirstlane(A.jit_info[0]), b = __builtin_amdgcn_readfirstlane(A.jit_info[1]);
+  return e == 0 && b > 0 && (uint64_t)(uint32_t)b <= A.jit_bytes;
+}
+// code address of program j of individual p (wave-uniform)
+__device__ __forceinline__ uint64_t dual_unit(const GradArgs& A, int p, int j) {
+  const uint32_t off = A.jit_offs[(size_t)p * A.n_prog + j];
+  return (uint64_t)(uintptr_t)A.jit_code + (uint32_t)__builtin_amdgcn_readfirstlane((int)off);
+}
+// Call one dual unit: data values v0-v7, tangents v48-v55, the lane's coefficient index in v25;
+// result (value, tangent) in (v8, v56).  Clobbers: mtgp_jit_dual.h's register ABI.
+__device__ __forceinline__ Dual dual_call(uint64_t addr_, const float (&dv)[8], const float (&dd)[8], int kk) {
+  const uint64_t addr = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)addr_) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(addr_ >> 32)) << 32;
+  float v, d;
+  asm volatile("s_swappc_b64 s[30:31], %[tgt]"
+               : "={v8}"(v), "={v56}"(d)
+               : [tgt] "s"(addr), "{v0}"(dv[0]), "{v1}"(dv[1]), "{v2}"(dv[2]), "{v3}"(dv[3]), "{v4}"(dv[4]),
+                 "{v5}"(dv[5]), "{v6}"(dv[6]), "{v7}"(dv[7]), "{v48}"(dd[0]), "{v49}"(dd[1]), "{v50}"(dd[2]),
+                 "{v51}"(dd[3]), "{v52}"(dd[4]), "{v53}"(dd[5]), "{v54}"(dd[6]), "{v55}"(dd[7]), "{v25}"(kk)
+               : "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19", "v20", "v21",
+                 "v22", "v23", "v24", "v26", "v27", "v28", "v29", "v57", "v58", "v59", "v60", "v61", "v62",
+                 "v63", "v64", "s30", "s31", "s34", "s35", "s36", "s37", "s38", "s39", "s40", "s41", "s42",
+                 "s43", "s44", "s45", "vcc", "scc", "memory");
+  return {v, d};
+}
 
 // Lane (individual p, parameter k, rollout r).  Each individual owns K * R lanes rounded up to
 // whole waves, so every wave belongs to ONE individual: its programs and coefficients are
@@ -228,6 +264,7 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
     return;
   }
   const int kk = k < np ? k : -1;
+  const bool use_jit = NV <= 4 && dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
   const int nv = A.m.n_var;
   const float* th = A.theta + (size_t)p * A.K;
   const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
@@ -262,12 +299,36 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
         sv[i] = stage == 0 ? x[i] : mtgp_rk4_in(stage, x[i], kx[i], dt);
         sd[i] = stage == 0 ? dx[i] : mtgp_rk4_in(stage, dx[i], dkx[i], dt);
       }
+      if constexpr (NV <= 4) {  // one program site: the dual-number code (mtgp_jit_dual.h) or the interpreter
+#pragma unroll 1
+        for (int i = 0; i < nv; ++i) {
+          Dual o;
+          if (use_jit) {
+            float dv8[8], dd8[8];
 #pragma unroll
-      for (int i = 0; i < NV; ++i) {
-        if (i >= nv) continue;
-        const Dual o = run_dual<NV>(progs + (size_t)i * A.L, sv, sd, nv, th, kk);
-        kx[i] = o.v;
-        dkx[i] = o.d;
+            for (int c = 0; c < 8; ++c) {
+              dv8[c] = c < NV ? sv[c < NV ? c : 0] : 0.0f;
+              dd8[c] = c < NV ? sd[c < NV ? c : 0] : 0.0f;
+            }
+            o = dual_call(dual_unit(A, p, A.m.prog_state + i), dv8, dd8, kk);
+          } else {
+            o = run_dual<NV>(progs + (size_t)i * A.L, sv, sd, nv, th, kk);
+          }
+#pragma unroll
+          for (int c = 0; c < NV; ++c)
+            if (c == i) {
+              kx[c] = o.v;
+              dkx[c] = o.d;
+            }
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) {
+          if (i >= nv) continue;
+          const Dual o = run_dual<NV>(progs + (size_t)i * A.L, sv, sd, nv, th, kk);
+          kx[i] = o.v;
+          dkx[i] = o.d;
+        }
       }
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -347,6 +408,7 @@ __global__ void __launch_bounds__(kGradBlock) k_sr_grad_dp(GradArgs A) {
     return;
   }
   const int kk = k < np ? k : -1;
+  const bool use_jit = NV <= 4 && dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
   const int nv = A.m.n_var;
   const float* th = A.theta + (size_t)p * A.K;
   const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
@@ -380,7 +442,18 @@ __global__ void __launch_bounds__(kGradBlock) k_sr_grad_dp(GradArgs A) {
     auto rhs = [&](const float (&xv)[NV], const float (&xd)[NV]) {
 #pragma unroll 1
       for (int i = 0; i < nv; ++i) {
-        const Dual o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
+        Dual o;
+        if (use_jit) {
+          float dv8[8], dd8[8];
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            dv8[c] = c < NV ? xv[c < NV ? c : 0] : 0.0f;
+            dd8[c] = c < NV ? xd[c < NV ? c : 0] : 0.0f;
+          }
+          o = dual_call(dual_unit(A, p, A.m.prog_state + i), dv8, dd8, kk);
+        } else {
+          o = run_dual<NV>(progs + (size_t)i * A.L, xv, xd, nv, th, kk, stk);
+        }
 #pragma unroll
         for (int c = 0; c < NV; ++c)
           if (c == i) {
@@ -718,6 +791,7 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   const uint32_t* key = A.ro.obs_keys ? A.ro.obs_keys + 2 * (size_t)r : nullptr;
   // the data vector of a program call, and its reader
   float dvv[kCtlData], dvd[kCtlData];
+  const bool use_jit = dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
   auto V = [&](uint32_t off) -> Dual {
     const int sl = (int)(off / MTGP_SLOT_BYTES);
     if (sl < D) {
@@ -813,7 +887,8 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
           if (i < no) put(i, y[i]);
         put(no + NA, u);
       }
-      const Dual o = run_dual_src(q == 0 ? p_read : p_state + (size_t)(q - 1) * A.L, V, stk);
+      const Dual o = use_jit ? dual_call(dual_unit(A, p, q == 0 ? A.m.prog_readout : A.m.prog_state + q - 1), dvv, dvd, kk)
+                             : run_dual_src(q == 0 ? p_read : p_state + (size_t)(q - 1) * A.L, V, stk);
       if (q == 0) u = o;
 #pragma unroll
       for (int j = 0; j < (DYN ? NA : 1); ++j)
@@ -843,12 +918,14 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
 #pragma unroll
       for (int j = 0; j < kCtlData; ++j)
         if (j < nt) put(no + NA + 1 + j, {tg[j], 0.0f});
-      u = run_dual_src(p_save, V, stk);  // dyn.py:101 [y, a, 0, tg]
+      u = use_jit ? dual_call(dual_unit(A, p, A.m.prog_readout_save), dvv, dvd, kk)
+                  : run_dual_src(p_save, V, stk);  // dyn.py:101 [y, a, 0, tg]
     } else {
 #pragma unroll
       for (int j = 0; j < kCtlData; ++j)
         if (j < nt) put(no + j, {tg[j], 0.0f});
-      u = run_dual_src(p_read, V, stk);  // ff.py:97
+      u = use_jit ? dual_call(dual_unit(A, p, A.m.prog_readout), dvv, dvd, kk)
+                  : run_dual_src(p_read, V, stk);  // ff.py:97
     }
     if constexpr (ENV == 0) {
       const MtgpDual ud = tod(u);
@@ -1062,7 +1139,113 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   out[1] = dF;
 }
 
+// ---- dual-number program code (mtgp_jit_dual.h): count, scan, subroutines, emit --------------
+// Units: one per (individual p, program j), each starting on a 64-byte line; the shared
+// subroutines (sin, cos, exp, log, tanh, sqrt) at the start of the buffer.  All on the stream, no
+// host round trip: the gradient kernel checks info and interprets when the code is unusable.
+struct DualJitArgs {
+  const MtgpInstr* prog;
+  int n_prog, L, P, K, D;
+  const float* theta;  // [P, K]
+};
+constexpr uint32_t kDualAlign = 64u;
+
+__global__ void __launch_bounds__(256) k_dual_count(DualJitArgs J, uint32_t* __restrict__ offs,
+                                                    int32_t* __restrict__ info) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= J.P * J.n_prog) return;
+  const int p = u / J.n_prog;
+  const int n = mtgp::jit_dual_words(J.prog + (size_t)u * J.L, J.L, J.D, J.theta + (size_t)p * J.K, J.K);
+  offs[u] = n > 0 ? ((uint32_t)n * 4u + kDualAlign - 1u) & ~(kDualAlign - 1u) : 0u;
+  if (n < 0) atomicMin(&info[0], n);
+}
+
+// exclusive scan of the unit spans in place (after the subroutine area); offs[total], info[1] = bytes
+__global__ void __launch_bounds__(1024) k_dual_scan(uint32_t* __restrict__ offs, int total, int32_t* __restrict__ info) {
+  __shared__ uint64_t part[1024];
+  const int t = threadIdx.x;
+  const int per = (total + 1023) / 1024;
+  const int b = t * per, e = b + per < total ? b + per : total;
+  uint64_t sum = 0;
+  for (int i = b; i < e; ++i) sum += offs[i];
+  part[t] = sum;
+  __syncthreads();
+  for (int d = 1; d < 1024; d <<= 1) {
+    const uint64_t v = t >= d ? part[t - d] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  const uint64_t sub = (mtgp::kJitTemplateBytes + kDualAlign - 1u) & ~(uint64_t)(kDualAlign - 1u);
+  uint64_t run = part[t] - sum + sub;
+  for (int i = b; i < e; ++i) {
+    const uint64_t w = offs[i];
+    offs[i] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+    run += w;
+  }
+  if (t == 1023) {
+    const uint64_t tot = part[1023] + sub;
+    offs[total] = (uint32_t)(tot < 0xffffffffull ? tot : 0xffffffffull);
+    info[1] = (int32_t)(tot < 0x7fffffffull ? tot : 0x7fffffffull);
+  }
+}
+
+__global__ void __launch_bounds__(256) k_dual_templates(uint32_t* __restrict__ code, uint64_t code_bytes) {
+  if (code_bytes < mtgp::kJitTemplateBytes) return;
+  for (int i = threadIdx.x; i < MTGP_JIT_SUB_WORDS; i += blockDim.x) code[i] = mtgp_jit_sub_blob[i];
+}
+
+__global__ void __launch_bounds__(256) k_dual_emit(DualJitArgs J, const uint32_t* __restrict__ offs,
+                                                   uint32_t* __restrict__ code, uint64_t code_bytes) {
+  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= J.P * J.n_prog) return;
+  const uint32_t b = offs[u], e = offs[u + 1];
+  if (e <= b || (uint64_t)e > code_bytes) return;  // untranslatable or short buffer (checked on use)
+  const int p = u / J.n_prog;
+  mtgp::JitOut o{code + b / 4, 0};
+  o.base = b;
+  mtgp::jit_dual_program(o, J.prog + (size_t)u * J.L, J.L, J.D, J.theta + (size_t)p * J.K, J.K);
+}
+
 }  // namespace
+
+// Emit the dual code of a launch (or do nothing without a buffer); fills A's jit fields.
+static int dual_jit_prepare(GradArgs& A, const MtgpGradJit* jit, int D, hipStream_t s) {
+  A.jit_code = nullptr;
+  A.jit_offs = nullptr;
+  A.jit_info = nullptr;
+  A.jit_bytes = 0;
+  if (!jit || !jit->code) return MTGP_OK;
+  if (!jit->offsets || !jit->info || jit->code_bytes < mtgp::kJitTemplateBytes) return MTGP_ERR_ARG;
+  const int units = A.P * A.n_prog;
+  DualJitArgs J{A.prog, A.n_prog, A.L, A.P, A.K, D, A.theta};
+  if (hipMemsetAsync(jit->info, 0, 2 * sizeof(int32_t), s) != hipSuccess) return MTGP_ERR_LAUNCH;
+  const dim3 g((unsigned)((units + 255) / 256)), b(256);
+  hipLaunchKernelGGL(k_dual_count, g, b, 0, s, J, jit->offsets, jit->info);
+  hipLaunchKernelGGL(k_dual_scan, dim3(1), dim3(1024), 0, s, jit->offsets, units, jit->info);
+  hipLaunchKernelGGL(k_dual_templates, dim3(1), dim3(256), 0, s, (uint32_t*)jit->code, (uint64_t)jit->code_bytes);
+  hipLaunchKernelGGL(k_dual_emit, g, b, 0, s, J, jit->offsets, (uint32_t*)jit->code, (uint64_t)jit->code_bytes);
+  if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
+  A.jit_code = (const uint8_t*)jit->code;
+  A.jit_offs = jit->offsets;
+  A.jit_info = jit->info;
+  A.jit_bytes = jit->code_bytes;
+  return MTGP_OK;
+}
+
+// host translation of one program in dual numbers (tests: the emulator runs it)
+extern "C" int mtgp_jit_dual_translate_host(const MtgpInstr* prog, int32_t L, int32_t D, const float* theta, int32_t K,
+                                            uint32_t base, uint32_t* out, int32_t max_words) {
+  if (!prog || L <= 0 || (K > 0 && !theta)) return MTGP_ERR_ARG;
+  const int n = mtgp::jit_dual_words(prog, L, D, theta, K);
+  if (n < 0) return n;
+  if (!out) return n;
+  if (n > max_words) return MTGP_ERR_ARG;
+  mtgp::JitOut o{out, 0};
+  o.base = base;
+  mtgp::jit_dual_program(o, prog, L, D, theta, K);
+  return o.n;
+}
 
 static bool grad_args(GradArgs& A, const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
                       const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro, float* scratch,
@@ -1079,12 +1262,17 @@ static bool grad_args(GradArgs& A, const MtgpModel* model, const MtgpInstr* prog
   A.part = scratch;
   A.loss = loss_out;
   A.grad = grad_out;
+  A.jit_code = nullptr;
+  A.jit_offs = nullptr;
+  A.jit_info = nullptr;
+  A.jit_bytes = 0;
   return true;
 }
 
-extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
-                             const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
-                             float* scratch, float* loss_out, float* grad_out, void* stream) {
+extern "C" int mtgp_ctl_grad_jit(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L,
+                                 int32_t P, const float* theta, const int32_t* nparam, int32_t K,
+                                 const MtgpRollouts* ro, float* scratch, float* loss_out, float* grad_out,
+                                 const MtgpGradJit* jit, void* stream) {
   if (!model || !prog || !ro || !nparam || !scratch || !loss_out || !grad_out || P < 0 || K < 1 || L <= 0 ||
       n_prog <= 0 || !theta)
     return MTGP_ERR_ARG;
@@ -1110,6 +1298,8 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
   GradArgs A;
   grad_args(A, model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out);
   hipStream_t s = (hipStream_t)stream;
+  const int jrc = dual_jit_prepare(A, jit, D, s);
+  if (jrc != MTGP_OK) return jrc;
   const long lanes = (long)P * grad_lanes_per(K, ro->R);  // whole waves per individual (grad_lane)
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
 #define MTGP_CG2(E, DPV)                                                                  \
@@ -1133,9 +1323,17 @@ extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int3
   return MTGP_OK;
 }
 
-extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
-                            const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
-                            float* scratch, float* loss_out, float* grad_out, void* stream) {
+extern "C" int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                             const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
+                             float* scratch, float* loss_out, float* grad_out, void* stream) {
+  return mtgp_ctl_grad_jit(model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out, nullptr,
+                           stream);
+}
+
+extern "C" int mtgp_sr_grad_jit(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L,
+                                int32_t P, const float* theta, const int32_t* nparam, int32_t K,
+                                const MtgpRollouts* ro, float* scratch, float* loss_out, float* grad_out,
+                                const MtgpGradJit* jit, void* stream) {
   if (!model || !prog || !ro || !nparam || !scratch || !loss_out || !grad_out || P < 0 || K < 1 || L <= 0 ||
       n_prog <= 0 || (K > 0 && !theta))
     return MTGP_ERR_ARG;
@@ -1162,6 +1360,9 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
   A.loss = loss_out;
   A.grad = grad_out;
   hipStream_t s = (hipStream_t)stream;
+  // dual-number code for the register-state kernels (n_var <= 4: data slots = the state)
+  const int jrc = dual_jit_prepare(A, model->n_var <= 4 ? jit : nullptr, model->n_var, s);
+  if (jrc != MTGP_OK) return jrc;
   const long lanes = (long)P * grad_lanes_per(K, ro->R);  // whole waves per individual (grad_lane)
   const dim3 grid((unsigned)((lanes + 255) / 256)), block(256);
   const int nv = model->n_var;
@@ -1178,4 +1379,11 @@ extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32
   hipLaunchKernelGGL(k_grad_reduce, dim3((unsigned)(((long)P * K + 255) / 256)), dim3(256), 0, s, A);
   if (hipGetLastError() != hipSuccess) return MTGP_ERR_LAUNCH;
   return MTGP_OK;
+}
+
+extern "C" int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
+                            const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* ro,
+                            float* scratch, float* loss_out, float* grad_out, void* stream) {
+  return mtgp_sr_grad_jit(model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out, nullptr,
+                          stream);
 }

@@ -438,6 +438,14 @@ struct AcroFit {
   float csum, c0incl, F;
 };
 
+// A read-only per-launch table (ts) read through the constant address space: a wave-uniform index
+// becomes a scalar load (scalar cache, lgkm wait) instead of a vector load with a vmcnt wait -- the
+// compiler cannot prove a plain pointer unwritten by the kernel's stores.  Nothing on the device
+// writes these tables, so the scalar cache sees them coherently.  (A divergent index still gets a
+// vector load.)
+__device__ __forceinline__ float ldc(const float* p, int i) {
+  return ((const __attribute__((address_space(4))) float*)p)[i];
+}
 __device__ __forceinline__ bool save_incl(const float* ts, int k);
 // incl (acrobot.py:82's mask at save k, save_incl) is needed only at save 0 and at a lane's first
 // success: it is evaluated there (a division and three loads) instead of at every save point
@@ -528,8 +536,8 @@ __device__ __forceinline__ void acro_fit_general(AcroFit& f, int k, int S, const
 }
 
 __device__ __forceinline__ bool save_incl(const float* ts, int k) {
-  const float dts = ts[1] - ts[0];
-  return !((ts[k] / dts) > (float)k);
+  const float dts = ldc(ts, 1) - ldc(ts, 0);
+  return !((ldc(ts, k) / dts) > (float)k);
 }
 
 // --------------------------------------------------------------------------------------
@@ -830,8 +838,8 @@ struct CsClock {
   float t, tn, t_end, dt0;
   int steps, max_steps;
   __device__ __forceinline__ void init(const KArgs& A) {
-    t = A.ro.ts[0];
-    t_end = A.ro.ts[A.m.n_save - 1];
+    t = ldc(A.ro.ts, 0);
+    t_end = ldc(A.ro.ts, A.m.n_save - 1);
     dt0 = A.m.h;
     tn = mtgp_cs_first_end(t, dt0, t_end);
     steps = 0;
@@ -847,7 +855,7 @@ struct CsClock {
     tn = mtgp_cs_next_end(t, dt0, t_end);
   }
   // save point k is taken in this step (ts[k] <= tn; k < S checked by the caller)
-  __device__ __forceinline__ bool saves(const float* ts, int k) const { return uni((int)(ts[k] <= tn)) != 0; }
+  __device__ __forceinline__ bool saves(const float* ts, int k) const { return uni((int)(ldc(ts, k) <= tn)) != 0; }
 };
 
 // RK4 stage input (stage 0: s itself; stages 1..3: s + (a f) dt, a = 0.5, 0.5, 1) and the running
@@ -1243,9 +1251,9 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   auto save_point = [&](int k, const float (&xs)[NV], const float (&as)[NA], bool fill) __attribute__((always_inline)) {
     float yo[NV];
     if (NOISE) {
-      const uint32_t tb = __float_as_uint(ts[k]);
+      const uint32_t tb = __float_as_uint(ldc(ts, k));
       if (tb != nzt) {  // (the noise of ts[k] is drawn unless the last stage was at that very time)
-        obs_noise_vec<NV>(nzc, ts[k], nzv);
+        obs_noise_vec<NV>(nzc, ldc(ts, k), nzv);
         nzt = tb;
       }
     }
@@ -1341,7 +1349,7 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
     }
     // SaveAt(ts): every pending ts[k] <= tn through this step's dense output
     while (k < S && clk.saves(ts, k)) {
-      const float th = mtgp_cs_rescale(t, ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(t, ldc(ts, k), clk.tn);
       float xs[NV], as[NA];
       cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
       cs_dense<NA>(NST == 1, dead, a, a1, fa0, ka, dt, th, as);
@@ -1445,7 +1453,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   // save-point readout on [y, a, 0, tar] (dyn.py:101), fitness, rows
   auto save_point = [&](int k, const float (&xs)[NV], const float (&as)[NA], bool fill) __attribute__((always_inline)) {
     float yo[NV];
-    ctl_obs<Env, NOISE>(nzc, A.ro.ts[k], xs, yo);
+    ctl_obs<Env, NOISE>(nzc, ldc(A.ro.ts, k), xs, yo);
 #pragma unroll
     for (int i = 0; i < NV; ++i) D.put(i, yo[i]);
 #pragma unroll
@@ -1531,7 +1539,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       prev_ok = ok;
     }
     while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
-      const float th = mtgp_cs_rescale(t, A.ro.ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(t, ldc(A.ro.ts, k), clk.tn);
       float xs[NV], as[NA];
       cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
       cs_dense<NA>(euler, dead, a, a1, fa0, ka, dt, th, as);
@@ -1605,9 +1613,9 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   auto save_point = [&](int k, const float (&xs)[NV], bool fill) __attribute__((always_inline)) {
     float yo[NV];
     if (NOISE) {
-      const uint32_t tb = __float_as_uint(ts[k]);
+      const uint32_t tb = __float_as_uint(ldc(ts, k));
       if (tb != nzt) {
-        obs_noise_vec<NV>(nzc, ts[k], nzv);
+        obs_noise_vec<NV>(nzc, ldc(ts, k), nzv);
         nzt = tb;
       }
     }
@@ -1671,7 +1679,7 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
       prev_ok = ok;
     }
     while (k < S && clk.saves(ts, k)) {
-      const float th = mtgp_cs_rescale(t, ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(t, ldc(ts, k), clk.tn);
       float xs[NV];
       cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
       save_point(k, xs, dead);
@@ -1748,7 +1756,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   // one save point: ys = f_obs(key, (ts[k], xs)) (ff.py:96), us = policy([ys, tar]) (ff.py:97)
   auto save_point = [&](int k, const float (&xs)[NV], bool fill) __attribute__((always_inline)) {
     float yo[NV];
-    ctl_obs<Env, NOISE>(nzc, A.ro.ts[k], xs, yo);
+    ctl_obs<Env, NOISE>(nzc, ldc(A.ro.ts, k), xs, yo);
 #pragma unroll
     for (int i = 0; i < NV; ++i) D.put(i, yo[i]);
     float ur[1];
@@ -1808,7 +1816,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       prev_ok = ok;
     }
     while (k < S && clk.saves(A.ro.ts, k)) {
-      const float th = mtgp_cs_rescale(t, A.ro.ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(t, ldc(A.ro.ts, k), clk.tn);
       float xs[NV];
       cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
       save_point(k, xs, dead);
@@ -2241,7 +2249,7 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
       prev_ok = ok;
     }
     while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
-      const float th = mtgp_cs_rescale(clk.t, A.ro.ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(clk.t, ldc(A.ro.ts, k), clk.tn);
       float xs[NV];
       cs_dense<NV>(euler, dead, x, x1, fx0, kx, dt, th, xs);
       save_point(k, xs, dead);
@@ -2632,7 +2640,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
       prev_ok = !bad;
     }
     while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
-      const float th = mtgp_cs_rescale(clk.t, A.ro.ts[k], clk.tn);
+      const float th = mtgp_cs_rescale(clk.t, ldc(A.ro.ts, k), clk.tn);
       float xs[kWideComp], f3[kWideComp];
 #pragma unroll
       for (int t = 0; t < kWideComp; ++t) f3[t] = (c0 + t < NV) ? cur[(c0 + t) * kWave] : 0.0f;
@@ -4594,6 +4602,20 @@ extern "C" int MTGP_DBG_CAT(mtgp_debug_violations_tu, MTGP_TU)(unsigned long lon
   const unsigned long long z[4] = {0, 0, 0, 0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_dbg_viol), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
+#if MTGP_TU == 0
+// positive control of the counters: one store at lane offset 5 into a row of 4 (counted, dropped)
+__global__ void k_dbg_selftest(float* buf) {
+  if (threadIdx.x == 0) store_row(buf, 0, 5, 1.0f, 4);
+}
+extern "C" int mtgp_debug_selftest(void) {
+  float* d = nullptr;
+  if (hipMalloc(&d, 4 * sizeof(float)) != hipSuccess) return -1;
+  hipLaunchKernelGGL(k_dbg_selftest, dim3(1), dim3(64), 0, 0, d);
+  const int rc = hipDeviceSynchronize() == hipSuccess ? 0 : -1;
+  (void)hipFree(d);
+  return rc;
+}
+#endif
 #endif
 #if MTGP_TU_ACRO && MTGP_AB_FBCOUNT
 extern "C" int mtgp_ab_fb_count(unsigned long long* host) {  // diagnostic build only; reads and clears

@@ -85,17 +85,34 @@ class DeviceEngine:
         self._jit_last = None        # (pinned host info, event, units) of a sampled build: capacity hint
         self._jit_builds = 0
         self._jit_bytes_per_unit = None  # learnt from earlier plans (None: estimate from G)
+        self._grad_code = None  # (pointer, bytes): the coefficient optimiser's dual-code buffer
 
     def __del__(self):
         try:
-            if any(a is not None for a in self._arenas):
+            if any(a is not None for a in self._arenas) or self._grad_code is not None:
                 torch.cuda.synchronize(self.device)
-                for a in self._arenas:
+                for a in self._arenas + [self._grad_code]:
                     if a is not None:
                         self.native.mtgp_jit_free(a[0])
                 self._arenas = [None, None]
+                self._grad_code = None
         except Exception:
             pass
+
+    def grad_code_buffer(self, nbytes: int):
+        """The executable buffer of the coefficient optimiser's dual-number code (mtgp_ctl_grad_jit),
+        grown when needed; every gradient call re-emits its code on the stream before the kernel."""
+        if self._grad_code is None or self._grad_code[1] < nbytes:
+            if self._grad_code is not None:
+                torch.cuda.synchronize(self.device)
+                self.native.mtgp_jit_free(self._grad_code[0])
+                self._grad_code = None
+            ptr = ctypes.c_void_p()
+            rc = self.native.mtgp_jit_alloc(self.device.index or 0, nbytes, ctypes.byref(ptr))
+            if rc != nat.OK or not ptr.value:
+                raise RuntimeError(f"mtgp_jit_alloc({nbytes}) failed: {rc}")
+            self._grad_code = (ptr.value, nbytes)
+        return self._grad_code
 
     # ------------------------------------------------------------------ jit
     def _arena(self, nbytes: int):

@@ -57,6 +57,8 @@ for step in "$@"; do
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench_c3q) run bench_c3q 300 python bench.py --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     bench_c3ext) run bench_c3ext 300 python bench.py --ext-ops --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
+    dbgcheck) run dbgcheck 600 env MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_dbg.so python -u scripts/debug_store_check.py \
+                tests/test_gpu_acrobot_mask.py tests/test_gpu_cstep.py tests/test_gpu_parity.py || exit 1 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_c3) run bench_c3 600 python bench.py || exit 1 ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 || exit 1 ;;

@@ -27,14 +27,17 @@ def test_struct_layouts_match_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mtgp.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(MtgpNodeLibrary), sizeof(MtgpProgramSpec), sizeof(MtgpInstr), sizeof(MtgpModel),'
                    'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));'
-                   'printf("%zu %zu\\n", offsetof(MtgpRollouts, lanes), offsetof(MtgpModel, dp_budget));return 0;}\n')
+                   'printf("%zu %zu %zu %zu\\n", offsetof(MtgpRollouts, lanes), offsetof(MtgpModel, dp_budget),'
+                   'sizeof(MtgpGradJit), offsetof(MtgpGradJit, info));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
     want = [ctypes.sizeof(t) for t in (nat.MtgpNodeLibrary, nat.MtgpProgramSpec, nat.MtgpInstr, nat.MtgpModel,
                                        nat.MtgpRollouts, nat.MtgpOutputs)] + [nat.MtgpModel.readout_save_same.offset,
                                                                               nat.MtgpRollouts.lanes.offset,
-                                                                              nat.MtgpModel.dp_budget.offset]
+                                                                              nat.MtgpModel.dp_budget.offset,
+                                                                              ctypes.sizeof(nat.MtgpGradJit),
+                                                                              nat.MtgpGradJit.info.offset]
     assert got == want
 
 
@@ -99,6 +102,7 @@ def test_constants_match_header():
     assert _define(text, "MTGP_STACK_MAX") == nat.STACK_MAX
     assert _define(text, "MTGP_MAX_ROLLOUTS") == nat.MAX_ROLLOUTS
     assert _define(text, "MTGP_DP_STATE_WORDS") == nat.DP_STATE_WORDS
+    assert _define(text, "MTGP_GRAD_JIT_WORDS_PER_INSTR") == nat.GRAD_JIT_WORDS_PER_INSTR
     ops = open(os.path.join(ROOT, "include", "mtgp_opcodes.h")).read()
     pairs = re.findall(r"MTGP_OP_(\w+) = (\d+),", ops)
     assert [n for n, _ in pairs] == nat.OP_NAMES and [int(v) for _, v in pairs] == list(range(len(pairs)))

@@ -793,3 +793,45 @@ def test_data_limits_raise_at_generation_0():
                                verbose=False)
     with pytest.raises(NotImplementedError, match="one-pass mask"):
         gp.evaluate_population(pop[None], data_off)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,env,solver,noise,ext", [
+    ("dynamic", "acrobot", "rk4", 0.0, False), ("dynamic", "acrobot", "dopri5", 0.0, False),
+    ("static", "reactor", "euler", 0.1, False), ("dynamic", "harmonic", "rk4", 0.1, True),
+    ("static", "acrobot", "dopri5", 0.0, True)])
+def test_gpu_ctl_grad_dual_jit_matches_interpreter(kind, env, solver, noise, ext):
+    """mtgp_ctl_grad_jit (the programs as dual-number machine code, csrc/mtgp_jit_dual.h) vs the
+    dual interpreter (mtgp_ctl_grad): loss and every gradient bit for bit, every program of the
+    launch translated (info[0] == 0) and the code in the buffer (info[1] <= its size) -- i.e. the
+    JIT path is the one that ran; the extended operators (/, exp, log, sqrt, tanh, abs) included."""
+    import torch
+    from helpers import _ctl_solver, _mode, CONTROL_OPS
+    from multitreegp_amd.engine import DeviceEngine
+    from multitreegp_amd.sampling import sample_population
+    cls = {"acrobot": mt.Acrobot, "harmonic": mt.HarmonicOscillator, "reactor": mt.StirredTankReactor}[env]
+    e = cls(0.0, noise)
+    ys = [f"y{i + 1}" for i in range(e.n_obs)]
+    tg = [f"tar{i + 1}" for i in range(e.n_targets)]
+    ops = CONTROL_OPS + ([("/", None, 2, 0.1), ("exp", None, 1, 0.05), ("log", None, 1, 0.05),
+                          ("sqrt", None, 1, 0.05), ("tanh", None, 1, 0.05), ("abs", None, 1, 0.05)] if ext else [])
+    sv = {"rk4": _ctl_solver(None), "euler": dict(solver=mt.Euler()),
+          "dopri5": _ctl_solver((1e-5, 1e-5, 0.002, 600))}[solver]
+    if kind == "dynamic":
+        lib = mt.NodeLibrary(ops, [ys + ["a1", "a2", "u"] + tg, ["a1", "a2"] + tg], [2, 1])
+        ff = mt.DynamicEvaluator(e, 2, 0.05, **sv)
+    else:
+        lib = mt.NodeLibrary(ops, [ys + tg], [1])
+        ff = mt.FeedforwardEvaluator(e, 0.05, **sv)
+    data = mt.control_data(e, 6, 0.05, None, seed=9, n_steps=30, mode=_mode(env))
+    pop = sample_population(13, lib, 30, 1, max_init_depth=5, max_nodes=24)[0]
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    opt_j = co.CoefficientOptimiser(eng, jit=True)
+    lj, gj = opt_j.loss_and_grad(pop, data)
+    info = opt_j.last_jit_info.cpu().numpy()
+    assert info[0] == 0 and 0 < info[1] <= eng._grad_code[1], info
+    li, gi = co.CoefficientOptimiser(eng, jit=False).loss_and_grad(pop, data)
+    assert sum(len(g) for g in gj) > 5
+    assert bits_equal(lj, li), mismatch_report(lj, li, "loss")
+    for p, (a, b) in enumerate(zip(gj, gi)):
+        assert bits_equal(a, b), (p, a, b)
