@@ -265,6 +265,7 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
   }
   const int kk = k < np ? k : -1;
   const bool use_jit = NV <= 4 && dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
+  if (use_jit) asm volatile("s_icache_inv");  // the code was written by this call's emit kernel
   const int nv = A.m.n_var;
   const float* th = A.theta + (size_t)p * A.K;
   const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
@@ -409,6 +410,7 @@ __global__ void __launch_bounds__(kGradBlock) k_sr_grad_dp(GradArgs A) {
   }
   const int kk = k < np ? k : -1;
   const bool use_jit = NV <= 4 && dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
+  if (use_jit) asm volatile("s_icache_inv");  // the code was written by this call's emit kernel
   const int nv = A.m.n_var;
   const float* th = A.theta + (size_t)p * A.K;
   const MtgpInstr* progs = A.prog + ((size_t)p * A.n_prog + A.m.prog_state) * A.L;
@@ -792,6 +794,9 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   // the data vector of a program call, and its reader
   float dvv[kCtlData], dvd[kCtlData];
   const bool use_jit = dual_jit_ok(A);  // the programs as dual-number code (mtgp_jit_dual.h)
+  // the code was written by this call's emit kernel, possibly over code an earlier launch ran from
+  // (the same buffer, or a freed buffer's address reused): drop the CU's stale instruction lines
+  if (use_jit) asm volatile("s_icache_inv");
   auto V = [&](uint32_t off) -> Dual {
     const int sl = (int)(off / MTGP_SLOT_BYTES);
     if (sl < D) {
