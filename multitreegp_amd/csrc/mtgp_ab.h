@@ -69,4 +69,8 @@
 #define MTGP_DEBUG_CHECKS 0
 #endif
 
+#ifndef MTGP_AB_WAVETIME
+#define MTGP_AB_WAVETIME 0    // record each k_ctl_dynamic wave's start / end clock and HW_ID (mtgp_ab_wave_times)
+#endif
+
 #endif  // MTGP_AB_H

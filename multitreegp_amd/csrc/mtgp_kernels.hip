@@ -422,6 +422,9 @@ struct KArgs {
   int32_t chain_save;       // ... and continues it into the save-point readout on request (s46; unused since ABI v18)
   int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
   int32_t chain_merge;      // (ABI v18) the dynamic policy's readout chains into its state programs, u put in its slot
+  uint32_t epoch;           // launch counter (low 16 bits tag the fair-share progress posts)
+  int32_t fair;             // fair share of the SIMDs' issue slots (FairShare; MTGP_FAIR)
+  int32_t fair_dp;          // the same for the Dopri5 attempt loops (MTGP_FAIR_DP)
   // Dopri5 in two launches (ABI v16, MtgpModel.dp_budget): launch 1 runs every wave for at most
   // dp_budget attempts and parks the lanes of waves that are not done (dp_state, word-major
   // [kDpStateWords][waves * 64]) in the list dp_pending ([0] = count, then wave ids); launch 2
@@ -1196,6 +1199,52 @@ __device__ __forceinline__ ChainOut jit_call_chain_nf(uint64_t addr_, const floa
   return jit_call_chain(addr_, d, fl, cont);
 }
 
+// Fair share of a SIMD's issue slots.  The SQ issues the oldest ready wave first, so of the four
+// waves a SIMD holds the oldest runs ahead and the youngest finishes long after it, alone on the
+// SIMD for its last stretch (profiles/r05 wavetime: residency 0.67, durations 0.69-1.50x the mean).
+// Each wave posts its step count to a per-SIMD table (HW_ID / XCC_ID) and reads the others' posts
+// of one step ago; a wave more than `margin` steps ahead of the slowest lowers its priority.
+// Measured (profiles/r05/v12_ab_fair.log, A/B in one process): C3 kernel 2.17 -> 1.81 ms, results
+// bit-identical (priorities only reorder issue).
+static __device__ uint32_t g_fair[8 * 8 * 2 * 16 * 4 * 16];
+struct FairShare {
+  uint32_t* tab;
+  uint32_t slot, tag, seen;
+  int margin;
+  bool low;
+  __device__ void init(const KArgs& A, int setting = -1) {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)) & 7u;  // HW_REG_XCC_ID
+    const uint32_t key = (((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) * 4u +
+                         ((hw >> 4) & 3u);
+    tab = g_fair + (size_t)key * 16u;
+    slot = hw & 15u;
+    tag = A.epoch;
+    margin = (setting < 0 ? A.fair : setting) - 1;
+    seen = 0u;
+    low = false;
+    __builtin_amdgcn_s_setprio(2);
+  }
+  __device__ __forceinline__ void step(int lane, uint32_t st) {
+    const bool valid = lane < 16 && (seen >> 16) == tag && (uint32_t)lane != slot;
+    int m = valid ? (int)(seen & 0xffffu) : 0xffff;
+#pragma unroll
+    for (int w = 1; w < 16; w <<= 1) {
+      const int o = __shfl_xor(m, w, kWave);
+      m = o < m ? o : m;
+    }
+    const int mn = __builtin_amdgcn_readfirstlane(m);
+    const bool ahead = mn != 0xffff && (int)st > mn + margin;
+    if (ahead != low) {
+      if (ahead) __builtin_amdgcn_s_setprio(0);
+      else __builtin_amdgcn_s_setprio(2);
+      low = ahead;
+    }
+    if (lane == 0) __hip_atomic_store(tab + slot, tag << 16 | st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < 16) seen = __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
+
 // The fixed-step dynamic policy with usable JIT code (see above), diffrax ConstantStepSize semantics
 // (include/mtgp_cstep.h): per step the NST stages at t + c_i dt, then the step's end state, the
 // event test, and every save point ts[k] <= tn of the step through the dense output -- observation
@@ -1289,7 +1338,11 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   CsClock clk;
   clk.init(A);
   int k = 0;  // next save point
+  const bool fair_on = uni(A.fair) != 0;
+  FairShare fair;
+  if (fair_on) fair.init(A);
   while (clk.live()) {
+    if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
     // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
     auto stage = [&](auto st_c) {
@@ -1390,8 +1443,32 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
 // state equations; at save points the save-time readout (dyn.py:101) is appended.
 // NOISE: observation noise on; the save-point observation uses ts[k] (dyn.py:99), which is
 // recomputed when it differs from the stage-0 time of that step.
+#if MTGP_AB_WAVETIME
+// diagnostic build only: per wave (grid order) its start / end shader clock and HW_ID / XCC_ID
+constexpr int kWaveTimeMax = 1 << 15;
+__device__ unsigned long long g_wave_time[kWaveTimeMax * 2];
+__device__ unsigned int g_wave_hw[kWaveTimeMax * 2];
+struct WaveTimer {
+  unsigned long long t0;
+  __device__ WaveTimer() : t0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ ~WaveTimer() {
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const int wv = (int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
+    if ((threadIdx.x & 63) == 0 && wv < kWaveTimeMax) {
+      g_wave_time[2 * wv] = t0;
+      g_wave_time[2 * wv + 1] = t1;
+      g_wave_hw[2 * wv] = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));   // HW_REG_HW_ID
+      g_wave_hw[2 * wv + 1] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11));  // HW_REG_XCC_ID
+    }
+  }
+};
+#endif
+
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dynamic(KArgs A) {
+#if MTGP_AB_WAVETIME
+  WaveTimer wave_timer;
+#endif
   constexpr int NV = Env::NV;
   // NA <= 3: the state size; NA = kNaRuntime: state_size 4 .. kNaRuntime at run time (interpreter
   // only: the data vector has up to kDWide slots, beyond the JIT's register-data ABI)
@@ -1641,7 +1718,11 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   CsClock clk;
   clk.init(A);
   int k = 0;
+  const bool fair_on = uni(A.fair) != 0;
+  FairShare fair;
+  if (fair_on) fair.init(A);
   while (clk.live()) {
+    if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
@@ -2081,7 +2162,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     live = active && t < t_end && steps < max_steps;
   }
   const int budget = A.dp_pass == 1 ? A.dp_budget : 0x7fffffff;
+  const bool fair_on = uni(A.fair_dp) != 0;  // fair share of the SIMDs by attempt count (FairShare)
+  FairShare fair;
+  if (fair_on) fair.init(A, A.fair_dp);
   for (int iter = 0; wave_any(live); ++iter) {
+    if (fair_on) fair.step(Ln.lane, (uint32_t)iter);
     if (iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
       park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
       if (Ln.lane == 0) A.dp_pending[1 + atomicAdd(A.dp_pending, 1)] = wv;
@@ -2225,7 +2310,11 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   CsClock clk;
   clk.init(A);
   int k = 0;
+  const bool fair_on = uni(A.fair) != 0;
+  FairShare fair;
+  if (fair_on) fair.init(A);
   while (clk.live()) {
+    if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
@@ -4617,6 +4706,14 @@ extern "C" int mtgp_debug_selftest(void) {
 }
 #endif
 #endif
+#if MTGP_AB_WAVETIME && defined(MTGP_TU) && MTGP_TU == 7
+extern "C" int mtgp_ab_wave_times(unsigned long long* t, unsigned int* hw, int n) {  // diagnostic build only
+  if (n > kWaveTimeMax) n = kWaveTimeMax;
+  if (hipMemcpyFromSymbol(t, HIP_SYMBOL(g_wave_time), (size_t)n * 2 * sizeof(unsigned long long)) != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(hw, HIP_SYMBOL(g_wave_hw), (size_t)n * 2 * sizeof(unsigned int)) != hipSuccess) return -1;
+  return n;
+}
+#endif
 #if MTGP_TU_ACRO && MTGP_AB_FBCOUNT
 extern "C" int mtgp_ab_fb_count(unsigned long long* host) {  // diagnostic build only; reads and clears
   if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ab_fb_count), 4 * sizeof(unsigned long long)) != hipSuccess) return -1;
@@ -5169,6 +5266,16 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     A.dp_pending = out->dp_pending;
   }
   A.chain_merge = 0;
+  static std::atomic<uint32_t> launch_epoch{0};
+  A.epoch = (launch_epoch.fetch_add(1, std::memory_order_relaxed) + 1u) & 0xffffu;
+  {  // MTGP_FAIR: 0 off, k >= 1 on with a lead margin of k - 1 steps (default 3: margin 2)
+    const char* f = getenv("MTGP_FAIR");
+    A.fair = f ? atoi(f) : 3;
+    if (A.fair < 0 || A.fair > 1000) A.fair = 3;
+    const char* fd = getenv("MTGP_FAIR_DP");  // (waves resume into freed slots there: off by default)
+    A.fair_dp = fd ? atoi(fd) : 0;
+    if (A.fair_dp < 0 || A.fair_dp > 1000) A.fair_dp = 0;
+  }
   if (jit && (jitc->chain.next | jitc->chain.cond | jitc->chain.store | jitc->chain.put) != 0u) {
     const MtgpJitChain want = jit_chain_for(*model, n_prog);  // must be the chain this model calls
     if (want.next != jitc->chain.next || want.cond != jitc->chain.cond || want.store != jitc->chain.store ||

@@ -59,6 +59,12 @@ for step in "$@"; do
     bench_c3ext) run bench_c3ext 300 python bench.py --ext-ops --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     dbgcheck) run dbgcheck 600 env MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_dbg.so python -u scripts/debug_store_check.py \
                 tests/test_gpu_acrobot_mask.py tests/test_gpu_cstep.py tests/test_gpu_parity.py || exit 1 ;;
+    wavetime) run wavetime 300 env MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_wt.so python -u scripts/wave_times.py --save $O/wavetime.npz || exit 1
+              run wavetime_nosched 300 env MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_wt.so python -u scripts/wave_times.py --no-schedule || exit 1 ;;
+    wavetime_fair) run wavetime_fair 300 env MTGP_FAIR=1 MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_wt.so python -u scripts/wave_times.py || exit 1 ;;
+    ab_fair_dp) run ab_fair_dp 600 python scripts/kvariants.py --solver dopri5 --rounds 3 --variants "prod,prod@MTGP_FAIR_DP=3" --tag dp_fair || exit 1 ;;
+    ab_fair_m) run ab_fair_m 500 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod@MTGP_FAIR=0,prod@MTGP_FAIR=1,prod@MTGP_FAIR=2,prod,prod@MTGP_FAIR=5" --tag c3_fair_margin || exit 1 ;;
+    ab_fair) run ab_fair 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,prod@MTGP_FAIR=1" --tag c3_fair || exit 1 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_c3) run bench_c3 600 python bench.py || exit 1 ;;
     bench_c2) run bench_c2 600 python bench.py --config c2 || exit 1 ;;
