@@ -2652,7 +2652,11 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   CsClock clk;
   clk.init(A);
   int k = 0;
+  const bool fair_on = uni(A.fair) != 0;  // (the workgroups sharing a SIMD: FairShare)
+  FairShare fair;
+  if (fair_on) fair.init(A);
   while (clk.live()) {
+    if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {

@@ -156,7 +156,13 @@ typedef struct {
   const float* prm;    /* this rollout's environment parameters */
   const uint32_t* key; /* this rollout's obs_noise_key or NULL */
   const float* W;
+  int32_t* save_at;    /* diagnostic: attempt index at which each save point was written, or NULL */
 } OrCtx;
+
+/* Diagnostic (scripts/dp_save_spread.py): Dopri5 save-point timing per rollout, [P, R, S] int32
+ * -- the attempt count when save k was written (0 for ts[0], -1 never); NULL turns it off. */
+static int32_t* g_save_trace = NULL;
+void oracle_set_save_trace(int32_t* buf) { g_save_trace = buf; }
 
 /* EnvironmentBase.f_obs (cbase.py:43-48) with C = eye(n_var)[:n_obs] (acrobot.py:48,
  * harmonic_oscillator.py:65, reactor.py:42):
@@ -410,6 +416,10 @@ static int solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float*
   int k = 1, steps = 0, accepted = 0;
   if (alt & OR_DP_ALT_INTERP_T0) k = 0;
   else for (int i = 0; i < n; ++i) saved[i] = y[i];
+  if (c->save_at) {
+    for (int q = 0; q < S; ++q) c->save_at[q] = -1;
+    if (k == 1) c->save_at[0] = 0;
+  }
   float t = ts[0];
   float tnext = t + m->h;
   if (tnext > t_end) tnext = t_end;
@@ -456,6 +466,7 @@ static int solve_dopri5(const OrCtx* c, const float* ts, const float* s0, float*
           const float ymid = dp_apply(y[i], h, dp_sum(CM, (const float (*)[OR_MAX_S])f, 7, i, lit), lit);
           saved[(size_t)k * n + i] = mtgp_dp_interp(y[i], y1[i], ymid, h * f[0][i], h * f[6][i], th);
         }
+        if (c->save_at) c->save_at[k] = steps;
         ++k;
       }
       t = t1;
@@ -584,7 +595,7 @@ int oracle_eval_ex(const OrModel* m, const float* pop, int P, int T, int N, int 
   const int R = ro->R, S = m->n_save, dim = state_dim(m);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int p = 0; p < P; ++p) {
-    OrCtx c;
+    OrCtx c = {0};
     c.m = m;
     c.cand = pop + (size_t)p * T * N * 4;
     c.N = N;
@@ -604,6 +615,7 @@ int oracle_eval_ex(const OrModel* m, const float* pop, int P, int T, int N, int 
       for (int i = 0; i < m->n_var; ++i) s0[i] = ro->x0[(size_t)r * m->n_var + i];
       c.key = ro->obs_keys ? ro->obs_keys + 2 * (size_t)r : NULL;
       c.W = ro->obs_w;
+      c.save_at = g_save_trace ? g_save_trace + ((size_t)p * R + r) * S : NULL;
       const int nst = m->solver == 1 ? solve_dopri5(&c, ro->ts, s0, saved) : solve_fixed(&c, ro->ts, s0, saved);
       if (steps_out) steps_out[(size_t)p * R + r] = nst;
       float f;
@@ -706,7 +718,7 @@ void oracle_wrap(const float* x, float* o, long n) {
 
 /* unit-test hooks: Acrobot pieces in isolation */
 void oracle_acro_drift(const float* params4, const float* state4, float u, float* out4) {
-  OrCtx c;
+  OrCtx c = {0};
   memset(&c, 0, sizeof(c));
   c.prm = params4;
   acro_drift(&c, state4, u, out4);
@@ -718,7 +730,7 @@ void oracle_env_drift(int env, const float* params, const float* state, float u,
   OrModel m;
   memset(&m, 0, sizeof(m));
   m.env = env;
-  OrCtx c;
+  OrCtx c = {0};
   memset(&c, 0, sizeof(c));
   c.m = &m;
   c.prm = params;
@@ -735,7 +747,7 @@ void oracle_acro_f_obs(const float* x4, float* y4) {
   memset(&m, 0, sizeof(m));
   m.n_var = m.n_obs = 4;
   m.env = ENV_ACROBOT;
-  OrCtx c;
+  OrCtx c = {0};
   memset(&c, 0, sizeof(c));
   c.m = &m;
   ctl_f_obs(&c, 0.0f, x4, y4);
@@ -1333,7 +1345,7 @@ int oracle_ctl_grad(const OrModel* m, const float* pop, int P, int T, int N, int
     const int p = (int)(pk / K), kq = (int)(pk % K);
     const int row = prow[(size_t)p * K + kq];
     if (row < 0 && kq > 0) { grad[pk] = 0.0f; continue; }
-    OrCtx c;
+    OrCtx c = {0};
     c.m = m;
     c.cand = pop + (size_t)p * T * N * 4;
     c.N = N;

@@ -64,6 +64,8 @@ for step in "$@"; do
     wavetime_fair) run wavetime_fair 300 env MTGP_FAIR=1 MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_wt.so python -u scripts/wave_times.py || exit 1 ;;
     ab_fair_dp) run ab_fair_dp 600 python scripts/kvariants.py --solver dopri5 --rounds 3 --variants "prod,prod@MTGP_FAIR_DP=3" --tag dp_fair || exit 1 ;;
     ab_fair_m) run ab_fair_m 500 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod@MTGP_FAIR=0,prod@MTGP_FAIR=1,prod@MTGP_FAIR=2,prod,prod@MTGP_FAIR=5" --tag c3_fair_margin || exit 1 ;;
+    ab_fair_c5) run ab_fair_c5 500 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod@MTGP_FAIR=0,prod" --tag c5_fair || exit 1 ;;
+    ab_fair_c2) run ab_fair_c2 300 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod@MTGP_FAIR=0,prod" --tag c2_fair || exit 1 ;;
     ab_fair) run ab_fair 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,prod@MTGP_FAIR=1" --tag c3_fair || exit 1 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_c3) run bench_c3 600 python bench.py || exit 1 ;;
