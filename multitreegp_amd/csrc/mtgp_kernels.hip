@@ -2576,7 +2576,7 @@ __device__ __forceinline__ uint32_t lds_address(const float* p) {
 // writes the fitness; the other waves skip the 64 LDS reads (every wave summing measured 0.7 %
 // slower at C5, profiles/r03/v10_ab_noprog_mse.log).
 template <bool TRAJ, bool JIT>
-__global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k_sr_wide(KArgs A) {
   extern __shared__ float wl[];
   Lane Ln;
   if (!lane_setup_wide(A, Ln)) return;  // uniform over the workgroup
@@ -2625,14 +2625,17 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   float tot = 0.0f;
   // one save point (every wave, uniform): the per-component squared errors meet in LDS (scratch
   // column buffer sq) and wave 0 sums them in index order (sr.py:24); fill: +inf, as k_sr
-  auto save_point = [&](int k, const float (&xs)[kWideComp], bool fill, float* sq) __attribute__((always_inline)) {
+  // xs_of(t): component t's saved value (evaluated once per component, so the save point holds no
+  // per-component array: the kernel stays within 128 VGPRs, two workgroups per CU)
+  auto save_point = [&](int k, auto xs_of, bool fill, float* sq) __attribute__((always_inline)) {
 #pragma unroll
     for (int t = 0; t < kWideComp; ++t) {
       const int c = c0 + t;
       if (c < NV) {
-        const float e = xs[t] - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
+        const float xv = xs_of(t);
+        const float e = xv - A.ro.ys_true[((size_t)k * NV + c) * R + rr];
         sq[c * kWave] = e * e;
-        if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, xs[t], PR);
+        if (TRAJ && active && A.out.xs) store_row(A.out.xs, ((size_t)k * NV + c) * PR, loff, xv, PR);
       }
     }
     __syncthreads();  // (uniform: a lane's fill flag is the same in every wave)
@@ -2652,11 +2655,7 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
   CsClock clk;
   clk.init(A);
   int k = 0;
-  const bool fair_on = uni(A.fair) != 0;  // (the workgroups sharing a SIMD: FairShare)
-  FairShare fair;
-  if (fair_on) fair.init(A);
-  while (clk.live()) {
-    if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
+  while (clk.live()) {  // (no FairShare: the workgroup's waves meet at a barrier every stage)
     const float dt = clk.dt();
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
@@ -2734,11 +2733,11 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
     }
     while (k < S && clk.saves(A.ro.ts, k)) {  // SaveAt(ts) through this step's dense output
       const float th = mtgp_cs_rescale(clk.t, ldc(A.ro.ts, k), clk.tn);
-      float xs[kWideComp], f3[kWideComp];
-#pragma unroll
-      for (int t = 0; t < kWideComp; ++t) f3[t] = (c0 + t < NV) ? cur[(c0 + t) * kWave] : 0.0f;
-      cs_dense<kWideComp>(euler, dead, x, x1, fx0, f3, dt, th, xs);
-      save_point(k, xs, dead, nxt);
+      save_point(k, [&](int t) __attribute__((always_inline)) {  // the dense output (cs_dense), cur = f3
+        const float v = euler ? mtgp_cs_linear(x[t], x1[t], th)
+                              : mtgp_cs_hermite(x[t], x1[t], fx0[t] * dt, cur[(c0 + t) * kWave] * dt, th);
+        return dead ? kInf : v;
+      }, dead, nxt);
       ++k;
     }
     if (!dead) {
@@ -2754,13 +2753,11 @@ __global__ void __launch_bounds__(512) k_sr_wide(KArgs A) {
     if (!TRAJ && wave_all(dead)) break;  // dead is identical in every wave: a uniform exit
   }
   if (k < S) {  // unsaved points (event / max_steps): +inf
-    float xs[kWideComp];
-#pragma unroll
-    for (int t = 0; t < kWideComp; ++t) xs[t] = kInf;
+    auto inf_of = [](int) { return kInf; };
     if (TRAJ) {
-      for (; k < S; ++k) save_point(k, xs, true, nxt);
+      for (; k < S; ++k) save_point(k, inf_of, true, nxt);
     } else {
-      save_point(k, xs, true, nxt);
+      save_point(k, inf_of, true, nxt);
     }
   }
   if (w == 0) finish_group(A, Ln, tot / (float)S);
@@ -5298,6 +5295,13 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   if (waves * kWave > (long)UINT32_MAX) return MTGP_ERR_ARG;
   A.dp_lanes = (uint32_t)(waves * kWave);
   const dim3 grid((unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock)), block(kWave * kWavesPerBlock);
+  {  // fair share needs companions: at least two waves per SIMD (C2's 256 waves: 7 % slower with it)
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                hipSuccess || waves < 2L * 4L * (long)cus)
+      A.fair = 0;
+    if (model->model == MTGP_MODEL_SR && model->n_var > 4) A.fair = 0;  // k_sr_wide: barrier-synced workgroups (C5: 1 % slower)
+  }
   const bool traj = out->xs || out->ys || out->us || out->acts;
   if (traj && (long)P * rollouts->R * 4 > (long)INT32_MAX) return MTGP_ERR_ARG;  // store_row's 31-bit byte offsets
   const bool noise = rollouts->obs_keys != nullptr;
