@@ -430,7 +430,10 @@ int mtgp_sr_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, 
  * primal values, as mtgp_sr_grad), observation noise included, state_size <= 3, R <= 64.
  * The programs read the reference's data vector [y(n_obs), a, u, targets] (MtgpProgramSpec gap 0)
  * followed by the K parameter slots.  Tangent rules: include/mtgp_dual.h (the environment drift,
- * f_obs, clip); the argmax step of the Acrobot fitness (acrobot.py:79) is piecewise constant. */
+ * f_obs, clip); the argmax step of the Acrobot fitness (acrobot.py:79) is piecewise constant.
+ * ABI v19: rollouts->fit_kof (the general Acrobot cost mask, ts off the one-pass grid) is
+ * differentiated too; scratch must then hold P * K * R * 2 * (1 + n_save) floats (the lanes' cost
+ * prefixes follow the partials). */
 int mtgp_ctl_grad(const MtgpModel* model, const MtgpInstr* prog, int32_t n_prog, int32_t L, int32_t P,
                   const float* theta, const int32_t* nparam, int32_t K, const MtgpRollouts* rollouts,
                   float* scratch, float* loss_out, float* grad_out, void* stream);

@@ -162,11 +162,8 @@ class CoefficientOptimiser:
         evaluator's `prepare`, host only), raised where the data is first seen
         (GeneticProgramming.evaluate_population at every generation with coefficient_optimisation,
         ADVICE r3), not at the first optimising generation (gp.py:418: generation 14): at most 64
-        rollouts (one lane set per candidate), and the Acrobot cost mask of ts on the save grid."""
-        if d.get("fit_kof") is not None:
-            raise NotImplementedError("coefficient optimisation of Acrobot with ts off the one-pass mask "
-                                      "(ts / (ts[1] - ts[0]) outside (k - 1, k + 1]): the general mask is not "
-                                      "differentiated")
+        rollouts (one lane set per candidate).  (Since round 5 the general Acrobot cost mask -- ts off
+        the one-pass grid, MtgpRollouts.fit_kof -- is differentiated too.)"""
         if d["R"] > 64:
             raise NotImplementedError("coefficient optimisation with more than 64 rollouts")
 
@@ -222,7 +219,9 @@ class CoefficientOptimiser:
                 raise ValueError(f"parameterised candidate does not flatten (status {worst})")
             th = torch.from_numpy(theta).to(dev)
             npd = torch.from_numpy(nparam).to(dev)
-            scratch = torch.empty((B * K * R * 2,), dtype=torch.float32, device=dev)
+            # (the general Acrobot mask keeps every lane's cost prefixes behind the partials, mtgp.h)
+            hist = d["n_save"] if d.get("fit_kof") is not None else 0
+            scratch = torch.empty((B * K * R * 2 * (1 + hist),), dtype=torch.float32, device=dev)
             lo_d = torch.empty((B,), dtype=torch.float32, device=dev)
             gr_d = torch.empty((B, K), dtype=torch.float32, device=dev)
             if self.use_jit and (eng.ff.model_id != nat.MODEL_SR or n_data <= 4):

@@ -67,6 +67,7 @@ struct GradArgs {
   const int32_t* nparam;  // [P]
   MtgpRollouts ro;
   float* part;            // [P, K, R, 2] per-rollout (F, dF/dtheta_k)
+  float* hist;            // [S, P * K * R, 2]: cost prefixes of the general Acrobot mask (fit_kof), else null
   float* loss;            // [P]
   float* grad;            // [P, K]
   // dual-number program code (mtgp_jit_dual.h; mtgp_ctl_grad_jit), or null: interpret
@@ -908,6 +909,28 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   bool settled = false;
   int fs = 0;
   MtgpDual cs = mtgp_dl(0.0f, 0.0f), c0 = mtgp_dl(0.0f, 0.0f);
+  // the general Acrobot mask (MtgpRollouts.fit_kof: ts / dts off the one-pass grid): the kept costs
+  // are the first K = kof[fs] saves, so the oracle's sum is A_K = ((0 + c_0) + ...) + c_{K-1}, then
+  // + 0 for the masked rest.  pre = the running prefix (its values kept in hist: K may lie behind
+  // the first success), Kt = K once known, AK = A_K once complete.
+  const int32_t* kof = ENV == 0 ? A.ro.fit_kof : nullptr;
+  const size_t nsl = (size_t)A.P * A.K * R;
+  MtgpDual pre = mtgp_dl(0.0f, 0.0f), AK = mtgp_dl(0.0f, 0.0f);
+  int Kt = -1, q_pre = -1;  // q_pre: the last save folded into pre
+  bool a_set = false;
+  auto hist_put = [&](int q, MtgpDual v) {
+    float* h = A.hist + ((size_t)q * nsl + slot) * 2;
+    h[0] = v.v;
+    h[1] = v.d;
+  };
+  auto hist_get = [&](int q) {
+    const float* h = A.hist + ((size_t)q * nsl + slot) * 2;
+    return mtgp_dl(h[0], h[1]);
+  };
+  auto prefix_done = [&]() {  // settled with Kt known: A_K from pre / hist when complete
+    if (Kt == 0) { AK = mtgp_dl(0.0f, 0.0f); a_set = true; }
+    else if (Kt - 1 <= q_pre) { AK = Kt - 1 == q_pre ? pre : hist_get(Kt - 1); a_set = true; }
+  };
   auto save_point = [&](int q, const Dual* xq) {
     Dual y[NV];
     f_obs(ts[q], xq, y);
@@ -936,6 +959,20 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
       const MtgpDual ud = tod(u);
       const MtgpDual cost = mtgp_dl_mul(mtgp_dl_mulc(ud, 0.01f), ud);
       const bool reached = ((-mtgp_cosf(xq[0].v)) - mtgp_cosf(xq[0].v + xq[1].v)) > 1.5f;
+      if (kof) {
+        if (!settled || !a_set) {  // fold c_q into the prefix while it may still be needed
+          pre = mtgp_dl_add(q == 0 ? mtgp_dl(0.0f, 0.0f) : pre, cost);
+          q_pre = q;
+          if (!settled) hist_put(q, pre);
+        }
+        if (!settled && reached) {
+          settled = true;
+          fs = q;
+          Kt = kof[fs];
+        }
+        if (settled && !a_set) prefix_done();
+        return;
+      }
       if (q == 0) {
         const bool incl0 = !((ts[0] / dts) > 0.0f);
         c0 = mtgp_dl_add(mtgp_dl(0.0f, 0.0f), incl0 ? cost : mtgp_dl(0.0f, 0.0f));
@@ -1128,6 +1165,29 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
   // costs become non-finite
   float F, dF;
   if constexpr (ENV == 0) {
+    if (kof) {
+      // the fill saves (+inf states: never a success) still count while the kept prefix runs into
+      // them: their readout costs are folded in as the oracle's full arrays hold them
+      Dual fillx[ND];
+#pragma unroll
+      for (int i = 0; i < ND; ++i) fillx[i] = {kInf, 0.0f};
+      for (int q = q_saved + 1; q < S; ++q) {
+        const int need = settled ? (a_set ? -1 : Kt - 1) : kof[0] - 1;
+        if (q > need) break;
+        save_point(q, fillx);
+      }
+      if (!settled) {  // no success: first_success = argmax of all-false = 0
+        fs = 0;
+        Kt = kof[0];
+        settled = true;
+        prefix_done();
+      }
+      cs = Kt < S ? mtgp_dl_add(AK, mtgp_dl(0.0f, 0.0f)) : AK;
+      const MtgpDual Fd = mtgp_dl_cadd((float)(fs + (fs == 0) * S), cs);
+      out[0] = Fd.v;
+      out[1] = Fd.d;
+      return;
+    }
     if (q_saved + 1 < S && settled) cs = mtgp_dl_add(cs, mtgp_dl(0.0f, 0.0f));
     if (!settled) {
       fs = 0;
@@ -1265,6 +1325,7 @@ static bool grad_args(GradArgs& A, const MtgpModel* model, const MtgpInstr* prog
   A.nparam = nparam;
   A.ro = *ro;
   A.part = scratch;
+  A.hist = nullptr;
   A.loss = loss_out;
   A.grad = grad_out;
   A.jit_code = nullptr;
@@ -1291,7 +1352,7 @@ extern "C" int mtgp_ctl_grad_jit(const MtgpModel* model, const MtgpInstr* prog, 
       model->n_control != 1 || model->n_targets < 0 || model->n_targets > 8 || !ro->params || !ro->x0 || !ro->ts ||
       (model->n_targets > 0 && !ro->targets) || (ro->obs_keys && !ro->obs_w) || ro->R < 1 || ro->R > 64 ||
       model->n_save < 2 || !(model->h > 0.0f) || model->prog_readout < 0 ||
-      model->prog_readout >= n_prog || ro->fit_kof)  // (the general Acrobot mask is not differentiated)
+      model->prog_readout >= n_prog || (ro->fit_kof && model->env != MTGP_ENV_ACROBOT))
     return MTGP_ERR_ARG;
   const int na = dyn ? model->state_size : 0;
   const int D = model->n_obs + (dyn ? na + 1 : 0) + model->n_targets;
@@ -1302,6 +1363,8 @@ extern "C" int mtgp_ctl_grad_jit(const MtgpModel* model, const MtgpInstr* prog, 
   if (P == 0) return MTGP_OK;
   GradArgs A;
   grad_args(A, model, prog, n_prog, L, P, theta, nparam, K, ro, scratch, loss_out, grad_out);
+  // the general Acrobot mask keeps its cost prefixes behind the partials (mtgp.h: scratch size)
+  if (ro->fit_kof) A.hist = scratch + (size_t)P * K * ro->R * 2;
   hipStream_t s = (hipStream_t)stream;
   const int jrc = dual_jit_prepare(A, jit, D, s);
   if (jrc != MTGP_OK) return jrc;
@@ -1362,6 +1425,7 @@ extern "C" int mtgp_sr_grad_jit(const MtgpModel* model, const MtgpInstr* prog, i
   A.nparam = nparam;
   A.ro = *ro;
   A.part = scratch;
+  A.hist = nullptr;
   A.loss = loss_out;
   A.grad = grad_out;
   hipStream_t s = (hipStream_t)stream;

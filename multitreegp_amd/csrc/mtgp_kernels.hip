@@ -425,6 +425,7 @@ struct KArgs {
   uint32_t epoch;           // launch counter (low 16 bits tag the fair-share progress posts)
   int32_t fair;             // fair share of the SIMDs' issue slots (FairShare; MTGP_FAIR)
   int32_t fair_dp;          // the same for the Dopri5 attempt loops (MTGP_FAIR_DP)
+  int32_t fair_mode;        // 0: two priority levels; 1: the slowest wave of a SIMD above the rest (MTGP_FAIR_MODE)
   // Dopri5 in two launches (ABI v16, MtgpModel.dp_budget): launch 1 runs every wave for at most
   // dp_budget attempts and parks the lanes of waves that are not done (dp_state, word-major
   // [kDpStateWords][waves * 64]) in the list dp_pending ([0] = count, then wave ids); launch 2
@@ -1210,8 +1211,7 @@ static __device__ uint32_t g_fair[8 * 8 * 2 * 16 * 4 * 16];
 struct FairShare {
   uint32_t* tab;
   uint32_t slot, tag, seen;
-  int margin;
-  bool low;
+  int margin, mode, level;
   __device__ void init(const KArgs& A, int setting = -1) {
     const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
     const uint32_t xcc = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (31 << 11)) & 7u;  // HW_REG_XCC_ID
@@ -1221,8 +1221,9 @@ struct FairShare {
     slot = hw & 15u;
     tag = A.epoch;
     margin = (setting < 0 ? A.fair : setting) - 1;
+    mode = A.fair_mode;
     seen = 0u;
-    low = false;
+    level = 2;
     __builtin_amdgcn_s_setprio(2);
   }
   __device__ __forceinline__ void step(int lane, uint32_t st) {
@@ -1234,11 +1235,12 @@ struct FairShare {
       m = o < m ? o : m;
     }
     const int mn = __builtin_amdgcn_readfirstlane(m);
-    const bool ahead = mn != 0xffff && (int)st > mn + margin;
-    if (ahead != low) {
-      if (ahead) __builtin_amdgcn_s_setprio(0);
-      else __builtin_amdgcn_s_setprio(2);
-      low = ahead;
+    const int lv = mn == 0xffff ? 2 : ((int)st > mn + margin ? 0 : ((mode == 1 && (int)st <= mn) ? 3 : 2));
+    if (lv != level) {  // (s_setprio takes an immediate)
+      if (lv == 0) __builtin_amdgcn_s_setprio(0);
+      else if (lv == 2) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(3);
+      level = lv;
     }
     if (lane == 0) __hip_atomic_store(tab + slot, tag << 16 | st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (lane < 16) seen = __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -5273,6 +5275,8 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
     const char* f = getenv("MTGP_FAIR");
     A.fair = f ? atoi(f) : 3;
     if (A.fair < 0 || A.fair > 1000) A.fair = 3;
+    const char* fm = getenv("MTGP_FAIR_MODE");
+    A.fair_mode = fm ? atoi(fm) : 0;
     const char* fd = getenv("MTGP_FAIR_DP");  // (waves resume into freed slots there: off by default)
     A.fair_dp = fd ? atoi(fd) : 0;
     if (A.fair_dp < 0 || A.fair_dp > 1000) A.fair_dp = 0;

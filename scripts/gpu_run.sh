@@ -66,6 +66,7 @@ for step in "$@"; do
     ab_fair_m) run ab_fair_m 500 python scripts/kvariants.py --config c3 --rounds 6 --variants "prod@MTGP_FAIR=0,prod@MTGP_FAIR=1,prod@MTGP_FAIR=2,prod,prod@MTGP_FAIR=5" --tag c3_fair_margin || exit 1 ;;
     ab_fair_c5) run ab_fair_c5 500 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod@MTGP_FAIR=0,prod" --tag c5_fair || exit 1 ;;
     ab_fair_c2) run ab_fair_c2 300 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod@MTGP_FAIR=0,prod" --tag c2_fair || exit 1 ;;
+    ab_fair_mode) run ab_fair_mode 500 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,prod@MTGP_FAIR_MODE=1,prod@MTGP_FAIR=9" --tag c3_fair_mode || exit 1 ;;
     ab_fair) run ab_fair 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,prod@MTGP_FAIR=1" --tag c3_fair || exit 1 ;;
     smoke) run smoke 180 python -c "import __graft_entry__ as g; g.smoke()" || exit 1 ;;
     bench_c3) run bench_c3 600 python bench.py || exit 1 ;;

@@ -774,9 +774,10 @@ def test_gpu_evaluate_population_optimises_control_coefficients():
 
 
 def test_data_limits_raise_at_generation_0():
-    """coefficient optimisation's data limits (at most 64 rollouts; Acrobot ts on the
-    one-pass mask) raise at the first evaluate_population, not at generation 14 when the first
-    optimisation runs (gp.py:418).  Host-side check: no GPU needed, every rank raises together."""
+    """coefficient optimisation's data limit (at most 64 rollouts) raises at the first
+    evaluate_population, not at generation 14 when the first optimisation runs (gp.py:418).
+    Host-side check: no GPU needed, every rank raises together.  (Acrobot ts off the one-pass
+    mask is differentiated since round 5: test_gpu_ctl_grad_offset_ts_bitexact.)"""
     from helpers import CONTROL_OPS, dynamic_setup
     e, lib, ff, data, pop = dynamic_setup(P=8, R=100, n_steps=10, depth=3, N=16, seed=2)
     gp = mt.GeneticProgramming(20, 8, ff, CONTROL_OPS, lib.variable_list, lib.layer_sizes, max_nodes=16,
@@ -785,14 +786,6 @@ def test_data_limits_raise_at_generation_0():
     assert gp.current_generation == 0
     with pytest.raises(NotImplementedError, match="64 rollouts"):
         gp.evaluate_population(pop[None], data)
-    e, lib, ff, data, pop = dynamic_setup(P=8, R=4, n_steps=10, depth=3, N=16, seed=2)
-    x0, ts, *rest = data
-    data_off = (x0, (ts + np.float32(1.0)).astype(np.float32), *rest)  # ts[0] = 1.0: off the one-pass mask
-    gp = mt.GeneticProgramming(20, 8, ff, CONTROL_OPS, lib.variable_list, lib.layer_sizes, max_nodes=16,
-                               migration_percentage=0.5, elite_percentage=0.0, coefficient_optimisation=True,
-                               verbose=False)
-    with pytest.raises(NotImplementedError, match="one-pass mask"):
-        gp.evaluate_population(pop[None], data_off)
 
 
 @pytest.mark.gpu
@@ -835,3 +828,56 @@ def test_gpu_ctl_grad_dual_jit_matches_interpreter(kind, env, solver, noise, ext
     assert bits_equal(lj, li), mismatch_report(lj, li, "loss")
     for p, (a, b) in enumerate(zip(gj, gi)):
         assert bits_equal(a, b), (p, a, b)
+
+
+OFFSET_CASES = [("dynamic", None, 1.0), ("dynamic", None, -0.35), ("static", None, 2.5), ("static", None, 0.07),
+                ("dynamic", (1e-5, 1e-5, 0.002, 600), 1.5), ("dynamic", (1e-5, 1e-5, 0.002, 600), -0.4)]
+
+
+def _offset_case(kind, solver, t0, P=10, R=8):
+    from helpers import dynamic_setup, static_setup
+    from test_gpu_acrobot_mask import _swing_data
+    setup = dynamic_setup if kind == "dynamic" else static_setup
+    kw = dict(P=P, R=R, n_steps=40, seed=13, solver=solver)
+    if kind == "dynamic":
+        kw["depth"], kw["N"] = 4, 24
+    env, lib, ff, data, pop = setup(**kw)
+    data = _swing_data(data, t0, seed=int(abs(t0) * 100) + 5)
+    return lib, ff, data, pop
+
+
+@pytest.mark.parametrize("kind,solver,t0", OFFSET_CASES[:3])
+def test_ctl_oracle_loss_is_the_fitness_offset_ts(kind, solver, t0):
+    """The oracle's dual Acrobot fitness on a grid off the one-pass form (the general mask,
+    acrobot.py:82) equals its evaluator fitness bit for bit."""
+    from multitreegp_amd.evaluators import acrobot_mask
+    lib, ff, data, pop = _offset_case(kind, solver, t0)
+    assert acrobot_mask(data[1]) is not None
+    d = ff.prepare(data)
+    rl, rg, rows = orc.ctl_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    fit = orc.evaluate(oracle_model(ff, d), pop, lib, oracle_rollouts(d))["fitness"]
+    assert bits_equal(rl, fit), mismatch_report(rl, fit, "loss")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind,solver,t0", OFFSET_CASES)
+def test_gpu_ctl_grad_offset_ts_bitexact(kind, solver, t0):
+    """Coefficient optimisation on Acrobot grids off the one-pass mask (MtgpRollouts.fit_kof: the
+    kept cost prefix behind the first success for positive offsets, running into the +inf fill for
+    negative ones): loss and every gradient bit for bit vs the oracle, loss = the evaluator's
+    fitness; RK4 and Dopri5, dynamic and static; JIT and interpreter alike."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    lib, ff, data, pop = _offset_case(kind, solver, t0)
+    eng = DeviceEngine(ff, lib, 0.0, torch.device("cuda", 0))
+    d = eng.prepare_data(data)
+    assert d.get("fit_kof") is not None
+    rl, rg, rows = orc.ctl_grad(oracle_model(ff, d), pop, lib, oracle_rollouts(d))
+    assert sum(len(r) for r in rows) > 5
+    for jit in (True, False):
+        loss, grads = co.CoefficientOptimiser(eng, jit=jit).loss_and_grad(pop, data)
+        assert bits_equal(loss, rl), mismatch_report(loss, rl, "loss")
+        for p, g in enumerate(grads):
+            assert bits_equal(g, rg[p, : len(g)]), (jit, p, g, rg[p, : len(g)])
+    fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
+    assert bits_equal(loss, fit), mismatch_report(loss, fit, "fitness")
