@@ -62,6 +62,13 @@
 #ifndef MTGP_AB_NOFIT
 #define MTGP_AB_NOFIT 0       // no online fitness update at the save points
 #endif
+// Save-point sections of the fixed-step static kernel (C2, round 5 ConstantStepSize cost):
+#ifndef MTGP_AB_NOHERMITE
+#define MTGP_AB_NOHERMITE 0   // the saved state is the step end y1 (no dense-output evaluation, no theta)
+#endif
+#ifndef MTGP_AB_NOSAVECALL
+#define MTGP_AB_NOSAVECALL 0  // no policy call at a save point (us = the last stage's u)
+#endif
 // Debug build (round 5, never shipped): bounds checks on every trajectory-row store and on the
 // Acrobot mask's fit_hist row index; a violation is counted (mtgp_debug_violations_tuN) and the
 // access skipped instead of trapping, so a bad offset can never fault the GPU or hide silently.

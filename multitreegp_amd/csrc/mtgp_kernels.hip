@@ -1701,7 +1701,7 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
     ctl_obs_apply<Env>(xs, nzv, yo);
 #pragma unroll
     for (int i = 0; i < NV; ++i) dv[i] = yo[i];
-    const float us = jit_call_nf(u_policy, dv);
+    const float us = MTGP_AB_NOSAVECALL ? dv[0] : jit_call_nf(u_policy, dv);
     if (!fill) env.fit_update(fit, k, S, ts, us, xs);
     if (TRAJ && active) {
       if (A.out.xs) {
@@ -1762,9 +1762,14 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
       prev_ok = ok;
     }
     while (k < S && clk.saves(ts, k)) {
-      const float th = mtgp_cs_rescale(t, ldc(ts, k), clk.tn);
       float xs[NV];
-      cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
+      if (MTGP_AB_NOHERMITE) {
+#pragma unroll
+        for (int i = 0; i < NV; ++i) xs[i] = x1[i];
+      } else {
+        const float th = mtgp_cs_rescale(t, ldc(ts, k), clk.tn);
+        cs_dense<NV>(NST == 1, dead, x, x1, fx0, kx, dt, th, xs);
+      }
       save_point(k, xs, dead);
       ++k;
     }

@@ -21,10 +21,17 @@ run() {  # name seconds cmd...
 }
 prof() {  # name config args...
   local n=$1 c=$2; shift 2
-  run $n 240 rocprofv3 --kernel-trace --stats -d $O/$n -o $n -- python3 scripts/kprof.py --iters 30 --config $c "$@" || return 1
-  python3 scripts/kstats_db.py $(find $O/$n -name "*.db" | head -1) $O/${n}_kernel_stats.csv 2>/dev/null || \
-    cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats.csv
-  head -6 $O/${n}_kernel_stats.csv
+  # 10 warmup evaluations (GPU clocks ramp up over the first ~15 dispatches), then the 30 the summary
+  # averages; the _all summary keeps every dispatch
+  run $n 240 rocprofv3 --kernel-trace --stats -d $O/$n -o $n -- python3 scripts/kprof.py --warmup 10 --iters 30 \
+      --config $c "$@" || return 1
+  local db=$(find $O/$n -name "*.db" | head -1)
+  if [ -n "$db" ]; then
+    python3 scripts/kstats_db.py $db $O/${n}_kernel_stats.csv --skip 10 && python3 scripts/kstats_db.py $db $O/${n}_kernel_stats_all.csv
+  else
+    cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats_all.csv
+  fi
+  head -6 $O/${n}_kernel_stats*.csv
 }
 pmcsq() {  # name config: one pass of SQ stall / instruction counters over kprof (2 evaluations)
   local n=$1 c=$2; shift 2
@@ -98,6 +105,8 @@ for step in "$@"; do
     ab_c5_bfm) run ab_c5_bfm 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,shift" --tag c5_bfm || exit 1 ;;
     ab_c3_bfm) run ab_c3_bfm 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,shift" --tag c3_bfm || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
+    ab_c2) V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
+      run ab_c2 400 python scripts/kvariants.py --config c2 --rounds 8 --variants $V --tag ab_c2 || exit 1 ;;
     listctr) run listctr 120 rocprofv3 -L || exit 1 ;;
     fbcount) run fbcount 300 python scripts/fb_count.py || exit 1 ;;
     ab_c3) V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done

@@ -17,6 +17,8 @@ import bench  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--iters", type=int, default=2)
+ap.add_argument("--warmup", type=int, default=0,
+                help="evaluations before the --iters ones (traced too; kstats_db.py --skip drops them)")
 ap.add_argument("--pop", type=int, default=None, help="default: the config's (bench.CONFIG_DEFAULTS)")
 ap.add_argument("--rollouts", type=int, default=None)
 ap.add_argument("--no-traj", action="store_true")
@@ -31,7 +33,7 @@ env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rol
                                                                       obs_noise=a.obs_noise), 0)
 eng = DeviceEngine(ff, lib, 0.0, "cuda:0", native=nat.load(a.lib))
 pd = torch.from_numpy(pop).cuda()
-for i in range(a.iters):  # statuses checked once (the timed bench loop never synchronises either)
+for i in range(a.warmup + a.iters):  # statuses checked once (the timed bench loop never synchronises either)
     eng.evaluate(pd, data, trajectories=not a.no_traj, step_counts=a.solver == "dopri5", check=i == 0)
 torch.cuda.synchronize()
 print("done")
