@@ -25,14 +25,16 @@ body_fun, gp.py:366-372).  Trees built by the reference's operators never read s
 (children sit below their parent, leaves ignore their index fields), so for them the gradients
 agree; for arbitrary arrays only coefficient rows are optimised.
 
-Deviation 2 (adaptive solves, Dopri5 + PIDController): the gradient is the derivative of the
-discrete solution along the step sequence the primal solve took -- step sizes, accept / reject
-decisions and the NaN event are held at their primal values.  ``jax.grad`` through diffrax's
-``DirectAdjoint`` may also differentiate the controller's next step size through the error norm
-(the "dt term"); no reference fixture pins it, so that term is absent here.  Measured against
-central differences of the float32 loss over every finite, unclipped candidate (no smoothness
-filter, tests/test_coefficients.py): median relative error 7e-4, 75th percentile 3e-3, 90th 3e-2
--- the dropped term matters only where a perturbation changes the accept / reject sequence.
+Adaptive solves (Dopri5 + PIDController): the gradient is the derivative of the discrete
+solution along the step sequence the primal solve took -- step sizes, accept / reject decisions
+and the NaN event carry no tangent.  That is diffrax's own rule under ``DirectAdjoint``: its
+PIDController applies ``lax.stop_gradient`` to the initial step size (``init``) and to the
+multiplicative step-size factor (``adapt_step_size``), so every step size has a zero tangent and
+``jax.grad`` differentiates the discretised solution, not the ODE solution (diffrax is absent here:
+restated from its published source, not executed).  Central differences of the float32 loss DO
+move the step sizes, so they differ from it where a perturbation changes the accept / reject
+sequence; over every finite, unclipped candidate (no smoothness filter, tests/test_coefficients.py)
+the median relative difference is 7e-4, 75th percentile 3e-3, 90th 3e-2.
 """
 from __future__ import annotations
 

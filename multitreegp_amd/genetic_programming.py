@@ -147,8 +147,8 @@ class GeneticProgramming:
         candidates (by fitness before parsimony) get `gradient_steps` optimiser steps on their
         coefficients (gp.py:418-422; multitreegp_amd.coefficients), split over the ranks like
         shard_optimise (gp.py:264-267) and all-gathered.  Under Dopri5 + PIDController the
-        gradients hold the step sizes at their primal values (the controller's dt term is not
-        differentiated: multitreegp_amd.coefficients, "Deviation 2")."""
+        step sizes carry no tangent, as diffrax's controller stops their gradient
+        (multitreegp_amd.coefficients)."""
         pops = np.asarray(populations, dtype=np.float32)
         P = self.num_populations * self.population_size
         flat = pops.reshape(P, *pops.shape[2:])

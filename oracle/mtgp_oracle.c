@@ -936,9 +936,10 @@ static ODual sr_rollout_dual(const OrModel* m, const float* cand, int N, const O
 
 /* sr_rollout_dual for the adaptive solve: solve_dopri5 (include/mtgp_dopri5.h) in dual numbers
  * with the step sizes, the accept / reject decisions and the event held at their primal values --
- * the derivative of the discrete solution along the step sequence the solve took.  (Whether
- * diffrax's DirectAdjoint also differentiates the controller's next-step size is not pinned here:
- * that term is of the order of the local error tolerance.)  The value half is solve_dopri5 + the
+ * the derivative of the discrete solution along the step sequence the solve took, which is what
+ * jax.grad gives through diffrax's DirectAdjoint: diffrax's PIDController stops the gradient of the
+ * initial step size (init) and of the step-size factor (adapt_step_size), so no step size carries
+ * a tangent.  The value half is solve_dopri5 + the
  * evaluator's MSE of the saved points bit for bit; the tangent half applies the same linear maps
  * (stage fma chains, dense output at the primal theta) to the tangents. */
 static ODual sr_rollout_dual_dp(const OrModel* m, const float* cand, int N, const OrLib* lib, const OrRollouts* ro,

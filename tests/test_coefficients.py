@@ -279,8 +279,9 @@ def test_oracle_dopri5_loss_is_the_fitness():
 
 def test_oracle_dopri5_gradient_matches_central_differences():
     """The Dopri5 sensitivities hold the step sizes at their primal values (oracle
-    sr_rollout_dual_dp); a central difference of the oracle's own float32 loss also moves the
-    controller's step sizes, by terms of the order of the tolerance.  Well-conditioned candidates
+    sr_rollout_dual_dp; diffrax's PIDController stops their gradient the same way); a central
+    difference of the oracle's own float32 loss also moves the controller's step sizes, by terms
+    of the order of the tolerance.  Well-conditioned candidates
     (finite, unclipped loss; forward and backward differences within 2 % of each other) agree to a
     few 1e-3."""
     lib, ff, data, d, pop = _setup_dp(P=24, seed=3)
