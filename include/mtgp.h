@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MTGP_ABI_VERSION 19
+#define MTGP_ABI_VERSION 20
 
 /* ---------------------------------------------------------------- limits */
 #define MTGP_MAX_FUNCS 128   /* node functions 2 + K + V (gp.py:135-199)       */
@@ -240,7 +240,14 @@ typedef struct {
   /* ABI v17 (scratch): [n_save, P*R] f32 running cost prefixes of the general Acrobot mask, or NULL */
   /* (see MtgpRollouts.fit_kof)                                                                     */
   float* fit_hist;
+  /* ABI v20: trajectory layout.  MTGP_TRAJ_TIME_MAJOR (0): the rows above.  MTGP_TRAJ_LANE_MAJOR */
+  /* (1): xs[((p*R + r)*n_save + k)*n_var + c] (ys / us / acts likewise) -- the reference's       */
+  /* [P, R, S, c] order; adaptive (MTGP_SOLVER_DOPRI5) solves only, MTGP_ERR_ARG otherwise: their */
+  /* save points are divergent, and lane-contiguous rows halve the write traffic.     */
+  int32_t traj_layout;
 } MtgpOutputs;
+#define MTGP_TRAJ_TIME_MAJOR 0
+#define MTGP_TRAJ_LANE_MAJOR 1
 #define MTGP_DP_STATE_WORDS 32
 
 /* ------------------------------------------------------------- entry points */

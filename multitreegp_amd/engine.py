@@ -494,14 +494,23 @@ class DeviceEngine:
             out.fit_hist = res["_fit_hist"].data_ptr()
         if trajectories:
             PR = P * R
-            if self.ff.model_id == nat.MODEL_SR:
-                res["xs"] = torch.empty((S, m.n_var, PR), dtype=torch.float32, device=dev)
-                out.xs = res["xs"].data_ptr()
-            else:
-                for name, c in (("xs", m.n_var), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size)):
-                    if c > 0:
-                        res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
-                        setattr(out, name, res[name].data_ptr())
+            # Adaptive solves write lane-major rows (mtgp.h traj_layout, ABI v20: each lane's divergent
+            # save points land contiguously -- half the write traffic); the result is handed back as
+            # the same [S, c, P*R] tensor a fixed-step solve gives, a strided view of the [P*R, S, c]
+            # buffer (whose [P, R, S, c] reading is the reference's layout: to_reference_layout).
+            # MTGP_TRAJ_LAYOUT=time forces time-major rows (A/B).
+            lane_major = m.solver == nat.SOLVER_DOPRI5 and os.environ.get("MTGP_TRAJ_LAYOUT", "auto") != "time"
+            out.traj_layout = nat.TRAJ_LANE_MAJOR if lane_major else nat.TRAJ_TIME_MAJOR
+            names = (("xs", m.n_var),) if self.ff.model_id == nat.MODEL_SR else \
+                (("xs", m.n_var), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size))
+            for name, c in names:
+                if c > 0:
+                    if lane_major:
+                        buf = torch.empty((PR, S, c), dtype=torch.float32, device=dev)
+                        res[name] = buf.permute(1, 2, 0)
+                    else:
+                        buf = res[name] = torch.empty((S, c, PR), dtype=torch.float32, device=dev)
+                    setattr(out, name, buf.data_ptr())
         stream = torch.cuda.current_stream(dev).cuda_stream
         jit = self.jit_build(fl, m, lanes, ro_order)
         jc = nat.MtgpJitCode()

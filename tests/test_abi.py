@@ -27,8 +27,8 @@ def test_struct_layouts_match_header(tmp_path):
     src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mtgp.h"\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu\\n",'
                    'sizeof(MtgpNodeLibrary), sizeof(MtgpProgramSpec), sizeof(MtgpInstr), sizeof(MtgpModel),'
                    'sizeof(MtgpRollouts), sizeof(MtgpOutputs), offsetof(MtgpModel, readout_save_same));'
-                   'printf("%zu %zu %zu %zu\\n", offsetof(MtgpRollouts, lanes), offsetof(MtgpModel, dp_budget),'
-                   'sizeof(MtgpGradJit), offsetof(MtgpGradJit, info));return 0;}\n')
+                   'printf("%zu %zu %zu %zu %zu\\n", offsetof(MtgpRollouts, lanes), offsetof(MtgpModel, dp_budget),'
+                   'sizeof(MtgpGradJit), offsetof(MtgpGradJit, info), offsetof(MtgpOutputs, traj_layout));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True).stdout.split()]
@@ -37,7 +37,8 @@ def test_struct_layouts_match_header(tmp_path):
                                                                               nat.MtgpRollouts.lanes.offset,
                                                                               nat.MtgpModel.dp_budget.offset,
                                                                               ctypes.sizeof(nat.MtgpGradJit),
-                                                                              nat.MtgpGradJit.info.offset]
+                                                                              nat.MtgpGradJit.info.offset,
+                                                                              nat.MtgpOutputs.traj_layout.offset]
     assert got == want
 
 
@@ -83,6 +84,12 @@ def test_argument_validation_without_gpu():
     out.dp_state = None                                                     # the parked-state buffer is required
     m.model, m.n_var, m.n_obs, m.n_control, m.state_size = 1, 4, 4, 1, 2  # otherwise a valid Acrobot model
     assert rk4() == nat.ERR_ARG
+    # lane-major trajectory rows (ABI v20) only for the adaptive solve; unknown layouts rejected
+    m.solver, m.dp_budget, m.max_steps, m.n_save = 0, 0, 0, 4
+    out.xs, out.traj_layout = one.ctypes.data, nat.TRAJ_LANE_MAJOR
+    assert rk4() == nat.ERR_ARG
+    out.traj_layout = 7
+    assert rk4() == nat.ERR_ARG
 
 
 def _define(text, name):
@@ -103,6 +110,8 @@ def test_constants_match_header():
     assert _define(text, "MTGP_MAX_ROLLOUTS") == nat.MAX_ROLLOUTS
     assert _define(text, "MTGP_DP_STATE_WORDS") == nat.DP_STATE_WORDS
     assert _define(text, "MTGP_GRAD_JIT_WORDS_PER_INSTR") == nat.GRAD_JIT_WORDS_PER_INSTR
+    assert _define(text, "MTGP_TRAJ_TIME_MAJOR") == nat.TRAJ_TIME_MAJOR
+    assert _define(text, "MTGP_TRAJ_LANE_MAJOR") == nat.TRAJ_LANE_MAJOR
     ops = open(os.path.join(ROOT, "include", "mtgp_opcodes.h")).read()
     pairs = re.findall(r"MTGP_OP_(\w+) = (\d+),", ops)
     assert [n for n, _ in pairs] == nat.OP_NAMES and [int(v) for _, v in pairs] == list(range(len(pairs)))

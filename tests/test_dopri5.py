@@ -432,3 +432,31 @@ def test_gpu_dopri5_two_launches_bitexact(kind, budget, jit):
     assert np.array_equal(res["steps"], one["steps"])
     if budget in (1, 7):  # these budgets split the solves (some waves were parked)
         assert (one["steps"] > budget).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["dynamic", "static_noise", "sr", "sr_wide"])
+def test_gpu_dopri5_traj_layouts_identical(kind, monkeypatch):
+    """MtgpOutputs.traj_layout (ABI v20): the adaptive kernels' lane-major rows (the engine's
+    default for Dopri5) hold exactly the time-major rows' values, element for element, in every
+    kernel family (control k_ctl_dopri5, register SR k_sr_dopri5, wide SR k_sr_wide_dopri5);
+    fixed-step solves keep time-major rows."""
+    from helpers import bits_equal, dynamic_setup, static_setup
+    solver = (1e-4, 1e-4, 0.001, 200)
+    if kind == "dynamic":
+        e, lib, ff, data, pop = dynamic_setup(P=21, R=12, n_steps=40, seed=4, solver=solver)
+    elif kind == "static_noise":
+        e, lib, ff, data, pop = static_setup(P=21, R=12, n_steps=40, seed=4, obs_noise=0.1, solver=solver)
+    else:
+        e, lib, ff, data, pop = sr_setup(P=19, R=8, n_save=21, save_every=4, h=0.01, seed=5,
+                                         n_var=2 if kind == "sr" else 6, solver=(1e-5, 1e-5, 0.001, 300))
+    monkeypatch.setenv("MTGP_TRAJ_LAYOUT", "time")
+    tm, _ = _gpu_run(ff, lib, data, pop, True)
+    monkeypatch.setenv("MTGP_TRAJ_LAYOUT", "auto")
+    lm, _ = _gpu_run(ff, lib, data, pop, True)
+    assert bits_equal(tm["fitness"], lm["fitness"])
+    names = [k for k in ("xs", "ys", "us", "acts") if k in tm]
+    assert names and all(k in lm for k in names)
+    for k in names:
+        assert tm[k].shape == lm[k].shape
+        assert bits_equal(tm[k], lm[k]), k
