@@ -27,7 +27,8 @@ prof() {  # name config args...
       --config $c "$@" || return 1
   local db=$(find $O/$n -name "*.db" | head -1)
   if [ -n "$db" ]; then
-    python3 scripts/kstats_db.py $db $O/${n}_kernel_stats.csv --skip 10 && python3 scripts/kstats_db.py $db $O/${n}_kernel_stats_all.csv
+    # (SKIP: dispatches of one kernel per evaluation x 10 -- the Dopri5 kernel runs twice per evaluation)
+    python3 scripts/kstats_db.py $db $O/${n}_kernel_stats.csv --skip ${SKIP:-10} && python3 scripts/kstats_db.py $db $O/${n}_kernel_stats_all.csv
   else
     cp $(find $O/$n -name '*kernel_stats.csv' | head -1) $O/${n}_kernel_stats_all.csv
   fi
@@ -84,8 +85,8 @@ for step in "$@"; do
     prof_c3) prof prof_c3 c3 || exit 1 ;;
     prof_c2) prof prof_c2 c2 || exit 1 ;;
     prof_c5) prof prof_c5 c5 || exit 1 ;;
-    prof_dp) prof prof_dp c3 --solver dopri5 || exit 1 ;;
-    prof_dpn) prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
+    prof_dp) SKIP=20 prof prof_dp c3 --solver dopri5 || exit 1 ;;
+    prof_dpn) SKIP=20 prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
     dpab) run dpab 600 python scripts/dp_budget_ab.py || exit 1 ;;
     dpab_legacy) run dpab_legacy 900 python scripts/dp_budget_ab.py --legacy-pop --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab2) run dpab2 900 python scripts/dp_budget_ab.py --budgets 0,500 --rounds 3 || exit 1 ;;
