@@ -76,7 +76,8 @@ def test_kernel_stores_are_guarded_by_active():
     src = open(os.path.join(os.path.dirname(__file__), "..", "multitreegp_amd", "csrc", "mtgp_kernels.hip")).read()
     # the guarded blocks: every store_row call is preceded (within its block) by one of these guards
     guard = re.compile(r"if \((TRAJ && )?[^)]*\bactive\b|if \(!on\) return;")
-    pos = [m.start() for m in re.finditer(r"store_row(<true>)?\(A\.out\.", src)]
+    # (store_row: the time-major rows; traj_put_dp: the adaptive kernels' rows in either layout, ABI v20)
+    pos = [m.start() for m in re.finditer(r"(store_row(<true>)?|traj_put_dp)\(A\.out\.", src)]
     assert len(pos) > 20
     for p in pos:
         window = src[max(0, p - 1200):p]
