@@ -61,12 +61,16 @@ class DeviceEngine:
         """lanes: lanes per individual (MtgpRollouts.lanes); None = lane_set's occupancy policy,
         0 = R rounded up to a power of two (the densest packing), else at least that many.
         dp_budget: Dopri5 control models -- step attempts of the first of two launches
-        (MtgpModel.dp_budget; 0 = one launch; None = MTGP_DP_BUDGET, else max_steps // 2)."""
+        (MtgpModel.dp_budget; 0 = one launch; None = MTGP_DP_BUDGET, else automatic: max_steps // 2,
+        or one launch while the last two-launch evaluation parked few waves -- `_dp_choose`)."""
         self.lanes = lanes
         if dp_budget is None and os.environ.get("MTGP_DP_BUDGET"):
             dp_budget = int(os.environ["MTGP_DP_BUDGET"])
         self.dp_budget = None if dp_budget is None else int(dp_budget)
         self._dp_bufs = None
+        self._dp_probe = None   # (event, pinned count, waves) of the last two-launch evaluation
+        self._dp_frac = None    # its parked fraction
+        self._dp_evals = 0
         self.ff = fitness_function
         self.lib = library
         self.parsimony = float(size_parsinomy)
@@ -479,8 +483,9 @@ class DeviceEngine:
         # Dopri5 in two launches: the waves still integrating after max_steps / 2 attempts are parked
         # and resumed by a second launch that spreads them over all SIMDs (DESIGN.md "Dopri5 tail":
         # C3 + obs_noise 0.1, the notebooks' setting, 70.6 -> 58.4 ms; without noise 31.2 vs 32.1)
-        budget = self.dp_budget if self.dp_budget is not None else m.max_steps // 2
-        if m.solver == nat.SOLVER_DOPRI5 and self.ff.model_id != nat.MODEL_SR and budget > 0:
+        dp_ctl = m.solver == nat.SOLVER_DOPRI5 and self.ff.model_id != nat.MODEL_SR
+        budget = self.dp_budget if self.dp_budget is not None else (self._dp_choose(m.max_steps) if dp_ctl else 0)
+        if dp_ctl and budget > 0:
             waves = self.native.mtgp_eval_waves(P, R, lanes)
             if waves < 0:
                 raise RuntimeError(f"mtgp_eval_waves({P}, {R}, {lanes}) failed")
@@ -522,10 +527,38 @@ class DeviceEngine:
                                            ctypes.byref(jc), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_eval_rk4 rejected the configuration (code {rc})")
+        if dp_ctl and budget > 0 and self.dp_budget is None:  # the parked-wave count, read back lazily
+            cnt = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+            cnt.copy_(self._dp_bufs[1][:1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            self._dp_probe = (ev, cnt, waves)
         if check:
             self.check_status(fl)
         res["_flat"] = fl
         return res
+
+    # Two launches pay when many waves are still integrating after max_steps / 2 attempts (launch 2
+    # spreads them over the SIMDs) and cost when few are: measured on the C3 Dopri5 workload with
+    # lane-major rows (profiles/r05/v27_dpab_*.log), noise-free 288 of 4,096 waves parked, one launch
+    # 18.2 ms vs two 20.1 ms; obs_noise 0.1 1,587 parked, one launch 64.5 ms vs two 55.1 ms.  So the
+    # automatic budget is one launch while the last two-launch evaluation parked fewer than
+    # kDpOneLaunchFrac of its waves, re-probed with two launches every kDpProbeEvery evaluations
+    # (populations drift over generations).  Results are bit-identical for every budget.
+    kDpOneLaunchFrac = 0.2
+    kDpProbeEvery = 16
+
+    def _dp_choose(self, max_steps: int) -> int:
+        self._dp_evals += 1
+        if self._dp_probe is not None:
+            ev, cnt, waves = self._dp_probe
+            if ev.query():
+                self._dp_frac = int(cnt[0]) / max(waves, 1)
+                self._dp_probe = None
+        two = max_steps // 2
+        if self._dp_frac is None or self._dp_evals % self.kDpProbeEvery == 0:
+            return two
+        return 0 if self._dp_frac < self.kDpOneLaunchFrac else two
 
     def eval_programs(self, fl: Flattened, data_vectors: torch.Tensor) -> torch.Tensor:
         """Batched tree_evaluator: every program on M data vectors -> [P, n_prog, M]."""

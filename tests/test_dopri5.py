@@ -460,3 +460,19 @@ def test_gpu_dopri5_traj_layouts_identical(kind, monkeypatch):
     for k in names:
         assert tm[k].shape == lm[k].shape
         assert bits_equal(tm[k], lm[k]), k
+
+
+def test_dp_budget_auto_choice():
+    """DeviceEngine's automatic Dopri5 budget (no GPU needed): two launches until a two-launch
+    evaluation has reported its parked fraction, one launch while that fraction is below
+    kDpOneLaunchFrac, and a two-launch re-probe every kDpProbeEvery evaluations."""
+    from multitreegp_amd.engine import DeviceEngine
+    eng = object.__new__(DeviceEngine)
+    eng._dp_probe, eng._dp_frac, eng._dp_evals = None, None, 0
+    assert eng._dp_choose(1000) == 500  # nothing measured yet
+    eng._dp_frac = 288 / 4096  # C3 noise-free (profiles/r05/v27_dpab_clean.log)
+    picks = [eng._dp_choose(1000) for _ in range(2 * DeviceEngine.kDpProbeEvery)]
+    assert picks.count(500) == 2 and picks.count(0) == len(picks) - 2
+    assert all(picks[i] == 500 for i in range(len(picks)) if (i + 2) % DeviceEngine.kDpProbeEvery == 0)
+    eng._dp_frac = 1587 / 4096  # C3 with obs_noise 0.1 (v27_dpab_noise.log)
+    assert {eng._dp_choose(1000) for _ in range(20)} == {500}
