@@ -71,6 +71,7 @@ class DeviceEngine:
         self._dp_probe = None   # (event, pinned count, waves) of the last two-launch evaluation
         self._dp_frac = None    # its parked fraction
         self._dp_evals = 0
+        self._dp_pinned = None
         self.ff = fitness_function
         self.lib = library
         self.parsimony = float(size_parsinomy)
@@ -527,12 +528,14 @@ class DeviceEngine:
                                            ctypes.byref(jc), stream)
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_eval_rk4 rejected the configuration (code {rc})")
-        if dp_ctl and budget > 0 and self.dp_budget is None:  # the parked-wave count, read back lazily
-            cnt = torch.empty((1,), dtype=torch.int32, pin_memory=True)
-            cnt.copy_(self._dp_bufs[1][:1], non_blocking=True)
+        if dp_ctl and budget > 0 and self.dp_budget is None and self._dp_probe is None:
+            # the parked-wave count, read back lazily (one pinned word, reused once consumed)
+            if self._dp_pinned is None:
+                self._dp_pinned = torch.empty((1,), dtype=torch.int32, pin_memory=True)
+            self._dp_pinned.copy_(self._dp_bufs[1][:1], non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(dev))
-            self._dp_probe = (ev, cnt, waves)
+            self._dp_probe = (ev, self._dp_pinned, waves)
         if check:
             self.check_status(fl)
         res["_flat"] = fl
