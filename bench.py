@@ -290,12 +290,17 @@ def build_record() -> dict:
             h.update(chunk)
     st = os.stat(path)
     newest = max(ge.HIP_SOURCES, key=os.path.getmtime)
+    embedded = nat.build_info().get("sources_sha256")
+    tree = ge.sources_hash()
     return {"lib": os.path.relpath(path, os.path.dirname(os.path.abspath(__file__))), "bytes": st.st_size,
             "mtime": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(st.st_mtime)), "sha256_16": h.hexdigest()[:16],
+            "sources_sha256_embedded": embedded, "sources_sha256_tree": tree,
+            "sources_hash_match": embedded == tree,
             "stale_vs_sources": bool(ge._stale(path, ge.HIP_SOURCES)),
             "newest_source": os.path.basename(newest),
             "newest_source_mtime": time.strftime("%Y-%m-%dT%H:%M:%S", time.gmtime(os.path.getmtime(newest))),
-            "note": "stale_vs_sources false: build() reuses this library as shipped (no recompilation)"}
+            "note": "sources_hash_match: the library's embedded SHA-256 of its sources + flags (mtgp_build_info) "
+                    "equals the hash of this tree's HIP_SOURCES"}
 
 
 def main():
@@ -379,7 +384,8 @@ def main():
     # line's frac keeps them and both are reported
     alg_bytes_s8d = alg_bytes - (res["ys"].numel() * 4 if "ys" in res else 0)
     kmean = float(np.mean(kernel_ms))
-    achieved = alg_bytes / (kmean / 1e3) / 1e9
+    achieved = alg_bytes_s8d / (kmean / 1e3) / 1e9  # SURVEY §8(d) bytes per launch / kernel time
+    achieved_ys = alg_bytes / (kmean / 1e3) / 1e9
     traffic = valu = None
     pmc = None
     if rank == 0 and ws == 1 and not args.no_pmc:
@@ -430,12 +436,17 @@ def main():
                    "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps, "trajectories": traj,
                    "parallelism": f"population-sharded dp{ws}"},
         "kernel_ms": kmean,
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+        # The kernel is bound by VALU issue / dependent-instruction latency, not by HBM (DESIGN.md
+        # "Roofline"): frac is the HBM fraction on SURVEY §8(d)'s bytes (alg_bytes_s8d / kernel_ms /
+        # 8 TB/s, reproducible from profiles/ with the rocprof average), valu_frac the primary figure
+        # (VALU wave-instructions issued / the SIMDs' issue capacity over the kernel's cycles)
+        "roofline": {"bound": "valu-issue", "primary": "valu_frac", "valu_frac": valu,
+                     "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes,
+                     "traffic_over_alg_ys": None if traffic is None else traffic / alg_bytes,
                      "alg_bytes_s8d": alg_bytes_s8d,
-                     "frac_s8d": alg_bytes_s8d / (kmean / 1e3) / 1e9 / PEAK_HBM_GBS,
-                     "valu_frac": valu,
+                     "alg_bytes_ys_inclusive": alg_bytes,
+                     "frac_ys_inclusive": achieved_ys / PEAK_HBM_GBS,
                      "pmc": None if pmc is None else {k: pmc[k] for k in ("FETCH_SIZE", "WRITE_SIZE", "SQ_INSTS_VALU",
                                                                            "SQ_WAVES", "GRBM_GUI_ACTIVE")
                                                       if k in pmc}},

@@ -253,6 +253,11 @@ typedef struct {
 /* ------------------------------------------------------------- entry points */
 int mtgp_abi_version(void);
 
+/* Build provenance (round 6): copies "sources_sha256=<hex>;..." -- the SHA-256 of the sources,
+ * flags and defines the library was compiled from (__graft_entry__.sources_hash) -- into out
+ * (NUL-terminated, truncated to cap - 1 bytes) and returns the full length. */
+int mtgp_build_info(char* out, int32_t cap);
+
 /* Flatten a device population f32 [P, T, N, 4] (gp.py:412 layout) into programs
  * prog_out[P, n_prog, L], lengths len_out[P, n_prog], node counts nodes_out[P]
  * (non-empty rows, gp.py:424) and per-program status_out[P, n_prog].  nodes_out is zeroed

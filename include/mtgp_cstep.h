@@ -16,7 +16,8 @@
  *   step n integrates [t_n, tn_n] with dt_n = tn_n - t_n (ODETerm.contr)
  *   t_{n+1} = tn_n;  tn_{n+1} = t_{n+1} + dt0, and t1 when > t1 - 1e-6   adapt_step_size + _clip_to_end
  *   the loop runs while t_n < t1 and fewer than max_steps steps were taken (max_steps reached:
- *   the unsaved points stay +inf, throw=False).  The step ends are ACCUMULATED in f32, so they
+ *   the unsaved points stay +inf, throw=False), and ends early on a stalled grid
+ *   (mtgp_cs_advancing).  The step ends are ACCUMULATED in f32, so they
  *   drift off n * dt0 (C3: 189 of 200 step ends differ) and the step count can exceed the
  *   nominal one (t1 = 2, dt0 = 0.01: 201 steps, the last 1.5e-6 long).
  * Stages (ODETerm: is_vf_expensive False, so diffrax keeps the vector-field values f_i and forms each
@@ -57,6 +58,14 @@ MTGP_INLINE MTGP_HD float mtgp_cs_next_end(float t, float dt0, float t1) {
   const float tn = t + dt0;
   return tn > t1 - MTGP_CS_END_TOL ? t1 : tn;
 }
+
+/* Loop guard against a stalled grid: when dt0 is below half an ulp of t, t + dt0 rounds back to t
+ * and diffrax keeps taking dt = 0 steps until max_steps (then the unsaved points are +inf).  Only
+ * the FIRST such step can save anything (ts[k] <= tn = t; every later stalled step has the same
+ * tn, whose points are then already saved) and none of them moves a saved value, so ending the
+ * solve before the second stalled step gives the same outputs and cannot loop forever when the
+ * solve has no max_steps (C entry: max_steps 0). */
+MTGP_INLINE MTGP_HD int mtgp_cs_advancing(int steps, float t, float tn) { return steps == 0 || tn > t; }
 
 /* diffrax misc.linear_rescale: (t - t0) / (t1 - t0), 0 when t0 == t1 */
 MTGP_INLINE MTGP_HD float mtgp_cs_rescale(float t0, float t, float t1) {

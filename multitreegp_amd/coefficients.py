@@ -226,12 +226,14 @@ class CoefficientOptimiser:
             scratch = torch.empty((B * K * R * 2 * (1 + hist),), dtype=torch.float32, device=dev)
             lo_d = torch.empty((B,), dtype=torch.float32, device=dev)
             gr_d = torch.empty((B, K), dtype=torch.float32, device=dev)
+            called = grad_fn
             if self.use_jit and (eng.ff.model_id != nat.MODEL_SR or n_data <= 4):
                 code, nbytes = eng.grad_code_buffer(nat.grad_jit_bytes(B, n_prog, L))
                 offs = torch.empty((B * n_prog + 1,), dtype=torch.int32, device=dev)
                 info = torch.empty((2,), dtype=torch.int32, device=dev)
                 gj = nat.MtgpGradJit(code, nbytes, offs.data_ptr(), info.data_ptr())
                 jit_fn = eng.native.mtgp_sr_grad_jit if eng.ff.model_id == nat.MODEL_SR else eng.native.mtgp_ctl_grad_jit
+                called = jit_fn
                 rc = jit_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
                             ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), ctypes.byref(gj),
                             stream)
@@ -240,7 +242,7 @@ class CoefficientOptimiser:
                 rc = grad_fn(ctypes.byref(m), prog.data_ptr(), n_prog, L, B, th.data_ptr(), npd.data_ptr(), K,
                              ctypes.byref(ro), scratch.data_ptr(), lo_d.data_ptr(), gr_d.data_ptr(), stream)
             if rc != nat.OK:
-                raise RuntimeError(f"{grad_fn.__name__} rejected the configuration (code {rc})")
+                raise RuntimeError(f"{called.__name__} rejected the configuration (code {rc})")
             g = gr_d.cpu().numpy()
             if loss is None:
                 loss = lo_d.cpu().numpy()

@@ -292,7 +292,7 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
   const float t_end = ts[S - 1], dt0 = A.m.h;
   float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
   int steps = 0, ks = 0;
-  while (t < t_end && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
+  while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
     const float dt = tn - t;
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
@@ -1121,7 +1121,7 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     float t = ts[0], tn = mtgp_cs_first_end(t, h, t_end);
     int steps = 0, ks = 0;
     Dual f0[ND], y1[ND], sk[ND], kx[ND], acc[ND], tmp[ND];
-    while (t < t_end && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
+    while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
       const float dt = tn - t;
       // the stages from one rhs site (stage 0 included; Euler: stage 0 only)
 #pragma unroll 1

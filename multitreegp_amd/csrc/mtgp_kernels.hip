@@ -872,7 +872,7 @@ struct CsClock {
     max_steps = A.m.max_steps;
   }
   __device__ __forceinline__ bool live() const {
-    return uni((int)(t < t_end && (max_steps <= 0 || steps < max_steps))) != 0;
+    return uni((int)(t < t_end && mtgp_cs_advancing(steps, t, tn) && (max_steps <= 0 || steps < max_steps))) != 0;
   }
   __device__ __forceinline__ float dt() const { return tn - t; }
   __device__ __forceinline__ void advance() {

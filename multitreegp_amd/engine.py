@@ -456,7 +456,13 @@ class DeviceEngine:
                  flattened: Optional[Flattened] = None, check: bool = True, schedule: bool = True,
                  step_counts: bool = False) -> dict:
         """Run flatten + fused RK4 kernel.  Returns device tensors:
-        fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts time-major [S, c, P*R]).
+        fitness [P] (+ rollout_fitness [P, R], xs/ys/us/acts indexed [S, c, P*R]).
+        The trajectory tensors are indexed [S, c, P*R] for every solver, but only a fixed-step
+        solve stores them that way (contiguous, time-major rows); an adaptive solve writes
+        lane-major rows [P*R, S, c] (ABI v20) and returns a permuted, NON-contiguous view of that
+        buffer.  res["_traj_layout"] names the storage (nat.TRAJ_TIME_MAJOR / TRAJ_LANE_MAJOR):
+        read the tensors through indexing or to_reference_layout, and never hand their
+        data_ptr() to native code without checking it.
         schedule: pair expensive with cheap individuals in each wave (results are identical)."""
         d = self.prepare_data(data)
         fl = flattened if flattened is not None else self.flatten(pop)
@@ -507,6 +513,7 @@ class DeviceEngine:
             # MTGP_TRAJ_LAYOUT=time forces time-major rows (A/B).
             lane_major = m.solver == nat.SOLVER_DOPRI5 and os.environ.get("MTGP_TRAJ_LAYOUT", "auto") != "time"
             out.traj_layout = nat.TRAJ_LANE_MAJOR if lane_major else nat.TRAJ_TIME_MAJOR
+            res["_traj_layout"] = out.traj_layout
             names = (("xs", m.n_var),) if self.ff.model_id == nat.MODEL_SR else \
                 (("xs", m.n_var), ("ys", m.n_obs), ("us", m.n_control), ("acts", m.state_size))
             for name, c in names:

@@ -117,6 +117,15 @@ def _check_solver(solver, controller, adaptive_ok: bool = False) -> str:
     return sname
 
 
+def _check_max_steps(max_steps) -> int:
+    """diffeqsolve takes a positive max_steps (or None, which the reference never passes: dyn.py:11,
+    ff.py:11, sr.py:21 default 16**4).  The C entry reads max_steps 0 as "no limit" for the
+    fixed-step solve; the Python mirror never hands it one."""
+    if isinstance(max_steps, bool) or int(max_steps) != max_steps or int(max_steps) <= 0:
+        raise ValueError(f"max_steps must be a positive integer, got {max_steps!r}")
+    return int(max_steps)
+
+
 def _solver_fields(kind: str, controller, max_steps: int) -> dict:
     if kind != "dopri5":  # ConstantStepSize: max_steps bounds the fixed-step solve too (ABI v18)
         return dict(solver=nat.SOLVER_EULER if kind == "euler" else nat.SOLVER_RK4, max_steps=int(max_steps), rtol=0.0,
@@ -128,9 +137,12 @@ def _solver_fields(kind: str, controller, max_steps: int) -> dict:
 def constant_step_grid(ts: np.ndarray, dt0: float, max_steps: Optional[int] = None) -> np.ndarray:
     """Step ends of diffrax.ConstantStepSize through diffeqsolve(t0=ts[0], t1=ts[-1], dt0)
     (include/mtgp_cstep.h): float32, accumulated t += dt0 (the first end min(t0 + dt0, t1), later
-    ends t1 once past t1 - 1e-6), at most max_steps of them.  -> float32 [n_steps + 1] = the step
-    boundaries from ts[0].  The kernels follow the same rules on the device; this host copy sizes
-    the work (bench unit-steps, MtgpModel.n_steps)."""
+    ends t1 once past t1 - 1e-6), at most max_steps of them, ending before a second step that
+    would not advance t (mtgp_cs_advancing).  -> float32 [n_steps + 1] = the step boundaries from
+    ts[0].  The kernels follow the same loop on the device; this host copy sizes the work (bench
+    unit-steps, MtgpModel.n_steps).  The accumulation runs in chunks (np.add.accumulate adds left
+    to right in float32, the device's order), so a grid whose f32 sums need many more steps than
+    (t1 - t0) / dt0 is counted exactly, bounded by max_steps."""
     f = np.float32
     ts = np.asarray(ts, dtype=f)
     t0, t1, dt0 = f(ts[0]), f(ts[-1]), f(dt0)
@@ -138,23 +150,37 @@ def constant_step_grid(ts: np.ndarray, dt0: float, max_steps: Optional[int] = No
         raise ValueError(f"dt0 must be a positive finite number, got {dt0}")
     if not t0 < t1:
         return np.array([t0], f)
-    first = min(f(t0 + dt0), t1)
-    cap = int(np.ceil((float(t1) - float(t0)) / float(dt0))) + 4
-    if max_steps is not None and max_steps > 0:
-        cap = min(cap, int(max_steps) + 1)
-    # sequential float32 accumulation (np.add.accumulate adds left to right in the array dtype)
-    ends = np.add.accumulate(np.concatenate([[first], np.full(max(cap - 1, 0), dt0, f)]).astype(f), dtype=f)
+    limit = int(max_steps) if max_steps is not None and max_steps > 0 else None
     tol = f(t1 - f(1e-6))
-    over = np.nonzero(ends[1:] > tol)[0]
-    n = (over[0] + 2) if len(over) else len(ends)  # step ends kept, the clipped one included
-    if first >= t1:
-        n = 1
-    ends = ends[:n].copy()
-    if n > 1 and ends[-1] > tol:
-        ends[-1] = t1
-    if max_steps is not None and max_steps > 0:
-        ends = ends[: int(max_steps)]
-    return np.concatenate([[t0], ends]).astype(f)
+    ends = [np.array([min(f(t0 + dt0), t1)], f)]
+    n, last = 1, ends[0][0]
+    done = last >= t1 or (limit is not None and n >= limit)
+    chunk = int(min(np.ceil((float(t1) - float(t0)) / float(dt0)) + 4, 1 << 22))
+    while not done:
+        if limit is not None:
+            chunk = max(1, min(chunk, limit - n))
+        e = np.add.accumulate(np.concatenate([[last], np.full(chunk, dt0, f)]).astype(f), dtype=f)[1:]
+        over = np.nonzero(e > tol)[0]
+        stall = np.nonzero(e <= np.concatenate([[last], e[:-1]]))[0]  # tn <= t: this step would not advance
+        cut = len(e)
+        if len(stall):
+            cut = min(cut, int(stall[0]))
+            done = True
+        if len(over) and over[0] < cut:
+            cut = int(over[0]) + 1
+            e = e.copy()
+            e[cut - 1] = t1  # _clip_to_end
+            done = True
+        ends.append(e[:cut])
+        n += cut
+        last = e[cut - 1] if cut else last
+        if limit is not None and n >= limit:
+            done = True
+        chunk *= 2
+    out = np.concatenate(ends)
+    if limit is not None:
+        out = out[:limit]
+    return np.concatenate([[t0], out]).astype(f)
 
 
 def fixed_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int, int]:
@@ -165,6 +191,8 @@ def fixed_schedule(ts: np.ndarray, dt0: float, max_steps: int) -> Tuple[int, int
     S = int(ts.shape[0])
     if S < 2 or np.any(np.diff(ts) < 0) or not np.all(np.isfinite(ts)):
         raise ValueError("ts needs at least two finite non-decreasing save points")
+    if not ts[0] < ts[-1]:  # diffrax's t0 == t1 special case (y0 at every save point): not built
+        raise ValueError("ts[0] == ts[-1]: an empty solve interval")
     n_steps = len(constant_step_grid(ts, dt0, max_steps)) - 1
     return n_steps, 1, S
 
@@ -179,6 +207,8 @@ def adaptive_schedule(ts: np.ndarray) -> Tuple[int, int, int]:
     S = int(ts.shape[0])
     if S < 2 or np.any(np.diff(ts) < 0):
         raise ValueError("ts needs at least two non-decreasing save points")
+    if not ts[0] < ts[-1]:  # diffrax's t0 == t1 special case (y0 at every save point): not built
+        raise ValueError("ts[0] == ts[-1]: an empty solve interval")
     return 0, 1, S
 
 
@@ -292,7 +322,7 @@ class _ControlEvaluator(_CandidateAPI):
         self.latent_size = env.n_var * env.n_dim
         self.dt0 = float(dt0)
         self.solver = solver
-        self.max_steps = max_steps
+        self.max_steps = _check_max_steps(max_steps)
         self.stepsize_controller = stepsize_controller
 
     def obs_gap(self) -> Tuple[int, int]:
@@ -410,7 +440,7 @@ class SREvaluator(_CandidateAPI):
         self.solver_kind = _check_solver(solver, stepsize_controller, adaptive_ok=True)
         self.dt0 = float(dt0)
         self.solver = solver
-        self.max_steps = max_steps
+        self.max_steps = _check_max_steps(max_steps)
         self.stepsize_controller = stepsize_controller
         self.state_size = 0
         self._n_var = None

@@ -336,7 +336,7 @@ static int solve_fixed(const OrCtx* c, const float* ts, const float* s0, float* 
   float prev = cond_fn(m, y);
   int k = 0, steps = 0;
   float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
-  while (t < t_end && (m->max_steps <= 0 || steps < m->max_steps)) {
+  while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (m->max_steps <= 0 || steps < m->max_steps)) {
     const float dt = tn - t;
     rhs(c, t, y, f0);
     if (euler) {
@@ -375,7 +375,7 @@ int oracle_cs_steps(const float* ts, int S, float dt0) {
   const float t_end = ts[S - 1];
   float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
   int steps = 0;
-  while (t < t_end) {
+  while (t < t_end && mtgp_cs_advancing(steps, t, tn)) {
     ++steps;
     t = tn;
     tn = mtgp_cs_next_end(t, dt0, t_end);
@@ -855,7 +855,7 @@ static int fixed_dual(const OrModel* m, const float* ts, const ODual* s0, OrDual
   float prev = cond_fn(m, sv);
   int k = 0, steps = 0;
   float t = ts[0], tn = mtgp_cs_first_end(t, dt0, t_end);
-  while (t < t_end && (m->max_steps <= 0 || steps < m->max_steps)) {
+  while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (m->max_steps <= 0 || steps < m->max_steps)) {
     const float dt = tn - t;
     rhs(ctx, t, y, f0);
     if (euler) {

@@ -127,6 +127,14 @@ for step in "$@"; do
           python3 scripts/kprof.py --iters 2 --config c3 --lib $L || exit 1
         python3 scripts/pmc_summary.py $O/budget_pmc_$v k_ctl_dynamic > $O/budget_pmc_$v.json; cat $O/budget_pmc_$v.json
       done ;;
+    pmc_fair)  # FETCH / WRITE of k_ctl_dynamic with the FairShare table off (MTGP_FAIR=0) and on (default)
+      for f in 0 3; do
+        for c in FETCH_SIZE WRITE_SIZE; do
+          run pmc_fair${f}_$c 120 env MTGP_FAIR=$f timeout -s KILL 90 rocprofv3 --pmc $c -d $O/pmc_fair${f}_$c -o pmc \
+            --output-format csv -- python3 scripts/kprof.py --iters 2 --config c3 || exit 1
+          python3 scripts/pmc_summary.py $O/pmc_fair${f}_$c k_ctl_dynamic > $O/pmc_fair${f}_$c.json; cat $O/pmc_fair${f}_$c.json
+        done
+      done ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;

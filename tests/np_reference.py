@@ -133,7 +133,7 @@ def cs_grid(ts, dt0, max_steps=None):
     t, t1, dt0 = f(ts[0]), f(ts[-1]), f(dt0)
     tn = min(f(t + dt0), t1)
     out = []
-    while t < t1 and (max_steps is None or len(out) < max_steps):
+    while t < t1 and (max_steps is None or len(out) < max_steps) and (not out or tn > t):
         out.append((t, tn))
         t = tn
         tn = f(t + dt0)

@@ -142,3 +142,37 @@ def test_unaligned_program_stride_rejected():
                              ctypes.byref(ro), ctypes.byref(out), None) == nat.ERR_ARG
     assert lib.mtgp_eval_programs(one.ctypes.data, one.ctypes.data, 1, 6, 1, one.ctypes.data, 1, 1,
                                   one.ctypes.data, None) == nat.ERR_ARG
+
+
+def _local_includes(path, seen):
+    """Every quoted #include reachable from path, resolved in csrc/ then include/."""
+    import __graft_entry__ as ge
+    for name in re.findall(r'^\s*#\s*include\s+"([^"]+)"', open(path).read(), re.M):
+        for d in (ge.CSRC, os.path.join(ge.ROOT, "include")):
+            p = os.path.join(d, name)
+            if os.path.exists(p):
+                if p not in seen:
+                    seen.add(p)
+                    _local_includes(p, seen)
+                break
+        else:
+            raise AssertionError(f"{path}: include {name} not found in csrc/ or include/")
+    return seen
+
+
+def test_hip_sources_cover_every_included_header():
+    """HIP_SOURCES decides when libmtgp_hip.so is rebuilt and what its sources hash covers: every
+    header a kernel source includes (transitively) must be listed (mtgp_jit_dual.h was not)."""
+    import __graft_entry__ as ge
+    listed = {os.path.realpath(p) for p in ge.HIP_SOURCES}
+    for src in [p for p in ge.HIP_SOURCES if p.endswith(".hip")]:
+        for h in _local_includes(src, set()):
+            assert os.path.realpath(h) in listed, f"{h} (included by {src}) is missing from HIP_SOURCES"
+
+
+def test_build_info_matches_tree():
+    """Build provenance by content: the library embeds the SHA-256 of the sources it was built from."""
+    import __graft_entry__ as ge
+    info = nat.build_info()
+    assert info.get("sources_sha256") == ge.sources_hash(), \
+        "libmtgp_hip.so was built from other sources than this tree: run __graft_entry__.build()"

@@ -160,3 +160,62 @@ def test_oracle_euler_known_answer():
         assert np.array_equal(out["xs"][0, r, :, 0].view(np.uint32), want.view(np.uint32))
     # and the textbook closed form of Euler's recursion within the grid's rounding
     assert np.allclose(out["xs"][0, 0, :, 0], (1.0 - 0.05) ** np.arange(21), rtol=1e-5)
+
+
+def test_max_steps_must_be_positive():
+    """diffeqsolve takes a positive max_steps; the C entry reads 0 as "no limit" for the fixed-step
+    solve, so the Python mirror never hands it 0 or a negative count."""
+    env = mt.Acrobot(0.0, 0.0)
+    for bad in (0, -1, 2.5, True):
+        with pytest.raises(ValueError):
+            mt.DynamicEvaluator(env, 2, 0.05, solver=mt.RK4(), max_steps=bad)
+        with pytest.raises(ValueError):
+            mt.FeedforwardEvaluator(env, 0.05, solver=mt.RK4(), max_steps=bad)
+        with pytest.raises(ValueError):
+            mt.SREvaluator(solver=mt.RK4(), dt0=0.05, max_steps=bad)
+    assert mt.SREvaluator(solver=mt.RK4(), dt0=0.05, max_steps=np.int64(7)).max_steps == 7
+
+
+def test_degenerate_interval_rejected():
+    """ts[0] == ts[-1]: diffrax special-cases t0 == t1 (y0 at every save point); not built, so it
+    raises instead of silently returning +inf saves."""
+    from multitreegp_amd.evaluators import adaptive_schedule
+    ts = np.array([1.0, 1.0, 1.0], np.float32)
+    with pytest.raises(ValueError):
+        fixed_schedule(ts, 0.05, 100)
+    with pytest.raises(ValueError):
+        adaptive_schedule(ts)
+
+
+def test_stalled_grid_is_finite():
+    """dt0 below half an ulp of t: t + dt0 rounds back to t.  diffrax would take dt = 0 steps until
+    max_steps; the loop guard (mtgp_cs_advancing) ends after the first such step, which is the only
+    one that can save anything -- the host grid, the numpy restatement and the oracle's step count
+    agree, and none of them loops forever without max_steps."""
+    import np_reference as npr
+    from oracle import oracle as orc
+    ts = np.array([1000.0, 1000.5, 1001.0], np.float32)
+    g = constant_step_grid(ts, 1e-5)
+    assert len(g) == 2 and g[1] == g[0]  # one (stalled) step
+    assert len(npr.cs_grid(ts, 1e-5)) == 1 and orc.cs_steps(ts, 1e-5) == 1
+    # stalls part-way: 2**24 + dt0 advances while t < 2**24, then stops advancing
+    ts2 = np.array([16777200.0, 16777300.0], np.float32)
+    g2 = constant_step_grid(ts2, 1.0, 10 ** 6)
+    ref = npr.cs_grid(ts2, 1.0, 10 ** 6)
+    assert len(g2) - 1 == len(ref) == orc.cs_steps(ts2, 1.0) and len(ref) < 100
+
+
+def test_stalled_grid_oracle_solve_ends_with_inf_saves():
+    """The oracle's fixed-step solve on a stalled grid with max_steps 0 (no limit, the C entry's
+    reading) terminates; the saves the grid never reaches are +inf (as diffrax's max_steps exit)."""
+    from oracle import oracle as orc
+    from test_oracle import _linear_sr_candidate
+    lib, cand = _linear_sr_candidate()
+    ts = np.array([1000.0, 1000.5, 1001.0], np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                 n_save=3, h=1e-5, max_fitness=1e5, parsimony=0.0, solver=0, max_steps=0)
+    x0 = np.array([[1.0, 0.0]], np.float32)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((1, 3, 2), np.float32)),
+                       trajectories=True)
+    xs = out["xs"][0, 0]
+    assert np.array_equal(xs[0], x0[0]) and np.all(np.isposinf(xs[1:]))

@@ -43,7 +43,7 @@ def test_schedule_is_balanced_permutation(P, R):
 def _eval(eng, pop_dev, data, **kw):
     res = eng.evaluate(pop_dev, data, trajectories=True, rollout_fitness=True, **kw)
     torch.cuda.synchronize()
-    return {k: v.cpu().numpy() for k, v in res.items() if k != "_flat"}
+    return {k: v.cpu().numpy() for k, v in res.items() if isinstance(v, torch.Tensor)}
 
 
 def _same(a, b):
