@@ -213,12 +213,18 @@ def adaptive_schedule(ts: np.ndarray) -> Tuple[int, int, int]:
 
 
 def acrobot_mask(ts: np.ndarray) -> Optional[Tuple[np.ndarray, bool]]:
-    """The Acrobot cost mask `ts / (ts[1] - ts[0]) > first_success` (acrobot.py:82) as the count
-    table MtgpRollouts.fit_kof: kof[f] = #{k : f32(ts[k] / (ts[1] - ts[0])) <= f32(f)} -- the mask
-    keeps the first kof[first_success] costs when the ratio is non-decreasing.  None when the ratio
-    of save k lies in (k - 1, k + 1] for every k (ts from 0 on a uniform grid: the kernels' one-pass
-    fitness).  -> (kof int32 [S], need_hist: some f >= 1 has 1 <= kof[f] <= f, so the kernels keep
-    the per-save cost prefixes in MtgpOutputs.fit_hist)."""
+    """The Acrobot cost mask `costs = where(ts / (ts[1] - ts[0]) > first_success, 0, cost)`
+    (acrobot.py:82) as the count table MtgpRollouts.fit_kof.  Save k's cost is kept for a
+    first_success f unless f32(ratio_k) > f32(f), so it is masked exactly for the integers
+    f < m_k with m_k = #{f in [0, S) : f < ratio_k} -- ceil(ratio_k) clipped to [0, S], 0 for a
+    NaN ratio (NaN > f is False: kept), S for +inf (masked), 0 for -inf (kept).  When m_k is
+    non-decreasing in k the kept costs for every f are the first kof[f] = #{k : m_k <= f} saves.
+    That holds for every valid ts: with ts[1] > ts[0] the ratio is non-decreasing, and with
+    ts[1] == ts[0] (a repeated first save time) the ratio is NaN where ts_k == 0, -inf below 0 and
+    +inf above, i.e. the kept saves are those with ts_k <= 0 for every f.
+    None when the ratio of save k lies in (k - 1, k + 1] for every k (ts from 0 on a uniform grid:
+    the kernels' one-pass fitness).  -> (kof int32 [S], need_hist: some f >= 1 has
+    1 <= kof[f] <= f, so the kernels keep the per-save cost prefixes in MtgpOutputs.fit_hist)."""
     ts = np.asarray(ts, dtype=np.float32)
     S = int(ts.shape[0])
     with np.errstate(divide="ignore", invalid="ignore"):
@@ -226,10 +232,14 @@ def acrobot_mask(ts: np.ndarray) -> Optional[Tuple[np.ndarray, bool]]:
     k = np.arange(S, dtype=np.float32)
     if np.all(ratio > k - 1) and np.all(ratio <= k + 1):
         return None
-    if np.any(np.isnan(ratio)) or np.any(np.diff(ratio) < 0):
-        raise NotImplementedError("Acrobot fitness mask: ts / (ts[1] - ts[0]) must be non-decreasing "
-                                  "(the mask is then a prefix of the save points)")
-    kof = np.searchsorted(ratio, np.arange(S, dtype=np.float32), side="right").astype(np.int32)
+    r = ratio.astype(np.float64)  # exact: every f32 ratio and every integer f < S compare the same
+    with np.errstate(invalid="ignore"):
+        m = np.where(np.isnan(r) | (r <= 0), 0.0, np.minimum(np.ceil(np.where(np.isfinite(r), r, S)), S))
+    m = m.astype(np.int64)
+    if np.any(np.diff(m) < 0):
+        raise NotImplementedError("Acrobot fitness mask: the kept save points are not a prefix for every "
+                                  "first_success (ts must be non-decreasing)")
+    kof = np.searchsorted(m, np.arange(S), side="right").astype(np.int32)
     f = np.arange(S)
     need_hist = bool(np.any((f >= 1) & (kof >= 1) & (kof <= f)))
     return kof, need_hist

@@ -53,6 +53,7 @@ for step in "$@"; do
     test) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmask) run pytest_mask 600 python -u -m pytest tests/test_gpu_acrobot_mask.py tests/test_gpu_parity.py tests/test_dopri5.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testmaskonly) run pytest_maskonly 300 python -u -m pytest tests/test_gpu_acrobot_mask.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
+    selection) run selection 600 env MTGP_REPORT_DIR=$O python -u -m pytest tests/test_notebook_selection.py -m gpu -x -v -s --timeout 300 --timeout-method thread || exit 1 ;;
     testpin) run pytest_pin 600 python -u -m pytest tests/test_gpu_parity.py tests/test_notebook_pin.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testcoef) run pytest_coef 600 python -u -m pytest tests/test_coefficients.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     gradtime) run gradtime 300 python scripts/grad_time.py || exit 1 ;;
