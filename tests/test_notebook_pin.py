@@ -387,10 +387,10 @@ def test_dynamic_notebook_printed_best_in_ensemble_tail(name):
     are chaotic at the last bit: sd 3-10 units), and the printed value is the minimum over 500
     evolving candidates, so it must sit in the ensemble's lower tail.  With the attempt limit
     relaxed (max_steps 4000, no solve cut) it does for all three: min <= printed <= mean.  At the
-    notebook's max_steps 1000 the gen-5 and gen-30 values lie below our whole ensemble: our solves
-    are cut more often than the reference's were (DESIGN.md "Parity pins": a few % more Dopri5
-    attempts than diffrax took would do it; not resolvable without diffrax).  The test asserts
-    what holds and pins the measured gap so that a change in either direction is noticed."""
+    notebook's max_steps 1000 the statement needs the selection-scale ensemble of
+    tests/test_notebook_selection.py (2,176 members per pin over the sympy form's hidden choices):
+    gen 30 and gen 50 then lie in the lower tail (quantiles 0.3 % and 5.6 %), gen 5 stays below
+    every member (DESIGN.md "Parity pins": an established discrepancy)."""
     printed = DYNAMIC_PINS[name][2]
     relaxed = _dyn_ensemble(name, 4000)
     assert np.all(np.isfinite(relaxed))
@@ -398,10 +398,9 @@ def test_dynamic_notebook_printed_best_in_ensemble_tail(name):
     assert relaxed.mean() - printed < 4.0 * relaxed.std() + 1.0, (name, relaxed.mean(), relaxed.std())
     notebook = _dyn_ensemble(name, 1000)
     assert printed <= notebook.max()
-    # the recorded, unexplained gap at the notebook's max_steps (DESIGN.md "Parity pins": every
-    # published-behaviour reading of diffrax leaves it; test_dynamic_notebook_gap_readings)
-    gap = {"gen5": (25.0, 35.0), "gen30": (3.0, 9.0), "gen50": (-1.0, 2.0)}[name]  # measured: 28.3 / 5.4 / -0.6
-    assert gap[0] <= notebook.min() - printed <= gap[1], (name, notebook.min(), printed)
+    # At the notebook's max_steps the 48-member ensemble is too small to place a minimum over 500
+    # candidates; the selection-scale statement (>= 2,000 members per pin, the printed value's
+    # quantile) is tests/test_notebook_selection.py::test_gpu_dynamic_notebook_selection_ensemble.
 
 
 # oracle-only alternative readings (oracle/mtgp_oracle.c OR_DP_ALT_*)

@@ -202,3 +202,13 @@ def test_gpu_dynamic_notebook_selection_ensemble(name):
     fit, steps, metas = _selection_ensemble(name)
     rep = _report(name, fit, steps, metas, 1000)
     assert rep["members"] >= 2000 and np.all(np.isfinite(fit))
+    printed, q = rep["printed"], rep["printed_quantile"]
+    if name == "gen5":
+        # The established discrepancy (DESIGN.md "Parity pins", round 6): gen 5's printed value lies
+        # below every one of the 2,176 members -- it survives selection at the notebook's scale (a
+        # minimum over 500 candidates would sit near the 0.2 % quantile).  Our members are cut at
+        # max_steps in 6-15 of 16 rollouts; 171.8 needs about 2.  Pinned so a change is noticed.
+        assert q == 0.0 and rep["min"] - printed > 15.0, (rep["min"], printed)
+    else:
+        # inside the lower tail, where a minimum over the notebook's 500 candidates belongs
+        assert 0.0 < q <= {"gen30": 0.02, "gen50": 0.2}[name], (name, q)
