@@ -422,7 +422,7 @@ struct KArgs {
   int32_t chain_save;       // ... and continues it into the save-point readout on request (s46; unused since ABI v18)
   int32_t chain_store;      // the wide-state SR code is LDS store chains: one call per wave and stage
   int32_t chain_merge;      // (ABI v18) the dynamic policy's readout chains into its state programs, u put in its slot
-  uint32_t epoch;           // launch counter (low 16 bits tag the fair-share progress posts)
+  uint32_t epoch;           // launch counter, never 0 (tags the fair-share progress posts)
   int32_t fair;             // fair share of the SIMDs' issue slots (FairShare; MTGP_FAIR)
   int32_t fair_dp;          // the same for the Dopri5 attempt loops (MTGP_FAIR_DP)
   int32_t fair_mode;        // 0: two priority levels; 1: the slowest wave of a SIMD above the rest (MTGP_FAIR_MODE)
@@ -1229,10 +1229,17 @@ __device__ __forceinline__ ChainOut jit_call_chain_nf(uint64_t addr_, const floa
 // of one step ago; a wave more than `margin` steps ahead of the slowest lowers its priority.
 // Measured (profiles/r05/v12_ab_fair.log, A/B in one process): C3 kernel 2.17 -> 1.81 ms, results
 // bit-identical (priorities only reorder issue).
-static __device__ uint32_t g_fair[8 * 8 * 2 * 16 * 4 * 16];
+// Table layout (round 6): one 128-B L2 line per SIMD, 16 posts of {launch tag : 32, step : 32}.
+// Every wave that reads or writes a SIMD's line runs on that SIMD, i.e. on one CU of one XCD, so
+// the posts never need to leave the XCD's L2: a plain vector store (write-through L1, the line stays
+// in L2) and sc1 loads (bypass this CU's L1, served by L2).  The round-5 form -- agent-scope atomic
+// stores, which drop the line from L2 -- sent every post and every read to memory: 105 MB of
+// FETCH and 25 MB of WRITE per C3 launch (profiles/r06/v1_pmc_fair{0,3}_*.json).
+static __device__ uint64_t g_fair[8 * 8 * 2 * 16 * 4 * 16];
 struct FairShare {
-  uint32_t* tab;
-  uint32_t slot, tag, seen;
+  uint64_t* tab;
+  uint64_t seen;
+  uint32_t slot, tag;
   int margin, mode, level;
   __device__ void init(const KArgs& A, int setting = -1) {
     const uint32_t hw = __builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11));    // HW_REG_HW_ID
@@ -1249,23 +1256,23 @@ struct FairShare {
     __builtin_amdgcn_s_setprio(2);
   }
   __device__ __forceinline__ void step(int lane, uint32_t st) {
-    const bool valid = lane < 16 && (seen >> 16) == tag && (uint32_t)lane != slot;
-    int m = valid ? (int)(seen & 0xffffu) : 0xffff;
+    const bool valid = lane < 16 && (uint32_t)(seen >> 32) == tag && (uint32_t)lane != slot;
+    int m = valid ? (int)(uint32_t)seen : 0x7fffffff;
 #pragma unroll
     for (int w = 1; w < 16; w <<= 1) {
       const int o = __shfl_xor(m, w, kWave);
       m = o < m ? o : m;
     }
     const int mn = __builtin_amdgcn_readfirstlane(m);
-    const int lv = mn == 0xffff ? 2 : ((int)st > mn + margin ? 0 : ((mode == 1 && (int)st <= mn) ? 3 : 2));
+    const int lv = mn == 0x7fffffff ? 2 : ((int)st > mn + margin ? 0 : ((mode == 1 && (int)st <= mn) ? 3 : 2));
     if (lv != level) {  // (s_setprio takes an immediate)
       if (lv == 0) __builtin_amdgcn_s_setprio(0);
       else if (lv == 2) __builtin_amdgcn_s_setprio(2);
       else __builtin_amdgcn_s_setprio(3);
       level = lv;
     }
-    if (lane == 0) __hip_atomic_store(tab + slot, tag << 16 | st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane < 16) seen = __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane == 0) *(volatile uint64_t*)(tab + slot) = (uint64_t)tag << 32 | st;  // vector store, line kept in L2
+    if (lane < 16) seen = __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: L2
   }
 };
 
@@ -5304,7 +5311,8 @@ int mtgp_eval_rk4_jit(const MtgpModel* model, const MtgpInstr* prog, const int32
   }
   A.chain_merge = 0;
   static std::atomic<uint32_t> launch_epoch{0};
-  A.epoch = (launch_epoch.fetch_add(1, std::memory_order_relaxed) + 1u) & 0xffffu;
+  A.epoch = launch_epoch.fetch_add(1, std::memory_order_relaxed) + 1u;
+  if (A.epoch == 0u) A.epoch = 1u;  // (a zero tag would match the table's initial contents)
   {  // MTGP_FAIR: 0 off, k >= 1 on with a lead margin of k - 1 steps (default 3: margin 2)
     const char* f = getenv("MTGP_FAIR");
     A.fair = f ? atoi(f) : 3;
