@@ -70,8 +70,12 @@ namespace {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kDMax = 8;  // data slots held in LDS by the small-state kernels
-constexpr int kDWide = 16;     // data slots of the runtime-state-size dynamic kernel (interpreter only)
-constexpr int kNaRuntime = 8;  // k_ctl_dynamic<Env, kNaRuntime, ...>: state_size 4 .. 8 at run time
+constexpr int kDWide = 16;     // data slots of the runtime-state-size dynamic kernels (interpreter only)
+constexpr int kNaRuntime = 8;  // k_ctl_dynamic / k_ctl_dopri5<Env, kNaRuntime, ...>: state_size 4 .. 8 at run time
+constexpr int kDWide2 = 24;    // data slots of the wide runtime-state-size kernels (round 6)
+constexpr int kNaWide = 16;    // k_ctl_dynamic / k_ctl_dopri5<Env, kNaWide, ...>: state_size 9 .. 16 at run time
+// data slots of a dynamic-policy kernel with state-size template NA (NA <= 3: the JIT's register ABI)
+constexpr int dyn_data_slots(int NA) { return NA <= 3 ? kDMax : (NA <= kNaRuntime ? kDWide : kDWide2); }
 constexpr int kSMax = MTGP_STACK_MAX;
 constexpr int kLdsWaveWords = (kDMax + kSMax) * kWave;  // per wave: data columns | stack columns
 constexpr float kInf = __builtin_huge_valf();
@@ -1231,8 +1235,8 @@ __device__ __forceinline__ ChainOut jit_call_chain_nf(uint64_t addr_, const floa
 // bit-identical (priorities only reorder issue).
 // Table layout (round 6): one 128-B L2 line per SIMD, 16 posts of {launch tag : 32, step : 32}.
 // Every wave that reads or writes a SIMD's line runs on that SIMD, i.e. on one CU of one XCD, so
-// the posts never need to leave the XCD's L2: a plain vector store (write-through L1, the line stays
-// in L2) and sc1 loads (bypass this CU's L1, served by L2).  The round-5 form -- agent-scope atomic
+// the posts never need to leave the XCD's L2: a non-temporal vector store (write-through L1, the
+// line stays in L2) and sc1 loads (bypass this CU's L1, served by L2).  The round-5 form -- agent-scope atomic
 // stores, which drop the line from L2 -- sent every post and every read to memory: 105 MB of
 // FETCH and 25 MB of WRITE per C3 launch (profiles/r06/v1_pmc_fair{0,3}_*.json).
 static __device__ uint64_t g_fair[8 * 8 * 2 * 16 * 4 * 16];
@@ -1271,7 +1275,9 @@ struct FairShare {
       else __builtin_amdgcn_s_setprio(3);
       level = lv;
     }
-    if (lane == 0) *(volatile uint64_t*)(tab + slot) = (uint64_t)tag << 32 | st;  // vector store, line kept in L2
+    // a non-temporal vector store: write-through L1, the line stays in L2 (a volatile store is sc0 sc1,
+    // an atomic one drops the line: both sent every read of the post to memory, profiles/r06/v2_*)
+    if (lane == 0) __builtin_nontemporal_store((uint64_t)tag << 32 | st, tab + slot);
     if (lane < 16) seen = __hip_atomic_load(tab + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1: L2
   }
 };
@@ -1496,14 +1502,15 @@ struct WaveTimer {
 #endif
 
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k_ctl_dynamic(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > kNaRuntime ? 2 : 4))) k_ctl_dynamic(KArgs A) {
 #if MTGP_AB_WAVETIME
   WaveTimer wave_timer;
 #endif
   constexpr int NV = Env::NV;
-  // NA <= 3: the state size; NA = kNaRuntime: state_size 4 .. kNaRuntime at run time (interpreter
-  // only: the data vector has up to kDWide slots, beyond the JIT's register-data ABI)
-  constexpr int DM = NA > 3 ? kDWide : kDMax;
+  // NA <= 3: the state size; NA = kNaRuntime / kNaWide: state_size 4 .. 8 / 9 .. 16 at run time
+  // (interpreter only: the data vector has up to kDWide / kDWide2 slots, beyond the JIT's
+  // register-data ABI)
+  constexpr int DM = dyn_data_slots(NA);
   __shared__ float lds[kWavesPerBlock][(DM + kSMax) * kWave];
   const int na = NA <= 3 ? NA : uni(A.m.state_size);
   Lane Ln;
@@ -2075,8 +2082,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   constexpr int NV = Env::NV;
   constexpr bool DYN = NA > 0;
   constexpr int NAX = DYN ? NA : 1;
-  constexpr int ND = NV + NA;  // integrated state
-  __shared__ float lds[kWavesPerBlock][kLdsWaveWords];
+  constexpr int ND = NV + NA;  // integrated state (NA > 3: the upper bound of a runtime state size)
+  // NA > 3 (round 6): state_size 4 .. NA at run time, interpreter only, one launch (no parking);
+  // the components past NV + na stay 0 and are left out of the error norm, the rows and the data
+  constexpr bool RT = NA > 3;
+  constexpr int DM = DYN ? dyn_data_slots(NA) : kDMax;
+  const int na = RT ? uni(A.m.state_size) : NA;
+  const int nd = NV + na;
+  __shared__ float lds[kWavesPerBlock][(DM + kSMax) * kWave];
   Lane Ln;
   int wv = (int)blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
   if (A.dp_pass == 2) {  // resume a parked wave of launch 1
@@ -2088,7 +2101,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   const bool active = Ln.active;
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
-  float* st = &lds[Ln.wave][kDMax * kWave + Ln.lane];
+  float* st = &lds[Ln.wave][DM * kWave + Ln.lane];
   DataVec<JIT> D(dcol, st);
   if (JIT) asm volatile("s_icache_inv");
   const int S = A.m.n_save, max_steps = A.m.max_steps;
@@ -2097,14 +2110,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   const float t_end = ts[S - 1];
   ObsNoise<NV> nzc;
   if (NOISE) nzc = obs_noise_setup<NV>(A.m, A.ro, rr);
-  constexpr int uslot = DYN ? NV + NA : NV;  // static: targets follow y directly
+  const int uslot = DYN ? NV + na : NV;  // static: targets follow y directly
   Env env;
   env.load(A.ro, rr, A.m.n_targets);
   const size_t PR = (size_t)A.P * R;
   const int loff = Ln.p * R + r;
   const int tslot = DYN ? uslot + 1 : NV;
 #pragma unroll
-  for (int t = 0; t < kDMax; ++t)
+  for (int t = 0; t < DM; ++t)
     if (t >= tslot && t - tslot < A.m.n_targets) D.put(t, A.ro.targets[rr * A.m.n_targets + (t - tslot)]);
   constexpr float E[7] = MTGP_DP_TABLE_E;
   constexpr float CM[7] = MTGP_DP_TABLE_CMID;
@@ -2119,14 +2132,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     float ur[1];
     if (DYN) {
 #pragma unroll
-      for (int j = 0; j < NA; ++j) D.put(NV + j, s[NV + j]);
+      for (int j = 0; j < NA; ++j)
+        if (!RT || j < na) D.put(NV + j, s[NV + j]);
       run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 0, A.m.prog_readout, D, ur);  // reads [0, a, 0, tar]
       env.drift(s, ur[0], ds);
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, ur[0]);
       float ka[NAX];
-      run_role<JIT, NAX, MTGP_DP_COLD != 0>(A, Ln, ng, 1, A.m.prog_state, D, ka, DYN && A.chain_state != 0);
+#pragma unroll
+      for (int j = 0; j < NAX; ++j) ka[j] = 0.0f;  // (RT: the slots j >= na stay 0)
+      run_role<JIT, NAX, MTGP_DP_COLD != 0>(A, Ln, ng, 1, A.m.prog_state, D, ka, DYN && !RT && A.chain_state != 0, -1,
+                                            nullptr, na);
 #pragma unroll
       for (int j = 0; j < NA; ++j) ds[NV + j] = ka[j];
     } else {
@@ -2146,7 +2163,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
     float ur[1];
     if (DYN) {
 #pragma unroll
-      for (int j = 0; j < NA; ++j) D.put(NV + j, sk[NV + j]);
+      for (int j = 0; j < NA; ++j)
+        if (!RT || j < na) D.put(NV + j, sk[NV + j]);
       D.put(uslot, 0.0f);
       run_role<JIT, 1, MTGP_DP_COLD != 0>(A, Ln, ng, 2, A.m.prog_readout_save, D, ur);  // readout([y, a, 0, tar]) dyn.py:101
     } else {
@@ -2169,7 +2187,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
       if (A.out.us) traj_put_dp(A.out.us, lm, k, 0, 1, loff, PR, S, ur[0]);
       if (DYN && A.out.acts) {
 #pragma unroll
-        for (int j = 0; j < NA; ++j) traj_put_dp(A.out.acts, lm, k, j, NAX, loff, PR, S, sk[NV + j]);
+        for (int j = 0; j < NA; ++j)
+          if (!RT || j < na) traj_put_dp(A.out.acts, lm, k, j, RT ? na : NAX, loff, PR, S, sk[NV + j]);
       }
     }
   };
@@ -2182,9 +2201,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   const int force_dtmin = !A.m.no_force_dtmin;
   float t, tnext;
   bool live;
-  DpParked<ND, typename Env::Fit> park{A.dp_state, A.dp_lanes, (uint32_t)wv * kWave + (uint32_t)Ln.lane};
-  if (A.dp_pass == 2) {
-    park.load(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+  // (RT: one launch only, the entry point rejects dp_budget; the parked state would not fit)
+  DpParked<RT ? 1 : ND, typename Env::Fit> park{A.dp_state, A.dp_lanes, (uint32_t)wv * kWave + (uint32_t)Ln.lane};
+  if (!RT && A.dp_pass == 2) {
+    if constexpr (!RT) park.load(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
   } else {
 #pragma unroll
     for (int i = 0; i < NV; ++i) y[i] = A.ro.x0[rr * NV + i];
@@ -2204,8 +2224,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   if (fair_on) fair.init(A, A.fair_dp);
   for (int iter = 0; wave_any(live); ++iter) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)iter);
-    if (iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
-      park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+    if (!RT && iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
+      if constexpr (!RT) park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
       if (Ln.lane == 0) A.dp_pending[1 + atomicAdd(A.dp_pending, 1)] = wv;
       return;
     }
@@ -2228,13 +2248,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
       float msum = 0.0f;
 #pragma unroll
       for (int i = 0; i < ND; ++i) {
+        if (RT && i >= nd) continue;  // (components past the runtime state size: not in the norm)
         float acc = 0.0f;
 #pragma unroll
         for (int j = 0; j < 7; ++j) acc = mtgp_dp_term(acc, E[j], f[j][i], j == 0);
         const float sc = mtgp_dp_scaled(h * acc, y[i], y1[i], rtol, atol);
         msum = (i == 0) ? sc * sc : msum + sc * sc;
       }
-      const float ms = msum / (float)ND;
+      const float ms = msum / (float)(RT ? nd : ND);
       int kp, fl;
       dt = mtgp_dp_control(ms, h, dtmin, dtmax, force_dtmin, &pid, &ctl, &kp, &fl);
       keep = kp != 0;
@@ -4623,7 +4644,7 @@ constexpr bool kTrajOnly = E::kMask;
 
 template <class Env, int NA>
 int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
-  if constexpr (NA > 3) {  // state_size 4 .. kNaRuntime: the interpreter (data vector beyond the JIT's 8 registers)
+  if constexpr (NA > 3) {  // state_size 4 .. kNaWide: the interpreter (data vector beyond the JIT's 8 registers)
     if (jit) return MTGP_ERR_ARG;
     return launch_timed([&] {
       if (noise) {
@@ -4640,6 +4661,21 @@ int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 
   }
 }
 
+// adaptive Dopri5 at a runtime state size (NA = kNaRuntime / kNaWide): interpreter variants only
+template <class Env, int NA>
+int launch_dp_rt(const KArgs& A, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
+  return launch_timed([&] {
+    if (noise) {
+      if (traj) hipLaunchKernelGGL((k_ctl_dopri5<Env, NA, true, true, false>), grid, block, 0, s, A);
+      else if constexpr (!Env::kMask) hipLaunchKernelGGL((k_ctl_dopri5<Env, NA, false, true, false>), grid, block, 0, s, A);
+    } else if (traj) {
+      hipLaunchKernelGGL((k_ctl_dopri5<Env, NA, true, false, false>), grid, block, 0, s, A);
+    } else if constexpr (!Env::kMask) {
+      hipLaunchKernelGGL((k_ctl_dopri5<Env, NA, false, false, false>), grid, block, 0, s, A);
+    }
+  }, s);
+}
+
 // adaptive Dopri5 variants (k_ctl_dopri5): static = NA 0
 template <class Env>
 int launch_ctl_dp(const KArgs& A, const MtgpModel* model, bool jit, bool noise, bool traj, dim3 grid, dim3 block,
@@ -4649,7 +4685,10 @@ int launch_ctl_dp(const KArgs& A, const MtgpModel* model, bool jit, bool noise, 
     case 1: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 1); }, s);
     case 2: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 2); }, s);
     case 3: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 3); }, s);
-    default: return MTGP_ERR_ARG;
+    default:  // runtime state size (round 6): interpreter only, one launch
+      if (jit || model->state_size < 4 || model->state_size > kNaWide) return MTGP_ERR_ARG;
+      return model->state_size > kNaRuntime ? launch_dp_rt<Env, kNaWide>(A, noise, traj, grid, block, s)
+                                            : launch_dp_rt<Env, kNaRuntime>(A, noise, traj, grid, block, s);
   }
 }
 // every environment's Dopri5 kernels live in their own translation unit (MTGP_TU 3, 4, 5)
@@ -4677,9 +4716,10 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
   if (model->env != MTGP_ENV_ACROBOT && model->n_targets < 1) return MTGP_ERR_ARG;  // x_d needs the target
   if (model->model == MTGP_MODEL_STATIC) {
     if (NV + model->n_targets > kDMax) return MTGP_ERR_ARG;
-  } else if (model->state_size > 3) {  // runtime state size: the wide interpreter kernel, fixed-step solvers
-    if (model->state_size > kNaRuntime || NV + model->state_size + 1 + model->n_targets > kDWide || jit ||
-        model->solver == MTGP_SOLVER_DOPRI5)
+  } else if (model->state_size > 3) {  // runtime state size: the wide interpreter kernels, every solver
+    const int dm = model->state_size > kNaRuntime ? kDWide2 : kDWide;
+    if (model->state_size > kNaWide || NV + model->state_size + 1 + model->n_targets > dm || jit ||
+        (model->solver == MTGP_SOLVER_DOPRI5 && A.dp_budget > 0))  // (one Dopri5 launch: no parking)
       return MTGP_ERR_ARG;
   } else if (NV + model->state_size + 1 + model->n_targets > kDMax) {
     return MTGP_ERR_ARG;
@@ -4708,8 +4748,10 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
     case 1: return launch_dyn<Env, 1>(A, jit, noise, traj, grid, block, s);
     case 2: return launch_dyn<Env, 2>(A, jit, noise, traj, grid, block, s);
     case 3: return launch_dyn<Env, 3>(A, jit, noise, traj, grid, block, s);
-    default: return model->state_size > 3 ? launch_dyn<Env, kNaRuntime>(A, jit, noise, traj, grid, block, s)
-                                          : MTGP_ERR_ARG;
+    default:
+      if (model->state_size < 4 || model->state_size > kNaWide) return MTGP_ERR_ARG;
+      return model->state_size > kNaRuntime ? launch_dyn<Env, kNaWide>(A, jit, noise, traj, grid, block, s)
+                                            : launch_dyn<Env, kNaRuntime>(A, jit, noise, traj, grid, block, s);
   }
 }
 

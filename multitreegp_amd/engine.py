@@ -326,7 +326,7 @@ class DeviceEngine:
     def _jit_usable(self) -> bool:
         """The program JIT serves every kernel: data vector in v0-v7 (control models, SR with
         n_var <= 4) or in the wide SR kernel's LDS stage vector (mtgp_jit.h kJitModeLds)."""
-        if not self.use_jit:
+        if not self.use_jit or getattr(self.ff, "state_size", 0) > 3:  # (runtime state sizes: interpreter kernels)
             return False
         return self.ff.n_data() <= 8 or self._jit_mode() == nat.JIT_MODE_LDS
 
@@ -490,7 +490,8 @@ class DeviceEngine:
         # Dopri5 in two launches: the waves still integrating after max_steps / 2 attempts are parked
         # and resumed by a second launch that spreads them over all SIMDs (DESIGN.md "Dopri5 tail":
         # C3 + obs_noise 0.1, the notebooks' setting, 70.6 -> 58.4 ms; without noise 31.2 vs 32.1)
-        dp_ctl = m.solver == nat.SOLVER_DOPRI5 and self.ff.model_id != nat.MODEL_SR
+        # (state_size > 3: one launch -- the runtime-state-size Dopri5 kernel does not park)
+        dp_ctl = m.solver == nat.SOLVER_DOPRI5 and self.ff.model_id != nat.MODEL_SR and m.state_size <= 3
         budget = self.dp_budget if self.dp_budget is not None else (self._dp_choose(m.max_steps) if dp_ctl else 0)
         if dp_ctl and budget > 0:
             waves = self.native.mtgp_eval_waves(P, R, lanes)

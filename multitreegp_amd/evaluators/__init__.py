@@ -397,10 +397,12 @@ class DynamicEvaluator(_ControlEvaluator):
         self.state_size = int(state_size)
         if self.state_size < 1:
             raise ValueError("state_size must be >= 1")
-        if self.state_size > 3:  # the runtime-state-size interpreter kernel (mtgp_kernels.hip kNaRuntime)
-            if self.state_size > 8 or self.solver_kind == "dopri5":
-                raise NotImplementedError("state_size 4 .. 8 runs with the fixed-step solvers (RK4 / Euler); "
-                                          "state_size <= 3 with every solver")
+        if self.state_size > 3:  # the runtime-state-size interpreter kernels (mtgp_kernels.hip kNaRuntime / kNaWide)
+            slots = 16 if self.state_size <= 8 else 24
+            need = env.n_var * env.n_dim + self.state_size + env.n_control + env.n_targets
+            if self.state_size > 16 or need > slots:
+                raise NotImplementedError(f"state_size {self.state_size}: the MI355X kernels run state_size <= 16 "
+                                          f"with a data vector of at most {slots} slots (this one needs {need})")
 
     def n_trees(self) -> int:
         return self.state_size + self.control_size

@@ -128,11 +128,11 @@ def test_environment_configuration_checks():
         mt.DynamicEvaluator(mt.HarmonicOscillator(0, 0, n_obs=3), 1, 0.05, solver=mt.RK4())
     with pytest.raises(ValueError):
         mt.FeedforwardEvaluator(mt.StirredTankReactor(0, 0, n_obs=0), 0.05, solver=mt.RK4())
-    with pytest.raises(NotImplementedError):  # state_size > 3: fixed-step solvers only
-        mt.DynamicEvaluator(mt.Acrobot(0, 0), 4, 0.05, solver=mt.Dopri5(),
-                            stepsize_controller=mt.PIDController(1e-4, 1e-4))
+    # state_size > 3: every solver (round 6), up to 16
+    mt.DynamicEvaluator(mt.Acrobot(0, 0), 4, 0.05, solver=mt.Dopri5(), stepsize_controller=mt.PIDController(1e-4, 1e-4))
+    mt.DynamicEvaluator(mt.Acrobot(0, 0), 9, 0.05, solver=mt.RK4())
     with pytest.raises(NotImplementedError):
-        mt.DynamicEvaluator(mt.Acrobot(0, 0), 9, 0.05, solver=mt.RK4())
+        mt.DynamicEvaluator(mt.Acrobot(0, 0), 17, 0.05, solver=mt.RK4())
     mt.DynamicEvaluator(mt.Acrobot(0, 0), 8, 0.05, solver=mt.RK4())
     # fewer observations than states: the data slots after y move up in the kernel's layout
     ev = mt.DynamicEvaluator(mt.Acrobot(0, 0, n_obs=2), 2, 0.05, solver=mt.RK4())

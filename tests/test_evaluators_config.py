@@ -238,3 +238,22 @@ def test_stalled_grid_oracle_solve_ends_with_inf_saves():
                        trajectories=True)
     xs = out["xs"][0, 0]
     assert np.array_equal(xs[0], x0[0]) and np.all(np.isposinf(xs[1:]))
+
+
+def test_state_size_limits():
+    """state_size 1 .. 16 with every solver (round 6: Dopri5 and 9 .. 16 on the runtime-state-size
+    kernels); beyond 16, or a data vector [y, a, u, targets] over the 24 LDS slots, raises."""
+    env = mt.Acrobot(0.0, 0.0)
+    pid = mt.PIDController(rtol=1e-4, atol=1e-4, dtmin=0.001)
+    for ss in (4, 8, 12, 16):
+        mt.DynamicEvaluator(env, ss, 0.05, solver=mt.RK4())
+        mt.DynamicEvaluator(env, ss, 0.05, solver=mt.Dopri5(), stepsize_controller=pid)
+    with pytest.raises(NotImplementedError):
+        mt.DynamicEvaluator(env, 17, 0.05, solver=mt.RK4())
+    reactor = mt.StirredTankReactor(0.0, 0.0)
+    need = reactor.n_var * reactor.n_dim + 16 + reactor.n_control + reactor.n_targets
+    if need > 24:
+        with pytest.raises(NotImplementedError):
+            mt.DynamicEvaluator(reactor, 16, 0.05, solver=mt.RK4())
+    else:
+        mt.DynamicEvaluator(reactor, 16, 0.05, solver=mt.RK4())

@@ -418,16 +418,25 @@ def test_fewer_observations_than_states(case):
     _check(res, ref, pop.shape[0], 8, names)
 
 
+DP_RT = (1e-4, 1e-4, 0.001, 600)  # Dopri5 + PID (rtol, atol, dtmin, max_steps)
+
+
 @pytest.mark.parametrize("case", [("acrobot", 4, None, 0.0), ("acrobot", 6, "euler", 0.1), ("harmonic", 5, None, 0.0),
-                                  ("reactor", 8, None, 0.1)])
+                                  ("reactor", 8, None, 0.1), ("acrobot", 8, None, 0.0), ("acrobot", 12, None, 0.0),
+                                  ("acrobot", 12, "euler", 0.1), ("harmonic", 16, None, 0.1), ("reactor", 9, None, 0.0),
+                                  ("acrobot", 4, "dopri5", 0.0), ("acrobot", 8, "dopri5", 0.1),
+                                  ("acrobot", 12, "dopri5", 0.0), ("harmonic", 16, "dopri5", 0.0),
+                                  ("reactor", 6, "dopri5", 0.1)])
 def test_state_size_above_three(case):
-    """state_size 4 .. 8 (dyn.py:83 takes any): the data vector [y, a, u, tg] no longer fits the
-    JIT's eight data registers, so the wide interpreter kernel (k_ctl_dynamic<Env, kNaRuntime>,
-    runtime state size, 16 LDS data columns) runs it -- bit-exact vs the oracle."""
+    """state_size 4 .. 16 (dyn.py:83 takes any): the data vector [y, a, u, tg] no longer fits the
+    JIT's eight data registers, so the wide interpreter kernels run it (k_ctl_dynamic /
+    k_ctl_dopri5<Env, kNaRuntime | kNaWide>: runtime state size, 16 / 24 LDS data columns; round 6:
+    Dopri5 and state_size 9 .. 16) -- bit-exact vs the oracle, trajectories included."""
     env_name, ss, solver, noise = case
     from helpers import dynamic_setup
     env, lib, ff, data, pop = dynamic_setup(P=21, R=8, n_steps=30, depth=5, N=30, seed=11, state_size=ss,
-                                            obs_noise=noise, env=env_name)
+                                            obs_noise=noise, env=env_name,
+                                            solver=DP_RT if solver == "dopri5" else None)
     if solver == "euler":
         ff = mt.DynamicEvaluator(env, ss, ff.dt0, solver=mt.Euler())
     res, ref, d = _run(ff, lib, data, pop, parsimony=0.25)
