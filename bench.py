@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--ext-ops", action="store_true",
                     help="C2/C3 node library + exp, log, sqrt, tanh, abs (p 0.1 each, like sin / cos): the JIT's "
                          "extended-operator templates under the headline workload (A/B line, not the headline)")
+    ap.add_argument("--state-size", type=int, default=2,
+                    help="C3 hidden-state trees (the notebook's 2); 4 .. 16 run the runtime-state-size interpreter "
+                         "kernels (A/B line, not the headline)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-pmc", action="store_true",
@@ -122,9 +125,12 @@ def setup_workload(args, rank):
                                  lambda: sample_population(3000 + rank, lib, args.pop, 1, max_init_depth=4,
                                                            max_nodes=30)[0])
         return env, lib, ff, data, pop
-    lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]], [2, 1])
-    ff = mt.DynamicEvaluator(env, 2, 0.05, max_steps=1000, **solver)
+    ss = getattr(args, "state_size", 2)
+    acts = [f"a{i + 1}" for i in range(ss)]
+    lib = mt.NodeLibrary(ops, [["y1", "y2", "y3", "y4"] + acts + ["u"], acts], [ss, 1])
+    ff = mt.DynamicEvaluator(env, ss, 0.05, max_steps=1000, **solver)
     data = mt.control_data(env, args.rollouts, 0.05, None, seed=1, n_steps=args.ode_steps)
+    tag += "" if ss == 2 else f"_ss{ss}"
     pop = _cached_population(f"c3{tag}_{args.pop}_r{rank}",
                              lambda: sample_population(1000 + rank, lib, args.pop, 1, max_init_depth=10,
                                                        max_nodes=64)[0])
@@ -158,7 +164,8 @@ def pmc_passes(args, kernel_substr):
     from pmc_summary import collect
     cmd_tail = ["--", sys.executable, os.path.join(ROOT, "scripts", "kprof.py"), "--iters", "1", "--config",
                 args.config, "--pop", str(args.pop), "--rollouts", str(args.rollouts), "--solver", args.solver,
-                "--obs-noise", str(args.obs_noise), "--ode-steps", str(args.ode_steps)] + \
+                "--obs-noise", str(args.obs_noise), "--ode-steps", str(args.ode_steps),
+                "--state-size", str(args.state_size)] + \
         (["--no-traj"] if args.no_traj else [])
     out = {}
     with tempfile.TemporaryDirectory(prefix="mtgp_pmc_") as d:
@@ -403,8 +410,9 @@ def main():
     solver_txt = ("Dopri5 PID rtol=atol=1e-4 dtmin=0.001 dt0=0.05, max_steps 1000" if adaptive else
                   f"RK4 + diffrax ConstantStepSize dt0={dt0} ({n_steps} accumulated f32 steps), SaveAt(ts) by dense output")
     workloads = {
-        "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, 3 trees, max_nodes 64, depth<=10, %s, S=%d"
-              % (P, R, solver_txt, S),
+        "c3": "C3 DynamicPolicy Acrobot: pop %d/GPU x %d rollouts, %d trees, max_nodes 64, depth<=10, %s, S=%d"
+              % (P, R, args.state_size + 1, solver_txt, S) + ("" if args.state_size == 2 else
+                                                                f", state_size {args.state_size} (runtime-state-size interpreter kernel)"),
         "c2": "C2 StaticPolicy Acrobot: pop %d/GPU x %d rollouts, 1 tree, max_nodes 30, depth<=4, %s, S=%d"
               % (P, R, solver_txt, S),
         "c5": "C5 64-dim SR (neural-ODE style): pop %d/GPU x %d rollouts, 64 trees, max_nodes 128, depth<=16, "
@@ -434,6 +442,7 @@ def main():
                    + (f", obs_noise {args.obs_noise} (threefry in-kernel)" if args.obs_noise else "")
                    + (", node library + exp log sqrt tanh abs (JIT subroutines)" if args.ext_ops else ""),
                    "pop_per_gpu": P, "rollouts": R, "ode_steps": n_steps, "trajectories": traj,
+                   "state_size": args.state_size if args.config == "c3" else None,
                    "parallelism": f"population-sharded dp{ws}"},
         "kernel_ms": kmean,
         # The kernel is bound by VALU issue / dependent-instruction latency, not by HBM (DESIGN.md

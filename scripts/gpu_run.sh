@@ -64,6 +64,9 @@ for step in "$@"; do
            run c5occ_2b 300 env MTGP_WIDE_LDS_MIN=60000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     testbuild) run pytest_build 300 python -u -m pytest tests/test_gpu_build.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    bench_ss8) run bench_ss8 600 python bench.py --state-size 8 --steps 30 --warmup 5 --e2e-steps 0 || exit 1 ;;
+    bench_ss12) run bench_ss12 600 python bench.py --state-size 12 --steps 20 --warmup 3 --e2e-steps 0 --no-cpu-baseline || exit 1 ;;
+    teststate) run pytest_state 600 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -v -k state_size --timeout 300 --timeout-method thread || exit 1 ;;
     bench_c3q) run bench_c3q 300 python bench.py --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     bench_c3ext) run bench_c3ext 300 python bench.py --ext-ops --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     dbgcheck) run dbgcheck 600 env MTGP_LIB=multitreegp_amd/lib/dbg/libmtgp_hip_dbg.so python -u scripts/debug_store_check.py \

@@ -27,10 +27,11 @@ ap.add_argument("--config", default="c3", choices=["c2", "c3", "c5"])
 ap.add_argument("--solver", default="rk4", choices=["rk4", "dopri5"])
 ap.add_argument("--obs-noise", type=float, default=0.0)
 ap.add_argument("--ode-steps", type=int, default=200)
+ap.add_argument("--state-size", type=int, default=2)
 a = bench.apply_config_defaults(ap.parse_args())
 env, lib, ff, data, pop = bench.setup_workload(argparse.Namespace(pop=a.pop, rollouts=a.rollouts, ode_steps=a.ode_steps,
                                                                       config=a.config, solver=a.solver,
-                                                                      obs_noise=a.obs_noise), 0)
+                                                                      obs_noise=a.obs_noise, state_size=a.state_size), 0)
 eng = DeviceEngine(ff, lib, 0.0, "cuda:0", native=nat.load(a.lib))
 pd = torch.from_numpy(pop).cuda()
 for i in range(a.warmup + a.iters):  # statuses checked once (the timed bench loop never synchronises either)
