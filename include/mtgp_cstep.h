@@ -21,14 +21,22 @@
  *   drift off n * dt0 (C3: 189 of 200 step ends differ) and the step count can exceed the
  *   nominal one (t1 = 2, dt0 = 0.01: 201 steps, the last 1.5e-6 long).
  * Stages (ODETerm: is_vf_expensive False, so diffrax keeps the vector-field values f_i and forms each
- * increment as (sum_j a_ij f_j) * dt; zero tableau entries skipped, products and sums rounded
- * separately, ascending j):
+ * increment as (sum_j a_ij f_j) * dt; products and sums rounded separately, ascending j).  Zero
+ * tableau entries are MULTIPLIED, not skipped (round 6): diffrax's
+ * AbstractRungeKutta runs its stages as a loop over a zero-padded lower-triangular tableau and forms
+ * each stage's increment as one dot product of that padded row with the buffer of stage values, so
+ * a_ij = 0 still contributes 0 * f_j -- +-0 for a finite f_j, NaN for an infinite or NaN one.  (The
+ * diffrax source is not in this image, and the reference pins no version: this is its published
+ * implementation as restated here, not a quotation.)  The padded row's trailing 0 * 0 terms of the
+ * stages not yet computed can only turn a -0 sum into +0 and are not restated.
  *   Euler   f0 = f(t, y);  y1 = y + f0 * dt
  *   RK4     f0 = f(t, y)
  *           f1 = f(t + 0.5 dt, y + (0.5 f0) dt)
- *           f2 = f(t + 0.5 dt, y + (0.5 f1) dt)
- *           f3 = f(t + 1.0 dt, y + (1.0 f2) dt)
+ *           f2 = f(t + 0.5 dt, y + (0 f0 + 0.5 f1) dt)
+ *           f3 = f(t + 1.0 dt, y + ((0 f0 + 0 f1) + 1.0 f2) dt)
  *           y1 = y + (((b0 f0 + b1 f1) + b2 f2) + b3 f3) dt,  b = f32(1/6, 1/3, 1/3, 1/6)
+ *           (the zero-entry part z = 0 f0 / 0 f0 + 0 f1 is +-0 or NaN: a non-finite earlier stage
+ *           derivative makes the stage input NaN in that component, where skipping it would not)
  * SaveAt(ts): after each step every pending ts[k] <= tn (k ascending, ts[0] included at step 0) is
  *   evaluated through the step's dense output at theta = linear_rescale(t, ts[k], tn):
  *   Euler   LocalLinearInterpolation: y + theta (y1 - y)
@@ -88,9 +96,16 @@ MTGP_INLINE MTGP_HD float mtgp_cs_hermite(float y0, float y1, float k0, float k1
 /* LocalLinearInterpolation of one component */
 MTGP_INLINE MTGP_HD float mtgp_cs_linear(float y0, float y1, float th) { return y0 + th * (y1 - y0); }
 
-/* RK4 stage input y + (a f) dt for stage st = 1, 2, 3 (a = 0.5, 0.5, 1.0) */
-MTGP_INLINE MTGP_HD float mtgp_rk4_in(int st, float y, float f, float dt) {
-  return st == 3 ? y + f * dt : y + (0.5f * f) * dt;
+/* RK4 stage input for stage st = 1, 2, 3 from f = the previous stage's derivative and z = the
+ * zero-entry terms of the stage's tableau row (stage 2: 0 f0; stage 3: 0 f0 + 0 f1; unused at
+ * stage 1): y + (0.5 f0) dt, y + (z + 0.5 f1) dt, y + (z + 1.0 f2) dt */
+MTGP_INLINE MTGP_HD float mtgp_rk4_in(int st, float y, float f, float z, float dt) {
+  return st == 1 ? y + (0.5f * f) * dt : st == 2 ? y + (z + 0.5f * f) * dt : y + (z + f) * dt;
+}
+/* the zero-entry sum after stage st's input was formed from f = f_{st-1}: stage 1 starts it (0 f0,
+ * for stage 2), stage 2 adds 0 f1 (for stage 3); stage 3 leaves it */
+MTGP_INLINE MTGP_HD float mtgp_rk4_zero(int st, float z, float f) {
+  return st == 1 ? 0.0f * f : st == 2 ? z + 0.0f * f : z;
 }
 /* RK4 stage time t + c dt for stage st = 1, 2, 3 (c = 0.5, 0.5, 1.0) */
 MTGP_INLINE MTGP_HD float mtgp_rk4_time(int st, float t, float dt) {

@@ -13,9 +13,11 @@
  * The stepping loop itself is written independently on each side.
  *
  * Per rollout (state y, time t, step h, FSAL derivative f0 = f(t, y)):
- *   stages  f_i = f(t + c_i h, y + h * sum_{j<i, a_ij != 0} a_ij f_j), i = 1..6 (ascending-j fma
- *           chain, first term a_i0 * f0); y1 = stage-6 input (Dopri5 is FSAL: b = a_6j);
- *   error   err = h * sum_j e_j f_j (e = b - b_hat, same chain form);
+ *   stages  f_i = f(t + c_i h, y + h * sum_{j<i} a_ij f_j), i = 1..6 (ascending-j fma chain, first
+ *           term a_i0 * f0, zero entries included: fma(0, f_j, acc) -- a non-finite f_j makes the
+ *           sum NaN as in diffrax's dot product over the padded tableau row, mtgp_cstep.h);
+ *           y1 = stage-6 input (Dopri5 is FSAL: b = a_6j, whose b_1 = 0 is such an entry);
+ *   error   err = h * sum_j e_j f_j (e = b - b_hat, same chain form, e_1 = 0 included);
  *   norm    m = mean_i (err_i / (atol + rtol * max(|y_i|, |y1_i|)))^2  (rms_norm squared,
  *           summed in index order; "scaled error < 1" is tested as m < 1);
  *   accept  keep = m < 1 || at_dtmin  (force_dtmin=True);
@@ -52,7 +54,7 @@
 #define MTGP_DP_C3 MTGP_DP_F(4, 5)
 #define MTGP_DP_C4 MTGP_DP_F(8, 9)
 
-/* a_ij rows 1..6 (row 6 = b); zero entries are skipped by the chain */
+/* a_ij rows 1..6 (row 6 = b); zero entries below the diagonal are multiplied by the chain */
 #define MTGP_DP_TABLE_A                                                                          \
   {                                                                                              \
     {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f},                                                        \
@@ -82,9 +84,10 @@ MTGP_INLINE MTGP_HD float mtgp_dp_c(int i) {
   return i == 0 ? 0.0f : i == 1 ? MTGP_DP_C1 : i == 2 ? MTGP_DP_C2 : i == 3 ? MTGP_DP_C3 : i == 4 ? MTGP_DP_C4 : 1.0f;
 }
 
-/* one term of a weighted chain: acc + w * f (fma), the first term (first != 0) w * f, w == 0 skipped */
+/* one term of a weighted chain: acc + w * f (fma), the first term (first != 0) w * f; a zero weight
+ * is a term too (0 * f: +-0, or NaN for a non-finite f) */
 MTGP_INLINE MTGP_HD float mtgp_dp_term(float acc, float w, float f, int first) {
-  return first ? w * f : (w != 0.0f ? MTGP_FMAF(w, f, acc) : acc);
+  return first ? w * f : MTGP_FMAF(w, f, acc);
 }
 
 /* PID step factor from m = mean squared scaled error (see the header comment) */

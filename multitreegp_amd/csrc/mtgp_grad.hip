@@ -294,12 +294,17 @@ __global__ void __launch_bounds__(256) k_sr_grad(GradArgs A) {
   int steps = 0, ks = 0;
   while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
     const float dt = tn - t;
+    float zv[NV], zd[NV];  // the zero tableau entries' terms, value and tangent (mtgp_cstep.h)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        sv[i] = stage == 0 ? x[i] : mtgp_rk4_in(stage, x[i], kx[i], dt);
-        sd[i] = stage == 0 ? dx[i] : mtgp_rk4_in(stage, dx[i], dkx[i], dt);
+        sv[i] = stage == 0 ? x[i] : mtgp_rk4_in(stage, x[i], kx[i], zv[i], dt);
+        sd[i] = stage == 0 ? dx[i] : mtgp_rk4_in(stage, dx[i], dkx[i], zd[i], dt);
+        if (stage == 1 || stage == 2) {
+          zv[i] = mtgp_rk4_zero(stage, zv[i], kx[i]);
+          zd[i] = mtgp_rk4_zero(stage, zd[i], dkx[i]);
+        }
       }
       if constexpr (NV <= 4) {  // one program site: the dual-number code (mtgp_jit_dual.h) or the interpreter
 #pragma unroll 1
@@ -1123,12 +1128,16 @@ __global__ void __launch_bounds__(kGradBlock) k_ctl_grad(GradArgs A) {
     Dual f0[ND], y1[ND], sk[ND], kx[ND], acc[ND], tmp[ND];
     while (t < t_end && mtgp_cs_advancing(steps, t, tn) && (A.m.max_steps <= 0 || steps < A.m.max_steps)) {
       const float dt = tn - t;
+      Dual z[ND];  // the zero tableau entries' terms (mtgp_cstep.h), value and tangent
       // the stages from one rhs site (stage 0 included; Euler: stage 0 only)
 #pragma unroll 1
       for (int st = 0; st <= (euler ? 0 : 3); ++st) {
 #pragma unroll
-        for (int i = 0; i < ND; ++i)
-          tmp[i] = st == 0 ? s[i] : Dual{mtgp_rk4_in(st, s[i].v, kx[i].v, dt), mtgp_rk4_in(st, s[i].d, kx[i].d, dt)};
+        for (int i = 0; i < ND; ++i) {
+          tmp[i] = st == 0 ? s[i]
+                           : Dual{mtgp_rk4_in(st, s[i].v, kx[i].v, z[i].v, dt), mtgp_rk4_in(st, s[i].d, kx[i].d, z[i].d, dt)};
+          if (st == 1 || st == 2) z[i] = Dual{mtgp_rk4_zero(st, z[i].v, kx[i].v), mtgp_rk4_zero(st, z[i].d, kx[i].d)};
+        }
         rhs(st == 0 ? t : mtgp_rk4_time(st, t, dt), tmp, kx);
 #pragma unroll
         for (int i = 0; i < ND; ++i) {

@@ -41,8 +41,9 @@
 // control kernels, MTGP_TU=3 / 4 / 5 the Dopri5 control kernels of Acrobot / HarmonicOscillator /
 // StirredTankReactor, MTGP_TU=6 the Acrobot kernels of the general cost mask (EnvAcrobotMask),
 // MTGP_TU=7 the fixed-step Acrobot control kernels (the C3 / C2 hot kernels: an A/B variant of
-// them recompiles this unit only, scripts/build_ab.py), MTGP_TU=8 the SR kernels, behind one hidden
-// C++ entry each.  Without MTGP_TU it is one monolithic TU.
+// them recompiles this unit only, scripts/build_ab.py), MTGP_TU=8 the SR kernels, MTGP_TU=9 the
+// runtime-state-size Dopri5 control kernels (state_size 4 .. 16, round 6), behind one hidden C++
+// entry each.  Without MTGP_TU it is one monolithic TU.
 #ifndef MTGP_TU
 #define MTGP_TU_MAIN 1
 #define MTGP_TU_HARMONIC 1
@@ -53,6 +54,7 @@
 #define MTGP_TU_ACRO_MASK 1
 #define MTGP_TU_ACRO 1
 #define MTGP_TU_SR 1
+#define MTGP_TU_DP_RT 1
 #else
 #define MTGP_TU_MAIN (MTGP_TU == 0)
 #define MTGP_TU_HARMONIC (MTGP_TU == 1)
@@ -63,6 +65,7 @@
 #define MTGP_TU_ACRO_MASK (MTGP_TU == 6)
 #define MTGP_TU_ACRO (MTGP_TU == 7)
 #define MTGP_TU_SR (MTGP_TU == 8)
+#define MTGP_TU_DP_RT (MTGP_TU == 9)
 #endif
 
 namespace {
@@ -888,10 +891,14 @@ struct CsClock {
   __device__ __forceinline__ bool saves(const float* ts, int k) const { return uni((int)(ldc(ts, k) <= tn)) != 0; }
 };
 
-// RK4 stage input (stage 0: s itself; stages 1..3: s + (a f) dt, a = 0.5, 0.5, 1) and the running
-// b-weighted sum of the stage derivatives (mtgp_cstep.h)
-__device__ __forceinline__ float stage_in(int stage, float s, float f, float dt) {
-  return stage == 0 ? s : mtgp_rk4_in(stage, s, f, dt);
+// RK4 stage input (stage 0: s itself; stages 1..3: s + (sum_j a_ij f_j) dt over the padded tableau
+// row, zero entries multiplied: z carries their sum 0 f0 / 0 f0 + 0 f1, mtgp_cstep.h) and the
+// running b-weighted sum of the stage derivatives
+__device__ __forceinline__ float stage_in(int stage, float s, float f, float& z, float dt) {
+  if (stage == 0) return s;
+  const float v = mtgp_rk4_in(stage, s, f, z, dt);
+  z = mtgp_rk4_zero(stage, z, f);
+  return v;
 }
 __device__ __forceinline__ float stage_acc(int stage, float acc, float f) { return mtgp_rk4_acc(stage, acc, f); }
 __device__ __forceinline__ float stage_time(int stage, float t, float dt) {
@@ -901,18 +908,27 @@ __device__ __forceinline__ float stage_time(int stage, float t, float dt) {
 // The same for a whole state vector, branching on the (wave-uniform) stage once instead of
 // selecting per component: the same operations, so the same bits.
 template <int N>
-__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], float dt,
-                                           float (&out)[N]) {
+__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], float (&z)[N],
+                                           float dt, float (&out)[N]) {
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = s[i];
-  } else if (st == 3) {
+  } else if (st == 1) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(3, s[i], f[i], dt);
+    for (int i = 0; i < N; ++i) {
+      out[i] = mtgp_rk4_in(1, s[i], f[i], z[i], dt);
+      z[i] = mtgp_rk4_zero(1, z[i], f[i]);
+    }
+  } else if (st == 2) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      out[i] = mtgp_rk4_in(2, s[i], f[i], z[i], dt);
+      z[i] = mtgp_rk4_zero(2, z[i], f[i]);
+    }
   } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(1, s[i], f[i], dt);
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(3, s[i], f[i], z[i], dt);
   }
 }
 template <int N>
@@ -1206,9 +1222,13 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 // constants and branches resolved at compile time), and the kernel runs the general loop below only
 // when the code is not usable.  The arithmetic is k_ctl_dynamic's, operation for operation.
 template <int N>
-__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], float dt, float (&out)[N]) {
+__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], float (&z)[N], float dt,
+                                      float (&out)[N]) {
 #pragma unroll
-  for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : mtgp_rk4_in(st, s[i], f[i], dt);
+  for (int i = 0; i < N; ++i) {
+    out[i] = st == 0 ? s[i] : mtgp_rk4_in(st, s[i], f[i], z[i], dt);
+    if (st == 1 || st == 2) z[i] = mtgp_rk4_zero(st, z[i], f[i]);
+  }
 }
 template <int N>
 __device__ __forceinline__ void rk_acc(int st, float (&acc)[N], const float (&f)[N]) {
@@ -1381,12 +1401,13 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
+    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h)
     // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], at[NA], y[NV];
-      rk_in<NV>(ST, x, kx, dt, xt);
-      rk_in<NA>(ST, a, ka, dt, at);
+      rk_in<NV>(ST, x, kx, zx, dt, xt);
+      rk_in<NA>(ST, a, ka, za, dt, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
       if (NOISE && ST != 2) {  // stages 1 and 2 share the time t + dt/2, hence the noise draw
@@ -1502,7 +1523,7 @@ struct WaveTimer {
 #endif
 
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > kNaRuntime ? 2 : 4))) k_ctl_dynamic(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > 3 ? 2 : 4))) k_ctl_dynamic(KArgs A) {
 #if MTGP_AB_WAVETIME
   WaveTimer wave_timer;
 #endif
@@ -1609,11 +1630,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
   int k = 0;  // next save point
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
+    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
-      stage_in_n<NV>(stage, x, kx, dt, xt);
-      stage_in_n<NA>(stage, a, ka, dt, at);
+      stage_in_n<NV>(stage, x, kx, zx, dt, xt);
+      stage_in_n<NA>(stage, a, ka, za, dt, at);
 #pragma unroll
       for (int j = 0; j < NA; ++j)
         if (j < na) D.put(NV + j, at[j]);
@@ -1762,10 +1784,11 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], y[NV];
-      rk_in<NV>(ST, x, kx, dt, xt);
+      rk_in<NV>(ST, x, kx, zx, dt, xt);
       if (NOISE && ST != 2) {
         const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
         obs_noise_vec<NV>(nzc, tc, nzv);
@@ -1912,10 +1935,11 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
-      stage_in_n<NV>(stage, x, kx, dt, xt);
+      stage_in_n<NV>(stage, x, kx, zx, dt, xt);
       // stages 1 and 2 share the time t + dt/2, hence the noise draw
       if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage_time(stage, t, dt), nzv);
       ctl_obs_apply<Env>(xt, nzv, y);
@@ -2374,10 +2398,11 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float dt = clk.dt();
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], dt));
+      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], zx[i], dt));
       run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
       if (stage == 0) {
 #pragma unroll
@@ -2716,6 +2741,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {  // (no FairShare: the workgroup's waves meet at a barrier every stage)
     const float dt = clk.dt();
+    float zx[kWideComp];  // the zero tableau entries' terms (mtgp_cstep.h)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; f parks in nxt
@@ -2772,7 +2798,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           const float kv = nxt[c * kWave];
           if (stage == 0) fx0[t] = kv;
           ax[t] = stage_acc(stage, ax[t], kv);
-          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, dt);  // the next stage's input
+          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, zx[t], dt);  // the next stage's input
         }
       }
       __syncthreads();
@@ -4661,7 +4687,10 @@ int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 
   }
 }
 
-// adaptive Dopri5 at a runtime state size (NA = kNaRuntime / kNaWide): interpreter variants only
+// adaptive Dopri5 at a runtime state size (NA = kNaRuntime / kNaWide): interpreter variants only;
+// the non-mask environments' kernels live in TU 9 (their register allocation dominates a build)
+__attribute__((visibility("hidden"))) int mtgp_tu_launch_dp_rt(const void* A, int env, bool wide, bool noise, bool traj,
+                                                                unsigned grid, unsigned block, hipStream_t s);
 template <class Env, int NA>
 int launch_dp_rt(const KArgs& A, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
   return launch_timed([&] {
@@ -4687,8 +4716,13 @@ int launch_ctl_dp(const KArgs& A, const MtgpModel* model, bool jit, bool noise, 
     case 3: return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dopri5, Env, 3); }, s);
     default:  // runtime state size (round 6): interpreter only, one launch
       if (jit || model->state_size < 4 || model->state_size > kNaWide) return MTGP_ERR_ARG;
-      return model->state_size > kNaRuntime ? launch_dp_rt<Env, kNaWide>(A, noise, traj, grid, block, s)
-                                            : launch_dp_rt<Env, kNaRuntime>(A, noise, traj, grid, block, s);
+      if constexpr (Env::kMask) {  // (the cost-mask kernels stay in their own TU)
+        return model->state_size > kNaRuntime ? launch_dp_rt<Env, kNaWide>(A, noise, traj, grid, block, s)
+                                              : launch_dp_rt<Env, kNaRuntime>(A, noise, traj, grid, block, s);
+      } else {
+        const int env = std::is_same<Env, EnvAcrobot>::value ? 0 : std::is_same<Env, EnvHarmonic>::value ? 1 : 2;
+        return mtgp_tu_launch_dp_rt(&A, env, model->state_size > kNaRuntime, noise, traj, grid.x, block.x, s);
+      }
   }
 }
 // every environment's Dopri5 kernels live in their own translation unit (MTGP_TU 3, 4, 5)
@@ -4817,6 +4851,21 @@ int mtgp_tu_launch_acrobot_mask(MTGP_TU_ENTRY_ARGS) {  // every solver; the traj
 #if MTGP_TU_ACRO_DOPRI5
 int mtgp_tu_launch_acrobot_dopri5(MTGP_TU_DP_ARGS) {
   return launch_ctl_dp<EnvAcrobot>(*(const KArgs*)A, model, jit, noise, traj, dim3(grid), dim3(block), s);
+}
+#endif
+#if MTGP_TU_DP_RT
+int mtgp_tu_launch_dp_rt(const void* Ap, int env, bool wide, bool noise, bool traj, unsigned grid, unsigned block,
+                         hipStream_t s) {
+  const KArgs& A = *(const KArgs*)Ap;
+  const dim3 g(grid), b(block);
+  switch (env) {
+    case 0: return wide ? launch_dp_rt<EnvAcrobot, kNaWide>(A, noise, traj, g, b, s)
+                        : launch_dp_rt<EnvAcrobot, kNaRuntime>(A, noise, traj, g, b, s);
+    case 1: return wide ? launch_dp_rt<EnvHarmonic, kNaWide>(A, noise, traj, g, b, s)
+                        : launch_dp_rt<EnvHarmonic, kNaRuntime>(A, noise, traj, g, b, s);
+    default: return wide ? launch_dp_rt<EnvReactor, kNaWide>(A, noise, traj, g, b, s)
+                         : launch_dp_rt<EnvReactor, kNaRuntime>(A, noise, traj, g, b, s);
+  }
 }
 #endif
 #if MTGP_TU_HARMONIC_DOPRI5

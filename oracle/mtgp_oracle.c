@@ -331,7 +331,7 @@ static int solve_fixed(const OrCtx* c, const float* ts, const float* s0, float* 
   const OrModel* m = c->m;
   const int n = state_dim(m), S = m->n_save, euler = m->solver == 2;
   const float t_end = ts[S - 1], dt0 = m->h;
-  float y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  float y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S], z[OR_MAX_S];
   for (int i = 0; i < n; ++i) y[i] = s0[i];
   float prev = cond_fn(m, y);
   int k = 0, steps = 0;
@@ -342,9 +342,12 @@ static int solve_fixed(const OrCtx* c, const float* ts, const float* s0, float* 
     if (euler) {
       for (int i = 0; i < n; ++i) y1[i] = y[i] + f0[i] * dt;
     } else {
-      for (int i = 0; i < n; ++i) { acc[i] = mtgp_rk4_acc(0, 0.0f, f0[i]); f[i] = f0[i]; }
+      for (int i = 0; i < n; ++i) { acc[i] = mtgp_rk4_acc(0, 0.0f, f0[i]); f[i] = f0[i]; z[i] = 0.0f; }
       for (int st = 1; st <= 3; ++st) {
-        for (int i = 0; i < n; ++i) yi[i] = mtgp_rk4_in(st, y[i], f[i], dt);
+        for (int i = 0; i < n; ++i) {
+          yi[i] = mtgp_rk4_in(st, y[i], f[i], z[i], dt);
+          z[i] = mtgp_rk4_zero(st, z[i], f[i]);
+        }
         rhs(c, mtgp_rk4_time(st, t, dt), yi, f);
         for (int i = 0; i < n; ++i) acc[i] = mtgp_rk4_acc(st, acc[i], f[i]);
       }
@@ -393,8 +396,7 @@ static float dp_sum(const float* w, const float (*f)[OR_MAX_S], int n_terms, int
   int first = 1;
   for (int j = 0; j < n_terms; ++j) {
     if (!literal) { acc = mtgp_dp_term(acc, w[j], f[j][i], j == 0); continue; }
-    if (w[j] == 0.0f) continue;
-    const float p = w[j] * f[j][i];
+    const float p = w[j] * f[j][i];  /* (zero entries included, as the spec's chain) */
     acc = first ? p : acc + p;
     first = 0;
   }
@@ -849,7 +851,7 @@ static int fixed_dual(const OrModel* m, const float* ts, const ODual* s0, OrDual
                       ODual* saved) {
   const int n = state_dim(m), S = m->n_save, euler = m->solver == 2;
   const float t_end = ts[S - 1], dt0 = m->h;
-  ODual y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S];
+  ODual y[OR_MAX_S], f0[OR_MAX_S], f[OR_MAX_S], acc[OR_MAX_S], yi[OR_MAX_S], y1[OR_MAX_S], zr[OR_MAX_S];
   float sv[OR_MAX_S];
   for (int i = 0; i < n; ++i) { y[i] = s0[i]; sv[i] = y[i].v; }
   float prev = cond_fn(m, sv);
@@ -864,10 +866,13 @@ static int fixed_dual(const OrModel* m, const float* ts, const ODual* s0, OrDual
       for (int i = 0; i < n; ++i) {
         acc[i] = od(mtgp_rk4_acc(0, 0.0f, f0[i].v), mtgp_rk4_acc(0, 0.0f, f0[i].d));
         f[i] = f0[i];
+        zr[i] = od(0.0f, 0.0f);
       }
       for (int st = 1; st <= 3; ++st) {
-        for (int i = 0; i < n; ++i)
-          yi[i] = od(mtgp_rk4_in(st, y[i].v, f[i].v, dt), mtgp_rk4_in(st, y[i].d, f[i].d, dt));
+        for (int i = 0; i < n; ++i) {  /* (the tangent's zero entries: JAX's jvp of the dot product) */
+          yi[i] = od(mtgp_rk4_in(st, y[i].v, f[i].v, zr[i].v, dt), mtgp_rk4_in(st, y[i].d, f[i].d, zr[i].d, dt));
+          zr[i] = od(mtgp_rk4_zero(st, zr[i].v, f[i].v), mtgp_rk4_zero(st, zr[i].d, f[i].d));
+        }
         rhs(ctx, mtgp_rk4_time(st, t, dt), yi, f);
         for (int i = 0; i < n; ++i) acc[i] = od(mtgp_rk4_acc(st, acc[i].v, f[i].v), mtgp_rk4_acc(st, acc[i].d, f[i].d));
       }

@@ -174,3 +174,29 @@ def test_gradients_constant_step_bitexact(kind):
         assert bits_equal(g, rg[p, : len(g)]), mismatch_report(g, rg[p, : len(g)], f"grad {p}")
     fit = eng.evaluate(torch.from_numpy(pop).cuda(), data)["fitness"].cpu().numpy()
     assert bits_equal(loss, fit), mismatch_report(loss, fit, "fitness")
+
+
+@pytest.mark.parametrize("solver", ["rk4", "dopri5"])
+def test_nonfinite_stage_zero_tableau_entries(solver):
+    """A stage derivative that is +inf only at one stage (dx0 = 1 / (x1 - 0.25) from x1 = 0.25): the
+    zero tableau entries multiply it into the later stage inputs as NaN (mtgp_cstep.h /
+    mtgp_dopri5.h, diffrax's padded-row dot product) -- GPU bit-exact vs the oracle, trajectories
+    included; RK4: x1's save at the event step is NaN."""
+    from test_oracle import _nonfinite_stage_candidate
+    lib, cand = _nonfinite_stage_candidate()
+    pop = np.repeat(cand, 4, axis=0)
+    R = 4
+    x0 = np.tile(np.array([[1.0, 0.25]], np.float32), (R, 1))
+    x0[1:, 0] += np.float32(0.5)  # (the singularity sits in x1: every rollout meets it)
+    ts = (np.arange(10, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+    data = (x0, ts, np.zeros((10, 2, R), np.float32).transpose(2, 0, 1).copy(), np.zeros((R, 2), np.uint32))
+    if solver == "rk4":
+        ff = mt.SREvaluator(solver=mt.RK4(), dt0=0.1)
+    else:
+        ff = mt.SREvaluator(solver=mt.Dopri5(), dt0=0.1, max_steps=200,
+                            stepsize_controller=mt.PIDController(rtol=1e-4, atol=1e-4, dtmin=0.001))
+    res, ref, d = _run(ff, lib, data, pop)
+    _check(res, ref, pop.shape[0], R, ["xs"])
+    if solver == "rk4":
+        xs = to_reference_layout(res["xs"], pop.shape[0], R)
+        assert np.isnan(xs[0, 0, 1, 1])

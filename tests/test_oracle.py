@@ -379,3 +379,51 @@ def test_constant_step_save_on_step_end_is_interpolated():
     want = npr.cs_solve(lambda t, s: np.array([s[1], f(0) - s[0]], f), x0[0], ts, 0.5, "rk4", np.float32)
     assert np.array_equal(out["xs"][0, 0], want)
     assert np.array_equal(out["xs"][0, 0, 0], x0[0])  # theta = 0: y0 exactly
+
+
+def _nonfinite_stage_candidate():
+    """dx0 = 1 / (x1 - 0.25), dx1 = 1 / x0 + 1 from x = (1, 0.25): the first RK4 stage derivative of
+    x0 is +inf, the second is finite (x1 has moved), so only the zero tableau entries (stage 2's
+    0 f0, stage 3's 0 f0 + 0 f1) carry the inf into the later stage inputs of x0 -- as NaN, which
+    1 / x0 passes on to x1 (1 / inf would be 0)."""
+    lib = mt.NodeLibrary(SR_OPS, [["x0", "x1"]], [2])
+    from helpers import tree_from_expr
+    cand = np.stack([tree_from_expr(("/", 1.0, ("-", "x1", 0.25)), lib, 8),
+                     tree_from_expr(("+", ("/", 1.0, "x0"), 1.0), lib, 8)])[None]
+    return lib, cand
+
+
+def test_rk4_zero_tableau_entries_are_multiplied():
+    """diffrax forms each stage increment as a dot product over the zero-padded tableau row, so a
+    zero entry still contributes 0 * f_j (include/mtgp_cstep.h): with f0 = +inf
+    in x0, x0's stage-2 input is NaN (skipping the zero it would be finite), f2 of x1 = 1 / NaN + 1
+    is NaN, and x1's end-of-step value -- and its save at ts[1] -- is NaN, not finite.  The numpy
+    restatement (tests/np_reference.py cs_solve, float32) agrees bit for bit."""
+    lib, cand = _nonfinite_stage_candidate()
+    ts = (np.arange(10, dtype=np.float32) * np.float32(0.1)).astype(np.float32)
+    x0 = np.array([[1.0, 0.25]], np.float32)
+    model = dict(model=3, n_var=2, state_size=0, n_obs=0, n_control=0, n_targets=0, n_steps=0, save_every=1,
+                 n_save=10, h=0.1, max_fitness=1e5, parsimony=0.0, solver=0, max_steps=100)
+    out = orc.evaluate(model, cand, lib, dict(x0=x0, ts=ts, ys_true=np.zeros((1, 10, 2), np.float32)), trajectories=True)
+    xs = out["xs"][0, 0]
+    # (ts[0] too is the first step's dense output: polyval's ... * theta + y0 with k0 = inf * dt and
+    # theta = 0 is NaN, as diffrax interpolates it)
+    assert np.isnan(xs[1, 1]) and not np.isfinite(xs[1, 0])  # the zero entries' NaN reached x1
+    assert np.all(np.isposinf(xs[2:]))  # the NaN event ended the solve after that step
+    f = np.float32
+    with np.errstate(all="ignore"):
+        rhs = lambda t, s: np.array([f(1) / (s[1] - f(0.25)), f(1) / s[0] + f(1)], f)
+        want = npr.cs_solve(rhs, x0[0], ts, 0.1, "rk4", np.float32,
+                            event=lambda s: not np.all(np.isfinite(s)))
+        # the zero entries skipped (the round-5 spec): x0's stage-2 / 3 inputs stay finite, so x1's
+        # end-of-step value is finite where diffrax's is NaN
+        dt, y = f(0.1), x0[0]
+        k0 = rhs(0, y)
+        k1 = rhs(0, y + (f(0.5) * k0) * dt)
+        k2 = rhs(0, y + (f(0.5) * k1) * dt)
+        k3 = rhs(0, y + k2 * dt)
+        b0, b1 = f(1.0 / 6.0), f(1.0 / 3.0)
+        skip_y1 = y + (((b0 * k0 + b1 * k1) + b1 * k2) + b0 * k3) * dt
+    from helpers import bits_equal
+    assert bits_equal(xs, want)
+    assert np.isfinite(skip_y1[1]) and np.isnan(out["xs"][0, 0, 1, 1])
