@@ -35,8 +35,14 @@
  *           f2 = f(t + 0.5 dt, y + (0 f0 + 0.5 f1) dt)
  *           f3 = f(t + 1.0 dt, y + ((0 f0 + 0 f1) + 1.0 f2) dt)
  *           y1 = y + (((b0 f0 + b1 f1) + b2 f2) + b3 f3) dt,  b = f32(1/6, 1/3, 1/3, 1/6)
- *           (the zero-entry part z = 0 f0 / 0 f0 + 0 f1 is +-0 or NaN: a non-finite earlier stage
- *           derivative makes the stage input NaN in that component, where skipping it would not)
+ *           The zero-entry part z = 0 f0 / 0 f0 + 0 f1 is +-0 for finite derivatives and NaN
+ *           otherwise; the spec reads a +-0 z as an exact no-op (its only effect on a sum is the
+ *           sign of an all-zero increment, the convention that also drops the trailing 0 * 0 terms)
+ *           and a NaN z as NaN: a non-finite earlier stage derivative makes the stage input NaN in
+ *           that component, where skipping the entry would not.  So with finite f0, f1 the inputs
+ *           are the plain y + (0.5 f1) dt, y + (1.0 f2) dt (mtgp_rk4_in_fast), and a non-finite
+ *           f0 or f1 always makes that component of y1 non-finite (every b_j != 0): the kernels run
+ *           the fast form and redo a step with z only when a live lane's y1 is not finite.
  * SaveAt(ts): after each step every pending ts[k] <= tn (k ascending, ts[0] included at step 0) is
  *   evaluated through the step's dense output at theta = linear_rescale(t, ts[k], tn):
  *   Euler   LocalLinearInterpolation: y + theta (y1 - y)
@@ -96,11 +102,18 @@ MTGP_INLINE MTGP_HD float mtgp_cs_hermite(float y0, float y1, float k0, float k1
 /* LocalLinearInterpolation of one component */
 MTGP_INLINE MTGP_HD float mtgp_cs_linear(float y0, float y1, float th) { return y0 + th * (y1 - y0); }
 
+/* the zero-entry sum z (+-0, or NaN when an earlier zero-weighted derivative was not finite) joined
+ * to the stage row's other terms v: NaN propagates, a +-0 z is a no-op */
+MTGP_INLINE MTGP_HD float mtgp_rk4_nz(float z, float v) { return z != z ? z : v; }
 /* RK4 stage input for stage st = 1, 2, 3 from f = the previous stage's derivative and z = the
  * zero-entry terms of the stage's tableau row (stage 2: 0 f0; stage 3: 0 f0 + 0 f1; unused at
- * stage 1): y + (0.5 f0) dt, y + (z + 0.5 f1) dt, y + (z + 1.0 f2) dt */
+ * stage 1): y + (0.5 f0) dt, y + [z; 0.5 f1] dt, y + [z; 1.0 f2] dt */
 MTGP_INLINE MTGP_HD float mtgp_rk4_in(int st, float y, float f, float z, float dt) {
-  return st == 1 ? y + (0.5f * f) * dt : st == 2 ? y + (z + 0.5f * f) * dt : y + (z + f) * dt;
+  return st == 1 ? y + (0.5f * f) * dt : st == 2 ? y + mtgp_rk4_nz(z, 0.5f * f) * dt : y + mtgp_rk4_nz(z, f) * dt;
+}
+/* the same with every z = +-0 (all earlier derivatives finite): the kernels' fast form */
+MTGP_INLINE MTGP_HD float mtgp_rk4_in_fast(int st, float y, float f, float dt) {
+  return st == 3 ? y + f * dt : y + (0.5f * f) * dt;
 }
 /* the zero-entry sum after stage st's input was formed from f = f_{st-1}: stage 1 starts it (0 f0,
  * for stage 2), stage 2 adds 0 f1 (for stage 3); stage 3 leaves it */

@@ -892,10 +892,12 @@ struct CsClock {
 };
 
 // RK4 stage input (stage 0: s itself; stages 1..3: s + (sum_j a_ij f_j) dt over the padded tableau
-// row, zero entries multiplied: z carries their sum 0 f0 / 0 f0 + 0 f1, mtgp_cstep.h) and the
-// running b-weighted sum of the stage derivatives
-__device__ __forceinline__ float stage_in(int stage, float s, float f, float& z, float dt) {
+// row) and the running b-weighted sum of the stage derivatives.  exact (wave-uniform): the zero
+// entries' terms ride in z (mtgp_cstep.h); otherwise the fast form, equal to it whenever the earlier
+// derivatives are finite -- the kernels redo a step exactly when a live lane's y1 is not finite.
+__device__ __forceinline__ float stage_in(int stage, float s, float f, float& z, float dt, bool exact) {
   if (stage == 0) return s;
+  if (!exact) return mtgp_rk4_in_fast(stage, s, f, dt);
   const float v = mtgp_rk4_in(stage, s, f, z, dt);
   z = mtgp_rk4_zero(stage, z, f);
   return v;
@@ -909,11 +911,19 @@ __device__ __forceinline__ float stage_time(int stage, float t, float dt) {
 // selecting per component: the same operations, so the same bits.
 template <int N>
 __device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], float (&z)[N],
-                                           float dt, float (&out)[N]) {
+                                           float dt, float (&out)[N], bool exact) {
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = s[i];
+  } else if (!exact) {
+    if (st == 3) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_fast(3, s[i], f[i], dt);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_fast(1, s[i], f[i], dt);
+    }
   } else if (st == 1) {
 #pragma unroll
     for (int i = 0; i < N; ++i) {
@@ -1223,10 +1233,15 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 // when the code is not usable.  The arithmetic is k_ctl_dynamic's, operation for operation.
 template <int N>
 __device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], float (&z)[N], float dt,
-                                      float (&out)[N]) {
+                                      float (&out)[N], bool exact) {
+  if (st == 0 || !exact) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : mtgp_rk4_in_fast(st, s[i], f[i], dt);
+    return;
+  }
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    out[i] = st == 0 ? s[i] : mtgp_rk4_in(st, s[i], f[i], z[i], dt);
+    out[i] = mtgp_rk4_in(st, s[i], f[i], z[i], dt);
     if (st == 1 || st == 2) z[i] = mtgp_rk4_zero(st, z[i], f[i]);
   }
 }
@@ -1401,13 +1416,14 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
-    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;    // (wave-uniform) the step redone with the zero entries' terms
     // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], at[NA], y[NV];
-      rk_in<NV>(ST, x, kx, zx, dt, xt);
-      rk_in<NA>(ST, a, ka, za, dt, at);
+      rk_in<NV>(ST, x, kx, zx, dt, xt, exact);
+      rk_in<NA>(ST, a, ka, za, dt, at, exact);
 #pragma unroll
       for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
       if (NOISE && ST != 2) {  // stages 1 and 2 share the time t + dt/2, hence the noise draw
@@ -1435,26 +1451,39 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
         rk_acc<NA>(ST, aa, ka);
       }
     };
-    stage(std::integral_constant<int, 0>{});
-    if constexpr (NST == 4) {
-      stage(std::integral_constant<int, 1>{});
-      stage(std::integral_constant<int, 2>{});
-      stage(std::integral_constant<int, 3>{});
-    }
-    // the step's end state and the event (Event(cond_fn_nan) after the step, dyn.py:94)
+    // the step's end state and the event (Event(cond_fn_nan) after the step, dyn.py:94); a live
+    // lane whose end state is bad may have met a non-finite stage derivative: the step is redone
+    // with the zero tableau entries' terms (mtgp_cstep.h; at most once per event)
     float x1[NV], a1[NA];
+    bool badn = false;
+    for (;;) {
+      stage(std::integral_constant<int, 0>{});
+      if constexpr (NST == 4) {
+        stage(std::integral_constant<int, 1>{});
+        stage(std::integral_constant<int, 2>{});
+        stage(std::integral_constant<int, 3>{});
+      }
 #pragma unroll
-    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+      for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
 #pragma unroll
-    for (int j = 0; j < NA; ++j) a1[j] = NST == 1 ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
+      for (int j = 0; j < NA; ++j) a1[j] = NST == 1 ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
+      if (!dead) {
+        float sn[NV + NA];
+#pragma unroll
+        for (int i = 0; i < NV; ++i) sn[i] = x1[i];
+#pragma unroll
+        for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
+        badn = Env::bad(sn, NV + NA);
+      }
+      if (NST == 4 && !exact && wave_any(!dead && badn)) {
+        exact = true;
+        continue;
+      }
+      break;
+    }
     bool ev = false;
     if (!dead) {
-      float sn[NV + NA];
-#pragma unroll
-      for (int i = 0; i < NV; ++i) sn[i] = x1[i];
-#pragma unroll
-      for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
-      const bool ok = !Env::bad(sn, NV + NA);
+      const bool ok = !badn;
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1523,7 +1552,7 @@ struct WaveTimer {
 #endif
 
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > 3 ? 2 : 4))) k_ctl_dynamic(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > kNaRuntime ? 2 : 4))) k_ctl_dynamic(KArgs A) {
 #if MTGP_AB_WAVETIME
   WaveTimer wave_timer;
 #endif
@@ -1630,12 +1659,16 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > 3
   int k = 0;  // next save point
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
-    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;    // (wave-uniform) the step redone with them: a live lane's end state is bad
+    float x1[NV], a1[NA];
+    bool badn = false;
+    for (;;) {
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
-      stage_in_n<NV>(stage, x, kx, zx, dt, xt);
-      stage_in_n<NA>(stage, a, ka, za, dt, at);
+      stage_in_n<NV>(stage, x, kx, zx, dt, xt, exact);
+      stage_in_n<NA>(stage, a, ka, za, dt, at, exact);
 #pragma unroll
       for (int j = 0; j < NA; ++j)
         if (j < na) D.put(NV + j, at[j]);
@@ -1659,19 +1692,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > 3
       stage_acc_n<NV>(stage, ax, kx);
       stage_acc_n<NA>(stage, aa, ka);
     }
-    float x1[NV], a1[NA];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
 #pragma unroll
     for (int j = 0; j < NA; ++j) a1[j] = euler ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
-    bool ev = false;
     if (!dead) {
       float sn[NV + NA];
 #pragma unroll
       for (int i = 0; i < NV; ++i) sn[i] = x1[i];
 #pragma unroll
       for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
-      const bool ok = !Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
+      badn = Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
+    }
+    if (!euler && !exact && wave_any(!dead && badn)) {
+      exact = true;
+      continue;
+    }
+    break;
+    }
+    bool ev = false;
+    if (!dead) {
+      const bool ok = !badn;
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1784,11 +1825,12 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], y[NV];
-      rk_in<NV>(ST, x, kx, zx, dt, xt);
+      rk_in<NV>(ST, x, kx, zx, dt, xt, exact);
       if (NOISE && ST != 2) {
         const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
         obs_noise_vec<NV>(nzc, tc, nzv);
@@ -1805,18 +1847,27 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
       }
       if (NST == 4) rk_acc<NV>(ST, ax, kx);
     };
-    stage(std::integral_constant<int, 0>{});
-    if constexpr (NST == 4) {
-      stage(std::integral_constant<int, 1>{});
-      stage(std::integral_constant<int, 2>{});
-      stage(std::integral_constant<int, 3>{});
-    }
     float x1[NV];
+    bool badn = false;
+    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
+      stage(std::integral_constant<int, 0>{});
+      if constexpr (NST == 4) {
+        stage(std::integral_constant<int, 1>{});
+        stage(std::integral_constant<int, 2>{});
+        stage(std::integral_constant<int, 3>{});
+      }
 #pragma unroll
-    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+      for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+      if (!dead) badn = Env::bad(x1, NV);
+      if (NST == 4 && !exact && wave_any(!dead && badn)) {
+        exact = true;
+        continue;
+      }
+      break;
+    }
     bool ev = false;
     if (!dead) {
-      const bool ok = !Env::bad(x1, NV);
+      const bool ok = !badn;
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1935,11 +1986,15 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;
+    float x1[NV];
+    bool badn = false;
+    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
-      stage_in_n<NV>(stage, x, kx, zx, dt, xt);
+      stage_in_n<NV>(stage, x, kx, zx, dt, xt, exact);
       // stages 1 and 2 share the time t + dt/2, hence the noise draw
       if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage_time(stage, t, dt), nzv);
       ctl_obs_apply<Env>(xt, nzv, y);
@@ -1954,12 +2009,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
       }
       stage_acc_n<NV>(stage, ax, kx);
     }
-    float x1[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+    if (!dead) badn = Env::bad(x1, NV);
+    if (!euler && !exact && wave_any(!dead && badn)) {
+      exact = true;
+      continue;
+    }
+    break;
+    }
     bool ev = false;
     if (!dead) {
-      const bool ok = !Env::bad(x1, NV);
+      const bool ok = !badn;
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -2061,7 +2122,9 @@ struct DpParked {
   float* base;
   uint32_t stride, gl;
   static constexpr int kFitWords = (int)((sizeof(Fit) + 3) / 4);
-  static_assert(7 + 2 * ND + kFitWords <= kDpStateWords, "Dopri5 parked state too large");
+  static_assert(7 + 2 * ND + kFitWords <= kDpStateWords - 1, "Dopri5 parked state too large");
+  // the last word of lane 0's column: the wave's remaining-work estimate (launch 2's order)
+  static constexpr int kEstWord = kDpStateWords - 1;
   __device__ __forceinline__ float& w(int i) const { return base[(size_t)i * stride + gl]; }
   __device__ __forceinline__ void save(float t, float tn, const MtgpDpCtl& c, bool ok, bool live, int k, int steps,
                                        const float (&y)[ND], const float (&f0)[ND], const Fit& fit) const {
@@ -2249,7 +2312,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MTGP_D
   for (int iter = 0; wave_any(live); ++iter) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)iter);
     if (!RT && iter == budget) {  // launch 1 of 2: park this wave (every lane), launch 2 resumes it
-      if constexpr (!RT) park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+      if constexpr (!RT) {
+        park.save(t, tnext, ctl, prev_ok, live, k, steps, y, f[0], fit);
+        // the wave's remaining work, for launch 2's longest-first order (k_dp_order): its slowest
+        // lane's attempts so far scaled by the time still to cover over the time covered
+        const float done = t - ts[0];
+        float est = !live ? 0.0f : (done > 0.0f ? (float)steps * ((t_end - t) / done) : (float)max_steps);
+        est = est < (float)max_steps ? est : (float)max_steps;
+#pragma unroll
+        for (int o = 1; o < kWave; o <<= 1) est = fmaxf(est, __shfl_xor(est, o, kWave));
+        if (Ln.lane == 0) park.w(park.kEstWord) = est;
+      }
       if (Ln.lane == 0) A.dp_pending[1 + atomicAdd(A.dp_pending, 1)] = wv;
       return;
     }
@@ -2398,11 +2471,15 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;
+    float x1[NV];
+    bool badn = false;
+    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], zx[i], dt));
+      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], zx[i], dt, exact));
       run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
       if (stage == 0) {
 #pragma unroll
@@ -2411,12 +2488,18 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
-    float x1[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+    if (!dead) badn = bad(x1);
+    if (!euler && !exact && wave_any(!dead && badn)) {
+      exact = true;
+      continue;
+    }
+    break;
+    }
     bool ev = false;
     if (!dead) {
-      const bool ok = !bad(x1);
+      const bool ok = !badn;
       ev = prev_ok && !ok;  // the NaN event (sr.py:93-94)
       prev_ok = ok;
     }
@@ -2741,7 +2824,11 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {  // (no FairShare: the workgroup's waves meet at a barrier every stage)
     const float dt = clk.dt();
-    float zx[kWideComp];  // the zero tableau entries' terms (mtgp_cstep.h)
+    float zx[kWideComp];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
+    bool exact = false;
+    float x1[kWideComp];
+    bool bad;
+    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; f parks in nxt
@@ -2798,7 +2885,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
           const float kv = nxt[c * kWave];
           if (stage == 0) fx0[t] = kv;
           ax[t] = stage_acc(stage, ax[t], kv);
-          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, zx[t], dt);  // the next stage's input
+          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, zx[t], dt, exact);  // the next stage's input
         }
       }
       __syncthreads();
@@ -2807,10 +2894,20 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       nxt = tmp;
     }
     // cur holds the last stage's derivatives f3 (Euler: f0); the step's end state and the event
-    float x1[kWideComp];
 #pragma unroll
     for (int t = 0; t < kWideComp; ++t) x1[t] = euler ? x[t] + fx0[t] * dt : mtgp_rk4_out(x[t], ax[t], dt);
-    const bool bad = any_bad(x1);
+    bad = any_bad(x1);
+    // (dead and bad are identical in every wave of the workgroup: a uniform branch)
+    if (!euler && !exact && wave_any(!dead && bad)) {
+      exact = true;
+#pragma unroll
+      for (int t = 0; t < kWideComp; ++t)  // the stage-0 input again (the stages left f3 in cur)
+        if (c0 + t < NV) cur[(c0 + t) * kWave] = dead ? kInf : x[t];
+      __syncthreads();
+      continue;
+    }
+    break;
+    }
     bool ev = false;
     if (!dead) {
       ev = prev_ok && bad;
@@ -4687,6 +4784,42 @@ int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 
   }
 }
 
+// Launch 2's order (round 6): the parked waves longest-first by their remaining-work estimate
+// (DpParked::kEstWord of lane 0), so the hardware dispatches the waves that bound the kernel's tail
+// before the short ones (longest-processing-time order).  One workgroup, a counting sort over 256
+// log-scale buckets in LDS (order inside a bucket arbitrary: results do not depend on the order);
+// more than kDpOrderMax parked waves keep the order they parked in.
+constexpr int kDpOrderMax = 8192;
+static __global__ void __launch_bounds__(1024) k_dp_order(int32_t* pending, const float* state, uint32_t stride) {
+  __shared__ int hist[256];
+  __shared__ int ids[kDpOrderMax];
+  __shared__ unsigned char keys[kDpOrderMax];
+  const int n = pending[0];
+  if (n <= 1 || n > kDpOrderMax) return;
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0;
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int id = pending[1 + i];
+    const float est = state[(size_t)(kDpStateWords - 1) * stride + (size_t)id * kWave];
+    const float q = est > 0.0f ? 16.0f * __log2f(est + 1.0f) : 0.0f;  // 1/16-octave buckets
+    const int key = 255 - (q >= 255.0f ? 255 : (int)q);               // longest first
+    ids[i] = id;
+    keys[i] = (unsigned char)key;
+    atomicAdd(&hist[key], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int acc = 0;
+    for (int b = 0; b < 256; ++b) {
+      const int c = hist[b];
+      hist[b] = acc;
+      acc += c;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) pending[1 + atomicAdd(&hist[keys[i]], 1)] = ids[i];
+}
+
 // adaptive Dopri5 at a runtime state size (NA = kNaRuntime / kNaWide): interpreter variants only;
 // the non-mask environments' kernels live in TU 9 (their register allocation dominates a build)
 __attribute__((visibility("hidden"))) int mtgp_tu_launch_dp_rt(const void* A, int env, bool wide, bool noise, bool traj,
@@ -4771,6 +4904,7 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
       A1.dp_pass = 1;
       rc = launch_dp_entry<Env>(&A1, model, jit, noise, traj, grid.x, block.x, s);
       if (rc != MTGP_OK) return;
+      hipLaunchKernelGGL(k_dp_order, dim3(1), dim3(1024), 0, s, A.dp_pending, (const float*)A.dp_state, A.dp_lanes);
       KArgs A2 = A;
       A2.dp_pass = 2;
       rc = launch_dp_entry<Env>(&A2, model, jit, noise, traj, grid.x, block.x, s);

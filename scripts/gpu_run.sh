@@ -92,6 +92,8 @@ for step in "$@"; do
     prof_dp) SKIP=20 prof prof_dp c3 --solver dopri5 || exit 1 ;;
     prof_dpn) SKIP=20 prof prof_dpn c3 --solver dopri5 --obs-noise 0.1 || exit 1 ;;
     dpab) run dpab 600 python scripts/dp_budget_ab.py || exit 1 ;;
+    dpab_lpt) run dpab_lpt 600 python scripts/dp_budget_ab.py --budgets 0,16,48,128,500 --rounds 3 || exit 1 ;;
+    dpab_lpt_noise) run dpab_lpt_noise 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,16,48,128,500 --rounds 2 || exit 1 ;;
     dpab_legacy) run dpab_legacy 900 python scripts/dp_budget_ab.py --legacy-pop --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab2) run dpab2 900 python scripts/dp_budget_ab.py --budgets 0,500 --rounds 3 || exit 1 ;;
     dpab_noise2) run dpab_noise2 900 python scripts/dp_budget_ab.py --obs-noise 0.1 --budgets 0,384,512,640,768 --rounds 3 || exit 1 ;;

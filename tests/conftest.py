@@ -15,17 +15,10 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session", autouse=True)
 def _built():
-    """Build what is stale, once: xdist workers take a file lock, so only the first one compiles
-    and the others find the libraries fresh."""
-    import fcntl
+    """Build what is stale, once (build_hip serialises concurrent callers on a file lock: the
+    first xdist worker compiles, the others find the library fresh)."""
     import __graft_entry__ as g
+    g.build_hip()
     from oracle import oracle as orc
-    os.makedirs(g.LIBDIR, exist_ok=True)
-    with open(os.path.join(g.LIBDIR, ".build.lock"), "w") as lock:
-        fcntl.flock(lock, fcntl.LOCK_EX)
-        try:
-            g.build_hip()
-            orc.build()
-        finally:
-            fcntl.flock(lock, fcntl.LOCK_UN)
+    orc.build()
     yield

@@ -164,10 +164,14 @@ def cs_solve(rhs, s0, ts, dt0, solver="rk4", dtype=np.float64, event=None):
             if solver == "euler":
                 y1 = y + f0 * dt
             else:
-                # zero tableau entries multiplied (diffrax's padded-row dot product, mtgp_cstep.h)
+                # zero tableau entries multiplied (diffrax's padded-row dot product, mtgp_cstep.h):
+                # 0 f_j is a no-op for a finite f_j and NaN otherwise
+                nz = lambda z, v: np.where(np.isnan(z), z, v)
                 f1 = np.asarray(rhs(np.float32(t + np.float32(0.5) * dtf), y + (d(0.5) * f0) * dt), d)
-                f2 = np.asarray(rhs(np.float32(t + np.float32(0.5) * dtf), y + (d(0) * f0 + d(0.5) * f1) * dt), d)
-                f3 = np.asarray(rhs(np.float32(t + dtf), y + ((d(0) * f0 + d(0) * f1) + f2) * dt), d)
+                z = d(0) * f0
+                f2 = np.asarray(rhs(np.float32(t + np.float32(0.5) * dtf), y + nz(z, d(0.5) * f1) * dt), d)
+                z = z + d(0) * f1
+                f3 = np.asarray(rhs(np.float32(t + dtf), y + nz(z, f2) * dt), d)
                 y1 = y + (((b0 * f0 + b1 * f1) + b1 * f2) + b0 * f3) * dt
             while k < S and ts[k] <= tn:
                 if t == tn:
