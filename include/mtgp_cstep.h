@@ -40,9 +40,8 @@
  *           sign of an all-zero increment, the convention that also drops the trailing 0 * 0 terms)
  *           and a NaN z as NaN: a non-finite earlier stage derivative makes the stage input NaN in
  *           that component, where skipping the entry would not.  So with finite f0, f1 the inputs
- *           are the plain y + (0.5 f1) dt, y + (1.0 f2) dt (mtgp_rk4_in_fast), and a non-finite
- *           f0 or f1 always makes that component of y1 non-finite (every b_j != 0): the kernels run
- *           the fast form and redo a step with z only when a live lane's y1 is not finite.
+ *           are the plain y + (0.5 f1) dt, y + (1.0 f2) dt; the kernels test the running
+ *           b-weighted sum instead of carrying z (mtgp_rk4_in_acc).
  * SaveAt(ts): after each step every pending ts[k] <= tn (k ascending, ts[0] included at step 0) is
  *   evaluated through the step's dense output at theta = linear_rescale(t, ts[k], tn):
  *   Euler   LocalLinearInterpolation: y + theta (y1 - y)
@@ -111,9 +110,15 @@ MTGP_INLINE MTGP_HD float mtgp_rk4_nz(float z, float v) { return z != z ? z : v;
 MTGP_INLINE MTGP_HD float mtgp_rk4_in(int st, float y, float f, float z, float dt) {
   return st == 1 ? y + (0.5f * f) * dt : st == 2 ? y + mtgp_rk4_nz(z, 0.5f * f) * dt : y + mtgp_rk4_nz(z, f) * dt;
 }
-/* the same with every z = +-0 (all earlier derivatives finite): the kernels' fast form */
-MTGP_INLINE MTGP_HD float mtgp_rk4_in_fast(int st, float y, float f, float dt) {
-  return st == 3 ? y + f * dt : y + (0.5f * f) * dt;
+/* The same in the kernels' register-free form: acc = the b-weighted sum of the earlier stage
+ * derivatives WITHOUT f's term (mtgp_rk4_acc through stage st - 2: b0 f0 at stage 2, b0 f0 + b1 f1
+ * at stage 3).  acc is non-finite exactly when one of those derivatives is (|b0 f0 + b1 f1| <=
+ * FLT_MAX / 2 for finite f0, f1: no overflow), i.e. exactly when z is NaN, so [z; v] is
+ * (acc finite ? v : NaN) -- mtgp_rk4_in bit for bit up to the NaN payload, with no z carried. */
+MTGP_INLINE MTGP_HD float mtgp_rk4_in_acc(int st, float y, float f, float acc, float dt) {
+  if (st == 1) return y + (0.5f * f) * dt;
+  const float v = st == 2 ? 0.5f * f : f;
+  return y + (mtgp_isfinite(acc) ? v : mtgp_u2f(0x7fc00000u)) * dt;
 }
 /* the zero-entry sum after stage st's input was formed from f = f_{st-1}: stage 1 starts it (0 f0,
  * for stage 2), stage 2 adds 0 f1 (for stage 3); stage 3 leaves it */

@@ -892,15 +892,11 @@ struct CsClock {
 };
 
 // RK4 stage input (stage 0: s itself; stages 1..3: s + (sum_j a_ij f_j) dt over the padded tableau
-// row) and the running b-weighted sum of the stage derivatives.  exact (wave-uniform): the zero
-// entries' terms ride in z (mtgp_cstep.h); otherwise the fast form, equal to it whenever the earlier
-// derivatives are finite -- the kernels redo a step exactly when a live lane's y1 is not finite.
-__device__ __forceinline__ float stage_in(int stage, float s, float f, float& z, float dt, bool exact) {
-  if (stage == 0) return s;
-  if (!exact) return mtgp_rk4_in_fast(stage, s, f, dt);
-  const float v = mtgp_rk4_in(stage, s, f, z, dt);
-  z = mtgp_rk4_zero(stage, z, f);
-  return v;
+// row, zero entries multiplied: mtgp_cstep.h) from f = the previous stage's derivative and acc = the
+// running b-weighted sum BEFORE f's term is added (mtgp_rk4_in_acc: no zero-entry sum carried), and
+// the running b-weighted sum of the stage derivatives
+__device__ __forceinline__ float stage_in(int stage, float s, float f, float acc, float dt) {
+  return stage == 0 ? s : mtgp_rk4_in_acc(stage, s, f, acc, dt);
 }
 __device__ __forceinline__ float stage_acc(int stage, float acc, float f) { return mtgp_rk4_acc(stage, acc, f); }
 __device__ __forceinline__ float stage_time(int stage, float t, float dt) {
@@ -910,35 +906,21 @@ __device__ __forceinline__ float stage_time(int stage, float t, float dt) {
 // The same for a whole state vector, branching on the (wave-uniform) stage once instead of
 // selecting per component: the same operations, so the same bits.
 template <int N>
-__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], float (&z)[N],
-                                           float dt, float (&out)[N], bool exact) {
+__device__ __forceinline__ void stage_in_n(int stage, const float (&s)[N], const float (&f)[N], const float (&acc)[N],
+                                           float dt, float (&out)[N]) {
   const int st = uni(stage);
   if (st == 0) {
 #pragma unroll
     for (int i = 0; i < N; ++i) out[i] = s[i];
-  } else if (!exact) {
-    if (st == 3) {
-#pragma unroll
-      for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_fast(3, s[i], f[i], dt);
-    } else {
-#pragma unroll
-      for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_fast(1, s[i], f[i], dt);
-    }
   } else if (st == 1) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      out[i] = mtgp_rk4_in(1, s[i], f[i], z[i], dt);
-      z[i] = mtgp_rk4_zero(1, z[i], f[i]);
-    }
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_acc(1, s[i], f[i], acc[i], dt);
   } else if (st == 2) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) {
-      out[i] = mtgp_rk4_in(2, s[i], f[i], z[i], dt);
-      z[i] = mtgp_rk4_zero(2, z[i], f[i]);
-    }
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_acc(2, s[i], f[i], acc[i], dt);
   } else {
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in(3, s[i], f[i], z[i], dt);
+    for (int i = 0; i < N; ++i) out[i] = mtgp_rk4_in_acc(3, s[i], f[i], acc[i], dt);
   }
 }
 template <int N>
@@ -1232,18 +1214,10 @@ __global__ void __launch_bounds__(256) k_rollout_mean(const float* __restrict__ 
 // constants and branches resolved at compile time), and the kernel runs the general loop below only
 // when the code is not usable.  The arithmetic is k_ctl_dynamic's, operation for operation.
 template <int N>
-__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], float (&z)[N], float dt,
-                                      float (&out)[N], bool exact) {
-  if (st == 0 || !exact) {
+__device__ __forceinline__ void rk_in(int st, const float (&s)[N], const float (&f)[N], const float (&acc)[N], float dt,
+                                      float (&out)[N]) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : mtgp_rk4_in_fast(st, s[i], f[i], dt);
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    out[i] = mtgp_rk4_in(st, s[i], f[i], z[i], dt);
-    if (st == 1 || st == 2) z[i] = mtgp_rk4_zero(st, z[i], f[i]);
-  }
+  for (int i = 0; i < N; ++i) out[i] = st == 0 ? s[i] : mtgp_rk4_in_acc(st, s[i], f[i], acc[i], dt);
 }
 template <int N>
 __device__ __forceinline__ void rk_acc(int st, float (&acc)[N], const float (&f)[N]) {
@@ -1416,14 +1390,18 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
-    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;    // (wave-uniform) the step redone with the zero entries' terms
-    // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant
+    // one RK stage (NST = 4) or the Euler step (NST = 1); ST is a compile-time constant.  The
+    // stage input reads the b-weighted sum before f_{ST-1}'s term (mtgp_rk4_in_acc: the zero
+    // tableau entries, mtgp_cstep.h), which is then added -- the same sums in the same order.
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], at[NA], y[NV];
-      rk_in<NV>(ST, x, kx, zx, dt, xt, exact);
-      rk_in<NA>(ST, a, ka, za, dt, at, exact);
+      rk_in<NV>(ST, x, kx, ax, dt, xt);
+      rk_in<NA>(ST, a, ka, aa, dt, at);
+      if (NST == 4 && ST > 0) {
+        rk_acc<NV>(ST - 1, ax, kx);
+        rk_acc<NA>(ST - 1, aa, ka);
+      }
 #pragma unroll
       for (int j = 0; j < NA; ++j) dv[NV + j] = at[j];
       if (NOISE && ST != 2) {  // stages 1 and 2 share the time t + dt/2, hence the noise draw
@@ -1446,44 +1424,29 @@ __device__ __forceinline__ void ctl_dynamic_jit(const KArgs& A, const Lane& Ln) 
 #pragma unroll
         for (int j = 0; j < NA; ++j) fa0[j] = ka[j];
       }
-      if (NST == 4) {
-        rk_acc<NV>(ST, ax, kx);
-        rk_acc<NA>(ST, aa, ka);
-      }
     };
-    // the step's end state and the event (Event(cond_fn_nan) after the step, dyn.py:94); a live
-    // lane whose end state is bad may have met a non-finite stage derivative: the step is redone
-    // with the zero tableau entries' terms (mtgp_cstep.h; at most once per event)
-    float x1[NV], a1[NA];
-    bool badn = false;
-    for (;;) {
-      stage(std::integral_constant<int, 0>{});
-      if constexpr (NST == 4) {
-        stage(std::integral_constant<int, 1>{});
-        stage(std::integral_constant<int, 2>{});
-        stage(std::integral_constant<int, 3>{});
-      }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
-#pragma unroll
-      for (int j = 0; j < NA; ++j) a1[j] = NST == 1 ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
-      if (!dead) {
-        float sn[NV + NA];
-#pragma unroll
-        for (int i = 0; i < NV; ++i) sn[i] = x1[i];
-#pragma unroll
-        for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
-        badn = Env::bad(sn, NV + NA);
-      }
-      if (NST == 4 && !exact && wave_any(!dead && badn)) {
-        exact = true;
-        continue;
-      }
-      break;
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (NST == 4) {
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      rk_acc<NV>(3, ax, kx);
+      rk_acc<NA>(3, aa, ka);
     }
+    // the step's end state and the event (Event(cond_fn_nan) after the step, dyn.py:94)
+    float x1[NV], a1[NA];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
+#pragma unroll
+    for (int j = 0; j < NA; ++j) a1[j] = NST == 1 ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
     bool ev = false;
     if (!dead) {
-      const bool ok = !badn;
+      float sn[NV + NA];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) sn[i] = x1[i];
+#pragma unroll
+      for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
+      const bool ok = !Env::bad(sn, NV + NA);
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1659,16 +1622,17 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
   int k = 0;  // next save point
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
-    float zx[NV], za[NA];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;    // (wave-uniform) the step redone with them: a live lane's end state is bad
-    float x1[NV], a1[NA];
-    bool badn = false;
-    for (;;) {
+    // (the stage input reads the b-weighted sum before f_{stage-1}'s term -- mtgp_rk4_in_acc, the
+    // zero tableau entries -- which is then added: the same sums in the same order)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], at[NA], y[NV];
-      stage_in_n<NV>(stage, x, kx, zx, dt, xt, exact);
-      stage_in_n<NA>(stage, a, ka, za, dt, at, exact);
+      stage_in_n<NV>(stage, x, kx, ax, dt, xt);
+      stage_in_n<NA>(stage, a, ka, aa, dt, at);
+      if (stage > 0) {
+        stage_acc_n<NV>(stage - 1, ax, kx);
+        stage_acc_n<NA>(stage - 1, aa, ka);
+      }
 #pragma unroll
       for (int j = 0; j < NA; ++j)
         if (j < na) D.put(NV + j, at[j]);
@@ -1689,30 +1653,22 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
 #pragma unroll
         for (int j = 0; j < NA; ++j) fa0[j] = ka[j];
       }
-      stage_acc_n<NV>(stage, ax, kx);
-      stage_acc_n<NA>(stage, aa, ka);
     }
+    stage_acc_n<NV>(n_stages - 1, ax, kx);
+    stage_acc_n<NA>(n_stages - 1, aa, ka);
+    float x1[NV], a1[NA];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
 #pragma unroll
     for (int j = 0; j < NA; ++j) a1[j] = euler ? a[j] + fa0[j] * dt : mtgp_rk4_out(a[j], aa[j], dt);
+    bool ev = false;
     if (!dead) {
       float sn[NV + NA];
 #pragma unroll
       for (int i = 0; i < NV; ++i) sn[i] = x1[i];
 #pragma unroll
       for (int j = 0; j < NA; ++j) sn[NV + j] = a1[j];
-      badn = Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
-    }
-    if (!euler && !exact && wave_any(!dead && badn)) {
-      exact = true;
-      continue;
-    }
-    break;
-    }
-    bool ev = false;
-    if (!dead) {
-      const bool ok = !badn;
+      const bool ok = !Env::bad(sn, NV + NA);  // (slots j >= na stay 0: ka / aa start at 0)
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1825,12 +1781,13 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float t = clk.t, dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;
+    // (the stage input reads the b-weighted sum before f_{ST-1}'s term -- mtgp_rk4_in_acc, the zero
+    // tableau entries -- which is then added: the same sums in the same order)
     auto stage = [&](auto st_c) {
       constexpr int ST = decltype(st_c)::value;
       float xt[NV], y[NV];
-      rk_in<NV>(ST, x, kx, zx, dt, xt, exact);
+      rk_in<NV>(ST, x, kx, ax, dt, xt);
+      if (NST == 4 && ST > 0) rk_acc<NV>(ST - 1, ax, kx);
       if (NOISE && ST != 2) {
         const float tc = ST == 0 ? t : mtgp_rk4_time(ST, t, dt);
         obs_noise_vec<NV>(nzc, tc, nzv);
@@ -1845,29 +1802,20 @@ __device__ __forceinline__ void ctl_static_jit(const KArgs& A, const Lane& Ln) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
       }
-      if (NST == 4) rk_acc<NV>(ST, ax, kx);
     };
-    float x1[NV];
-    bool badn = false;
-    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
-      stage(std::integral_constant<int, 0>{});
-      if constexpr (NST == 4) {
-        stage(std::integral_constant<int, 1>{});
-        stage(std::integral_constant<int, 2>{});
-        stage(std::integral_constant<int, 3>{});
-      }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
-      if (!dead) badn = Env::bad(x1, NV);
-      if (NST == 4 && !exact && wave_any(!dead && badn)) {
-        exact = true;
-        continue;
-      }
-      break;
+    stage(std::integral_constant<int, 0>{});
+    if constexpr (NST == 4) {
+      stage(std::integral_constant<int, 1>{});
+      stage(std::integral_constant<int, 2>{});
+      stage(std::integral_constant<int, 3>{});
+      rk_acc<NV>(3, ax, kx);
     }
+    float x1[NV];
+#pragma unroll
+    for (int i = 0; i < NV; ++i) x1[i] = NST == 1 ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
     bool ev = false;
     if (!dead) {
-      const bool ok = !badn;
+      const bool ok = !Env::bad(x1, NV);
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -1986,15 +1934,13 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {
     const float t = clk.t, dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;
-    float x1[NV];
-    bool badn = false;
-    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
+    // (the stage input reads the b-weighted sum before f_{stage-1}'s term -- mtgp_rk4_in_acc, the
+    // zero tableau entries -- which is then added: the same sums in the same order)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       float xt[NV], y[NV];
-      stage_in_n<NV>(stage, x, kx, zx, dt, xt, exact);
+      stage_in_n<NV>(stage, x, kx, ax, dt, xt);
+      if (stage > 0) stage_acc_n<NV>(stage - 1, ax, kx);
       // stages 1 and 2 share the time t + dt/2, hence the noise draw
       if (NOISE && stage != 2) obs_noise_vec<NV>(nzc, stage_time(stage, t, dt), nzv);
       ctl_obs_apply<Env>(xt, nzv, y);
@@ -2007,20 +1953,14 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) k
 #pragma unroll
         for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
       }
-      stage_acc_n<NV>(stage, ax, kx);
     }
+    stage_acc_n<NV>(n_stages - 1, ax, kx);
+    float x1[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
-    if (!dead) badn = Env::bad(x1, NV);
-    if (!euler && !exact && wave_any(!dead && badn)) {
-      exact = true;
-      continue;
-    }
-    break;
-    }
     bool ev = false;
     if (!dead) {
-      const bool ok = !badn;
+      const bool ok = !Env::bad(x1, NV);
       ev = prev_ok && !ok;
       prev_ok = ok;
     }
@@ -2471,35 +2411,29 @@ __global__ void __launch_bounds__(256) k_sr(KArgs A) {
   while (clk.live()) {
     if (fair_on) fair.step(Ln.lane, (uint32_t)clk.steps);
     const float dt = clk.dt();
-    float zx[NV];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;
-    float x1[NV];
-    bool badn = false;
-    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
+    // (the stage input reads the b-weighted sum before f_{stage-1}'s term -- mtgp_rk4_in_acc, the
+    // zero tableau entries -- which is then added: the same sums in the same order)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
 #pragma unroll
-      for (int i = 0; i < NV; ++i) D.put(i, stage_in(stage, x[i], kx[i], zx[i], dt, exact));
+      for (int i = 0; i < NV; ++i) {
+        D.put(i, stage_in(stage, x[i], kx[i], ax[i], dt));
+        if (stage > 0) ax[i] = stage_acc(stage - 1, ax[i], kx[i]);
+      }
       run_role<JIT, NV>(A, Ln, ng, 0, A.m.prog_state, D, kx, A.chain_state != 0);
       if (stage == 0) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
       }
-#pragma unroll
-      for (int i = 0; i < NV; ++i) ax[i] = stage_acc(stage, ax[i], kx[i]);
     }
+#pragma unroll
+    for (int i = 0; i < NV; ++i) ax[i] = stage_acc(n_stages - 1, ax[i], kx[i]);
+    float x1[NV];
 #pragma unroll
     for (int i = 0; i < NV; ++i) x1[i] = euler ? x[i] + fx0[i] * dt : mtgp_rk4_out(x[i], ax[i], dt);
-    if (!dead) badn = bad(x1);
-    if (!euler && !exact && wave_any(!dead && badn)) {
-      exact = true;
-      continue;
-    }
-    break;
-    }
     bool ev = false;
     if (!dead) {
-      const bool ok = !badn;
+      const bool ok = !bad(x1);
       ev = prev_ok && !ok;  // the NaN event (sr.py:93-94)
       prev_ok = ok;
     }
@@ -2824,11 +2758,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
   int k = 0;
   while (clk.live()) {  // (no FairShare: the workgroup's waves meet at a barrier every stage)
     const float dt = clk.dt();
-    float zx[kWideComp];  // the zero tableau entries' terms (mtgp_cstep.h), exact mode only
-    bool exact = false;
-    float x1[kWideComp];
-    bool bad;
-    for (;;) {  // (redone once with the zero tableau entries' terms when a live lane's end state is bad)
+    // (the next stage's input reads the b-weighted sum before this stage's term -- mtgp_rk4_in_acc,
+    // the zero tableau entries -- which is then added: the same sums in the same order)
 #pragma unroll 1
     for (int stage = 0; stage < n_stages; ++stage) {
       // trees of this wave's components on the shared stage vector; f parks in nxt
@@ -2884,8 +2815,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
         if (c < NV) {
           const float kv = nxt[c * kWave];
           if (stage == 0) fx0[t] = kv;
+          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, ax[t], dt);  // the next stage's input
           ax[t] = stage_acc(stage, ax[t], kv);
-          if (!last) nxt[c * kWave] = stage_in(stage + 1, x[t], kv, zx[t], dt, exact);  // the next stage's input
         }
       }
       __syncthreads();
@@ -2894,20 +2825,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(4))) k
       nxt = tmp;
     }
     // cur holds the last stage's derivatives f3 (Euler: f0); the step's end state and the event
+    float x1[kWideComp];
 #pragma unroll
     for (int t = 0; t < kWideComp; ++t) x1[t] = euler ? x[t] + fx0[t] * dt : mtgp_rk4_out(x[t], ax[t], dt);
-    bad = any_bad(x1);
-    // (dead and bad are identical in every wave of the workgroup: a uniform branch)
-    if (!euler && !exact && wave_any(!dead && bad)) {
-      exact = true;
-#pragma unroll
-      for (int t = 0; t < kWideComp; ++t)  // the stage-0 input again (the stages left f3 in cur)
-        if (c0 + t < NV) cur[(c0 + t) * kWave] = dead ? kInf : x[t];
-      __syncthreads();
-      continue;
-    }
-    break;
-    }
+    const bool bad = any_bad(x1);
     bool ev = false;
     if (!dead) {
       ev = prev_ok && bad;
