@@ -1153,6 +1153,42 @@ __device__ __forceinline__ void run_role(const KArgs& A, const Lane& L, int ng, 
 
 
 
+// Programs first .. first+mr-1 of every live group -> out[0..mr-1] from LDS-data JIT code (mtgp_jit.h
+// kJitModeLds: v0 = this lane's LDS byte address of data slot 0, the interpreter's own data
+// columns): the runtime-state-size control kernels (round 6), one unit call per program; the
+// interpreter for lanes that need it (no template sets that flag) and for unusable code.
+__device__ __forceinline__ uint32_t lds_address(const float* p);
+__device__ __forceinline__ float jit_call_lds(uint64_t addr_, uint32_t lds_addr, uint64_t& flag);
+template <int M>
+__device__ __forceinline__ void run_role_lds(const KArgs& A, const Lane& L, int ng, int first, float* dcol, float* st,
+                                             float (&out)[M], int mr = M) {
+  if (__builtin_expect(L.jok, 1)) {
+    const uint32_t la = lds_address(dcol);
+#pragma unroll 1
+    for (int q = 0; q < mr; ++q) {
+      const uint32_t off = (uint32_t)__builtin_amdgcn_readlane((int)L.jtab, first + q);
+      uint64_t fl = 0;
+      float v = jit_call_lds(A.jit_base + off, la, fl);
+      if (__builtin_expect(fl != 0, 0)) {
+        for (int gi = 0; gi < ng; ++gi) {
+          if (!(fl & __ballot(L.g == gi && L.active))) continue;
+          const float t = run_one_interp<MTGP_COLD_INTERP != 0>(A, L, gi, first + q, dcol, st);
+          v = (L.g == gi) ? t : v;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
+    }
+    return;
+  }
+#pragma unroll 1
+  for (int q = 0; q < mr; ++q) {
+    const float v = run_groups_interp<MTGP_COLD_INTERP != 0>(A, L, ng, first + q, dcol, st, 0.0f);
+#pragma unroll
+    for (int j = 0; j < M; ++j) out[j] = (q == j) ? v : out[j];
+  }
+}
+
 __device__ __forceinline__ void finish_group(const KArgs& A, const Lane& L, float F) {
   const float mx = A.m.max_fitness;
   if (A.out.rollout_fitness && L.active) A.out.rollout_fitness[(size_t)L.p * A.ro.R + L.r] = F;
@@ -1541,7 +1577,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
   const int R = A.ro.R;
   float* dcol = &lds[Ln.wave][Ln.lane];
   float* st = &lds[Ln.wave][DM * kWave + Ln.lane];
-  DataVec<JIT> D(dcol, st);
+  // NA > 3 with JIT (round 6): LDS-data code reads the interpreter's own data columns, so the
+  // data vector stays in LDS (no register copy)
+  constexpr bool LJ = JIT && NA > 3;
+  DataVec<JIT && !LJ> D(dcol, st);
 
   const int S = A.m.n_save;
   ObsNoise<NV> nzc;
@@ -1589,7 +1628,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
       if (j < na) D.put(NV + j, as[j]);
     D.put(uslot, 0.0f);
     float sr[1];
-    run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
+    if constexpr (LJ) run_role_lds<1>(A, Ln, ng, A.m.prog_readout_save, dcol, st, sr);
+    else run_role<JIT, 1>(A, Ln, ng, 2, A.m.prog_readout_save, D, sr);
     const float us = sr[0];
     if constexpr (Env::kMask) {
       if (active) env.fit_save(fit, k, S, A, PR, loff, fill, us, xs);
@@ -1637,7 +1677,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
       for (int j = 0; j < NA; ++j)
         if (j < na) D.put(NV + j, at[j]);
       float ur[1];
-      run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
+      if constexpr (LJ) run_role_lds<1>(A, Ln, ng, A.m.prog_readout, dcol, st, ur);
+      else run_role<JIT, 1>(A, Ln, ng, 0, A.m.prog_readout, D, ur);
       const float u = ur[0];
       env.drift(xt, u, kx);
       // stages 1 and 2 share the time t + dt/2, hence the noise draw
@@ -1646,7 +1687,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > k
 #pragma unroll
       for (int i = 0; i < NV; ++i) D.put(i, y[i]);
       D.put(uslot, u);
-      run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0, -1, nullptr, na);
+      if constexpr (LJ) run_role_lds<NA>(A, Ln, ng, A.m.prog_state, dcol, st, ka, na);
+      else run_role<JIT, NA>(A, Ln, ng, 1, A.m.prog_state, D, ka, A.chain_state != 0, -1, nullptr, na);
       if (stage == 0) {
 #pragma unroll
         for (int i = 0; i < NV; ++i) fx0[i] = kx[i];
@@ -4545,6 +4587,7 @@ MtgpJitChain jit_chain_for(const MtgpModel& m, int n_prog) {
     }
     M = m.n_var;
   } else if (m.model == MTGP_MODEL_DYNAMIC) {
+    if (m.state_size > 3) return c;  // runtime state size: LDS-data code, one unit per program (round 6)
     M = m.state_size;
     // fixed step (ABI v18): readout -> u into its data slot -> state programs, one call per stage
     // (the readout reads [0, a, 0, tar] with y and u folded, so y may already sit in its slots)
@@ -4688,21 +4731,9 @@ constexpr bool kTrajOnly = E::kMask;
 
 template <class Env, int NA>
 int launch_dyn(const KArgs& A, bool jit, bool noise, bool traj, dim3 grid, dim3 block, hipStream_t s) {
-  if constexpr (NA > 3) {  // state_size 4 .. kNaWide: the interpreter (data vector beyond the JIT's 8 registers)
-    if (jit) return MTGP_ERR_ARG;
-    return launch_timed([&] {
-      if (noise) {
-        if (traj) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, true, false>), grid, block, 0, s, A);
-        else if constexpr (!Env::kMask) hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, true, false>), grid, block, 0, s, A);
-      } else if (traj) {
-        hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, true, false, false>), grid, block, 0, s, A);
-      } else if constexpr (!Env::kMask) {
-        hipLaunchKernelGGL((k_ctl_dynamic<Env, NA, false, false, false>), grid, block, 0, s, A);
-      }
-    }, s);
-  } else {
-    return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
-  }
+  // (NA > 3, state_size 4 .. kNaWide: the data vector lives in LDS -- interpreter, or LDS-data JIT
+  // code, round 6)
+  return launch_timed([&] { MTGP_CTL_VARIANTS(k_ctl_dynamic, Env, NA); }, s);
 }
 
 // Launch 2's order (round 6): the parked waves longest-first by their remaining-work estimate
@@ -4806,8 +4837,9 @@ int launch_ctl(const KArgs& A, const MtgpModel* model, const MtgpRollouts* ro, b
     if (NV + model->n_targets > kDMax) return MTGP_ERR_ARG;
   } else if (model->state_size > 3) {  // runtime state size: the wide interpreter kernels, every solver
     const int dm = model->state_size > kNaRuntime ? kDWide2 : kDWide;
-    if (model->state_size > kNaWide || NV + model->state_size + 1 + model->n_targets > dm || jit ||
-        (model->solver == MTGP_SOLVER_DOPRI5 && A.dp_budget > 0))  // (one Dopri5 launch: no parking)
+    // (JIT: LDS-data code, fixed-step solvers; Dopri5: interpreter, one launch -- no parking)
+    if (model->state_size > kNaWide || NV + model->state_size + 1 + model->n_targets > dm ||
+        (model->solver == MTGP_SOLVER_DOPRI5 && (jit || A.dp_budget > 0)))
       return MTGP_ERR_ARG;
   } else if (NV + model->state_size + 1 + model->n_targets > kDMax) {
     return MTGP_ERR_ARG;

@@ -210,6 +210,8 @@ class DeviceEngine:
         ch = nat.MtgpJitChain(0, 0, 0)
         if os.environ.get("MTGP_JIT_CHAIN", "1") == "0":
             return ch
+        if self._jit_mode() == nat.JIT_MODE_LDS and self.ff.model_id != nat.MODEL_SR:
+            return ch  # (the runtime-state-size control kernels call one unit per program)
         rc = self.native.mtgp_jit_chain(ctypes.byref(m), n_prog, ctypes.byref(ch))
         if rc != nat.OK:
             raise RuntimeError(f"mtgp_jit_chain failed: {rc}")
@@ -326,13 +328,19 @@ class DeviceEngine:
     def _jit_usable(self) -> bool:
         """The program JIT serves every kernel: data vector in v0-v7 (control models, SR with
         n_var <= 4) or in the wide SR kernel's LDS stage vector (mtgp_jit.h kJitModeLds)."""
-        if not self.use_jit or getattr(self.ff, "state_size", 0) > 3:  # (runtime state sizes: interpreter kernels)
+        if not self.use_jit:
             return False
+        if getattr(self.ff, "state_size", 0) > 3:  # runtime state sizes: LDS-data code, fixed-step kernels only
+            return self.ff.solver_kind != "dopri5"
         return self.ff.n_data() <= 8 or self._jit_mode() == nat.JIT_MODE_LDS
 
     def _jit_mode(self) -> int:
         """LDS-data code for the wide-state SR kernel (n_var > 4), register-data code otherwise."""
-        return nat.JIT_MODE_LDS if self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4 else nat.JIT_MODE_REGS
+        if self.ff.model_id == nat.MODEL_SR and self.ff.n_data() > 4:
+            return nat.JIT_MODE_LDS
+        if getattr(self.ff, "state_size", 0) > 3:  # the runtime-state-size kernels' LDS data vector (round 6)
+            return nat.JIT_MODE_LDS
+        return nat.JIT_MODE_REGS
 
     @staticmethod
     def check_status(fl: Flattened):

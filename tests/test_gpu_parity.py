@@ -440,6 +440,14 @@ def test_state_size_above_three(case):
     if solver == "euler":
         ff = mt.DynamicEvaluator(env, ss, ff.dt0, solver=mt.Euler())
     res, ref, d = _run(ff, lib, data, pop, parsimony=0.25)
-    assert not DeviceEngine.jit_ok(res["_flat"])  # (n_data > 8: interpreter)
+    # fixed-step solvers: LDS-data JIT code (round 6); Dopri5: the interpreter
+    assert DeviceEngine.jit_ok(res["_flat"]) == (solver != "dopri5")
     _check(res, ref, pop.shape[0], 8, ["xs", "ys", "us", "acts"])
     assert res["acts"].shape[1] == ss
+    if solver != "dopri5":  # the interpreter on the same population: the same bits
+        eng = DeviceEngine(ff, lib, 0.25, "cuda:0", jit=False)
+        r2 = eng.evaluate(torch.from_numpy(np.ascontiguousarray(pop)).cuda(), data, trajectories=True,
+                          rollout_fitness=True)
+        assert not DeviceEngine.jit_ok(r2["_flat"])
+        for k in ("fitness", "rollout_fitness", "xs", "acts"):
+            assert bits_equal(res[k].cpu().numpy(), r2[k].cpu().numpy()), k
