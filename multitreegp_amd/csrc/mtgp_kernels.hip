@@ -1551,7 +1551,7 @@ struct WaveTimer {
 #endif
 
 template <class Env, int NA, bool TRAJ, bool NOISE, bool JIT>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(NA > kNaRuntime ? 2 : 4))) k_ctl_dynamic(KArgs A) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu((NA > kNaRuntime || (JIT && NA > 3)) ? 2 : 4))) k_ctl_dynamic(KArgs A) {
 #if MTGP_AB_WAVETIME
   WaveTimer wave_timer;
 #endif

@@ -212,3 +212,37 @@ def test_gpu_dynamic_notebook_selection_ensemble(name):
     else:
         # inside the lower tail, where a minimum over the notebook's 500 candidates belongs
         assert 0.0 < q <= {"gen30": 0.02, "gen50": 0.2}[name], (name, q)
+
+
+# ------------------------------------------------------------------ StaticPolicy.ipynb
+N_ULP_STATIC = 512  # one-ulp x0 moves: the printed static bests are exact trees (no hidden coefficients)
+
+
+@pytest.mark.gpu
+def test_gpu_static_notebook_ulp_ensemble():
+    """StaticPolicy.ipynb's coefficient-free bests (136.4901, 133.3388; StaticPolicy.ipynb:117-124)
+    against 512 one-ulp moves of the notebook's initial states, on the GPU (the 16-member oracle
+    ensemble of test_notebook_pin.test_static_notebook_printed_bests_in_lower_tail, scaled up).
+    Each printed value is the minimum over the notebook's evolving population, so it belongs in the
+    lower tail: the test asserts it lies at or above the ensemble minimum and below the median."""
+    import torch
+    from multitreegp_amd.engine import DeviceEngine
+    from test_notebook_pin import STATIC_BESTS, _static_pop, static_notebook
+    env, lib, ff, data = static_notebook()
+    pop = _static_pop(lib)
+    eng = DeviceEngine(ff, lib, 1.0, "cuda:0")  # size_parsinomy 1 (StaticPolicy.ipynb)
+    pt = torch.from_numpy(pop).cuda()
+    fits = np.stack([eng.evaluate(pt, ulp_moved(data, 5000 + s))["fitness"].cpu().numpy()
+                     for s in range(N_ULP_STATIC)])
+    rep = {}
+    for i, (name, (_, printed)) in enumerate(STATIC_BESTS.items()):
+        f = fits[:, i].astype(np.float64)
+        rep[name] = dict(printed=printed, members=int(f.size), printed_quantile=float((f <= printed).mean()),
+                         min=float(f.min()), median=float(np.median(f)), mean=float(f.mean()), sd=float(f.std()))
+        assert np.all(np.isfinite(f))
+        assert f.min() <= printed <= np.median(f), (name, rep[name])
+    out = os.environ.get("MTGP_REPORT_DIR")
+    if out:
+        with open(os.path.join(out, "static_ulp_ensemble.json"), "w") as fh:
+            json.dump(rep, fh, indent=1)
+    print(json.dumps(rep))
