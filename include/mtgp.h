@@ -271,8 +271,9 @@ int mtgp_flatten(const float* population, int32_t P, int32_t T, int32_t N,
  * translation pass of its own: jit_words_out[P, n_prog] = code words of the program's
  * fall-through translation (mtgp_jit.h jit_program; < 0: untranslatable) and jit_cost_out[P,
  * n_prog] = the schedule weight mtgp_jit_cost would compute.  Either may be NULL.  jit_mode:
- * MTGP_JIT_MODE_REGS (data vector in v0-v7: control models, SR n_var <= 4) or MTGP_JIT_MODE_LDS
- * (data vector = the LDS stage vector of the wide-state SR kernel, n_var 5..64).  population
+ * MTGP_JIT_MODE_REGS (data vector in v0-v7: control models with state_size <= 3, SR n_var <= 4) or
+ * MTGP_JIT_MODE_LDS (data vector in LDS: the wide-state SR kernel, n_var 5..64, and -- round 6 --
+ * the dynamic policy with state_size 4..16 under the fixed-step solvers).  population
  * must be 16-byte aligned (rows are loaded as 16-byte vectors). */
 enum { MTGP_JIT_MODE_REGS = 0, MTGP_JIT_MODE_LDS = 1 };
 int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N,
@@ -334,8 +335,11 @@ int mtgp_eval_rk4(const MtgpModel* model, const MtgpInstr* prog, const int32_t* 
  *    estimate when info is passed on to the evaluator, which then checks it on the device)
  *   mtgp_jit_emit   -> writes the code
  *   mtgp_eval_rk4_jit with MtgpJitCode{code, offsets}.
- * Every evaluator uses the code; the wide-state SR kernel (n_var > 4) needs it built in
- * MTGP_JIT_MODE_LDS (mtgp_flatten_ex / mtgp_jit_emit_words), the others in MTGP_JIT_MODE_REGS. */
+ * Every evaluator uses the code except Dopri5 at state_size > 3 (interpreted; pass no code); the
+ * wide-state SR kernel (n_var > 4) and the dynamic policy at state_size 4..16 need it built in
+ * MTGP_JIT_MODE_LDS (mtgp_flatten_ex / mtgp_jit_emit_words; the latter without role chains:
+ * mtgp_jit_chain returns none for it), the others in MTGP_JIT_MODE_REGS.  The code carries no mode
+ * tag: code of the other mode is undefined behaviour. */
 /* Role chains (ABI v13).  A role whose programs run back to back (the state_size state
  * equations of a dynamic policy, the n_var trees of SR with n_var <= 4) can be built as ONE
  * callable chain: bit j of `next` makes unit j fall through into unit j + 1 (laid out right
