@@ -3936,82 +3936,101 @@ __global__ void __launch_bounds__(256) k_sched_hist(const int32_t* __restrict__ 
   if (p < P) atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
 }
 
+// Exclusive scan of one value per thread over a 1024-thread block: a wave scan by shuffles and one
+// barrier for the 16 wave totals (wsum: 16 ints of LDS).  Replaces a Hillis-Steele scan through
+// LDS (twenty barriers).
+__device__ __forceinline__ int block_excl_scan_1024(int v, int32_t* wsum) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  int inc = v;
+  for (int d = 1; d < kWave; d <<= 1) {
+    const int y = __shfl_up(inc, d, kWave);
+    if (lane >= d) inc += y;
+  }
+  if (lane == kWave - 1) wsum[w] = inc;
+  __syncthreads();
+  int base = inc - v;
+  for (int q = 0; q < 16; ++q)
+    if (q < w) base += wsum[q];
+  return base;
+}
+
 // exclusive scan of the histogram (one block, MTGP_SCHED_BINS / 1024 bins per thread)
 __global__ void __launch_bounds__(1024) k_sched_scan(const int32_t* __restrict__ hist, int32_t* __restrict__ offs) {
   constexpr int kPer = MTGP_SCHED_BINS / 1024;
-  __shared__ int32_t part[1024];
+  __shared__ int32_t wsum[16];
   const int t = threadIdx.x;
   int loc[kPer], sum = 0;
+#pragma unroll
   for (int i = 0; i < kPer; ++i) { loc[i] = sum; sum += hist[t * kPer + i]; }
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan
-    const int v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  const int base = part[t] - sum;
+  const int base = block_excl_scan_1024(sum, wsum);
+#pragma unroll
   for (int i = 0; i < kPer; ++i) offs[t * kPer + i] = base + loc[i];
 }
 
 // ascending rank s -> slot: G >= 2 interleaves (most expensive, cheapest, 2nd, 2nd cheapest, ...)
 // so every wave holds a balanced mix; G == 1 runs the most expensive first.
+__device__ __forceinline__ int sched_slot(int s, int P, int G) {
+  if (G == 1) return P - 1 - s;
+  const int h = P / 2;
+  if (s < h) return 2 * s + 1;
+  if (s >= P - h) return 2 * (P - 1 - s);
+  return P - 1;  // middle element of an odd P
+}
+
 __global__ void __launch_bounds__(256) k_sched_scatter(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
                                                        int G, int32_t* __restrict__ offs, int32_t* __restrict__ order) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= P) return;
-  const int s = atomicAdd(&offs[sched_cost(plen, p, n_prog, W)], 1);
-  int q;
-  if (G == 1) {
-    q = P - 1 - s;
-  } else {
-    const int h = P / 2;
-    if (s < h) q = 2 * s + 1;
-    else if (s >= P - h) q = 2 * (P - 1 - s);
-    else q = P - 1;  // middle element of an odd P
-  }
-  order[q] = p;
+  order[sched_slot(atomicAdd(&offs[sched_cost(plen, p, n_prog, W)], 1), P, G)] = p;
 }
 
 // The whole schedule in ONE block (P * n_prog <= kSchedFusedMax): histogram, exclusive scan and scatter in
 // LDS (no memset, no global atomics, one launch instead of three + a fill).  Same slot formula as
-// k_sched_scatter; ties are ordered arbitrarily as there.
+// k_sched_scatter; ties are ordered arbitrarily as there.  KP > 0 (P <= 1024 * KP): every thread's
+// costs are computed once, their loads issued together, and held in registers for both atomic
+// passes (9.6 -> 7.7 us at P = 8192, scripts/overhead_mb.hip); KP = 0 recomputes them in strided loops.
 constexpr long kSchedFusedMax = 1 << 16;  // program entries (P * n_prog): C3 32768 -> fused, C5 262144 -> 3 kernels
+constexpr int kSchedRegP = 8;              // costs per thread held in registers (P <= 8192)
+template <int KP>
 __global__ void __launch_bounds__(1024) k_sched_fused(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
                                                       int G, int32_t* __restrict__ order) {
   __shared__ int32_t hist[MTGP_SCHED_BINS];
-  __shared__ int32_t part[1024];
+  __shared__ int32_t wsum[16];
   constexpr int kPer = MTGP_SCHED_BINS / 1024;
+  constexpr int KR = KP > 0 ? KP : 1;
   const int t = threadIdx.x;
-  for (int i = t; i < MTGP_SCHED_BINS; i += 1024) hist[i] = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) hist[i * 1024 + t] = 0;
+  int c[KR];
+  if constexpr (KP > 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k) {
+      const int p = k * 1024 + t;
+      c[k] = p < P ? sched_cost(plen, p, n_prog, W) : -1;
+    }
+  }
   __syncthreads();
-  for (int p = t; p < P; p += 1024) atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
+  if constexpr (KP > 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (c[k] >= 0) atomicAdd(&hist[c[k]], 1);
+  } else {
+    for (int p = t; p < P; p += 1024) atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
+  }
   __syncthreads();
   int loc[kPer], sum = 0;
 #pragma unroll
   for (int i = 0; i < kPer; ++i) { loc[i] = sum; sum += hist[t * kPer + i]; }
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < 1024; d <<= 1) {  // Hillis-Steele inclusive scan of the per-thread sums
-    const int v = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += v;
-    __syncthreads();
-  }
-  const int base = part[t] - sum;
+  const int base = block_excl_scan_1024(sum, wsum);
 #pragma unroll
   for (int i = 0; i < kPer; ++i) hist[t * kPer + i] = base + loc[i];  // (each thread rewrites its own bins)
   __syncthreads();
-  const int h = P / 2;
-  for (int p = t; p < P; p += 1024) {
-    const int sr = atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1);
-    int q;
-    if (G == 1) q = P - 1 - sr;
-    else if (sr < h) q = 2 * sr + 1;
-    else if (sr >= P - h) q = 2 * (P - 1 - sr);
-    else q = P - 1;  // middle element of an odd P
-    order[q] = p;
+  if constexpr (KP > 0) {
+#pragma unroll
+    for (int k = 0; k < KP; ++k)
+      if (c[k] >= 0) order[sched_slot(atomicAdd(&hist[c[k]], 1), P, G)] = k * 1024 + t;
+  } else {
+    for (int p = t; p < P; p += 1024) order[sched_slot(atomicAdd(&hist[sched_cost(plen, p, n_prog, W)], 1), P, G)] = p;
   }
 }
 
@@ -4201,17 +4220,33 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes(uint32_t* __restrict__ 
 }
 
 // The same scan with every thread's PER sizes held in registers (one read, one write pass),
-// wave scans by shuffles and one barrier for the 16 wave totals (units <= 1024 * PER).
+// wave scans by shuffles and one barrier for the 16 wave totals (units <= 1024 * PER).  The sizes
+// are read and the offsets written coalesced (unit k * 1024 + t by thread t) and transposed
+// through LDS to the thread-contiguous runs the scan needs: a thread reading its run straight
+// from global memory touches a cache line per unit, which through the one CU this block runs on
+// took 16.0 us at 16384 units against 5.6 us (scripts/overhead_mb.hip).  One pad word per 64
+// keeps the run reads conflict-free on the 64 LDS banks.
+__device__ __forceinline__ int scan_lds_ix(int i) { return i + (i >> 6); }
 template <int PER>
 __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restrict__ offs, int total,
                                                              int32_t* __restrict__ info) {
+  constexpr int kUnits = 1024 * PER;
+  __shared__ uint32_t s_u[kUnits + kUnits / 64];
   __shared__ uint64_t wsum[16];
   __shared__ int32_t werr[16];
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const int b = t * PER;
   uint32_t v[PER];
 #pragma unroll
-  for (int k = 0; k < PER; ++k) v[k] = (b + k < total) ? offs[b + k] : 0u;
+  for (int k = 0; k < PER; ++k) {
+    const int i = k * 1024 + t;
+    v[k] = i < total ? offs[i] : 0u;
+  }
+#pragma unroll
+  for (int k = 0; k < PER; ++k) s_u[scan_lds_ix(k * 1024 + t)] = v[k];
+  __syncthreads();
+  const int b = t * PER;
+#pragma unroll
+  for (int k = 0; k < PER; ++k) v[k] = s_u[scan_lds_ix(b + k)];  // (units >= total read as 0)
   uint64_t sum = 0;
   int bad = 0;
 #pragma unroll
@@ -4242,11 +4277,16 @@ __global__ void __launch_bounds__(1024) k_jit_scan_sizes_reg(uint32_t* __restric
   }
   uint64_t run = wbase + inc - sum + mtgp::kJitTemplateBytes;  // the shared subroutines come first
 #pragma unroll
+  for (int k = 0; k < PER; ++k) {  // (the sizes re-read from LDS: v is not held over the scan)
+    const uint32_t x = s_u[scan_lds_ix(b + k)];
+    s_u[scan_lds_ix(b + k)] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
+    run += (x & 0x80000000u) ? 0u : x;
+  }
+  __syncthreads();
+#pragma unroll
   for (int k = 0; k < PER; ++k) {
-    if (b + k < total) {
-      offs[b + k] = (uint32_t)(run < 0xffffffffull ? run : 0xffffffffull);
-      run += (v[k] & 0x80000000u) ? 0u : v[k];
-    }
+    const int i = k * 1024 + t;
+    if (i < total) offs[i] = s_u[scan_lds_ix(i)];
   }
   if (t == 1023) {
     const uint64_t tot = wbase + inc + mtgp::kJitTemplateBytes;
@@ -5384,7 +5424,10 @@ int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t*
   const int G = Rp >= kWave ? 1 : kWave / Rp;
   hipStream_t s = (hipStream_t)stream;
   if ((long)P * n_prog <= kSchedFusedMax) {  // small populations: one block does it all
-    hipLaunchKernelGGL(k_sched_fused, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
+    if (P <= 1024 * kSchedRegP)
+      hipLaunchKernelGGL(k_sched_fused<kSchedRegP>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
+    else
+      hipLaunchKernelGGL(k_sched_fused<0>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
     return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
   }
   int32_t* hist = scratch;

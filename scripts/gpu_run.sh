@@ -62,6 +62,7 @@ for step in "$@"; do
     c5occ) run c5occ_2 300 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1
            run c5occ_1 300 env MTGP_WIDE_LDS_MIN=90000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1
            run c5occ_2b 300 env MTGP_WIDE_LDS_MIN=60000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
+    testsched) run pytest_sched 600 python -u -m pytest tests/test_gpu_schedule.py tests/test_gpu_build.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     testbuild) run pytest_build 300 python -u -m pytest tests/test_gpu_build.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench_ss8) run bench_ss8 600 python bench.py --state-size 8 --steps 30 --warmup 5 --e2e-steps 0 || exit 1 ;;
@@ -141,6 +142,12 @@ for step in "$@"; do
           python3 scripts/pmc_summary.py $O/pmc_fair${f}_$c k_ctl_dynamic > $O/pmc_fair${f}_$c.json; cat $O/pmc_fair${f}_$c.json
         done
       done ;;
+    pmcsq_flat) KSUB=k_flatten_wave pmcsq pmcsq_flat c3 && python3 scripts/pmc_summary.py $O/pmcsq_flat k_jit_emit_waves > $O/pmcsq_emit.json && cat $O/pmcsq_emit.json || exit 1 ;;
+    pmcmem_flat) run pmcmem_flat 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_INSTS_SMEM SQ_INSTS_VMEM_RD \
+        SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_BRANCH -d $O/pmcmem_flat -o pmcmem_flat --output-format csv \
+        -- python3 scripts/kprof.py --iters 2 --config c3 || exit 1
+      python3 scripts/pmc_summary.py $O/pmcmem_flat k_flatten_wave > $O/pmcmem_flat.json && cat $O/pmcmem_flat.json
+      python3 scripts/pmc_summary.py $O/pmcmem_flat k_jit_emit_waves > $O/pmcmem_emit.json && cat $O/pmcmem_emit.json || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;
