@@ -3664,6 +3664,25 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
     s_val[i] = row[k].w;
     cnt += __popcll(__ballot(i < N && row[k].x != 0.0f));
   }
+  // Few trees (T <= kFlatDirectTrees): the individual's first program counts them all (see the end);
+  // the other trees' node columns are loaded here, in flight together with this tree's rows,
+  // instead of one dependent load per tree after the passes
+  const bool direct = T <= kFlatDirectTrees;
+  int cnt_others = 0;
+  if (direct && j == 0) {
+    float xo[kFlatDirectTrees][RPL];
+#pragma unroll
+    for (int t = 0; t < kFlatDirectTrees; ++t)
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) {
+        const int i = k * kWave + lane;
+        xo[t][k] = (t < T && t != sp.tree && i < N) ? pop[(((size_t)p * T + t) * N + i) * 4] : 0.0f;
+      }
+#pragma unroll
+    for (int t = 0; t < kFlatDirectTrees; ++t)
+#pragma unroll
+      for (int k = 0; k < RPL; ++k) cnt_others += __popcll(__ballot(xo[t][k] != 0.0f));
+  }
   auto operand = [&](int jj, int i, uint32_t& w, ULeaf& lf, int& len, int& flen, bool& leaf) {
     if (jj < i) {
       w = s_w[jj];
@@ -3851,7 +3870,8 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
             if (leafa) {
               MtgpInstr w2[2];
               const int nw = u_unary_leaf(fn, la, push, w2);
-              for (int q = 0; q < nw; ++q) emit(pos + q, w2[q]);
+              emit(pos, w2[0]);  // (nw is 1 or 2; no dynamic index into w2, which would put it in scratch)
+              if (nw > 1) emit(pos + 1, w2[1]);
             } else { visit(ca, pos, push); emit(pos + flena, un); }
           } else if (leafa && leafb) {
             fuse_pair(u_load(la, push), u_op_leaf(fn, 0, lb), &x);
@@ -3900,10 +3920,9 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
   // program counts them all and stores the sum (no zeroing pass before the launch); many trees
   // (C5: 64): tree t is counted by program t % n_prog and summed with atomics into the zeroed
   // nodes_out, so no single wave walks the whole individual.
-  const bool direct = T <= kFlatDirectTrees;
   if (direct && j != 0) return;
-  int c = 0;
-  for (int t = direct ? 0 : j; t < T; t += direct ? 1 : n_prog) {
+  int c = direct ? cnt + cnt_others : 0;
+  for (int t = j; !direct && t < T; t += n_prog) {
     if (t == sp.tree) { c += cnt; continue; }
     const float4* tt = reinterpret_cast<const float4*>(pop + ((size_t)p * T + t) * N * 4);
 #pragma unroll

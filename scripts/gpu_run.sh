@@ -148,6 +148,7 @@ for step in "$@"; do
         -- python3 scripts/kprof.py --iters 2 --config c3 || exit 1
       python3 scripts/pmc_summary.py $O/pmcmem_flat k_flatten_wave > $O/pmcmem_flat.json && cat $O/pmcmem_flat.json
       python3 scripts/pmc_summary.py $O/pmcmem_flat k_jit_emit_waves > $O/pmcmem_emit.json && cat $O/pmcmem_emit.json || exit 1 ;;
+    pmcsq_flat5) KSUB=k_flatten_wave pmcsq pmcsq_flat5 c5 && python3 scripts/pmc_summary.py $O/pmcsq_flat5 k_jit_emit_groups > $O/pmcsq_emit5.json && cat $O/pmcsq_emit5.json || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;
