@@ -149,6 +149,10 @@ for step in "$@"; do
       python3 scripts/pmc_summary.py $O/pmcmem_flat k_flatten_wave > $O/pmcmem_flat.json && cat $O/pmcmem_flat.json
       python3 scripts/pmc_summary.py $O/pmcmem_flat k_jit_emit_waves > $O/pmcmem_emit.json && cat $O/pmcmem_emit.json || exit 1 ;;
     pmcsq_flat5) KSUB=k_flatten_wave pmcsq pmcsq_flat5 c5 && python3 scripts/pmc_summary.py $O/pmcsq_flat5 k_jit_emit_groups > $O/pmcsq_emit5.json && cat $O/pmcsq_emit5.json || exit 1 ;;
+    pmcmem_c3) run pmcmem_c3 120 timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD \
+        SQ_INSTS_VMEM_WR SQ_INSTS_FLAT SQ_INSTS_SMEM SQ_INSTS_LDS -d $O/pmcmem_c3 -o pmcmem_c3 --output-format csv \
+        -- python3 scripts/kprof.py --iters 2 --config c3 || exit 1
+      python3 scripts/pmc_summary.py $O/pmcmem_c3 k_ctl_dynamic > $O/pmcmem_c3.json && cat $O/pmcmem_c3.json || exit 1 ;;
     pmcsq_c5) KSUB=k_sr_wide pmcsq pmcsq_c5 c5 || exit 1 ;;
     pmcsq_c3) KSUB=k_ctl_dynamic pmcsq pmcsq_c3 c3 || exit 1 ;;
     pmcsq_c2) KSUB=k_ctl_static pmcsq pmcsq_c2 c2 || exit 1 ;;

@@ -21,8 +21,11 @@ def _costs(eng, fl):
     return np.clip(c, 0, nat.SCHED_BINS - 1)
 
 
-@pytest.mark.parametrize("P", [1, 2, 7, 300])
-@pytest.mark.parametrize("R", [8, 32, 64])
+# P up to 8192: the one-block schedule with the costs in registers; 9000: the one-block form that
+# recomputes them (P * n_prog <= 65536 with 3 or 4 programs); 24000: histogram / scan / scatter in
+# three launches
+@pytest.mark.parametrize("P,R", [(P, R) for P in (1, 2, 7, 300) for R in (8, 32, 64)]
+                         + [(8192, 32), (9000, 32), (9000, 64), (24000, 32), (24000, 64)])
 def test_schedule_is_balanced_permutation(P, R):
     env, lib, ff, data, pop = dynamic_setup(P=P, R=R, n_steps=4, seed=3)
     eng = DeviceEngine(ff, lib, 0.0, "cuda:0")
