@@ -53,6 +53,14 @@ def _check_status(status, err):
         raise RankFailed(f"rank(s) {bad} failed in their shard (see their own error)")
 
 
+def all_gather_device(buf: torch.Tensor, ws: int, group=None) -> torch.Tensor:
+    """The RCCL collective of gather_fitness / sharded_rows: one all_gather_into_tensor of every
+    rank's equal-shape device buffer -> [ws, *buf.shape] on the same device."""
+    full = torch.empty((ws * buf.shape[0],) + tuple(buf.shape[1:]), dtype=buf.dtype, device=buf.device)
+    dist.all_gather_into_tensor(full, buf.contiguous(), group=group)
+    return full.view((ws,) + tuple(buf.shape))
+
+
 def gather_fitness(local, P: int, per: int, group=None, err=None, check: bool = True) -> torch.Tensor:
     """All-gather fixed-size fitness shards (padded to `per`) and trim to [P].  Each rank's block
     carries one status word (local is None / err set when this rank's shard failed), so a failure
@@ -75,9 +83,7 @@ def gather_fitness(local, P: int, per: int, group=None, err=None, check: bool = 
         dist.all_gather(parts, buf, group=group)
         full = torch.stack(parts)
     else:
-        full = torch.empty((ws * (per + 1),), dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(full, buf, group=group)  # RCCL over xGMI
-        full = full.view(ws, per + 1)
+        full = all_gather_device(buf, ws, group)  # RCCL over xGMI
     if check or err is not None:
         _check_status(full[:, per].tolist(), err)
     return full[:, :per].reshape(-1)[:P]
@@ -128,10 +134,7 @@ def sharded_rows(compute: Callable[[int, int], Tuple["np.ndarray", "np.ndarray"]
         dist.all_gather(parts, t, group=group)
         full = torch.stack(parts)
     else:  # RCCL: device buffers
-        dev = local_device()
-        full = torch.empty((ws * (per + 1), width), dtype=torch.float32, device=dev)
-        dist.all_gather_into_tensor(full, t.to(dev), group=group)
-        full = full.cpu().view(ws, per + 1, width)
+        full = all_gather_device(t.to(local_device()), ws, group).cpu()
     full = full.numpy()
     _check_status(full[:, per, 0].tolist(), err)
     full = full[:, :per].reshape(ws * per, width)[:n]

@@ -63,6 +63,7 @@ for step in "$@"; do
            run c5occ_1 300 env MTGP_WIDE_LDS_MIN=90000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1
            run c5occ_2b 300 env MTGP_WIDE_LDS_MIN=60000 python bench.py --config c5 --no-cpu-baseline --e2e-steps 0 || exit 1 ;;
     testsched) run pytest_sched 600 python -u -m pytest tests/test_gpu_schedule.py tests/test_gpu_build.py tests/test_gpu_parity.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
+    testrccl) run pytest_rccl 300 python -u -m pytest tests/test_gpu_rccl.py -m gpu -x -v --timeout 240 --timeout-method thread || exit 1 ;;
     testbuild) run pytest_build 300 python -u -m pytest tests/test_gpu_build.py -m gpu -x -v --timeout 120 --timeout-method thread || exit 1 ;;
     testext) run pytest_ext 600 python -u -m pytest tests/test_gpu_ext_ops.py tests/test_gpu_build.py -m gpu -x -v --timeout 300 --timeout-method thread || exit 1 ;;
     bench_ss8) run bench_ss8 600 python bench.py --state-size 8 --steps 30 --warmup 5 --e2e-steps 0 || exit 1 ;;
