@@ -50,8 +50,12 @@ def parse():
                     help="C2/C3 node library + exp, log, sqrt, tanh, abs (p 0.1 each, like sin / cos): the JIT's "
                          "extended-operator templates under the headline workload (A/B line, not the headline)")
     ap.add_argument("--state-size", type=int, default=2,
-                    help="C3 hidden-state trees (the notebook's 2); 4 .. 16 run the runtime-state-size interpreter "
-                         "kernels (A/B line, not the headline)")
+                    help="C3 hidden-state trees (the notebook's 2); 4 .. 16 run the runtime-state-size kernels "
+                         "with LDS-data JIT code (A/B line, not the headline)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process group for N > 1: nccl (= RCCL, the product) or gloo -- a rehearsal of the "
+                         "multi-rank flow (barriers, fitness all-gather, max-over-ranks timing) with several "
+                         "ranks on one GPU, which RCCL refuses; never a measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-pmc", action="store_true",
@@ -241,6 +245,16 @@ def host_evolve_threads() -> str:
     return f"{min(len(os.sched_getaffinity(0)), 64)} (affinity)"
 
 
+def reduce_scalar(x: float, op, dev) -> float:
+    """all_reduce of one float64 over the ranks: a device tensor under RCCL, a host one under gloo"""
+    import torch
+    import torch.distributed as dist
+    on = dev if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([x], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=op)
+    return float(t.item())
+
+
 def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
     """SURVEY §8(d) end-to-end rate: GeneticProgramming.evaluate_population (gp.py:403-433) on a
     host numpy population of P*ws individuals, as the user's loop calls it -- H2D copy of this
@@ -268,9 +282,7 @@ def end_to_end(args, ff, lib, data, pop, ws, rank, dev):
         dist.barrier()
     el = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+        el = reduce_scalar(el, dist.ReduceOp.MAX, dev)
     # the host half of a generation: GeneticProgramming.evolve (gp.py:475-497) on the same
     # population (native host library, include/mtgp_host.h)
     ev = []
@@ -317,11 +329,15 @@ def main():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+    rccl = args.dist_backend == "nccl"
+    # (a gloo rehearsal may run more ranks than the box has GPUs: they share the devices)
+    dev = torch.device("cuda", local if rccl else local % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
+    if ws > 1:
+        if rccl:
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
     from multitreegp_amd import _native as nat
     from multitreegp_amd import distributed as mdist
     from multitreegp_amd.engine import DeviceEngine
@@ -355,9 +371,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if ws > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        elapsed = reduce_scalar(elapsed, dist.ReduceOp.MAX, dev)
     ms_per_step = elapsed * 1e3 / args.steps
     n_hist = min(args.steps, 1024)  # the evaluator launches' hipEvent durations (ring of 1024), read after the run
     hist = (ctypes.c_float * n_hist)()
@@ -370,10 +384,9 @@ def main():
     R, S, n_steps = d["R"], d["n_save"], d["n_steps"]
     steps_host = res["steps"].cpu().numpy() if adaptive else None
     if adaptive:  # step attempts of this rank; every rank evaluates its own shard of the same size
-        t = torch.tensor([int(steps_host.sum())], dtype=torch.float64, device=dev)
+        units_per_step = float(int(steps_host.sum()))
         if ws > 1:
-            dist.all_reduce(t)
-        units_per_step = float(t.item())
+            units_per_step = reduce_scalar(units_per_step, dist.ReduceOp.SUM, dev)
     else:
         units_per_step = P * R * n_steps * ws
     value = units_per_step / (ms_per_step / 1e3)
@@ -461,6 +474,8 @@ def main():
                                                       if k in pmc}},
     }
     out["build"] = build_record()
+    if ws > 1 and not rccl:
+        out["rehearsal"] = "gloo process group, ranks sharing GPUs: a check of the multi-rank flow, not a measurement"
     if adaptive:
         out["metric"] = ("population x rollout ODE-steps/sec (adaptive Dopri5 + PIDController; a step = one step "
                          "attempt, rejected ones included)")
@@ -480,7 +495,7 @@ def main():
             "host_evolve_ms": evolve_ms,
             "host_evolve_what": f"GeneticProgramming.evolve of the {P * ws}-candidate population (native host "
                                 f"library on {host_evolve_threads()} threads), median of 3"}
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and ws == 1 and not args.no_cpu_baseline:  # (the contract: rank 0 at N = 1 only)
         out["cpu_baseline"] = cpu_baseline(args, lib, ff, data, pop, steps_host)
     if rank == 0:
         print(json.dumps(out), flush=True)

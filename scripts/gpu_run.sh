@@ -117,6 +117,7 @@ for step in "$@"; do
     ab_c2_fuse) run ab_c2_fuse 400 python scripts/kvariants.py --config c2 --rounds 10 --variants "prod,nofuse" --tag c2_fuse || exit 1 ;;
     ab_c2) V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
       run ab_c2 400 python scripts/kvariants.py --config c2 --rounds 8 --variants $V --tag ab_c2 || exit 1 ;;
+    bench_gloo2) run bench_gloo2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --dist-backend gloo --steps 10 --warmup 2 --no-pmc --e2e-steps 3 || exit 1 ;;
     rccl2) run rccl2 180 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29531 scripts/rccl_two_ranks.py || exit 1 ;;
     ab_dp_layout) run ab_dp_layout 600 python scripts/kvariants.py --solver dopri5 --rounds 4 --variants "prod@MTGP_TRAJ_LAYOUT=time,prod" --tag dp_layout || exit 1 ;;
     ab_dpw3) run ab_dpw3 600 python scripts/kvariants.py --solver dopri5 --rounds 4 --variants "prod,dpw3" --tag dp_w3 && run ab_dpw3n 600 python scripts/kvariants.py --solver dopri5 --obs-noise 0.1 --rounds 2 --variants "prod,dpw3" --tag dpn_w3 || exit 1 ;;
