@@ -4166,16 +4166,24 @@ __device__ __forceinline__ int jit_unit_words_from(const JitUnitArgs& U, const i
   return n;
 }
 
-// pass 1, one thread per unit: its size in bytes, or 0x80000000 | -error
+// pass 1, one thread per unit: its size in bytes, or 0x80000000 | -error.  A chain member's span
+// needs the words of the members packed in front of it: those of this block are read from LDS
+// (every thread sizes its own unit first), only members in an earlier block are sized again
+// (C5's store chains run over all 64 programs of a wave: up to 63 members x 8 groups of loads
+// per thread before).
 __global__ void __launch_bounds__(256) k_jit_sizes(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                    uint32_t* __restrict__ offs) {
-  const int u = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ int s_words[256];
+  const int u0 = blockIdx.x * blockDim.x;
+  const int u = u0 + threadIdx.x;
+  const int n = u < U.n_units ? jit_unit_words_from(U, jw, u) : 0;
+  s_words[threadIdx.x] = n;
+  __syncthreads();
   if (u >= U.n_units) return;
-  const int n = jit_unit_words_from(U, jw, u);
   uint32_t pre = 0u;  // the chain members packed in front of this unit
   int bad = 0;
   for (int v = u - 1; v >= 0 && v / U.n_prog == u / U.n_prog && mtgp::jit_unit_packed(U.next, v % U.n_prog, U.store, U.n_prog); --v) {
-    const int m = jit_unit_words_from(U, jw, v);
+    const int m = v >= u0 ? s_words[v - u0] : jit_unit_words_from(U, jw, v);
     if (m < 0) bad = m;
     else pre += (uint32_t)m * 4u;
   }
