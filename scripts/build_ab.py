@@ -41,7 +41,8 @@ def main():
         if p.wait() != 0:
             raise SystemExit(f"hipcc failed for {name}")
         objs = [obj0] + [os.path.join(objdir, f"mtgp_kernels_tu{tu}.o") for tu in g.HIP_TUS if tu != TU] + \
-               [os.path.join(objdir, "mtgp_grad.o")]
+               [os.path.join(objdir, "mtgp_grad.o"), os.path.join(objdir, "mtgp_build_info.o")]  # (the
+        # product's build info: a variant reports the product's sources hash)
         out = os.path.join(out_dir, f"libmtgp_hip_{name}.so")
         subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-fPIC", "-shared", *objs, "-o", out,
                         "-L/opt/rocm/lib", "-lhsa-runtime64"], check=True)

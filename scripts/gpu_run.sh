@@ -114,6 +114,7 @@ for step in "$@"; do
     ab_c5_bfm) run ab_c5_bfm 400 python scripts/kvariants.py --config c5 --rounds 6 --variants "prod,shift" --tag c5_bfm || exit 1 ;;
     ab_c3_bfm) run ab_c3_bfm 400 python scripts/kvariants.py --config c3 --rounds 8 --variants "prod,shift" --tag c3_bfm || exit 1 ;;
     ab_c2_noprog) run ab_c2_noprog 400 python scripts/kvariants.py --config c2 --rounds 6 --variants "prod,noprog" --tag c2_noprog || exit 1 ;;
+    ab_c2_merge) run ab_c2_merge 400 python scripts/kvariants.py --config c2 --rounds 10 --variants "prod,nomerge" --tag c2_merge || exit 1 ;;
     ab_c2_fuse) run ab_c2_fuse 400 python scripts/kvariants.py --config c2 --rounds 10 --variants "prod,nofuse" --tag c2_fuse || exit 1 ;;
     ab_c2) V=prod; for f in multitreegp_amd/lib/abrun/libmtgp_hip_*.so; do b=$(basename $f .so); V=$V,${b#libmtgp_hip_}; done
       run ab_c2 400 python scripts/kvariants.py --config c2 --rounds 8 --variants $V --tag ab_c2 || exit 1 ;;
