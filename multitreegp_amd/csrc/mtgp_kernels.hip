@@ -4436,6 +4436,92 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   }
 }
 
+// The same emit with TWO (unit, group) pairs per wave, one per 32-lane half (chunks of 32
+// instructions, prefix sums within the half).  The register-mode programs are short (C3: most
+// under 32 instructions), so a whole wave per pair left half of it idle and 32,768 waves ran in
+// four rounds at full occupancy; the same words as k_jit_emit_waves (tests/test_gpu_build.py).
+template <int KI>  // chunks of 32 instructions
+__global__ void __launch_bounds__(256) k_jit_emit_halves(JitUnitArgs U, const int32_t* __restrict__ jw,
+                                                         const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
+                                                         uint64_t code_bytes, JitOpTable optab) {
+  constexpr int kHalf = kWave / 2;
+  if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
+    for (int k = threadIdx.x; k < MTGP_JIT_SUB_WORDS; k += blockDim.x) code[k] = mtgp_jit_sub_blob[k];
+  }
+  const int lane = threadIdx.x & (kWave - 1), hl = lane & (kHalf - 1), half = lane / kHalf;
+  const long i = (((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave) * 2 + half;  // (half-uniform)
+  bool live = i < (long)U.n_units * U.G;
+  int u = 0, g = 0, wave = 0, j = 0, q = 0;
+  if (live) {
+    u = (int)(i / U.G);
+    g = (int)(i - (long)u * U.G);
+    wave = u / U.n_prog;
+    j = u - wave * U.n_prog;
+    q = wave * U.G + g;
+    live = q < U.P;
+  }
+  uint32_t b = 0u;
+  if (live) {
+    b = offs[u];
+    const uint32_t e = offs[u + 1];
+    live = !(e <= b || (uint64_t)e > code_bytes);  // untranslatable unit or short buffer (checked on use)
+  }
+  const int remap = live ? mtgp::jit_put_remap(U.next, U.put, j) : -1;
+  uint32_t start = 0;  // words before group g inside the unit
+  for (int h = 0; live && h < g; ++h) {
+    const int ind = U.order ? U.order[wave * U.G + h] : wave * U.G + h;
+    start += (uint32_t)jw[(size_t)ind * U.n_prog + j] + (uint32_t)mtgp::jit_merge_words(h);
+  }
+  const bool last = (g == U.G - 1) || (q + 1 >= U.P);
+  const uint32_t at = b + start * 4u;  // byte address of the group's first word
+  uint32_t* out = code + at / 4;
+  const int ind = live ? (U.order ? U.order[q] : q) : 0;
+  const MtgpInstr* prog = U.prog + ((size_t)ind * U.n_prog + j) * U.L;
+  const int pre = mtgp::jit_merge_keep(g) ? 1 : 0;  // v_mov v25, v8
+  MtgpInstr end;
+  end.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
+  end.imm = 0.0f;
+  int woff = 0, sp = 0;  // words and stack depth before this chunk
+  bool ended = !live;    // (half-uniform)
+#pragma unroll
+  for (int k = 0; k < KI; ++k) {
+    if (__ballot(!ended) == 0ull) break;  // (wave-uniform: both halves done)
+    const int ii = k * kHalf + hl;
+    const MtgpInstr x = (!ended && ii < U.L) ? prog[ii] : end;
+    const uint32_t c = x.op >> MTGP_OP_SHIFT;
+    const uint32_t ends = (uint32_t)(__ballot(c == (uint32_t)MTGP_OP_END) >> (half * kHalf));
+    const int first_end = ends ? __ffs(ends) - 1 : kHalf;
+    const bool in = !ended && hl < first_end;
+    const uint32_t f = (in && c < 64u) ? optab.flags[c] : 0u;
+    const int w = (in && c < 64u) ? optab.words[c] : 0;
+    const int d = (f & kOpPush) ? 1 : ((f & kOpPop) ? -1 : 0);
+    int wi = w, di = d;  // inclusive prefix sums over the chunk (within the half)
+#pragma unroll
+    for (int off = 1; off < kHalf; off <<= 1) {
+      const int vw = __shfl_up(wi, off, kHalf), vd = __shfl_up(di, off, kHalf);
+      if (hl >= off) { wi += vw; di += vd; }
+    }
+    if (in) {
+      const MtgpInstr t[2] = {x, end};
+      mtgp::JitOut o{out + pre + woff + (wi - w), 0};
+      o.base = at + (uint32_t)(pre + woff + (wi - w)) * 4u;
+      (void)mtgp::jit_program(o, t, 2, false, mtgp::kJitModeRegs, 0, mtgp::kJitPre, 0, nullptr, sp + di - d,
+                              nullptr, 0, remap < 0 ? -1 : U.put_slot, remap);
+    }
+    woff += __shfl(wi, kHalf - 1, kHalf);
+    sp += __shfl(di, kHalf - 1, kHalf);
+    ended = ended || ends != 0u;
+  }
+  if (live && hl == 0) {
+    mtgp::JitOut o{out, 0};
+    o.base = at;
+    if (mtgp::jit_merge_keep(g)) o.movv(mtgp::kJitKeep, mtgp::kJitAcc);
+    o.n = pre + woff;
+    if (g > 0) mtgp::jit_merge_tail(o, g, U.Rp, last);
+    if (last) mtgp::jit_unit_end(o, U.next, U.cond, j, U.store, U.n_prog);
+  }
+}
+
 // LDS-data emit with one WAVE per (unit, group) (the wide-state SR kernel's pipelined units,
 // mtgp_jit.h jit_lds_region): the lanes first find the preload tables of the group's program and
 // of the next group's (the first kJitPreSlots distinct data slots in order of first use: per slot
@@ -5237,6 +5323,18 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   hipStream_t s = (hipStream_t)stream;
   const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
   const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread / wave (read per call: tests switch it)
+  if (U.mode == mtgp::kJitModeRegs && !(ew && (strcmp(ew, "thread") == 0 || strcmp(ew, "wave64") == 0)) &&
+      U.L <= 5 * kWave) {  // (MTGP_JIT_EMIT=wave64: one wave per pair, the round-4 emitter)
+    static const JitOpTable optab = jit_op_table();
+    const long hthreads = (threads + 1) / 2 * kWave;
+    if (U.L <= 3 * kWave)
+      hipLaunchKernelGGL(k_jit_emit_halves<6>, dim3((unsigned)((hthreads + 255) / 256)), dim3(256), 0, s, U,
+                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    else
+      hipLaunchKernelGGL(k_jit_emit_halves<10>, dim3((unsigned)((hthreads + 255) / 256)), dim3(256), 0, s, U,
+                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
+  }
   if (U.mode == mtgp::kJitModeRegs && !(ew && strcmp(ew, "thread") == 0) && U.L <= 5 * kWave) {
     static const JitOpTable optab = jit_op_table();
     const long wthreads = threads * kWave;
