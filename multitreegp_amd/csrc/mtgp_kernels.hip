@@ -3219,14 +3219,17 @@ JitOpTable jit_op_table() {
   return t;
 }
 
-template <int KI>
+// LP: the lanes sizing one program (the wave, or a 32-lane half of it -- k_flatten_wave's two
+// programs per wave); lane = the lane within them, KI chunks of LP instructions
+template <int KI, int LP = kWave>
 __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n, const JitOpTable& T,
                                                    int32_t* jit_words_out, int32_t* jit_cost_out, size_t pj, int lane) {
+  const int shift = LP == kWave ? 0 : (int)(threadIdx.x & (kWave - 1) & ~(LP - 1));  // this segment's first lane
   int words = 0, sub = 0, carry = 0, rc = 0;
   bool failed = false;
 #pragma unroll
   for (int k = 0; k < KI; ++k) {
-    const int i = k * kWave + lane;
+    const int i = k * LP + lane;
     const bool in = i < n;
     int d = 0, e = 0;
     if (in) {
@@ -3245,23 +3248,24 @@ __device__ __forceinline__ void flat_jit_size_wave(const MtgpInstr* prog, int n,
     }
     int incl = d;  // inclusive prefix sum of the stack effects over this chunk
 #pragma unroll
-    for (int off = 1; off < kWave; off <<= 1) {
-      const int v = __shfl_up(incl, off);
+    for (int off = 1; off < LP; off <<= 1) {
+      const int v = __shfl_up(incl, off, LP);
       if (lane >= off) incl += v;
     }
     const int before = carry + incl - d;
     if (in && e == 0 && ((d > 0 && before >= MTGP_STACK_MAX) || (d < 0 && before <= 0))) e = mtgp::kJitErrStack;
-    carry += __shfl(incl, kWave - 1);
-    const uint64_t bad = __ballot(in && e != 0);
+    carry += __shfl(incl, LP - 1, LP);
+    uint64_t bad = __ballot(in && e != 0) >> shift;
+    if (LP < kWave) bad &= (1ull << LP) - 1ull;
     if (!failed && bad) {
       failed = true;
-      rc = __shfl(e, __ffsll((unsigned long long)bad) - 1);
+      rc = __shfl(e, __ffsll((unsigned long long)bad) - 1, LP);
     }
   }
 #pragma unroll
-  for (int off = kWave / 2; off > 0; off >>= 1) {
-    words += __shfl_xor(words, off);
-    sub += __shfl_xor(sub, off);
+  for (int off = LP / 2; off > 0; off >>= 1) {
+    words += __shfl_xor(words, off, LP);
+    sub += __shfl_xor(sub, off, LP);
   }
   if (lane == 0) {
     if (jit_words_out) jit_words_out[pj] = failed ? rc : words;
@@ -3626,7 +3630,7 @@ constexpr int kFlatDirectTrees = 8;
 // lane-per-tree kernel needs 16 B x N per LANE).  Output = k_flatten's word for word.
 // (8 waves per SIMD: the kernel is latency-bound -- one wave walks a tree level by level through
 // LDS -- so occupancy is its throughput; 64 VGPRs fit without spills for NMAX <= 128)
-template <int NMAX>
+template <int NMAX, int LP = kWave>  // LP: lanes per program (32: two programs per wave)
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(NMAX <= 128 ? 8 : 4)))
 k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
                                                      MtgpNodeLibrary lib, const MtgpProgramSpec* __restrict__ specs,
@@ -3634,20 +3638,32 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
                                                      int32_t* nodes_out, int32_t* status_out, int32_t* jit_words_out,
                                                      int32_t* jit_cost_out, int jit_mode, JitOpTable optab) {
   using namespace mtgp;
-  constexpr int RPL = NMAX / kWave;  // rows per lane
-  __shared__ uint32_t s_w[NMAX];   // packed row record (u_pack)
-  __shared__ uint32_t s_len[NMAX]; // unfused length (low 16, saturated) | fused length (high 16)
-  __shared__ float s_cv[NMAX];     // folded constant
-  __shared__ float s_val[NMAX];    // the original value column (operands j >= i, gp.py:366-369)
-  __shared__ int32_t s_pos[NMAX];  // pass 2: first word of the node's code | push << 16
-  __shared__ uint32_t s_flag[NMAX];  // pass 1: resolved; pass 2: times reached
+  static_assert(LP == kWave || LP == kWave / 2, "a program per wave or per half");
+  constexpr int PPW = kWave / LP;  // programs per wave
+  constexpr int RPL = NMAX / LP;   // rows per lane
+  struct Tables {          // one program's tables (24 B per row + the program as written)
+    uint32_t w[NMAX];       // packed row record (u_pack)
+    uint32_t len[NMAX];     // unfused length (low 16, saturated) | fused length (high 16)
+    float cv[NMAX];         // folded constant
+    float val[NMAX];        // the original value column (operands j >= i, gp.py:366-369)
+    int32_t pos[NMAX];      // pass 2: first word of the node's code | push << 16
+    uint32_t flag[NMAX];    // pass 1: resolved; pass 2: times reached
+    MtgpInstr prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
+  };
+  __shared__ Tables s_tab[PPW];
   __shared__ int8_t s_fn[MTGP_MAX_FUNCS];
-  __shared__ MtgpInstr s_prog[NMAX + 8];  // the program as written (read back by the JIT sizing)
   __shared__ int s_fpos[MTGP_MAX_DATA];   // LDS-data sizing: first operand position per data slot
-  const int lane = threadIdx.x;
-  for (int k = lane; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
-  const long pj = blockIdx.x;
-  if (pj >= (long)P * n_prog) return;  // (uniform: one wave per block)
+  const int half = LP == kWave ? 0 : (int)(threadIdx.x / LP);
+  const int lane = threadIdx.x & (LP - 1);  // the lane within this program's lanes
+  Tables& S = s_tab[half];  // (one base address; the tables at constant offsets from it)
+  // this program's lanes' ballot (the other program's lanes masked off)
+  auto seg_ballot = [&](bool x) -> uint64_t {
+    if constexpr (LP == kWave) return __ballot(x);
+    else return (__ballot(x) >> (half * LP)) & ((1ull << LP) - 1ull);
+  };
+  for (int k = threadIdx.x; k < MTGP_MAX_FUNCS; k += kWave) s_fn[k] = lib.fn[k];
+  const long pj = (long)blockIdx.x * PPW + half;
+  if (pj >= (long)P * n_prog) return;  // (one wave per block: the other program's lanes run on alone)
   const int p = (int)(pj / n_prog), j = (int)(pj % n_prog);
   const MtgpProgramSpec sp = specs[j];
   const float4* tr = reinterpret_cast<const float4*>(pop + ((size_t)p * T + sp.tree) * N * 4);
@@ -3659,10 +3675,10 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
   int cnt = 0;  // non-empty rows of this tree (gp.py:424)
 #pragma unroll
   for (int k = 0; k < RPL; ++k) {
-    const int i = k * kWave + lane;
+    const int i = k * LP + lane;
     row[k] = i < N ? tr[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    s_val[i] = row[k].w;
-    cnt += __popcll(__ballot(i < N && row[k].x != 0.0f));
+    S.val[i] = row[k].w;
+    cnt += __popcll(seg_ballot(i < N && row[k].x != 0.0f));
   }
   // Few trees (T <= kFlatDirectTrees): the individual's first program counts them all (see the end);
   // the other trees' node columns are loaded here, in flight together with this tree's rows,
@@ -3675,28 +3691,28 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
     for (int t = 0; t < kFlatDirectTrees; ++t)
 #pragma unroll
       for (int k = 0; k < RPL; ++k) {
-        const int i = k * kWave + lane;
+        const int i = k * LP + lane;
         xo[t][k] = (t < T && t != sp.tree && i < N) ? pop[(((size_t)p * T + t) * N + i) * 4] : 0.0f;
       }
 #pragma unroll
     for (int t = 0; t < kFlatDirectTrees; ++t)
 #pragma unroll
-      for (int k = 0; k < RPL; ++k) cnt_others += __popcll(__ballot(xo[t][k] != 0.0f));
+      for (int k = 0; k < RPL; ++k) cnt_others += __popcll(seg_ballot(xo[t][k] != 0.0f));
   }
   auto operand = [&](int jj, int i, uint32_t& w, ULeaf& lf, int& len, int& flen, bool& leaf) {
     if (jj < i) {
-      w = s_w[jj];
-      const uint32_t ln = s_len[jj];
+      w = S.w[jj];
+      const uint32_t ln = S.len[jj];
       len = (int)(ln & 0xffffu);
       flen = (int)(ln >> 16);
       lf.isc = u_isc(w);
-      lf.v = s_cv[jj];
+      lf.v = S.cv[jj];
       lf.slot = u_slot(w);
       leaf = u_leaf(w);
     } else {
       w = u_pack(K_CONST, 0, 0, 1, 1, 0);
       lf.isc = true;
-      lf.v = s_val[jj];
+      lf.v = S.val[jj];
       lf.slot = 0;
       len = flen = 1;
       leaf = true;
@@ -3707,7 +3723,7 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
   bool done[RPL];
 #pragma unroll
   for (int k = 0; k < RPL; ++k) {
-    const int i = k * kWave + lane;
+    const int i = k * LP + lane;
     fnr[k] = -1;
     ja[k] = jb[k] = -1;
     done[k] = true;
@@ -3733,11 +3749,11 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
       }  // else: empty node (gp.py:135) -> +0.0
     }
     if (done[k]) {
-      s_w[i] = u_pack(kind, MTGP_FN_ZERO, slot, isc, 1, 0);
-      s_len[i] = 1u | 1u << 16;
-      s_cv[i] = cv;
+      S.w[i] = u_pack(kind, MTGP_FN_ZERO, slot, isc, 1, 0);
+      S.len[i] = 1u | 1u << 16;
+      S.cv[i] = cv;
     }
-    s_flag[i] = done[k] ? 1u : 0u;
+    S.flag[i] = done[k] ? 1u : 0u;
   }
   // ---- pass 1, later rounds: an operator row resolves once its operand rows (j < i) have
   for (;;) {
@@ -3745,8 +3761,8 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
     bool ready[RPL], pend = false;
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
-      const int i = k * kWave + lane;
-      ready[k] = !done[k] && (ja[k] >= i || s_flag[ja[k]] != 0u) && (jb[k] < 0 || jb[k] >= i || s_flag[jb[k]] != 0u);
+      const int i = k * LP + lane;
+      ready[k] = !done[k] && (ja[k] >= i || S.flag[ja[k]] != 0u) && (jb[k] < 0 || jb[k] >= i || S.flag[jb[k]] != 0u);
       pend = pend || (!done[k] && !ready[k]);
     }
     bool any_ready = false;
@@ -3756,7 +3772,7 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
       if (!ready[k]) continue;
-      const int i = k * kWave + lane;
+      const int i = k * LP + lane;
       const int fn = fnr[k], ar = fn_arity(fn);
       uint32_t kind = ar == 1 ? K_UNARY : K_BINARY, isc = 1, afirst = 1, need = 0;
       int len = 1, flen = 1;
@@ -3789,41 +3805,43 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
           else { afirst = 0; need = qb > pa + 1 ? qb : pa + 1; }
         }
       }
-      s_w[i] = u_pack(kind, (uint32_t)fn, 0, isc, afirst, need > 31u ? 31u : need);
-      s_len[i] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
-      s_cv[i] = cv;
+      S.w[i] = u_pack(kind, (uint32_t)fn, 0, isc, afirst, need > 31u ? 31u : need);
+      S.len[i] = (uint32_t)(len > 65535 ? 65535 : len) | (uint32_t)(flen > 65535 ? 65535 : flen) << 16;
+      S.cv[i] = cv;
     }
     __syncthreads();  // every read of this round's flags precedes the new ones
 #pragma unroll
     for (int k = 0; k < RPL; ++k)
       if (ready[k]) {
-        s_flag[k * kWave + lane] = 1u;
+        S.flag[k * LP + lane] = 1u;
         done[k] = true;
       }
     (void)pend;
   }
-  const uint32_t wr = s_w[N - 1], lr = s_len[N - 1];
+  const uint32_t wr = S.w[N - 1], lr = S.len[N - 1];
   int n;
   if ((int)u_need(wr) > MTGP_STACK_MAX) n = -MTGP_ERR_STACK;
   else if ((int)(lr & 0xffffu) > cap) n = -MTGP_ERR_PROG_TOO_LONG;
   else n = (int)(lr >> 16);
   // ---- pass 2: postorder positions top-down, one word per reached node, one level per round
+  // (the walk's barriers stay in wave-uniform control flow: with two programs per wave, a program
+  // that does not walk takes part with no row reached)
   bool shared = false;
-  if (n > 0) {
-    if (u_leaf(wr)) {  // the whole tree is one leaf
-      if (lane == 0) {
-        ULeaf x;
-        x.isc = u_isc(wr); x.v = s_cv[N - 1]; x.slot = u_slot(wr);
-        out[0] = s_prog[0] = u_load(x, false);
-      }
-    } else {
+  const bool walk = n > 0 && !u_leaf(wr);
+  if (n > 0 && u_leaf(wr) && lane == 0) {  // the whole tree is one leaf
+    ULeaf x;
+    x.isc = u_isc(wr); x.v = S.cv[N - 1]; x.slot = u_slot(wr);
+    out[0] = S.prog[0] = u_load(x, false);
+  }
+  {
+    if (LP == kWave ? walk : wave_any(walk)) {
       __syncthreads();
 #pragma unroll
-      for (int k = 0; k < RPL; ++k) s_flag[k * kWave + lane] = 0u;
+      for (int k = 0; k < RPL; ++k) S.flag[k * LP + lane] = 0u;
       __syncthreads();
-      if (lane == 0) {
-        s_flag[N - 1] = 1u;
-        s_pos[N - 1] = 0;
+      if (walk && lane == 0) {
+        S.flag[N - 1] = 1u;
+        S.pos[N - 1] = 0;
       }
       bool emitted[RPL];
 #pragma unroll
@@ -3833,8 +3851,8 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
         bool go[RPL], any = false;
 #pragma unroll
         for (int k = 0; k < RPL; ++k) {
-          const int i = k * kWave + lane;
-          go[k] = i < N && !emitted[k] && s_flag[i] != 0u;
+          const int i = k * LP + lane;
+          go[k] = i < N && !emitted[k] && S.flag[i] != 0u;
           any = any || go[k];
         }
         if (!wave_any(any)) break;
@@ -3843,9 +3861,9 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
         for (int k = 0; k < RPL; ++k) {
           if (!go[k]) continue;
           emitted[k] = true;
-          const int i = k * kWave + lane;
-          const uint32_t w = s_w[i];
-          const int pp = s_pos[i], pos = pp & 0xffff;
+          const int i = k * LP + lane;
+          const uint32_t w = S.w[i];
+          const int pp = S.pos[i], pos = pp & 0xffff;
           const bool push = (pp >> 16) != 0;
           const int fn = (int)u_fn(w);
           uint32_t wa, wb;
@@ -3857,13 +3875,13 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
           const int cb = u_kind(w) == K_BINARY ? jb[k] : 0;
           if (u_kind(w) == K_BINARY) operand(cb, i, wb, lb, lenb, flenb, leafb);
           auto visit = [&](int c, int cpos, bool cpush) {
-            s_pos[c] = cpos | (cpush ? 1 << 16 : 0);
-            shared = shared || atomicAdd(&s_flag[c], 1u) != 0u;  // a sub-DAG reached twice
+            S.pos[c] = cpos | (cpush ? 1 << 16 : 0);
+            shared = shared || atomicAdd(&S.flag[c], 1u) != 0u;  // a sub-DAG reached twice
           };
           MtgpInstr x;
           auto emit = [&](int at, const MtgpInstr& v) {
             out[at] = v;
-            s_prog[at] = v;
+            S.prog[at] = v;
           };
           if (u_kind(w) == K_UNARY) {
             const MtgpInstr un = u_instr(mtgp::unary_op(fn), 0, 0.0f);
@@ -3893,7 +3911,7 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
       }
     }
   }
-  shared = wave_any(shared);
+  shared = seg_ballot(shared) != 0ull;
   __syncthreads();  // every lane's program words (LDS copy) precede the END and the JIT sizing
   if (lane == 0) {
     if (shared) {  // arbitrary arrays only: the serial walk duplicates the shared subtree
@@ -3904,17 +3922,18 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
       e.op = (uint32_t)MTGP_OP_END << MTGP_OP_SHIFT;
       e.imm = 0.0f;
       out[n > 0 ? n : 0] = e;
-      s_prog[n > 0 ? n : 0] = e;
+      S.prog[n > 0 ? n : 0] = e;
       len_out[pj] = n > 0 ? n : 0;
       status_out[pj] = n > 0 ? 0 : -n;
     }
   }
   if (!shared && (jit_words_out || jit_cost_out)) {  // (shared: wave-uniform)
-    constexpr int KI = (2 * NMAX + 8 + kWave - 1) / kWave;
-    if (jit_mode == kJitModeRegs)
-      flat_jit_size_wave<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
-    else
-      flat_jit_size_wave_lds<KI>(s_prog, n, optab, jit_words_out, jit_cost_out, pj, lane, s_fpos);
+    constexpr int KI = (2 * NMAX + 8 + LP - 1) / LP;
+    if (jit_mode == kJitModeRegs) {
+      flat_jit_size_wave<KI, LP>(S.prog, n, optab, jit_words_out, jit_cost_out, pj, lane);
+    } else if constexpr (LP == kWave) {  // (two programs per wave: register mode only, mtgp_flatten_ex)
+      flat_jit_size_wave_lds<KI>(S.prog, n, optab, jit_words_out, jit_cost_out, pj, lane, s_fpos);
+    }
   }
   // node count (gp.py:424 parsimony).  Few trees (T <= kFlatDirectTrees): the individual's first
   // program counts them all and stores the sum (no zeroing pass before the launch); many trees
@@ -3927,8 +3946,8 @@ k_flatten_wave(const float* __restrict__ pop, int P, int T, int N,
     const float4* tt = reinterpret_cast<const float4*>(pop + ((size_t)p * T + t) * N * 4);
 #pragma unroll
     for (int k = 0; k < RPL; ++k) {
-      const int i = k * kWave + lane;
-      c += __popcll(__ballot(i < N && tt[i < N ? i : 0].x != 0.0f));
+      const int i = k * LP + lane;
+      c += __popcll(seg_ballot(i < N && tt[i < N ? i : 0].x != 0.0f));
     }
   }
   if (lane == 0) {
@@ -5486,6 +5505,12 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   const char* fm = getenv("MTGP_FLAT_MODE");
   const bool wave_mode = !MTGP_AB_FLAT_LANE || !(fm && strcmp(fm, "lane") == 0);
   static const JitOpTable optab = jit_op_table();  // (host probe of jit_program, once per process)
+  // trees of <= 64 rows: two programs per wave, one per 32-lane half (register-mode JIT sizing or
+  // none; C3 flatten 75 -> see DESIGN.md "Per-step overhead kernels"); A/B knob MTGP_FLAT_HALVES=0,
+  // read per call
+  const char* fh = getenv("MTGP_FLAT_HALVES");
+  const bool halves = !(fh && strcmp(fh, "0") == 0) &&
+                      (jit_mode == mtgp::kJitModeRegs || (!jit_words_out && !jit_cost_out));
   if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
   // node counts are summed with atomics into zeros, except by the wave kernel for few trees
   if ((!wave_mode || T > kFlatDirectTrees) && hipMemsetAsync(nodes_out, 0, (size_t)P * sizeof(int32_t), s) != hipSuccess)
@@ -5501,7 +5526,11 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
 #define MTGP_FLAT_LAUNCH(NM)                                                                                \
   do {                                                                                                      \
     const int tp = NM * lanes_env > 2048 ? 2048 / NM : lanes_env; /* LDS: 16 B x NM x lanes <= 32 KB */   \
-    if (wave_mode)                                                                                          \
+    if (wave_mode && NM == 64 && halves)                                                                    \
+      hipLaunchKernelGGL((k_flatten_wave<64, kWave / 2>), dim3((unsigned)((total + 1) / 2)), dim3(kWave), 0, s, \
+                         population, P, T, N, libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, \
+                         jit_words_out, jit_cost_out, jit_mode, optab);                                     \
+    else if (wave_mode)                                                                                     \
       hipLaunchKernelGGL((k_flatten_wave<NM>), dim3((unsigned)total), dim3(kWave), 0, s, population, P, T, N, \
                          libv, specs, n_prog, L, prog_out, len_out, nodes_out, status_out, jit_words_out,  \
                          jit_cost_out, jit_mode, optab);                                                    \
