@@ -41,11 +41,13 @@ def _flatten_ex(pop, lib, specs, L, mode=0):
 
 def _population(kind, P, seed=0):
     rng = np.random.default_rng(seed)
-    if kind == "dynamic":
+    if kind in ("dynamic", "dynamic3"):
         vl = [["y1", "y2", "y3", "y4", "a1", "a2", "u"], ["a1", "a2"]]
         lib = mt.NodeLibrary(CONTROL_OPS, vl, [2, 1])
         pop = sample_population(seed, lib, P, 1, max_init_depth=10, max_nodes=64)[0]
         specs = [(0, 7, 0), (1, 7, 0), (2, 7, 0b1001111), (2, 7, 0b1000000)]
+        if kind == "dynamic3":  # an odd number of programs (two per flatten wave: the last half idle)
+            specs = specs[:3]
     elif kind == "sr40":  # 40 variables, deep trees: programs read more than kJitPreSlots distinct slots
         lib = mt.NodeLibrary(SR_OPS, [[f"x{i}" for i in range(40)]], [4])
         pop = sample_population(seed, lib, P, 1, max_init_depth=9, max_nodes=128)[0]
@@ -75,7 +77,8 @@ def _population(kind, P, seed=0):
     return lib, pop, specs
 
 
-@pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("sr12", 0), ("sr12", 1), ("sr40", 1), ("dynamic", 1)])
+@pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("dynamic3", 0), ("sr12", 0), ("sr12", 1), ("sr40", 1),
+                                       ("dynamic", 1)])
 def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
     lib, pop, specs = _population(kind, 301)
     P, T, N, _ = pop.shape
