@@ -4455,20 +4455,22 @@ __global__ void __launch_bounds__(256) k_jit_emit_waves(JitUnitArgs U, const int
   }
 }
 
-// The same emit with TWO (unit, group) pairs per wave, one per 32-lane half (chunks of 32
-// instructions, prefix sums within the half).  The register-mode programs are short (C3: most
-// under 32 instructions), so a whole wave per pair left half of it idle and 32,768 waves ran in
-// four rounds at full occupancy; the same words as k_jit_emit_waves (tests/test_gpu_build.py).
-template <int KI>  // chunks of 32 instructions
+// The same emit with 64 / LP (unit, group) pairs per wave, LP lanes each (chunks of LP
+// instructions, prefix sums within the LP lanes; "halves" below for any LP).  The register-mode
+// programs are short, so a whole wave per pair left most of it idle and C3's 32,768 waves ran in
+// four rounds at full occupancy: 40.3 us one pair per wave, 28.2 two, 20.0 four (LP = 16, the
+// default; profiles/r06/v21_*, v25_*).  The same words as k_jit_emit_waves (tests/test_gpu_build.py).
+template <int KI, int LP = kWave / 2>  // KI chunks of LP instructions; LP lanes per pair
 __global__ void __launch_bounds__(256) k_jit_emit_halves(JitUnitArgs U, const int32_t* __restrict__ jw,
                                                          const uint32_t* __restrict__ offs, uint32_t* __restrict__ code,
                                                          uint64_t code_bytes, JitOpTable optab) {
-  constexpr int kHalf = kWave / 2;
+  constexpr int kHalf = LP;  // (a "half": the LP lanes of one pair)
+  constexpr int PPW = kWave / LP;
   if (blockIdx.x == 0 && code_bytes >= mtgp::kJitTemplateBytes) {  // the shared subroutines
     for (int k = threadIdx.x; k < MTGP_JIT_SUB_WORDS; k += blockDim.x) code[k] = mtgp_jit_sub_blob[k];
   }
   const int lane = threadIdx.x & (kWave - 1), hl = lane & (kHalf - 1), half = lane / kHalf;
-  const long i = (((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave) * 2 + half;  // (half-uniform)
+  const long i = (((long)blockIdx.x * blockDim.x + threadIdx.x) / kWave) * PPW + half;  // (half-uniform)
   bool live = i < (long)U.n_units * U.G;
   int u = 0, g = 0, wave = 0, j = 0, q = 0;
   if (live) {
@@ -4508,7 +4510,7 @@ __global__ void __launch_bounds__(256) k_jit_emit_halves(JitUnitArgs U, const in
     const int ii = k * kHalf + hl;
     const MtgpInstr x = (!ended && ii < U.L) ? prog[ii] : end;
     const uint32_t c = x.op >> MTGP_OP_SHIFT;
-    const uint32_t ends = (uint32_t)(__ballot(c == (uint32_t)MTGP_OP_END) >> (half * kHalf));
+    const uint32_t ends = (uint32_t)((__ballot(c == (uint32_t)MTGP_OP_END) >> (half * kHalf)) & ((1ull << kHalf) - 1ull));
     const int first_end = ends ? __ffs(ends) - 1 : kHalf;
     const bool in = !ended && hl < first_end;
     const uint32_t f = (in && c < 64u) ? optab.flags[c] : 0u;
@@ -5342,16 +5344,26 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   hipStream_t s = (hipStream_t)stream;
   const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
   const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread / wave (read per call: tests switch it)
+  // register-data units: four (unit, group) pairs per wave (16 lanes each) by default;
+  // MTGP_JIT_EMIT=halves: two per wave; wave64: one wave per pair (the round-4 emitter)
   if (U.mode == mtgp::kJitModeRegs && !(ew && (strcmp(ew, "thread") == 0 || strcmp(ew, "wave64") == 0)) &&
-      U.L <= 5 * kWave) {  // (MTGP_JIT_EMIT=wave64: one wave per pair, the round-4 emitter)
+      U.L <= 5 * kWave) {
     static const JitOpTable optab = jit_op_table();
-    const long hthreads = (threads + 1) / 2 * kWave;
-    if (U.L <= 3 * kWave)
-      hipLaunchKernelGGL(k_jit_emit_halves<6>, dim3((unsigned)((hthreads + 255) / 256)), dim3(256), 0, s, U,
-                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+    const bool quarters = !(ew && strcmp(ew, "halves") == 0);  // four pairs per wave (A/B: two)
+    const long hthreads = quarters ? (threads + 3) / 4 * kWave : (threads + 1) / 2 * kWave;
+    const dim3 grid((unsigned)((hthreads + 255) / 256));
+    if (quarters && U.L <= 3 * kWave)
+      hipLaunchKernelGGL((k_jit_emit_halves<12, 16>), grid, dim3(256), 0, s, U, jit_words, offsets, (uint32_t*)code,
+                         (uint64_t)code_bytes, optab);
+    else if (quarters)
+      hipLaunchKernelGGL((k_jit_emit_halves<20, 16>), grid, dim3(256), 0, s, U, jit_words, offsets, (uint32_t*)code,
+                         (uint64_t)code_bytes, optab);
+    else if (U.L <= 3 * kWave)
+      hipLaunchKernelGGL(k_jit_emit_halves<6>, grid, dim3(256), 0, s, U, jit_words, offsets, (uint32_t*)code,
+                         (uint64_t)code_bytes, optab);
     else
-      hipLaunchKernelGGL(k_jit_emit_halves<10>, dim3((unsigned)((hthreads + 255) / 256)), dim3(256), 0, s, U,
-                         jit_words, offsets, (uint32_t*)code, (uint64_t)code_bytes, optab);
+      hipLaunchKernelGGL(k_jit_emit_halves<10>, grid, dim3(256), 0, s, U, jit_words, offsets, (uint32_t*)code,
+                         (uint64_t)code_bytes, optab);
     return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
   }
   if (U.mode == mtgp::kJitModeRegs && !(ew && strcmp(ew, "thread") == 0) && U.L <= 5 * kWave) {

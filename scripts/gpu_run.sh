@@ -91,6 +91,7 @@ for step in "$@"; do
     prof_c3) prof prof_c3 c3 || exit 1 ;;
     prof_c3_w64) MTGP_JIT_EMIT=wave64 prof prof_c3_w64 c3 || exit 1 ;;
     prof_c3_fw) MTGP_FLAT_HALVES=0 prof prof_c3_fw c3 || exit 1 ;;
+    prof_c3_h) MTGP_JIT_EMIT=halves prof prof_c3_h c3 || exit 1 ;;
     prof_c2) prof prof_c2 c2 || exit 1 ;;
     prof_c5) prof prof_c5 c5 || exit 1 ;;
     prof_dp) SKIP=20 prof prof_dp c3 --solver dopri5 || exit 1 ;;

@@ -114,16 +114,16 @@ def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
         assert max(distinct) > 16
 
 
-@pytest.mark.parametrize("emit", ["halves", "wave64"])
+@pytest.mark.parametrize("emit", ["quarters", "halves", "wave64"])
 @pytest.mark.parametrize("kind", ["dynamic", "sr12"])
 @pytest.mark.parametrize("R", [1, 8, 32, 64])
 def test_word_based_jit_plan_and_emit_match_translation(kind, R, emit, monkeypatch):
     """Register-mode units from the word-based plan and emit equal the thread-per-unit translation:
-    the default emitter (two (unit, group) pairs per wave, one per 32-lane half) and the
-    wave-per-pair one (MTGP_JIT_EMIT=wave64)."""
+    the default emitter (four (unit, group) pairs per wave, 16 lanes each), two per wave
+    (MTGP_JIT_EMIT=halves) and one wave per pair (MTGP_JIT_EMIT=wave64)."""
     import torch
-    if emit == "wave64":
-        monkeypatch.setenv("MTGP_JIT_EMIT", "wave64")
+    if emit != "quarters":
+        monkeypatch.setenv("MTGP_JIT_EMIT", emit)
     lib, pop, specs = _population(kind, 257, seed=R)
     P, T, N, _ = pop.shape
     n_prog = len(specs)
