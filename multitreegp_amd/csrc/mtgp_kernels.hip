@@ -3616,6 +3616,9 @@ __global__ void __launch_bounds__(TPB) k_flatten(const float* __restrict__ pop, 
 // (Four independent waves per flatten block with wave-level syncs measured slower: 90 vs 71 us at
 // C3, a block holds its LDS and wave slots until its slowest program is done; r02/v18.)
 constexpr int kFlatDirectTrees = 8;
+// waves resident at once at eight per SIMD (256 CUs x 4 SIMDs x 8): the build kernels pack two or
+// four programs / JIT units per wave only when one per wave would need more than one such round
+constexpr long kResidentWaves = 8192;
 
 // Flatten, one WAVE per (individual, program spec): lane l owns rows l, l + 64, ... (NMAX / 64 per
 // lane), loaded with one coalesced 1-KB read per 64 rows.  The same two passes as k_flatten, but
@@ -5344,12 +5347,16 @@ int mtgp_jit_emit_words_chain(const MtgpInstr* prog, const int32_t* jit_words, i
   hipStream_t s = (hipStream_t)stream;
   const long threads = (long)U.n_units * U.G;  // (block 0 also writes the shared sin/cos templates)
   const char* ew = getenv("MTGP_JIT_EMIT");  // A/B knob: MTGP_JIT_EMIT=thread / wave (read per call: tests switch it)
-  // register-data units: four (unit, group) pairs per wave (16 lanes each) by default;
-  // MTGP_JIT_EMIT=halves: two per wave; wave64: one wave per pair (the round-4 emitter)
-  if (U.mode == mtgp::kJitModeRegs && !(ew && (strcmp(ew, "thread") == 0 || strcmp(ew, "wave64") == 0)) &&
-      U.L <= 5 * kWave) {
+  // register-data units: as many (unit, group) pairs per wave as keep the launch within one round of
+  // resident waves (kResidentWaves): one wave per pair up to 8,192 pairs, two up to 16,384, else
+  // four (C3: 32,768 pairs; C2's 1,024 run one per wave -- packing only lengthens a wave's chain
+  // when the chip has room for all of them).  MTGP_JIT_EMIT=wave64 / halves / quarters force one.
+  const bool force64 = ew && strcmp(ew, "wave64") == 0, forceh = ew && strcmp(ew, "halves") == 0,
+             forceq = ew && strcmp(ew, "quarters") == 0;
+  const bool pack = forceh || forceq || (!force64 && threads > kResidentWaves);
+  if (U.mode == mtgp::kJitModeRegs && !(ew && strcmp(ew, "thread") == 0) && pack && U.L <= 5 * kWave) {
     static const JitOpTable optab = jit_op_table();
-    const bool quarters = !(ew && strcmp(ew, "halves") == 0);  // four pairs per wave (A/B: two)
+    const bool quarters = forceq || (!forceh && threads > 2 * kResidentWaves);
     const long hthreads = quarters ? (threads + 3) / 4 * kWave : (threads + 1) / 2 * kWave;
     const dim3 grid((unsigned)((hthreads + 255) / 256));
     if (quarters && U.L <= 3 * kWave)
@@ -5520,8 +5527,8 @@ int mtgp_flatten_ex(const float* population, int32_t P, int32_t T, int32_t N, co
   // trees of <= 64 rows: two programs per wave, one per 32-lane half (register-mode JIT sizing or
   // none; C3 flatten 75 -> see DESIGN.md "Per-step overhead kernels"); A/B knob MTGP_FLAT_HALVES=0,
   // read per call
-  const char* fh = getenv("MTGP_FLAT_HALVES");
-  const bool halves = !(fh && strcmp(fh, "0") == 0) &&
+  const char* fh = getenv("MTGP_FLAT_HALVES");  // (0 / 1 force; default: more programs than one round)
+  const bool halves = (fh ? strcmp(fh, "0") != 0 : total > kResidentWaves) &&
                       (jit_mode == mtgp::kJitModeRegs || (!jit_words_out && !jit_cost_out));
   if (total > (long)UINT32_MAX) return MTGP_ERR_ARG;
   // node counts are summed with atomics into zeros, except by the wave kernel for few trees

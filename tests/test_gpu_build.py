@@ -77,9 +77,13 @@ def _population(kind, P, seed=0):
     return lib, pop, specs
 
 
+@pytest.mark.parametrize("halves", ["1", "0"])
 @pytest.mark.parametrize("kind,mode", [("dynamic", 0), ("dynamic3", 0), ("sr12", 0), ("sr12", 1), ("sr40", 1),
                                        ("dynamic", 1)])
-def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode):
+def test_flatten_ex_matches_host_flatten_and_jit_sizes(kind, mode, halves, monkeypatch):
+    """MTGP_FLAT_HALVES=1 forces two programs per flatten wave (trees of <= 64 rows, register-mode
+    sizing; by default only launches of more than 8,192 programs pack), 0 one per wave."""
+    monkeypatch.setenv("MTGP_FLAT_HALVES", halves)
     lib, pop, specs = _population(kind, 301)
     P, T, N, _ = pop.shape
     L = (2 * N + 8 + 3) // 4 * 4
@@ -122,8 +126,7 @@ def test_word_based_jit_plan_and_emit_match_translation(kind, R, emit, monkeypat
     the default emitter (four (unit, group) pairs per wave, 16 lanes each), two per wave
     (MTGP_JIT_EMIT=halves) and one wave per pair (MTGP_JIT_EMIT=wave64)."""
     import torch
-    if emit != "quarters":
-        monkeypatch.setenv("MTGP_JIT_EMIT", emit)
+    monkeypatch.setenv("MTGP_JIT_EMIT", emit)  # (by default the packing follows the launch size)
     lib, pop, specs = _population(kind, 257, seed=R)
     P, T, N, _ = pop.shape
     n_prog = len(specs)
