@@ -3971,6 +3971,14 @@ __device__ __forceinline__ int sched_cost(const int32_t* plen, int p, int n_prog
   return c < 0 ? 0 : (c >= MTGP_SCHED_BINS ? MTGP_SCHED_BINS - 1 : c);
 }
 
+// the same with the four programs of an individual read as one 16-byte load (n_prog == 4, plen
+// 16-byte aligned; integer sums: any order gives the same cost)
+__device__ __forceinline__ int sched_cost4(const int32_t* plen, int p, const SchedW& W) {
+  const int4 v = reinterpret_cast<const int4*>(plen)[p];
+  const int c = W.w[0] * v.x + W.w[1] * v.y + W.w[2] * v.z + W.w[3] * v.w;
+  return c < 0 ? 0 : (c >= MTGP_SCHED_BINS ? MTGP_SCHED_BINS - 1 : c);
+}
+
 __global__ void __launch_bounds__(256) k_sched_hist(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
                                                     int32_t* __restrict__ hist) {
   const int p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -4034,7 +4042,7 @@ constexpr long kSchedFusedMax = 1 << 16;  // program entries (P * n_prog): C3 32
 constexpr int kSchedRegP = 8;              // costs per thread held in registers (P <= 8192)
 template <int KP>
 __global__ void __launch_bounds__(1024) k_sched_fused(const int32_t* __restrict__ plen, int P, int n_prog, SchedW W,
-                                                      int G, int32_t* __restrict__ order) {
+                                                      int G, int32_t* __restrict__ order, int vec4) {
   __shared__ int32_t hist[MTGP_SCHED_BINS];
   __shared__ int32_t wsum[16];
   constexpr int kPer = MTGP_SCHED_BINS / 1024;
@@ -4047,7 +4055,7 @@ __global__ void __launch_bounds__(1024) k_sched_fused(const int32_t* __restrict_
 #pragma unroll
     for (int k = 0; k < KP; ++k) {
       const int p = k * 1024 + t;
-      c[k] = p < P ? sched_cost(plen, p, n_prog, W) : -1;
+      c[k] = p < P ? (vec4 ? sched_cost4(plen, p, W) : sched_cost(plen, p, n_prog, W)) : -1;
     }
   }
   __syncthreads();
@@ -5597,10 +5605,11 @@ int mtgp_schedule(const int32_t* plen, int32_t P, int32_t n_prog, const int32_t*
   const int G = Rp >= kWave ? 1 : kWave / Rp;
   hipStream_t s = (hipStream_t)stream;
   if ((long)P * n_prog <= kSchedFusedMax) {  // small populations: one block does it all
+    const int vec4 = n_prog == 4 && (reinterpret_cast<uintptr_t>(plen) & 15u) == 0;  // (C3)
     if (P <= 1024 * kSchedRegP)
-      hipLaunchKernelGGL(k_sched_fused<kSchedRegP>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
+      hipLaunchKernelGGL(k_sched_fused<kSchedRegP>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out, vec4);
     else
-      hipLaunchKernelGGL(k_sched_fused<0>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out);
+      hipLaunchKernelGGL(k_sched_fused<0>, dim3(1), dim3(1024), 0, s, plen, P, n_prog, W, G, order_out, 0);
     return hipGetLastError() == hipSuccess ? MTGP_OK : MTGP_ERR_LAUNCH;
   }
   int32_t* hist = scratch;
